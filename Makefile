@@ -1,0 +1,38 @@
+# Build for netc-mi355x: the host C library, the gfx950 HIP library, and the
+# test-only oracle (oracle/Makefile).  Outputs stay in-tree so they travel to
+# the GPU box with the repository snapshot.
+#
+#   make            libnetc.so + libnetc_ws_gpu.so + oracle
+#   make host       libnetc.so only (no hipcc needed)
+#   make clean
+
+HIPCC      ?= /opt/rocm/bin/hipcc
+CC         ?= gcc
+ARCH       ?= gfx950
+LIBDIR     := netc_amd/lib
+CFLAGS     ?= -O3 -g -Wall -Wextra -Wno-unused-parameter -fPIC -std=gnu11 -fvisibility=default
+HIPFLAGS   ?= -O3 -g -fPIC -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-result
+
+HOST_SRCS  := $(wildcard netc_amd/csrc/host/*.c)
+HOST_HDRS  := $(wildcard include/*.h include/*/*.h)
+GPU_SRCS   := netc_amd/csrc/ws_mask_gpu.hip netc_amd/csrc/ws_mask_api.hip
+GPU_HDRS   := netc_amd/csrc/ws_mask_gpu.h include/ws/mask.h
+
+.PHONY: all host gpu oracle clean
+all: host gpu oracle
+host: $(LIBDIR)/libnetc.so
+gpu: $(LIBDIR)/libnetc_ws_gpu.so
+
+$(LIBDIR)/libnetc.so: $(HOST_SRCS) $(HOST_HDRS)
+	@mkdir -p $(LIBDIR)
+	$(CC) $(CFLAGS) -shared -o $@ $(HOST_SRCS) -lpthread
+
+$(LIBDIR)/libnetc_ws_gpu.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN'
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -f $(LIBDIR)/*.so
+	$(MAKE) -C oracle clean

@@ -1,0 +1,309 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident WebSocket payload XOR-mask throughput on MI355X.
+
+Metric (BASELINE.json): GiB/s device-resident WS payload XOR-mask at 1/2/4/8 GPUs; % HBM roofline.
+
+A "step" is one call of the hot path, netc_gpu_mask_batch (include/ws/mask.h), over
+one batch of frames already resident in HBM -- by default BASELINE config 2:
+65,536 frames x 1 KiB (64 MiB), an independent random 4-byte key per frame, unmasked
+in place (the reference's receive direction, src/ws/common.c:317-323).  Each step
+uses the next of R distinct batches (>= 1 GiB in total) so the 256 MiB Infinity
+Cache cannot serve a batch from the previous touch.
+
+Multi-GPU: one process per GPU (torchrun); every rank masks its own shard of
+frames -- no data-path collective (frames are independent); the
+only collectives are the timing barrier and the max-over-ranks of the elapsed time.
+
+Prints ONE JSON line on rank 0.  Roofline: 2 x payload bytes per launch (read +
+write) / mean kernel duration (HIP events on the launch stream) vs 8.0 TB/s.
+cpu_baseline: the oracle's restatement of the reference loop on this host, rank 0,
+N = 1 only, bounded sample (see --cpu-seconds).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s device-resident WS payload XOR-mask at 1/2/4/8 GPUs; % HBM roofline"
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+GIB = float(1 << 30)
+
+WORKLOADS = {
+    "c2": "65,536 x 1 KiB frames (64 MiB) per GPU, independent random key per frame, in place",
+    "c3": "1,024 x 1 MiB frames (1 GiB) per GPU, one random key per frame, in place",
+    "c4": "1 GiB per GPU of mixed 256 B - 64 KiB frames packed back to back (unaligned), in place",
+}
+
+
+def parse_args():
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    p.add_argument("--rotation-bytes", type=int, default=2 << 30, help="distinct device bytes the steps rotate over")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 disables)")
+    p.add_argument("--unroll", type=int, default=None)
+    p.add_argument("--max-blocks", type=int, default=None)
+    p.add_argument("--no-copy-ceiling", action="store_true")
+    return p.parse_args()
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+def make_batches(torch, workload: str, rank: int, rotation_bytes: int, device):
+    """R device batches of the workload shape (own seeds per rank / batch)."""
+    from netc_amd import synth
+
+    off, keys, total = synth.config(workload, shard=rank)
+    nb = max(2, -(-rotation_bytes // total))
+    batches = []
+    gen = torch.Generator(device=device).manual_seed(1000 + rank)
+    off_t = torch.from_numpy(off.view(np.int64)).to(device)
+    for b in range(nb):
+        payload = torch.randint(0, 256, (total,), dtype=torch.uint8, device=device, generator=gen)
+        k = synth.random_keys(keys.size, stream=300 + 1000 * rank + b)
+        batches.append((payload, off_t, torch.from_numpy(k.view(np.int32)).to(device)))
+    return batches, total, keys.size
+
+
+def copy_ceiling(torch, device, nbytes=64 << 20, reps=64):
+    """Practical roofline: device-to-device copy of rotating 64 MiB buffers (read + write bytes / time)."""
+    nb = 16
+    bufs = [torch.empty(nbytes, dtype=torch.uint8, device=device) for _ in range(nb + 1)]
+    for i in range(8):
+        bufs[(i + 1) % (nb + 1)].copy_(bufs[i % (nb + 1)])
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for i in range(reps):
+        bufs[(i + 1) % (nb + 1)].copy_(bufs[i % (nb + 1)])
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / reps
+    del bufs
+    return 2 * nbytes / (ms * 1e-3) / 1e9
+
+
+def cpu_baseline(workload: str, budget_s: float):
+    """Oracle restatement of the reference loop timed on this host (rank 0, N = 1).
+
+    Primary: liboracle.so (-O2), one thread, the exact per-byte expression of
+    src/ws/common.c:321 over the workload's frames.  Variants: the reference's own
+    flags (-O0, Makefile:3), all host cores (frames split by bytes over threads; ctypes
+    releases the GIL), and -- when oracle/_ref was built -- the reference's compiled
+    ws_parse_frame receiving the same frames over a socketpair.
+    """
+    from concurrent.futures import ThreadPoolExecutor
+
+    from netc_amd import synth
+    from oracle import oracle as orc
+
+    off, keys, total = synth.config(workload)
+    # bounded sample: the first frames of the workload, at most 256 MiB
+    sample_bytes = min(total, 256 << 20)
+    nf = int(np.searchsorted(off, sample_bytes, side="right")) - 1
+    nf = max(1, nf)
+    s_off = off[: nf + 1].copy()
+    s_keys = keys[:nf].copy()
+    s_total = int(s_off[-1])
+    buf = synth.host_payload(s_total, stream=77)
+
+    def timed(fn, share):
+        reps, t = 0, 0.0
+        t0 = time.perf_counter()
+        while True:
+            fn()
+            reps += 1
+            t = time.perf_counter() - t0
+            if t >= share:
+                break
+        return reps * s_total / t / GIB, reps
+
+    per = budget_s / 4.0
+    o2 = orc.lib("O2")
+    o0 = orc.lib("O0")
+    bp = buf.ctypes.data
+    po, pk = s_off.ctypes.data, s_keys.ctypes.data
+    v_o2, r_o2 = timed(lambda: o2.oracle_mask_batch(bp, po, pk, nf), per)
+    v_o0, r_o0 = timed(lambda: o0.oracle_mask_batch(bp, po, pk, nf), per)
+
+    ncores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    ncores = max(1, min(ncores, 64))
+    from netc_amd.mask import shard_frames
+
+    cuts = shard_frames(s_off, ncores)
+    parts = []
+    for i in range(ncores):
+        a, b = int(cuts[i]), int(cuts[i + 1])
+        if b > a:
+            parts.append((a, b))
+    pool = ThreadPoolExecutor(max_workers=len(parts))
+
+    def all_cores():
+        list(pool.map(lambda ab: o2.oracle_mask_batch(bp, s_off[ab[0]:].ctypes.data, s_keys[ab[0]:].ctypes.data,
+                                                      ab[1] - ab[0]), parts))
+
+    v_mt, r_mt = timed(all_cores, per)
+    pool.shutdown()
+    variants = {
+        "port_O2_1thread_GiBps": round(v_o2, 4),
+        "port_O0_reference_flags_1thread_GiBps": round(v_o0, 4),
+        f"port_O2_{len(parts)}threads_GiBps": round(v_mt, 4),
+    }
+    if orc.ref_available():
+        wire = build_wire(buf, s_off, s_keys, limit_frames=min(nf, 65536))
+        got, secs = orc.ref_receive_timed(wire)
+        variants["reference_ws_parse_frame_O0_1thread_GiBps"] = round(got / secs / GIB, 4)
+    cpu = os.popen("lscpu 2>/dev/null | grep 'Model name' | head -1").read().split(":")[-1].strip() or platform.processor()
+    return {
+        "value": round(v_o2, 4),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"first {nf} frames ({s_total / (1 << 20):.0f} MiB) of workload {workload}, host-resident, "
+                  f"{r_o2} passes; oracle/ws_oracle.c -O2 (exact expression of src/ws/common.c:321)",
+        "cpu_model": cpu,
+        "host_cores_visible": ncores,
+        "variants": variants,
+    }
+
+
+def build_wire(buf, off, keys, limit_frames):
+    """Masked client frames (header + key + payload) for the first `limit_frames` frames."""
+    from oracle import oracle as orc
+
+    out = []
+    for k in range(limit_frames):
+        a, b = int(off[k]), int(off[k + 1])
+        key = int(keys[k]).to_bytes(4, "little")
+        out.append(orc.encode_frame(buf[a:b].tobytes(), 2, key))
+    return np.frombuffer(b"".join(out), dtype=np.uint8)
+
+
+def main():
+    args = parse_args()
+    world, rank, local = dist_env()
+    import torch
+
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from netc_amd import mask as nm
+
+    if args.unroll or args.max_blocks:
+        nm.tune(args.unroll or 4, args.max_blocks or 2048)
+    nm.gpu_init(local)
+    batches, total, nframes = make_batches(torch, args.workload, rank, args.rotation_bytes, device)
+    stream = torch.cuda.current_stream(device)
+
+    def step(i):
+        p, o, k = batches[i % len(batches)]
+        nm.mask_batch(p, p, o, k, stream=stream)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(device)
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        step(args.warmup + i)
+        ends[i].record(stream)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = np.array([s.elapsed_time(e) for s, e in zip(starts, ends)])
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+        km = torch.tensor([kern_ms.mean()], dtype=torch.float64, device=device)
+        torch.distributed.all_reduce(km, op=torch.distributed.ReduceOp.MAX)
+        kern_mean = float(km.item())
+    else:
+        kern_mean = float(kern_ms.mean())
+
+    ceiling = None
+    if rank == 0 and not args.no_copy_ceiling:
+        ceiling = copy_ceiling(torch, device)
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        del batches
+        torch.cuda.empty_cache()
+        cpu = cpu_baseline(args.workload, args.cpu_seconds)
+
+    if rank == 0:
+        payload_all = float(total) * world * args.steps
+        value = payload_all / elapsed / GIB
+        achieved = 2.0 * total / (kern_mean * 1e-3) / 1e9
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded random payload bytes and keys, device-generated)",
+            "config": {
+                "workload": f"{args.workload}: {WORKLOADS[args.workload]}",
+                "frames_per_gpu": nframes,
+                "batch_bytes_per_gpu": total,
+                "rotation_batches": args.rotation_bytes and max(2, -(-args.rotation_bytes // total)),
+                "parallelism": f"shard{world} (independent frames, no collective)",
+                "entry": "netc_gpu_mask_batch (include/ws/mask.h)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": None,
+                "kernel_ms_mean": round(kern_mean, 5),
+                "kernel_ms_min": round(float(kern_ms.min()), 5),
+                "algorithmic_bytes_per_launch": 2 * total,
+                "copy_ceiling_GBps": round(ceiling, 1) if ceiling else None,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,143 @@
+#ifndef NETC_WS_MASK_H
+#define NETC_WS_MASK_H
+
+/*
+ * RFC 6455 §5.3 payload masking — the drop-in C-ABI for netc's WebSocket
+ * masking path, MI355X (gfx950) edition.
+ *
+ * The reference (Altanis/netc @ 2024-08-07) masks in two scalar per-byte loops:
+ *   - receive / unmask  src/ws/common.c:317-323
+ *       buffer_ptr[i] ^= frame.masking_key[(received_length + i) % 4];
+ *   - send / mask       src/ws/common.c:104-107
+ *       payload_data_encoded[i] ^= payload_masking_key[i % 4];
+ * Both are out[i] = in[i] ^ key[(phase + i) mod 4] with the phase reset at
+ * every frame start.  This header replaces those loops with:
+ *
+ *   netc_ws_mask()                 host CPU entry, one (partial) frame
+ *                                  (libnetc.so; called by ws_parse_frame and
+ *                                  ws_send_message of this repo)
+ *   netc_gpu_mask_batch()          device-resident batch of frames on one GPU
+ *                                  (libnetc_ws_gpu.so, HIP / gfx950)
+ *   netc_gpu_mask_batch_multi()    the same, sharded across several GPUs of
+ *                                  one node, no collective
+ *   netc_gpu_mask_stream_host()    host→device→host pipeline through pinned
+ *                                  staging slots on overlapped HIP streams
+ *   netc_shard_frames()            byte-balanced frame partition (host)
+ *
+ * No HIP / torch types appear here: device buffers are plain pointers and a
+ * stream is an opaque `void *` (a hipStream_t, NULL = the default stream).
+ *
+ * Key packing.  A frame's 4 wire key bytes k0 k1 k2 k3 (the order they appear
+ * on the wire, struct ws_frame.masking_key in include/ws/common.h) travel as
+ * one little-endian word: key32 = k0 | k1 << 8 | k2 << 16 | k3 << 24.
+ *
+ * Frame layout.  Frame k covers payload bytes [offsets[k], offsets[k+1]) of
+ * the batch; offsets has nframes + 1 entries, is non-decreasing and
+ * offsets[nframes] <= total_bytes.  Bytes of [0, total_bytes) that lie in no
+ * frame are passed through unmasked (copied when dst != src).  Frames may be
+ * of any length, including 0, and start at any byte offset (frames are packed
+ * back to back, unpadded).  Each frame's phase starts at 0 (RFC 6455; the
+ * reference's receive path, src/ws/common.c:301,337).
+ *
+ * Errors.  Every int-returning entry returns 0 on success or a negative
+ * NETC_GPU_E* code; the failing call also sets the thread-local
+ * netc_errno_reason (include/utils/error.h) to NETC_REASON_GPU and records
+ * a message readable with netc_gpu_strerror().  Nothing here aborts, and the
+ * caller owns every buffer.  Entry points are reentrant and thread-safe;
+ * the first GPU call on a thread initialises the HIP runtime (call
+ * netc_gpu_init() up front to keep that off an event loop).
+ */
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* -------------------------------------------------------------- errors -- */
+#define NETC_GPU_OK        0
+#define NETC_GPU_EINVAL   -1   /* bad argument (null buffer, bad sizes, partial overlap) */
+#define NETC_GPU_ENODEV   -2   /* no such device / HIP runtime has no GPU                */
+#define NETC_GPU_ELAUNCH  -3   /* kernel launch failed                                   */
+#define NETC_GPU_ERUNTIME -4   /* a HIP runtime call failed (memcpy, stream, event …)    */
+#define NETC_GPU_ENOMEM   -5   /* device or pinned host allocation failed                */
+
+/** netc_errno_reason value set by a failing GPU entry (extends include/utils/error.h:28-45). */
+#define NETC_REASON_GPU   18
+
+/* ---------------------------------------------------------------- host -- */
+
+/**
+ * dst[i] = src[i] ^ key[(phase + i) & 3] for i < len.  dst == src is allowed
+ * (in place, as the reference's receive path); other overlaps are not.
+ * Replaces src/ws/common.c:319-322 (phase = received_length) and
+ * src/ws/common.c:104-107 (phase = 0).  Host memory only; never touches a GPU.
+ */
+void netc_ws_mask(uint8_t *dst, const uint8_t *src, size_t len, const uint8_t key[4], size_t phase);
+
+/**
+ * Partition frames 0..nframes-1 (host offsets, nframes + 1 entries) into
+ * nshards contiguous ranges balanced by payload bytes, cutting only at frame
+ * boundaries.  Writes nshards + 1 frame indices to cuts (cuts[0] = 0,
+ * cuts[nshards] = nframes).  Returns 0 or NETC_GPU_EINVAL.
+ */
+int netc_shard_frames(const uint64_t *offsets, size_t nframes, size_t nshards, size_t *cuts);
+
+/* ----------------------------------------------------------------- gpu -- */
+
+/** Number of visible GPUs (0 when the runtime has none); never negative. */
+int netc_gpu_device_count(void);
+
+/** Eagerly initialise the HIP runtime on `device`.  Optional. */
+int netc_gpu_init(int device);
+
+/** Message for the last failing netc_gpu_* call on this thread ("" if none). */
+const char *netc_gpu_strerror(void);
+
+/**
+ * Mask (or unmask — the operation is an involution) a device-resident batch of
+ * frames on `device`, asynchronously on `stream`.
+ *   d_dst, d_src      device buffers of total_bytes; d_dst == d_src is in place
+ *   d_frame_offsets   device, nframes + 1 uint64 (see "Frame layout")
+ *   d_keys            device, nframes packed key32 words
+ * Returns once the kernel is queued; synchronise `stream` before reading d_dst.
+ * The batch is processed by one kernel launch whose only device traffic is the
+ * payload read + write plus 12 B per frame of descriptors.
+ */
+int netc_gpu_mask_batch(int device, void *d_dst, const void *d_src, size_t total_bytes,
+                        const uint64_t *d_frame_offsets, const uint32_t *d_keys, size_t nframes,
+                        void *stream);
+
+/**
+ * One shard per device, already resident: shard i lives on devices[i] and is
+ * described exactly as for netc_gpu_mask_batch (offsets rebased to the shard's
+ * own payload start).  All shards are launched before any is waited for; with
+ * `synchronize` != 0 the call returns after every shard has completed.
+ * streams may be NULL (each device's default stream).  No collective is used:
+ * frames are independent.
+ */
+int netc_gpu_mask_batch_multi(int nshards, const int *devices, void *const *d_dst, const void *const *d_src,
+                              const size_t *total_bytes, const uint64_t *const *d_frame_offsets,
+                              const uint32_t *const *d_keys, const size_t *nframes, void *const *streams,
+                              int synchronize);
+
+/**
+ * Host-resident batch: h_src → device → mask → h_dst, through `nslots`
+ * device/pinned staging slots of `slot_bytes` payload bytes each, cut at frame
+ * boundaries, with H2D copy, kernel and D2H copy of consecutive slots
+ * overlapped on separate HIP streams.  h_offsets / h_keys are host arrays laid
+ * out as for netc_gpu_mask_batch.  h_dst == h_src is allowed.  A frame longer
+ * than slot_bytes is split across slots (its phase is carried).  Synchronous:
+ * returns when h_dst is complete.  Pinned (hipHostMalloc / hipHostRegister)
+ * h_src / h_dst run at the PCIe rate; pageable memory works but is slower.
+ */
+int netc_gpu_mask_stream_host(int device, void *h_dst, const void *h_src, size_t total_bytes,
+                              const uint64_t *h_frame_offsets, const uint32_t *h_keys, size_t nframes,
+                              size_t slot_bytes, int nslots);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NETC_WS_MASK_H */

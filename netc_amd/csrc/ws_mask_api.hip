@@ -1,0 +1,282 @@
+// C-ABI for the gfx950 masking kernels: include/ws/mask.h (GPU half).
+// Built into libnetc_ws_gpu.so, which links libnetc.so for netc_errno_reason.
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "ws_mask_gpu.h"
+
+extern "C" {
+#include "../../include/ws/mask.h"
+// netc's thread-local error side channel (include/utils/error.h:19-23, src/utils/error.c:5)
+extern __thread int netc_errno_reason;
+}
+
+namespace {
+
+thread_local char g_err[512];
+netc_gpu::LaunchCfg g_cfg;   // process-wide tuning (netc_gpu_tune); read-mostly
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    netc_errno_reason = NETC_REASON_GPU;
+    return code;
+}
+
+int fail_hip(int code, const char* what, hipError_t e) {
+    return fail(code, "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+}
+
+// Selects `device` for the calling thread for the lifetime of the guard.
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int device) {
+        err = hipGetDevice(&prev);
+        if (err != hipSuccess) return;
+        if (prev != device) err = hipSetDevice(device);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) {
+            int cur = -1;
+            if (hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+        }
+    }
+};
+
+int check_device(int device) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) return fail(NETC_GPU_ENODEV, "no HIP device available");
+    if (device < 0 || device >= n) return fail(NETC_GPU_ENODEV, "device %d out of range [0, %d)", device, n);
+    return 0;
+}
+
+bool partial_overlap(const void* a, const void* b, size_t n) {
+    const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+    if (x == y) return false;
+    return x < y + n && y < x + n;
+}
+
+int mask_batch_on_current(void* d_dst, const void* d_src, size_t total, const uint64_t* d_off,
+                          const uint32_t* d_keys, size_t nframes, hipStream_t stream) {
+    if (total == 0) return 0;
+    if (!d_dst || !d_src) return fail(NETC_GPU_EINVAL, "null payload buffer");
+    if (!d_off) return fail(NETC_GPU_EINVAL, "null frame offsets");
+    if (nframes && !d_keys) return fail(NETC_GPU_EINVAL, "null keys with %zu frames", nframes);
+    if (partial_overlap(d_dst, d_src, total)) return fail(NETC_GPU_EINVAL, "dst and src partially overlap");
+    hipError_t e = netc_gpu::launch_mask_frames((uint8_t*)d_dst, (const uint8_t*)d_src, total, d_off, d_keys,
+                                                nframes, stream, g_cfg);
+    if (e != hipSuccess) return fail_hip(NETC_GPU_ELAUNCH, "mask kernel launch", e);
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int netc_gpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n < 0 ? 0 : n;
+}
+
+int netc_gpu_init(int device) {
+    if (int r = check_device(device)) return r;
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+    hipError_t e = hipFree(nullptr);   // forces context creation
+    if (e != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "context init", e);
+    return 0;
+}
+
+const char* netc_gpu_strerror(void) { return g_err; }
+
+int netc_gpu_tune(int unroll, int max_blocks) {
+    if (!(unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8))
+        return fail(NETC_GPU_EINVAL, "unroll must be 1, 2, 4 or 8 (got %d)", unroll);
+    if (max_blocks < 1 || max_blocks > (1 << 24)) return fail(NETC_GPU_EINVAL, "max_blocks out of range");
+    g_cfg.unroll = unroll;
+    g_cfg.max_blocks = max_blocks;
+    return 0;
+}
+
+int netc_gpu_mask_batch(int device, void* d_dst, const void* d_src, size_t total_bytes,
+                        const uint64_t* d_frame_offsets, const uint32_t* d_keys, size_t nframes, void* stream) {
+    if (int r = check_device(device)) return r;
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+    return mask_batch_on_current(d_dst, d_src, total_bytes, d_frame_offsets, d_keys, nframes,
+                                 (hipStream_t)stream);
+}
+
+int netc_gpu_mask_batch_multi(int nshards, const int* devices, void* const* d_dst, const void* const* d_src,
+                              const size_t* total_bytes, const uint64_t* const* d_frame_offsets,
+                              const uint32_t* const* d_keys, const size_t* nframes, void* const* streams,
+                              int synchronize) {
+    if (nshards < 0) return fail(NETC_GPU_EINVAL, "negative shard count");
+    if (nshards == 0) return 0;
+    if (!devices || !d_dst || !d_src || !total_bytes || !d_frame_offsets || !d_keys || !nframes)
+        return fail(NETC_GPU_EINVAL, "null shard array");
+    for (int i = 0; i < nshards; ++i)
+        if (int r = check_device(devices[i])) return r;
+    // launch every shard before waiting on any: the shards run concurrently
+    for (int i = 0; i < nshards; ++i) {
+        DeviceGuard g(devices[i]);
+        if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+        hipStream_t s = streams ? (hipStream_t)streams[i] : nullptr;
+        if (int r = mask_batch_on_current(d_dst[i], d_src[i], total_bytes[i], d_frame_offsets[i], d_keys[i],
+                                          nframes[i], s))
+            return r;
+    }
+    if (synchronize) {
+        for (int i = 0; i < nshards; ++i) {
+            DeviceGuard g(devices[i]);
+            if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+            hipStream_t s = streams ? (hipStream_t)streams[i] : nullptr;
+            hipError_t e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipStreamSynchronize", e);
+        }
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Host → device → host pipeline (BASELINE config 5).  Slots are fixed byte
+// ranges of the payload; a frame cut by a slot edge continues in the next slot
+// with its key pre-rotated by the bytes already consumed (the phase carry of
+// the reference's received_length, src/ws/common.c:301,321).
+// ---------------------------------------------------------------------------
+
+namespace {
+
+struct Slot {
+    uint8_t* d_buf = nullptr;
+    uint64_t* d_off = nullptr;
+    uint32_t* d_key = nullptr;
+    uint64_t* h_off = nullptr;   // pinned descriptor staging
+    uint32_t* h_key = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t desc_free = nullptr;   // descriptor staging may be rewritten
+};
+
+size_t upper_frame(const uint64_t* off, size_t n, uint64_t pos) {
+    // number of frame starts <= pos among off[0..n-1]
+    return (size_t)(std::upper_bound(off, off + n, pos) - off);
+}
+
+}  // namespace
+
+int netc_gpu_mask_stream_host(int device, void* h_dst, const void* h_src, size_t total, const uint64_t* h_off,
+                              const uint32_t* h_keys, size_t nframes, size_t slot_bytes, int nslots) {
+    if (int r = check_device(device)) return r;
+    if (total == 0) return 0;
+    if (!h_dst || !h_src || !h_off || (nframes && !h_keys)) return fail(NETC_GPU_EINVAL, "null host buffer");
+    if (partial_overlap(h_dst, h_src, total)) return fail(NETC_GPU_EINVAL, "dst and src partially overlap");
+    if (slot_bytes < 4096 || nslots < 2 || nslots > 16)
+        return fail(NETC_GPU_EINVAL, "need slot_bytes >= 4096 and 2 <= nslots <= 16");
+    if (h_off[nframes] > total) return fail(NETC_GPU_EINVAL, "offsets[nframes] > total_bytes");
+    slot_bytes &= ~(size_t)15;
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+
+    const size_t nchunks = (total + slot_bytes - 1) / slot_bytes;
+    // descriptor capacity: frames overlapping any one slot
+    size_t cap = 1;
+    for (size_t c = 0; c < nchunks; ++c) {
+        const uint64_t lo = c * slot_bytes, hi = std::min<uint64_t>(total, lo + slot_bytes);
+        const size_t k0 = upper_frame(h_off, nframes, lo), k1 = upper_frame(h_off, nframes, hi - 1);
+        const size_t first = k0 ? k0 - 1 : 0;
+        cap = std::max(cap, k1 - first + 1);
+    }
+
+    std::vector<Slot> slots((size_t)nslots);
+    int rc = 0;
+    hipError_t e = hipSuccess;
+    auto cleanup = [&]() {
+        for (Slot& s : slots) {
+            if (s.stream) (void)hipStreamSynchronize(s.stream);
+            if (s.d_buf) (void)hipFree(s.d_buf);
+            if (s.d_off) (void)hipFree(s.d_off);
+            if (s.d_key) (void)hipFree(s.d_key);
+            if (s.h_off) (void)hipHostFree(s.h_off);
+            if (s.h_key) (void)hipHostFree(s.h_key);
+            if (s.desc_free) (void)hipEventDestroy(s.desc_free);
+            if (s.stream) (void)hipStreamDestroy(s.stream);
+        }
+    };
+    for (Slot& s : slots) {
+        if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&s.desc_free, hipEventDisableTiming)) != hipSuccess) {
+            rc = fail_hip(NETC_GPU_ERUNTIME, "stream/event create", e);
+            break;
+        }
+        if ((e = hipMalloc(&s.d_buf, slot_bytes)) != hipSuccess ||
+            (e = hipMalloc(&s.d_off, (cap + 1) * sizeof(uint64_t))) != hipSuccess ||
+            (e = hipMalloc(&s.d_key, cap * sizeof(uint32_t))) != hipSuccess ||
+            (e = hipHostMalloc(&s.h_off, (cap + 1) * sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess ||
+            (e = hipHostMalloc(&s.h_key, cap * sizeof(uint32_t), hipHostMallocDefault)) != hipSuccess) {
+            rc = fail_hip(NETC_GPU_ENOMEM, "slot allocation", e);
+            break;
+        }
+    }
+    for (size_t c = 0; rc == 0 && c < nchunks; ++c) {
+        Slot& s = slots[c % (size_t)nslots];
+        const uint64_t lo = c * slot_bytes, hi = std::min<uint64_t>(total, lo + slot_bytes);
+        const size_t len = (size_t)(hi - lo);
+        // the previous chunk of this slot must have consumed its descriptors
+        if ((e = hipEventSynchronize(s.desc_free)) != hipSuccess) {
+            rc = fail_hip(NETC_GPU_ERUNTIME, "hipEventSynchronize", e);
+            break;
+        }
+        // clip frames to [lo, hi), rebase to the slot, rotate a cut frame's key
+        size_t m = 0;
+        const size_t k0 = upper_frame(h_off, nframes, lo);
+        size_t k = k0 ? k0 - 1 : 0;
+        for (; k < nframes && h_off[k] < hi; ++k) {
+            const uint64_t fs = h_off[k], fe = h_off[k + 1];
+            if (fe <= lo) continue;
+            const uint64_t cs = std::max<uint64_t>(fs, lo);
+            const uint32_t key = h_keys[k];
+            const uint32_t r = (uint32_t)((cs - fs) & 3u) * 8u;
+            s.h_off[m] = cs - lo;
+            s.h_key[m] = r ? (key >> r) | (key << (32u - r)) : key;
+            ++m;
+            s.h_off[m] = std::min<uint64_t>(fe, hi) - lo;
+        }
+        if (m == 0) s.h_off[0] = 0;
+        const uint8_t* src = (const uint8_t*)h_src + lo;
+        uint8_t* dst = (uint8_t*)h_dst + lo;
+        if ((e = hipMemcpyAsync(s.d_buf, src, len, hipMemcpyHostToDevice, s.stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(s.d_off, s.h_off, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream)) !=
+                hipSuccess ||
+            (m && (e = hipMemcpyAsync(s.d_key, s.h_key, m * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream)) !=
+                      hipSuccess) ||
+            (e = hipEventRecord(s.desc_free, s.stream)) != hipSuccess) {
+            rc = fail_hip(NETC_GPU_ERUNTIME, "H2D copy", e);
+            break;
+        }
+        if ((rc = mask_batch_on_current(s.d_buf, s.d_buf, len, s.d_off, s.d_key, m, s.stream)) != 0) break;
+        if ((e = hipMemcpyAsync(dst, s.d_buf, len, hipMemcpyDeviceToHost, s.stream)) != hipSuccess) {
+            rc = fail_hip(NETC_GPU_ERUNTIME, "D2H copy", e);
+            break;
+        }
+    }
+    for (Slot& s : slots) {
+        if (rc == 0 && s.stream && (e = hipStreamSynchronize(s.stream)) != hipSuccess)
+            rc = fail_hip(NETC_GPU_ERUNTIME, "hipStreamSynchronize", e);
+    }
+    cleanup();
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,31 @@
+// Internal interface between the gfx950 kernels (ws_mask_gpu.hip) and the
+// C-ABI layer (ws_mask_api.hip).  Not installed; the public surface is
+// include/ws/mask.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace netc_gpu {
+
+// Kernel arguments (passed by value in the kernarg segment).
+struct Args {
+    uint8_t* dst_base;         // dst rounded down to 16 B
+    const uint8_t* src_base;   // src - (dst & 15): same P coordinates as dst_base
+    uint64_t total;            // payload bytes in the batch
+    const uint64_t* off;       // n + 1 frame offsets (payload coordinates)
+    const uint32_t* keys;      // n packed keys
+    uint64_t n;                // frames
+    uint64_t mis;              // dst & 15
+    uint64_t nwin;             // windows of U KiB covering [0, mis + total)
+};
+
+struct LaunchCfg {
+    int unroll = 4;            // U: 1 KiB spans per window (1, 2, 4, 8)
+    int max_blocks = 2048;     // cap on 256-thread workgroups (each wave then loops)
+};
+
+hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,
+                              const uint32_t* keys, uint64_t n, hipStream_t stream, const LaunchCfg& cfg);
+
+}  // namespace netc_gpu

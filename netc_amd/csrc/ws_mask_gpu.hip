@@ -1,0 +1,270 @@
+// MI355X (gfx950 / CDNA4) WebSocket payload masking — device kernels.
+//
+// Replaces the reference's scalar per-byte loops
+//   src/ws/common.c:317-323  buffer_ptr[i] ^= masking_key[(received_length + i) % 4]   (unmask)
+//   src/ws/common.c:104-107  payload[i]    ^= payload_masking_key[i % 4]              (mask)
+// for a batch of independent frames resident in HBM.  Pure stream: 16 B read +
+// 16 B written per 16 B of payload, no arithmetic worth a matrix core.
+//
+// Data layout (see DESIGN.md "Kernel"):
+//   * the payload is walked in 16-byte vectors aligned to the *destination*
+//     address; "P" below is a byte position measured from dst rounded down to
+//     16, so vector v covers P in [16v, 16v+16).  mis = dst & 15.
+//   * frames are [off[k], off[k+1]) in payload coordinates, i.e.
+//     [off[k]+mis, off[k+1]+mis) in P coordinates.  Two virtual frames with a
+//     zero key close the range: -1 = [0, off[0]+mis) and n = [off[n]+mis, inf).
+//   * every wavefront owns a contiguous run of windows (U spans of 64 vectors =
+//     U KiB) and keeps a 64-entry "frame table" in registers: lane j holds the
+//     start and key of virtual frame kb + j.  A span's frame is found with one
+//     ballot; the (rare) frame boundaries inside a span are applied with a
+//     wave-uniform loop; the table slides forward with one coalesced 768-byte
+//     reload whenever the window runs past it.
+//   * the key stays in registers and is rotated per vector with v_alignbit
+//     (rotr by 8*((P - frame_start) & 3)); it is the same for the 4 dwords of a
+//     16-B vector, and the same for every lane of a span.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ws_mask_gpu.h"
+
+namespace netc_gpu {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+static constexpr int kWave = 64;
+static constexpr uint64_t kSpan = 64ull * 16ull;          // bytes one wave-instruction moves
+static constexpr uint64_t kInf = ~0ull;
+
+__device__ __forceinline__ uint32_t rotr8(uint32_t key, uint64_t r) {
+    // rotate right by 8 * (r & 3) bits: v_alignbit_b32 key, key, sh
+    return __builtin_amdgcn_alignbit(key, key, (uint32_t)((r & 3u) << 3));
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int lane) {
+    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)x, lane);
+    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t readlane32(uint32_t x, int lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, lane);
+}
+
+// Bytes [t, 16) of a vector selected, as 4 dword masks; t is clamped to [0, 16].
+__device__ __forceinline__ u32x4 select_from(int64_t t) {
+    t = t < 0 ? 0 : (t > 16 ? 16 : t);
+    u32x4 s;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        int64_t b = t - 4 * w;
+        b = b < 0 ? 0 : (b > 4 ? 4 : b);
+        s[w] = (uint32_t)(0xFFFFFFFFull << (8 * b));
+    }
+    return s;
+}
+
+struct Table {
+    int64_t kb;       // virtual frame index held by lane 0
+    uint64_t start;   // this lane's entry: start of frame kb + lane (P coords)
+    uint32_t key;     // this lane's entry: packed key of frame kb + lane
+    uint64_t last;    // start of frame kb + 63 (uniform)
+    bool tail;        // frame n (the open-ended pass-through frame) is in the table
+};
+
+// start / key of virtual frame v in P coordinates
+__device__ __forceinline__ void frame_entry(const Args& a, int64_t v, uint64_t& s, uint32_t& k) {
+    if (v < 0) {
+        s = 0;
+        k = 0;
+    } else if ((uint64_t)v <= a.n) {
+        s = a.off[v] + a.mis;
+        k = (uint64_t)v < a.n ? a.keys[v] : 0u;
+    } else {
+        s = kInf;
+        k = 0;
+    }
+}
+
+__device__ __forceinline__ void table_load(const Args& a, Table& t, int64_t kb, int lane) {
+    t.kb = kb;
+    frame_entry(a, kb + lane, t.start, t.key);
+    t.last = readlane64(t.start, kWave - 1);
+    t.tail = kb + (kWave - 1) >= (int64_t)a.n;
+}
+
+// Largest virtual frame v in [-1, n] whose start is <= P (wave-uniform result).
+// 64-ary search: every step is one coalesced load of 64 probes and one ballot.
+__device__ int64_t locate(const Args& a, uint64_t P, int lane) {
+    if (P < a.mis) return -1;
+    const uint64_t q = P - a.mis;
+    uint64_t lo = 0, cnt = a.n + 1;   // candidate frame indices [lo, lo + cnt)
+    while (cnt > (uint64_t)kWave) {
+        const uint64_t step = (cnt + kWave - 1) / kWave;
+        uint64_t idx = lo + (uint64_t)lane * step;
+        const bool valid = idx < lo + cnt;
+        const uint64_t val = valid ? a.off[idx] : kInf;
+        const uint64_t m = __ballot(valid && val <= q);
+        if (m == 0) return (int64_t)lo - 1;
+        const uint64_t j = 63 - __builtin_clzll(m);
+        lo += j * step;
+        const uint64_t rem = a.n + 1 - lo;
+        cnt = step < rem ? step : rem;
+    }
+    const bool valid = (uint64_t)lane < cnt;
+    const uint64_t val = valid ? a.off[lo + lane] : kInf;
+    const uint64_t m = __ballot(valid && val <= q);
+    if (m == 0) return (int64_t)lo - 1;
+    return (int64_t)(lo + (63 - __builtin_clzll(m)));
+}
+
+// Mask for this lane's vector in the span starting at A0 (P coords, 16-aligned,
+// lane's vector = A0 + 16 * lane).  Slides the table forward when needed.
+__device__ __forceinline__ u32x4 span_mask(const Args& a, Table& t, uint64_t A0, int lane) {
+    const uint64_t Aend = A0 + kSpan;
+    // invariant: entry 0 starts at or before A0.  Make the table cover the span.
+    if (!t.tail && t.last < Aend) {
+        const uint64_t m = __ballot(t.start <= A0);
+        const int j0 = __popcll(m) - 1;
+        if (j0 > 0) table_load(a, t, t.kb + j0, lane);
+    }
+    const uint64_t m0 = __ballot(t.start <= A0);
+    const int j0 = __popcll(m0) - 1;
+    const uint64_t s0 = readlane64(t.start, j0);
+    const uint32_t rk0 = rotr8(readlane32(t.key, j0), A0 - s0);
+    u32x4 mask = {rk0, rk0, rk0, rk0};
+    // frame boundaries strictly inside (A0, Aend)
+    uint64_t b = __ballot(t.start > A0 && t.start < Aend);
+    if (b == 0 && (t.tail || t.last >= Aend)) return mask;   // common case: one frame
+
+    const uint64_t a_lane = A0 + 16ull * (uint64_t)lane;
+    for (;;) {
+        while (b) {
+            const int j = __builtin_ctzll(b);
+            b &= b - 1;
+            const uint64_t sj = readlane64(t.start, j);
+            const uint32_t rkj = rotr8(readlane32(t.key, j), A0 - sj);
+            const u32x4 sel = select_from((int64_t)(sj - a_lane));
+            const u32x4 kv = {rkj, rkj, rkj, rkj};
+            mask = (mask & ~sel) | (kv & sel);
+        }
+        if (t.tail || t.last >= Aend) break;
+        // more than 63 boundaries in one span: advance the table past the last
+        // applied entry (re-applying entry 0 again is idempotent) and continue
+        table_load(a, t, t.kb + (kWave - 1), lane);
+        b = __ballot(t.start > A0 && t.start < Aend);
+    }
+    return mask;
+}
+
+template <bool SRC_ALIGNED>
+__device__ __forceinline__ u32x4 load_vec(const Args& a, uint64_t P) {
+    if constexpr (SRC_ALIGNED) {
+        return *reinterpret_cast<const u32x4*>(a.src_base + P);
+    } else {
+        const uint8_t* p = a.src_base + P;
+        u32x4 v;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            v[w] = (uint32_t)p[4 * w] | ((uint32_t)p[4 * w + 1] << 8) | ((uint32_t)p[4 * w + 2] << 16) |
+                   ((uint32_t)p[4 * w + 3] << 24);
+        return v;
+    }
+}
+
+// Partial vector at either end of the buffer: byte-granular, only bytes in
+// P in [mis, mis + total) are read or written.
+__device__ __forceinline__ void edge_vec(const Args& a, uint64_t P, u32x4 mask) {
+    const uint64_t lo = a.mis, hi = a.mis + a.total;
+#pragma unroll
+    for (int bi = 0; bi < 16; ++bi) {
+        const uint64_t p = P + bi;
+        if (p >= lo && p < hi) {
+            const uint8_t mb = (uint8_t)(mask[bi >> 2] >> (8 * (bi & 3)));
+            a.dst_base[p] = a.src_base[p] ^ mb;
+        }
+    }
+}
+
+template <int U, bool SRC_ALIGNED>
+__global__ __launch_bounds__(256) void mask_frames_kernel(Args a) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / kWave);
+    const uint64_t w_begin = wave * a.nwin / nwaves;
+    const uint64_t w_end = (wave + 1) * a.nwin / nwaves;
+    if (w_begin >= w_end) return;
+
+    constexpr uint64_t kWin = kSpan * U;
+    const uint64_t full_lo = a.mis ? 16 : 0;                       // first full vector's P
+    const uint64_t full_hi = (a.mis + a.total) & ~15ull;           // end of the last full vector
+    const uint64_t vec_end = (a.mis + a.total + 15) & ~15ull;      // end of the last vector
+
+    uint64_t W0 = w_begin * kWin;
+    Table t;
+    table_load(a, t, locate(a, W0, lane), lane);
+
+    for (uint64_t w = w_begin; w < w_end; ++w, W0 += kWin) {
+        u32x4 d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t P = W0 + (uint64_t)u * kSpan + 16ull * lane;
+            if (P >= full_lo && P < full_hi) d[u] = load_vec<SRC_ALIGNED>(a, P);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t A0 = W0 + (uint64_t)u * kSpan;
+            if (A0 >= vec_end) break;                               // wave-uniform
+            const u32x4 m = span_mask(a, t, A0, lane);
+            const uint64_t P = A0 + 16ull * lane;
+            if (P >= full_lo && P < full_hi) {
+                *reinterpret_cast<u32x4*>(a.dst_base + P) = d[u] ^ m;
+            } else if (P < vec_end) {
+                edge_vec(a, P, m);
+            }
+        }
+    }
+}
+
+}  // namespace netc_gpu
+
+// ------------------------------------------------------------------ launch --
+
+namespace netc_gpu {
+
+template <int U, bool AL>
+static hipError_t launch_u(const Args& a, int blocks, hipStream_t s) {
+    hipLaunchKernelGGL((mask_frames_kernel<U, AL>), dim3(blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,
+                              const uint32_t* keys, uint64_t n, hipStream_t stream, const LaunchCfg& cfg) {
+    Args a;
+    a.mis = (uint64_t)(uintptr_t)dst & 15u;
+    a.dst_base = dst - a.mis;
+    a.src_base = src - a.mis;
+    a.total = total;
+    a.off = off;
+    a.keys = keys;
+    a.n = n;
+    const bool aligned = (((uintptr_t)src ^ (uintptr_t)dst) & 15u) == 0;
+    const int U = cfg.unroll;
+    const uint64_t nvec = (a.mis + total + 15) / 16;
+    const uint64_t win_vec = 64ull * (uint64_t)U;
+    a.nwin = (nvec + win_vec - 1) / win_vec;
+    const uint64_t max_waves = (uint64_t)cfg.max_blocks * 4;
+    const uint64_t waves = a.nwin < max_waves ? a.nwin : max_waves;
+    const int blocks = (int)((waves + 3) / 4);
+    if (blocks <= 0) return hipSuccess;
+    if (aligned) {
+        switch (U) {
+            case 1: return launch_u<1, true>(a, blocks, stream);
+            case 2: return launch_u<2, true>(a, blocks, stream);
+            case 8: return launch_u<8, true>(a, blocks, stream);
+            default: return launch_u<4, true>(a, blocks, stream);
+        }
+    }
+    return launch_u<4, false>(a, blocks, stream);
+}
+
+}  // namespace netc_gpu

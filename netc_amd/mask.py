@@ -1,0 +1,171 @@
+"""Python mirror of the masking C-ABI (include/ws/mask.h).
+
+Same names, argument meaning and error behaviour as the C entry points; device
+buffers are torch tensors (uint8 payload, int64 offsets, int32 packed keys) and
+host buffers numpy arrays.  Every call goes straight to the in-tree shared
+libraries; a failing call raises :class:`NetcGpuError` carrying the negative
+NETC_GPU_E* code and the library's message.  There is no CPU fallback for the
+GPU entries.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+
+NETC_GPU_OK = 0
+NETC_GPU_EINVAL = -1
+NETC_GPU_ENODEV = -2
+NETC_GPU_ELAUNCH = -3
+NETC_GPU_ERUNTIME = -4
+NETC_GPU_ENOMEM = -5
+NETC_REASON_GPU = 18
+
+
+class NetcGpuError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"netc_gpu error {code}: {message}")
+        self.code = code
+        self.message = message
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        msg = _lib.gpu().netc_gpu_strerror()
+        raise NetcGpuError(rc, msg.decode(errors="replace") if msg else "")
+
+
+def _ptr(a) -> int:
+    """Address of a torch tensor / numpy array / bytearray."""
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    if isinstance(a, bytearray):
+        return ctypes.addressof((ctypes.c_char * len(a)).from_buffer(a))
+    raise TypeError(f"unsupported buffer type {type(a)!r}")
+
+
+# ------------------------------------------------------------------ host ---
+
+def pack_keys(keys) -> np.ndarray:
+    """(n, 4) wire key bytes -> n packed key32 = k0 | k1<<8 | k2<<16 | k3<<24 (uint32)."""
+    k = np.ascontiguousarray(np.asarray(keys, dtype=np.uint8).reshape(-1, 4))
+    return k.view("<u4").reshape(-1).astype(np.uint32)
+
+
+def mask_host(src, key: bytes, phase: int = 0, out: Optional[np.ndarray] = None) -> np.ndarray:
+    """netc_ws_mask: out[i] = src[i] ^ key[(phase + i) & 3] (host CPU entry)."""
+    s = np.ascontiguousarray(np.frombuffer(bytes(src), dtype=np.uint8) if isinstance(src, (bytes, bytearray)) else src)
+    if s.dtype != np.uint8:
+        raise TypeError("src must be uint8")
+    if out is None:
+        out = np.empty_like(s)
+    kb = (ctypes.c_uint8 * 4)(*bytes(key)[:4])
+    _lib.host().netc_ws_mask(_ptr(out), _ptr(s), s.size, kb, phase)
+    return out
+
+
+def shard_frames(offsets: np.ndarray, nshards: int) -> np.ndarray:
+    """netc_shard_frames: byte-balanced contiguous frame ranges, nshards + 1 cut indices."""
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    cuts = np.zeros(nshards + 1, dtype=np.uintp)
+    rc = _lib.host().netc_shard_frames(_ptr(off), off.size - 1, nshards, _ptr(cuts))
+    if rc != 0:
+        raise NetcGpuError(rc, "netc_shard_frames: invalid offsets or shard count")
+    return cuts.astype(np.int64)
+
+
+# ------------------------------------------------------------------- gpu ---
+
+def device_count() -> int:
+    return int(_lib.gpu().netc_gpu_device_count())
+
+
+def gpu_init(device: int = 0) -> None:
+    _check(_lib.gpu().netc_gpu_init(device))
+
+
+def tune(unroll: int = 4, max_blocks: int = 2048) -> None:
+    """Process-wide launch shape: U (KiB per wave per loop trip) and the workgroup cap."""
+    _check(_lib.gpu().netc_gpu_tune(unroll, max_blocks))
+
+
+def _stream_handle(stream) -> int:
+    import torch
+
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def _check_batch(dst, src, offsets, keys) -> Tuple[int, int]:
+    import torch
+
+    for name, t in (("dst", dst), ("src", src), ("offsets", offsets), ("keys", keys)):
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"{name} must be a torch tensor")
+        if not t.is_cuda:
+            raise ValueError(f"{name} must be a device tensor")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+    if src.dtype != torch.uint8 or dst.dtype != torch.uint8:
+        raise TypeError("payload tensors must be uint8")
+    if offsets.dtype not in (torch.int64, torch.uint64):
+        raise TypeError("offsets must be int64 (uint64 bit pattern)")
+    if keys.dtype not in (torch.int32, torch.uint32):
+        raise TypeError("keys must be int32 (packed key32 bit pattern)")
+    if dst.numel() != src.numel():
+        raise ValueError("dst and src sizes differ")
+    n = keys.numel()
+    if offsets.numel() != n + 1:
+        raise ValueError(f"offsets must have nframes + 1 = {n + 1} entries, got {offsets.numel()}")
+    return src.numel(), n
+
+
+def mask_batch(dst, src, offsets, keys, stream=None, device: Optional[int] = None) -> None:
+    """netc_gpu_mask_batch on the tensors' device, queued on `stream` (default: torch's current stream)."""
+    total, n = _check_batch(dst, src, offsets, keys)
+    dev = src.device.index if device is None else device
+    _check(_lib.gpu().netc_gpu_mask_batch(dev, dst.data_ptr(), src.data_ptr(), total, offsets.data_ptr(),
+                                          keys.data_ptr(), n, _stream_handle(stream)))
+
+
+def mask_batch_multi(shards: Sequence[Tuple], streams: Optional[Sequence] = None, synchronize: bool = True) -> None:
+    """netc_gpu_mask_batch_multi: shards = [(dst, src, offsets, keys), ...], each on its own device."""
+    k = len(shards)
+    devs = (ctypes.c_int * k)()
+    dsts = (ctypes.c_void_p * k)()
+    srcs = (ctypes.c_void_p * k)()
+    totals = (ctypes.c_size_t * k)()
+    offs = (ctypes.c_void_p * k)()
+    keys = (ctypes.c_void_p * k)()
+    ns = (ctypes.c_size_t * k)()
+    strs = (ctypes.c_void_p * k)()
+    for i, (d, s, o, kk) in enumerate(shards):
+        total, n = _check_batch(d, s, o, kk)
+        devs[i] = s.device.index
+        dsts[i], srcs[i], offs[i], keys[i] = d.data_ptr(), s.data_ptr(), o.data_ptr(), kk.data_ptr()
+        totals[i], ns[i] = total, n
+        strs[i] = streams[i].cuda_stream if streams else None
+    _check(_lib.gpu().netc_gpu_mask_batch_multi(k, devs, dsts, srcs, totals, offs, keys, ns,
+                                                strs if streams else None, 1 if synchronize else 0))
+
+
+def mask_stream_host(dst: np.ndarray, src: np.ndarray, offsets: np.ndarray, keys: np.ndarray,
+                     slot_bytes: int = 256 << 20, nslots: int = 4, device: int = 0) -> None:
+    """netc_gpu_mask_stream_host: host buffers through pinned slots on overlapped streams."""
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    kk = np.ascontiguousarray(keys, dtype=np.uint32)
+    if src.dtype != np.uint8 or dst.dtype != np.uint8 or dst.size != src.size:
+        raise ValueError("dst/src must be uint8 arrays of equal size")
+    if off.size != kk.size + 1:
+        raise ValueError("offsets must have nframes + 1 entries")
+    _check(_lib.gpu().netc_gpu_mask_stream_host(device, _ptr(dst), _ptr(src), src.size, _ptr(off), _ptr(kk),
+                                                kk.size, slot_bytes, nslots))

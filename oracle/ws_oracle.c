@@ -1,0 +1,148 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C restatement of the reference's WebSocket masking path
+ * (Altanis/netc @ 2024-08-07, src/ws/common.c), used as the checker for the
+ * GPU kernels and the host framing library.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it; no product code links it.
+ *
+ * Pinned by: the reference's own round-trip payloads (tests/ws/test001.c:90,
+ * 144, 248, 268), the RFC 6455 §5.7 known answer, and golden vectors produced
+ * by the reference's compiled src/ws/common.c itself (oracle/_ref, recipe in
+ * oracle/Makefile, generator tests/golden/make_golden.py) — see
+ * tests/test_oracle.py.
+ *
+ * Every masking statement is the reference's exact expression, byte by byte,
+ * with `%` (not `&`): the point is fidelity, not speed.
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+/* src/ws/common.c:319-322 — unmask `n` received bytes at frame phase `received_length` */
+void oracle_unmask(uint8_t *buffer_ptr, size_t n, const uint8_t masking_key[4], uint64_t received_length)
+{
+    for (size_t i = 0; i < n; ++i)
+    {
+        buffer_ptr[i] ^= masking_key[(received_length + i) % 4];
+    }
+}
+
+/* src/ws/common.c:104-107 — mask one frame's payload copy (phase always 0) */
+void oracle_mask(uint8_t *payload_data_encoded, uint64_t frame_payload_length, const uint8_t payload_masking_key[4])
+{
+    for (size_t i = 0; i < frame_payload_length; ++i)
+    {
+        payload_data_encoded[i] ^= payload_masking_key[i % 4];
+    }
+}
+
+/*
+ * A batch as the GPU C-ABI describes it (include/ws/mask.h): frame k covers
+ * [off[k], off[k+1]) of buf, key32 packs the wire key bytes little-endian.
+ * Each frame is unmasked from phase 0, as the reference's receive path does
+ * for every frame (received_length reset at src/ws/common.c:337).
+ */
+void oracle_mask_batch(uint8_t *buf, const uint64_t *off, const uint32_t *keys, size_t nframes)
+{
+    for (size_t k = 0; k < nframes; ++k)
+    {
+        const uint8_t key[4] = {(uint8_t)keys[k], (uint8_t)(keys[k] >> 8), (uint8_t)(keys[k] >> 16),
+                                (uint8_t)(keys[k] >> 24)};
+        oracle_unmask(buf + off[k], (size_t)(off[k + 1] - off[k]), key, 0);
+    }
+}
+
+/* src/ws/common.c:19-27 — the per-thread key sequence, with the seed made explicit */
+void oracle_build_masking_key(uint8_t masking_key[4], int *seed)
+{
+    masking_key[0] = (uint8_t)((*seed)++ * 97);
+    masking_key[1] = (uint8_t)((*seed)++ * 97);
+    masking_key[2] = (uint8_t)((*seed)++ * 97);
+    masking_key[3] = (uint8_t)((*seed)++ * 97);
+}
+
+/*
+ * src/ws/common.c:53-125 for ONE frame of a message (the part of
+ * ws_send_message with defined behaviour: a single frame, i.e. num_frames = 1).
+ * Writes the wire bytes to out (capacity >= 14 + len) and returns their count.
+ */
+size_t oracle_encode_frame(uint8_t *out, int fin, uint8_t opcode, const uint8_t *payload, uint64_t len,
+                           const uint8_t *masking_key)
+{
+    size_t h = 0;
+    uint8_t header = 0;
+    header |= (uint8_t)((fin ? 1 : 0) << 7);
+    header |= opcode;                                                         /* :56-60 */
+    const uint8_t payload_encoded = len <= 125 ? (uint8_t)len : (len <= 0xFFFF ? 126 : 127); /* :63 */
+    uint8_t payload_length = 0;
+    payload_length |= (uint8_t)((masking_key != NULL) << 7);
+    payload_length |= payload_encoded;                                        /* :65-67 */
+    out[h++] = header;
+    out[h++] = payload_length;
+    if (payload_encoded == 126)
+    {
+        out[h++] = (uint8_t)((len >> 8) & 0xFF);
+        out[h++] = (uint8_t)(len & 0xFF);                                     /* :71-75 */
+    }
+    else if (payload_encoded == 127)
+    {
+        for (int i = 0; i < 8; ++i) out[h++] = (uint8_t)((len >> (8 * (7 - i))) & 0xFF); /* :76-82 */
+    }
+    if (masking_key != NULL && len != 0)
+    {
+        memcpy(out + h, masking_key, 4);                                      /* :119 */
+        h += 4;
+    }
+    memcpy(out + h, payload, (size_t)len);
+    if (masking_key != NULL) oracle_mask(out + h, len, masking_key);          /* :104-107 */
+    return h + (size_t)len;
+}
+
+/*
+ * src/ws/common.c:146-347 as a pure function over a complete byte stream:
+ * decodes frames until one with FIN completes a message.  On success returns
+ * the wire bytes consumed and writes the message (payload bytes, unmasked, no
+ * NUL appended) to out / *out_len and its opcode to *opcode.  Returns 0 when
+ * the stream ends before a message completes.
+ */
+size_t oracle_decode_message(const uint8_t *wire, size_t wire_len, uint8_t *out, size_t out_cap, size_t *out_len,
+                             uint8_t *opcode)
+{
+    size_t p = 0, n = 0;
+    *opcode = 0;
+    for (;;)
+    {
+        if (p + 2 > wire_len) return 0;
+        const uint8_t b0 = wire[p++], b1 = wire[p++];
+        const int fin = (b0 & 0x80) >> 7;                                     /* :157 */
+        const uint8_t op = b0 & 0x0F;                                         /* :161 */
+        if (op != 0) *opcode = op;                                            /* :163-164 */
+        const int mask = (b1 & 0x80) >> 7;                                    /* :180 */
+        uint64_t len = b1 & 0x7F;                                             /* :181 */
+        if (len == 126 || len == 127)
+        {
+            const size_t nb = len == 126 ? 2 : 8;                             /* :226-227 */
+            if (p + nb > wire_len) return 0;
+            len = 0;
+            for (size_t i = 0; i < nb; ++i) len = (len << 8) | wire[p++];     /* big endian, :245-257 */
+        }
+        uint8_t key[4] = {0, 0, 0, 0};
+        if (mask)
+        {
+            if (p + 4 > wire_len) return 0;
+            memcpy(key, wire + p, 4);                                         /* :278-296 */
+            p += 4;
+        }
+        if (p + len > wire_len || n + len > out_cap) return 0;
+        memcpy(out + n, wire + p, (size_t)len);
+        if (mask) oracle_unmask(out + n, (size_t)len, key, 0);                /* :317-323 */
+        n += (size_t)len;
+        p += (size_t)len;
+        if (fin)
+        {
+            *out_len = n;
+            return p;
+        }
+    }
+}

@@ -1,0 +1,268 @@
+"""GPU parity: netc_gpu_mask_batch (gfx950 kernel, through the C-ABI) vs the oracle.
+
+The oracle (oracle/ws_oracle.c) is the reference's exact per-byte expression
+(src/ws/common.c:321); the bar is bit-exact output for every byte of the
+buffer, plus untouched guard bytes around it.
+"""
+
+import numpy as np
+import pytest
+
+from netc_amd import mask as nm
+from netc_amd import synth
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+GUARD = 64
+SENTINEL = 0xA5
+
+
+def _dev(torch, a: np.ndarray, _unused=None):
+    """uint64 offsets / uint32 keys -> device int64 / int32 tensors with the same bits."""
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint64:
+        a = a.view(np.int64)
+    elif a.dtype == np.uint32:
+        a = a.view(np.int32)
+    return torch.from_numpy(a).cuda()
+
+
+def run_case(torch, payload: np.ndarray, off: np.ndarray, keys: np.ndarray, dst_shift=0, src_shift=0, inplace=False):
+    total = payload.size
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    keys = np.ascontiguousarray(keys, dtype=np.uint32)
+    src_buf = torch.full((total + 2 * GUARD,), SENTINEL, dtype=torch.uint8, device="cuda")
+    src = src_buf[GUARD + src_shift: GUARD + src_shift + total]
+    src.copy_(torch.from_numpy(payload))
+    if inplace:
+        dst_buf, dst, dst_shift = src_buf, src, src_shift
+    else:
+        dst_buf = torch.full((total + 2 * GUARD,), SENTINEL, dtype=torch.uint8, device="cuda")
+        dst = dst_buf[GUARD + dst_shift: GUARD + dst_shift + total]
+    off_t = _dev(torch, off, None)
+    keys_t = _dev(torch, keys, None)
+    nm.mask_batch(dst, src, off_t, keys_t)
+    torch.cuda.synchronize()
+    expected = orc.mask_batch(payload, off, keys)
+    whole = dst_buf.cpu().numpy()
+    got = whole[GUARD + dst_shift: GUARD + dst_shift + total]
+    if not np.array_equal(got, expected):
+        bad = np.nonzero(got != expected)[0]
+        raise AssertionError(f"{bad.size} bytes differ, first at {bad[:8].tolist()} "
+                             f"(total={total}, frames={keys.size}, shifts={dst_shift},{src_shift}, inplace={inplace})")
+    lo, hi = GUARD + dst_shift, GUARD + dst_shift + total
+    assert (whole[:lo] == SENTINEL).all() and (whole[hi:] == SENTINEL).all(), "write outside the destination"
+
+
+def frames_from_sizes(sizes, start=0):
+    off = np.zeros(len(sizes) + 1, dtype=np.uint64)
+    off[0] = start
+    off[1:] = start + np.cumsum(np.asarray(sizes, dtype=np.uint64))
+    return off
+
+
+# ------------------------------------------------------------ known answers --
+
+def test_rfc6455_known_answer(torch_cuda):
+    # RFC 6455 §5.7: "Hello" masked with 37 fa 21 3d -> 7f 9f 4d 51 58
+    key = np.frombuffer(bytes.fromhex("37fa213d"), dtype=np.uint8)
+    masked = np.frombuffer(bytes.fromhex("7f9f4d5158"), dtype=np.uint8).copy()
+    for shift in range(16):
+        torch = torch_cuda
+        buf = torch.zeros(64, dtype=torch.uint8, device="cuda")[shift: shift + 5]
+        buf.copy_(torch.from_numpy(masked))
+        off = torch.tensor([0, 5], dtype=torch.int64, device="cuda")
+        k = torch.from_numpy(nm.pack_keys(key).view(np.int32)).cuda()
+        nm.mask_batch(buf, buf, off, k)
+        assert bytes(buf.cpu().numpy()) == b"Hello"
+
+
+def test_reference_test_payloads(torch_cuda):
+    # the payloads tests/ws/test001.c round-trips, with the keys ws_build_masking_key
+    # yields on a fresh thread (src/ws/common.c:19-27)
+    payloads = [bytes([0, 233, 5, 11, 65, 115, 112, 101, 99, 116, 108, 44, 108, 44, 107]),   # :233-246
+                b"hello client masked",                                                      # :95-108
+                b"hello server multiple frames masked",                                      # :253-266
+                b"hello client multiple frames masked"]                                      # :149-162
+    keys = np.frombuffer(orc.key_sequence(4), dtype=np.uint8).reshape(4, 4)
+    buf = np.frombuffer(b"".join(payloads), dtype=np.uint8).copy()
+    off = frames_from_sizes([len(p) for p in payloads])
+    run_case(torch_cuda, buf, off, nm.pack_keys(keys))
+
+
+# ------------------------------------------------------------- edge cases ---
+
+@pytest.mark.parametrize("dst_shift,src_shift", [(0, 0), (1, 1), (7, 7), (15, 15), (3, 0), (0, 9), (5, 12)])
+def test_ragged_frames_and_alignment(torch_cuda, dst_shift, src_shift):
+    g = synth.rng(11, dst_shift * 16 + src_shift)
+    sizes = list(range(0, 40)) + [63, 64, 65, 255, 256, 257, 1023, 1024, 1025, 4095, 4097, 70000, 3, 0, 0, 1]
+    g.shuffle(sizes)
+    off = frames_from_sizes(sizes)
+    total = int(off[-1])
+    payload = synth.host_payload(total, 11, 3)
+    keys = synth.random_keys(len(sizes), 11, 4)
+    run_case(torch_cuda, payload, off, keys, dst_shift, src_shift)
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_in_place_and_out_of_place(torch_cuda, inplace):
+    off = synth.mixed_offsets(3 << 20, 256, 65536, seed=5)
+    keys = synth.random_keys(off.size - 1, 5)
+    payload = synth.host_payload(int(off[-1]), 5)
+    run_case(torch_cuda, payload, off, keys, 3, 3, inplace=inplace)
+
+
+def test_dense_tiny_frames(torch_cuda):
+    # > 63 frame boundaries inside one 1 KiB span: exercises the table walk
+    g = synth.rng(7)
+    sizes = g.integers(0, 4, size=20000)
+    off = frames_from_sizes(sizes)
+    payload = synth.host_payload(int(off[-1]), 7)
+    run_case(torch_cuda, payload, off, synth.random_keys(sizes.size, 7), 0, 0)
+    run_case(torch_cuda, payload, off, synth.random_keys(sizes.size, 8), 5, 5)
+
+
+def test_unframed_bytes_pass_through(torch_cuda):
+    off = frames_from_sizes([100, 5000, 7, 0, 33333], start=123)
+    total = int(off[-1]) + 77
+    payload = synth.host_payload(total, 9)
+    run_case(torch_cuda, payload, off, synth.random_keys(off.size - 1, 9), 2, 2)
+
+
+def test_no_frames_is_a_copy(torch_cuda):
+    payload = synth.host_payload(100003, 10)
+    run_case(torch_cuda, payload, np.zeros(1, dtype=np.uint64), np.zeros(0, dtype=np.uint32), 1, 1)
+
+
+def test_tiny_buffers(torch_cuda):
+    for total in range(1, 40):
+        for shift in (0, 1, 14, 15):
+            payload = synth.host_payload(total, total, shift)
+            off = frames_from_sizes([total // 3, total - total // 3])
+            run_case(torch_cuda, payload, off, synth.random_keys(2, total, shift), shift, shift)
+
+
+def test_empty_batch_is_noop(torch_cuda):
+    torch = torch_cuda
+    empty = torch.empty(0, dtype=torch.uint8, device="cuda")
+    nm.mask_batch(empty, empty, torch.zeros(1, dtype=torch.int64, device="cuda"),
+                  torch.zeros(0, dtype=torch.int32, device="cuda"))
+    torch.cuda.synchronize()
+
+
+def test_one_huge_frame(torch_cuda):
+    total = (10 << 20) + 13
+    payload = synth.host_payload(total, 12)
+    run_case(torch_cuda, payload, frames_from_sizes([total]), np.array([0xDEADBEEF], dtype=np.uint32), 6, 6)
+
+
+@pytest.mark.parametrize("unroll,max_blocks", [(1, 2048), (2, 64), (8, 2048), (4, 1), (4, 100000)])
+def test_launch_shapes(torch_cuda, unroll, max_blocks):
+    try:
+        nm.tune(unroll, max_blocks)
+        off = synth.mixed_offsets(5 << 20, 1, 9000, seed=13)
+        payload = synth.host_payload(int(off[-1]), 13)
+        run_case(torch_cuda, payload, off, synth.random_keys(off.size - 1, 13), 4, 4)
+    finally:
+        nm.tune(4, 2048)
+
+
+# ------------------------------------------------------------- full sizes ---
+
+def test_c2_full_exact(torch_cuda):
+    off, keys, total = synth.config("c2")
+    payload = synth.host_payload(total, synth.SEED, 2)
+    run_case(torch_cuda, payload, off, keys)
+
+
+@pytest.mark.slow
+def test_c4_shard_full_exact(torch_cuda):
+    torch = torch_cuda
+    off, keys, total = synth.config("c4", shard=3)
+    g = torch.Generator(device="cuda").manual_seed(44)
+    src = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda", generator=g)
+    host = src.cpu().numpy()
+    nm.mask_batch(src, src, _dev(torch, off, None), _dev(torch, keys, None))
+    torch.cuda.synchronize()
+    orc.mask_batch_inplace(host, off, keys)
+    assert np.array_equal(src.cpu().numpy(), host)
+
+
+@pytest.mark.slow
+def test_c3_full_properties(torch_cuda):
+    """1 GiB: involution over the whole buffer, keystream linearity, oracle on sampled frames."""
+    torch = torch_cuda
+    off, keys, total = synth.config("c3")
+    off_t, keys_t = _dev(torch, off, None), _dev(torch, keys, None)
+    g = torch.Generator(device="cuda").manual_seed(33)
+    x = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda", generator=g)
+    y = torch.empty_like(x)
+    nm.mask_batch(y, x, off_t, keys_t)
+    z = torch.zeros_like(x)
+    nm.mask_batch(z, z, off_t, keys_t)              # keystream = mask(0)
+    assert torch.equal(torch.bitwise_xor(x, y), z)  # mask(x) ^ x == mask(0)
+    nm.mask_batch(y, y, off_t, keys_t)              # involution
+    assert torch.equal(y, x)
+    del y
+    picks = synth.rng(33).choice(keys.size, size=16, replace=False)
+    zs = z.cpu().numpy()
+    for k in picks:
+        a, b = int(off[k]), int(off[k + 1])
+        exp = orc.mask_batch(np.zeros(b - a, dtype=np.uint8), np.array([0, b - a], dtype=np.uint64), keys[k:k + 1])
+        assert np.array_equal(zs[a:b], exp)
+
+
+# ------------------------------------------------------- other entry points --
+
+def test_multi_shard_entry(torch_cuda):
+    torch = torch_cuda
+    shards, expect = [], []
+    for i in range(3):
+        off = synth.mixed_offsets((1 << 20) + 7 * i, 1, 5000, seed=20 + i)
+        keys = synth.random_keys(off.size - 1, 20 + i)
+        payload = synth.host_payload(int(off[-1]), 20 + i)
+        src = torch.from_numpy(payload).cuda()
+        shards.append((torch.empty_like(src), src, _dev(torch, off, None), _dev(torch, keys, None)))
+        expect.append(orc.mask_batch(payload, off, keys))
+    nm.mask_batch_multi(shards, synchronize=True)
+    for (dst, _, _, _), e in zip(shards, expect):
+        assert np.array_equal(dst.cpu().numpy(), e)
+
+
+@pytest.mark.parametrize("slot", [4096, 1 << 16, 3 << 20])
+def test_stream_host_pipeline(torch_cuda, slot):
+    off = synth.mixed_offsets(9 << 20, 1, 300000, seed=30)
+    off = np.concatenate([[np.uint64(0)], off + np.uint64(5)]).astype(np.uint64)   # 5 unframed bytes first
+    keys = synth.random_keys(off.size - 1, 30)
+    total = int(off[-1]) + 3
+    payload = synth.host_payload(total, 30)
+    out = np.zeros_like(payload)
+    nm.mask_stream_host(out, payload, off, keys, slot_bytes=slot, nslots=3)
+    assert np.array_equal(out, orc.mask_batch(payload, off, keys))
+    inplace = payload.copy()
+    nm.mask_stream_host(inplace, inplace, off, keys, slot_bytes=slot, nslots=4)
+    assert np.array_equal(inplace, out)
+
+
+def test_errors_are_reported(torch_cuda):
+    torch = torch_cuda
+    from netc_amd import _lib
+
+    lib = _lib.gpu()
+    x = torch.zeros(100, dtype=torch.uint8, device="cuda")
+    off = torch.tensor([0, 100], dtype=torch.int64, device="cuda")
+    k = torch.zeros(1, dtype=torch.int32, device="cuda")
+    assert lib.netc_gpu_mask_batch(0, None, x.data_ptr(), 100, off.data_ptr(), k.data_ptr(), 1, None) == nm.NETC_GPU_EINVAL
+    assert b"null" in lib.netc_gpu_strerror()
+    assert lib.netc_gpu_mask_batch(0, x.data_ptr(), x.data_ptr(), 100, None, k.data_ptr(), 1, None) == nm.NETC_GPU_EINVAL
+    # partial overlap
+    assert lib.netc_gpu_mask_batch(0, x.data_ptr() + 1, x.data_ptr(), 99, off.data_ptr(), k.data_ptr(), 1, None) \
+        == nm.NETC_GPU_EINVAL
+    assert lib.netc_gpu_mask_batch(1 << 20, x.data_ptr(), x.data_ptr(), 100, off.data_ptr(), k.data_ptr(), 1, None) \
+        == nm.NETC_GPU_ENODEV
+    with pytest.raises(nm.NetcGpuError) as ei:
+        nm.tune(3, 10)
+    assert ei.value.code == nm.NETC_GPU_EINVAL
+    assert nm.device_count() >= 1
+    nm.gpu_init(0)
