@@ -19,7 +19,7 @@ GPU_SRCS   := netc_amd/csrc/ws_mask_gpu.hip netc_amd/csrc/ws_mask_api.hip
 GPU_HDRS   := netc_amd/csrc/ws_mask_gpu.h include/ws/mask.h
 
 .PHONY: all host gpu oracle clean
-all: host gpu oracle
+all: host gpu oracle diag
 host: $(LIBDIR)/libnetc.so
 gpu: $(LIBDIR)/libnetc_ws_gpu.so
 
@@ -36,3 +36,8 @@ oracle:
 clean:
 	rm -f $(LIBDIR)/*.so
 	$(MAKE) -C oracle clean
+
+# diagnostics (tools/, not part of the product)
+diag: tools/libdiag_stream.so
+tools/libdiag_stream.so: tools/diag_stream.hip
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<

@@ -55,6 +55,7 @@ def parse_args():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 disables)")
     p.add_argument("--unroll", type=int, default=None)
     p.add_argument("--max-blocks", type=int, default=None)
+    p.add_argument("--nt-flags", type=int, default=None)
     p.add_argument("--no-copy-ceiling", action="store_true")
     return p.parse_args()
 
@@ -211,8 +212,8 @@ def main():
 
     from netc_amd import mask as nm
 
-    if args.unroll or args.max_blocks:
-        nm.tune(args.unroll or 4, args.max_blocks or 2048)
+    if args.unroll or args.max_blocks or args.nt_flags:
+        nm.tune(args.unroll or 4, args.max_blocks or 0, args.nt_flags or 0)
     nm.gpu_init(local)
     batches, total, nframes = make_batches(torch, args.workload, rank, args.rotation_bytes, device)
     stream = torch.cuda.current_stream(device)

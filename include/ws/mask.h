@@ -92,6 +92,18 @@ int netc_gpu_device_count(void);
 /** Eagerly initialise the HIP runtime on `device`.  Optional. */
 int netc_gpu_init(int device);
 
+/**
+ * Process-wide launch shape of the batch kernel (defaults: 4, 0, 0).
+ * unroll: KiB each wavefront moves per loop trip (1, 2, 4 or 8); max_blocks:
+ * cap on 256-thread workgroups, 0 = exactly the workgroups the device holds
+ * at once (each wavefront walks an equal contiguous run); flags:
+ * NETC_GPU_TUNE_NT_* cache hints for the payload stream.  Call
+ * before launching work; it is not synchronised with concurrent launches.
+ */
+#define NETC_GPU_TUNE_NT_LOADS  1
+#define NETC_GPU_TUNE_NT_STORES 2
+int netc_gpu_tune(int unroll, int max_blocks, int flags);
+
 /** Message for the last failing netc_gpu_* call on this thread ("" if none). */
 const char *netc_gpu_strerror(void);
 

@@ -76,7 +76,7 @@ def gpu() -> ctypes.CDLL:
             lib.netc_gpu_init.restype = ctypes.c_int
             lib.netc_gpu_strerror.argtypes = []
             lib.netc_gpu_strerror.restype = ctypes.c_char_p
-            lib.netc_gpu_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+            lib.netc_gpu_tune.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
             lib.netc_gpu_tune.restype = ctypes.c_int
             lib.netc_gpu_mask_batch.argtypes = [ctypes.c_int, vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp]
             lib.netc_gpu_mask_batch.restype = ctypes.c_int

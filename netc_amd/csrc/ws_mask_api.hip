@@ -53,10 +53,18 @@ struct DeviceGuard {
     }
 };
 
+// device count, queried once per process (HIP's device list is fixed at runtime init)
+int cached_device_count() {
+    static const int n = [] {
+        int c = 0;
+        return hipGetDeviceCount(&c) == hipSuccess && c > 0 ? c : 0;
+    }();
+    return n;
+}
+
 int check_device(int device) {
-    int n = 0;
-    hipError_t e = hipGetDeviceCount(&n);
-    if (e != hipSuccess || n <= 0) return fail(NETC_GPU_ENODEV, "no HIP device available");
+    const int n = cached_device_count();
+    if (n <= 0) return fail(NETC_GPU_ENODEV, "no HIP device available");
     if (device < 0 || device >= n) return fail(NETC_GPU_ENODEV, "device %d out of range [0, %d)", device, n);
     return 0;
 }
@@ -84,11 +92,7 @@ int mask_batch_on_current(void* d_dst, const void* d_src, size_t total, const ui
 
 extern "C" {
 
-int netc_gpu_device_count(void) {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
-    return n < 0 ? 0 : n;
-}
+int netc_gpu_device_count(void) { return cached_device_count(); }
 
 int netc_gpu_init(int device) {
     if (int r = check_device(device)) return r;
@@ -101,12 +105,14 @@ int netc_gpu_init(int device) {
 
 const char* netc_gpu_strerror(void) { return g_err; }
 
-int netc_gpu_tune(int unroll, int max_blocks) {
+int netc_gpu_tune(int unroll, int max_blocks, int flags) {
     if (!(unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8))
         return fail(NETC_GPU_EINVAL, "unroll must be 1, 2, 4 or 8 (got %d)", unroll);
-    if (max_blocks < 1 || max_blocks > (1 << 24)) return fail(NETC_GPU_EINVAL, "max_blocks out of range");
+    if (max_blocks < 0 || max_blocks > (1 << 24)) return fail(NETC_GPU_EINVAL, "max_blocks out of range");
+    if (flags & ~(NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES)) return fail(NETC_GPU_EINVAL, "unknown tune flags");
     g_cfg.unroll = unroll;
     g_cfg.max_blocks = max_blocks;
+    g_cfg.flags = flags;
     return 0;
 }
 

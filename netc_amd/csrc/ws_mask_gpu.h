@@ -20,9 +20,12 @@ struct Args {
     uint64_t nwin;             // windows of U KiB covering [0, mis + total)
 };
 
+enum : int { kNtLoads = 1, kNtStores = 2 };   // LaunchCfg::flags (NETC_GPU_TUNE_NT_*)
+
 struct LaunchCfg {
     int unroll = 4;            // U: 1 KiB spans per window (1, 2, 4, 8)
-    int max_blocks = 2048;     // cap on 256-thread workgroups (each wave then loops)
+    int max_blocks = 0;        // cap on 256-thread workgroups; 0 = one resident round (occupancy x CUs)
+    int flags = 0;             // kNtLoads | kNtStores: non-temporal payload loads / stores
 };
 
 hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,

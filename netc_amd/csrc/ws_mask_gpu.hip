@@ -35,6 +35,10 @@ static constexpr int kWave = 64;
 static constexpr uint64_t kSpan = 64ull * 16ull;          // bytes one wave-instruction moves
 static constexpr uint64_t kInf = ~0ull;
 
+// waves per SIMD the register budget must allow: 8 (<= 64 VGPRs, full
+// occupancy) while the U in-flight vectors fit, 4 for U = 8
+constexpr int min_waves(int U) { return U >= 8 ? 4 : 8; }
+
 __device__ __forceinline__ uint32_t rotr8(uint32_t key, uint64_t r) {
     // rotate right by 8 * (r & 3) bits: v_alignbit_b32 key, key, sh
     return __builtin_amdgcn_alignbit(key, key, (uint32_t)((r & 3u) << 3));
@@ -92,29 +96,53 @@ __device__ __forceinline__ void table_load(const Args& a, Table& t, int64_t kb, 
     t.tail = kb + (kWave - 1) >= (int64_t)a.n;
 }
 
-// Largest virtual frame v in [-1, n] whose start is <= P (wave-uniform result).
-// 64-ary search: every step is one coalesced load of 64 probes and one ballot.
+// Virtual frame index L whose start is <= P and such that the frame containing
+// P is among L .. L+63, i.e. a valid base for the frame table (wave-uniform).
+// Invariant of the search: off'[L] <= q (L = -1: the virtual head frame) and
+// H > n or off[H] > q, so the containing frame is in [L, H - 1].
+//   1. interpolation probe: frames are usually spread evenly over the batch, so
+//      64 lanes probe a +-512-frame comb (stride 16) around q * n / total; when
+//      it brackets q (always, for uniform frames) H - L <= 16 after ONE load;
+//   2. otherwise 64-ary narrowing, one coalesced probe + one ballot per step.
+// The caller's table load is the final (second) dependent load.
 __device__ int64_t locate(const Args& a, uint64_t P, int lane) {
     if (P < a.mis) return -1;
     const uint64_t q = P - a.mis;
-    uint64_t lo = 0, cnt = a.n + 1;   // candidate frame indices [lo, lo + cnt)
-    while (cnt > (uint64_t)kWave) {
-        const uint64_t step = (cnt + kWave - 1) / kWave;
-        uint64_t idx = lo + (uint64_t)lane * step;
-        const bool valid = idx < lo + cnt;
-        const uint64_t val = valid ? a.off[idx] : kInf;
-        const uint64_t m = __ballot(valid && val <= q);
-        if (m == 0) return (int64_t)lo - 1;
-        const uint64_t j = 63 - __builtin_clzll(m);
-        lo += j * step;
-        const uint64_t rem = a.n + 1 - lo;
-        cnt = step < rem ? step : rem;
+    int64_t L = -1, H = (int64_t)a.n + 1;
+    if (a.n > (uint64_t)kWave && a.total > 0) {
+        constexpr int64_t kStride = 16;
+        const double fg = (double)q * ((double)a.n / (double)a.total);
+        int64_t g = (int64_t)fg;
+        g = g > (int64_t)a.n ? (int64_t)a.n : g;
+        const int64_t base = g - 31 * kStride;
+        const int64_t idx = base + (int64_t)lane * kStride;
+        const bool valid = idx >= 0 && idx <= (int64_t)a.n;
+        const uint64_t val = valid ? a.off[idx] : 0;
+        const uint64_t le = __ballot(valid && val <= q);   // probes at or before q
+        const uint64_t gt = __ballot(valid && val > q);    // probes after q
+        if (le) {
+            const int j = 63 - __builtin_clzll(le);
+            L = base + (int64_t)j * kStride;
+        }
+        if (gt) {
+            const int j = __builtin_ctzll(gt);
+            H = base + (int64_t)j * kStride;
+        }
+        // probes are sorted, so [L, H) is a valid bracket whenever both sides
+        // were seen; an unseen side keeps its global bound (-1 / n + 1)
     }
-    const bool valid = (uint64_t)lane < cnt;
-    const uint64_t val = valid ? a.off[lo + lane] : kInf;
-    const uint64_t m = __ballot(valid && val <= q);
-    if (m == 0) return (int64_t)lo - 1;
-    return (int64_t)(lo + (63 - __builtin_clzll(m)));
+    while (H - L > kWave) {
+        const int64_t lo = L + 1;
+        const int64_t step = (H - lo + kWave - 1) / kWave;   // probes lo, lo + step, ... cover [lo, H)
+        const int64_t idx = lo + (int64_t)lane * step;
+        const bool valid = idx < H;
+        const uint64_t val = valid ? a.off[idx] : kInf;
+        const uint64_t le = __ballot(valid && val <= q);
+        const uint64_t gt = __ballot(valid && val > q);
+        if (le) L = lo + (int64_t)(63 - __builtin_clzll(le)) * step;
+        if (gt) H = lo + (int64_t)__builtin_ctzll(gt) * step;
+    }
+    return L;
 }
 
 // Mask for this lane's vector in the span starting at A0 (P coords, 16-aligned,
@@ -156,10 +184,12 @@ __device__ __forceinline__ u32x4 span_mask(const Args& a, Table& t, uint64_t A0,
     return mask;
 }
 
-template <bool SRC_ALIGNED>
+template <bool SRC_ALIGNED, bool NT>
 __device__ __forceinline__ u32x4 load_vec(const Args& a, uint64_t P) {
     if constexpr (SRC_ALIGNED) {
-        return *reinterpret_cast<const u32x4*>(a.src_base + P);
+        const u32x4* p = reinterpret_cast<const u32x4*>(a.src_base + P);
+        if constexpr (NT) return __builtin_nontemporal_load(p);
+        return *p;
     } else {
         const uint8_t* p = a.src_base + P;
         u32x4 v;
@@ -169,6 +199,13 @@ __device__ __forceinline__ u32x4 load_vec(const Args& a, uint64_t P) {
                    ((uint32_t)p[4 * w + 3] << 24);
         return v;
     }
+}
+
+template <bool NT>
+__device__ __forceinline__ void store_vec(const Args& a, uint64_t P, u32x4 v) {
+    u32x4* p = reinterpret_cast<u32x4*>(a.dst_base + P);
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
 }
 
 // Partial vector at either end of the buffer: byte-granular, only bytes in
@@ -185,8 +222,11 @@ __device__ __forceinline__ void edge_vec(const Args& a, uint64_t P, u32x4 mask) 
     }
 }
 
-template <int U, bool SRC_ALIGNED>
-__global__ __launch_bounds__(256) void mask_frames_kernel(Args a) {
+// One wavefront = one contiguous run of windows [w_begin, w_end); a window is U
+// spans of 1 KiB, one 16-B vector per lane per span.  The first window's loads
+// are issued before the frame search so the search latency hides under them.
+template <int U, bool SRC_ALIGNED, bool NT_LOAD, bool NT_STORE>
+__global__ __launch_bounds__(256, min_waves(U)) void mask_frames_kernel(Args a) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / kWave);
@@ -200,16 +240,16 @@ __global__ __launch_bounds__(256) void mask_frames_kernel(Args a) {
     const uint64_t vec_end = (a.mis + a.total + 15) & ~15ull;      // end of the last vector
 
     uint64_t W0 = w_begin * kWin;
+    u32x4 d[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t P = W0 + (uint64_t)u * kSpan + 16ull * lane;
+        if (P >= full_lo && P < full_hi) d[u] = load_vec<SRC_ALIGNED, NT_LOAD>(a, P);
+    }
     Table t;
     table_load(a, t, locate(a, W0, lane), lane);
 
-    for (uint64_t w = w_begin; w < w_end; ++w, W0 += kWin) {
-        u32x4 d[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t P = W0 + (uint64_t)u * kSpan + 16ull * lane;
-            if (P >= full_lo && P < full_hi) d[u] = load_vec<SRC_ALIGNED>(a, P);
-        }
+    for (uint64_t w = w_begin;;) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t A0 = W0 + (uint64_t)u * kSpan;
@@ -217,10 +257,17 @@ __global__ __launch_bounds__(256) void mask_frames_kernel(Args a) {
             const u32x4 m = span_mask(a, t, A0, lane);
             const uint64_t P = A0 + 16ull * lane;
             if (P >= full_lo && P < full_hi) {
-                *reinterpret_cast<u32x4*>(a.dst_base + P) = d[u] ^ m;
+                store_vec<NT_STORE>(a, P, d[u] ^ m);
             } else if (P < vec_end) {
                 edge_vec(a, P, m);
             }
+        }
+        if (++w >= w_end) break;
+        W0 += kWin;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t P = W0 + (uint64_t)u * kSpan + 16ull * lane;
+            if (P >= full_lo && P < full_hi) d[u] = load_vec<SRC_ALIGNED, NT_LOAD>(a, P);
         }
     }
 }
@@ -231,10 +278,43 @@ __global__ __launch_bounds__(256) void mask_frames_kernel(Args a) {
 
 namespace netc_gpu {
 
-template <int U, bool AL>
-static hipError_t launch_u(const Args& a, int blocks, hipStream_t s) {
-    hipLaunchKernelGGL((mask_frames_kernel<U, AL>), dim3(blocks), dim3(256), 0, s, a);
+// Workgroups that fit on the device at once for one kernel instantiation
+// (occupancy x CUs), cached per device.  The grid is sized to exactly one
+// resident round: every wavefront gets an equal contiguous share, so a second,
+// partial round of workgroups would only add a tail.
+template <int U, bool AL, bool NL, bool NS>
+static int resident_blocks() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
+    if (cache[dev] > 0) return cache[dev];
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mask_frames_kernel<U, AL, NL, NS>, 256, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 || cus <= 0)
+        return 1024;
+    cache[dev] = per_cu * cus;
+    return cache[dev];
+}
+
+template <int U, bool AL, bool NL, bool NS>
+static hipError_t launch_u(const Args& a, int max_blocks, hipStream_t s) {
+    const uint64_t cap = (uint64_t)(max_blocks > 0 ? max_blocks : resident_blocks<U, AL, NL, NS>());
+    const uint64_t want = (a.nwin + 3) / 4;                   // one window per wavefront at most
+    const int blocks = (int)(want < cap ? want : cap);
+    if (blocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL((mask_frames_kernel<U, AL, NL, NS>), dim3(blocks), dim3(256), 0, s, a);
     return hipGetLastError();
+}
+
+template <bool NL, bool NS>
+static hipError_t launch_nt(const Args& a, int U, bool aligned, int max_blocks, hipStream_t s) {
+    if (!aligned) return launch_u<4, false, NL, NS>(a, max_blocks, s);
+    switch (U) {
+        case 1: return launch_u<1, true, NL, NS>(a, max_blocks, s);
+        case 2: return launch_u<2, true, NL, NS>(a, max_blocks, s);
+        case 8: return launch_u<8, true, NL, NS>(a, max_blocks, s);
+        default: return launch_u<4, true, NL, NS>(a, max_blocks, s);
+    }
 }
 
 hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,
@@ -248,23 +328,17 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
     a.keys = keys;
     a.n = n;
     const bool aligned = (((uintptr_t)src ^ (uintptr_t)dst) & 15u) == 0;
-    const int U = cfg.unroll;
+    const int U = aligned ? cfg.unroll : 4;
     const uint64_t nvec = (a.mis + total + 15) / 16;
     const uint64_t win_vec = 64ull * (uint64_t)U;
     a.nwin = (nvec + win_vec - 1) / win_vec;
-    const uint64_t max_waves = (uint64_t)cfg.max_blocks * 4;
-    const uint64_t waves = a.nwin < max_waves ? a.nwin : max_waves;
-    const int blocks = (int)((waves + 3) / 4);
-    if (blocks <= 0) return hipSuccess;
-    if (aligned) {
-        switch (U) {
-            case 1: return launch_u<1, true>(a, blocks, stream);
-            case 2: return launch_u<2, true>(a, blocks, stream);
-            case 8: return launch_u<8, true>(a, blocks, stream);
-            default: return launch_u<4, true>(a, blocks, stream);
-        }
-    }
-    return launch_u<4, false>(a, blocks, stream);
+    if (a.nwin == 0) return hipSuccess;
+    const bool nl = cfg.flags & kNtLoads, ns = cfg.flags & kNtStores;
+    const int mb = cfg.max_blocks;
+    if (nl && ns) return launch_nt<true, true>(a, U, aligned, mb, stream);
+    if (nl) return launch_nt<true, false>(a, U, aligned, mb, stream);
+    if (ns) return launch_nt<false, true>(a, U, aligned, mb, stream);
+    return launch_nt<false, false>(a, U, aligned, mb, stream);
 }
 
 }  // namespace netc_gpu

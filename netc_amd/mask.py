@@ -90,9 +90,13 @@ def gpu_init(device: int = 0) -> None:
     _check(_lib.gpu().netc_gpu_init(device))
 
 
-def tune(unroll: int = 4, max_blocks: int = 2048) -> None:
-    """Process-wide launch shape: U (KiB per wave per loop trip) and the workgroup cap."""
-    _check(_lib.gpu().netc_gpu_tune(unroll, max_blocks))
+NETC_GPU_TUNE_NT_LOADS = 1
+NETC_GPU_TUNE_NT_STORES = 2
+
+
+def tune(unroll: int = 4, max_blocks: int = 0, flags: int = 0) -> None:
+    """netc_gpu_tune: process-wide launch shape (KiB per wave per trip, workgroup cap, NT flags)."""
+    _check(_lib.gpu().netc_gpu_tune(unroll, max_blocks, flags))
 
 
 def _stream_handle(stream) -> int:

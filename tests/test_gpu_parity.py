@@ -157,7 +157,7 @@ def test_one_huge_frame(torch_cuda):
     run_case(torch_cuda, payload, frames_from_sizes([total]), np.array([0xDEADBEEF], dtype=np.uint32), 6, 6)
 
 
-@pytest.mark.parametrize("unroll,max_blocks", [(1, 2048), (2, 64), (8, 2048), (4, 1), (4, 100000)])
+@pytest.mark.parametrize("unroll,max_blocks", [(1, 2048), (2, 64), (8, 0), (4, 1), (4, 100000), (4, 0)])
 def test_launch_shapes(torch_cuda, unroll, max_blocks):
     try:
         nm.tune(unroll, max_blocks)
@@ -165,7 +165,7 @@ def test_launch_shapes(torch_cuda, unroll, max_blocks):
         payload = synth.host_payload(int(off[-1]), 13)
         run_case(torch_cuda, payload, off, synth.random_keys(off.size - 1, 13), 4, 4)
     finally:
-        nm.tune(4, 2048)
+        nm.tune()
 
 
 # ------------------------------------------------------------- full sizes ---
