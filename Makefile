@@ -18,7 +18,7 @@ HOST_HDRS  := $(wildcard include/*.h include/*/*.h)
 GPU_SRCS   := netc_amd/csrc/ws_mask_gpu.hip netc_amd/csrc/ws_mask_api.hip
 GPU_HDRS   := netc_amd/csrc/ws_mask_gpu.h include/ws/mask.h
 
-.PHONY: all host gpu oracle clean
+.PHONY: all host gpu oracle diag clean
 all: host gpu oracle diag
 host: $(LIBDIR)/libnetc.so
 gpu: $(LIBDIR)/libnetc_ws_gpu.so
@@ -38,6 +38,8 @@ clean:
 	$(MAKE) -C oracle clean
 
 # diagnostics (tools/, not part of the product)
-diag: tools/libdiag_stream.so
+diag: tools/libdiag_stream.so tools/libnetc_ws_gpu_stamps.so
 tools/libdiag_stream.so: tools/diag_stream.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+tools/libnetc_ws_gpu_stamps.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
+	$(HIPCC) $(HIPFLAGS) -DNETC_MASK_STAMPS -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'

@@ -102,6 +102,7 @@ int netc_gpu_init(int device);
  */
 #define NETC_GPU_TUNE_NT_LOADS  1
 #define NETC_GPU_TUNE_NT_STORES 2
+#define NETC_GPU_TUNE_PIPELINE  4   /* keep the next window's loads in flight while storing */
 int netc_gpu_tune(int unroll, int max_blocks, int flags);
 
 /** Message for the last failing netc_gpu_* call on this thread ("" if none). */

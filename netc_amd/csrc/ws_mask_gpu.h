@@ -20,7 +20,7 @@ struct Args {
     uint64_t nwin;             // windows of U KiB covering [0, mis + total)
 };
 
-enum : int { kNtLoads = 1, kNtStores = 2 };   // LaunchCfg::flags (NETC_GPU_TUNE_NT_*)
+enum : int { kNtLoads = 1, kNtStores = 2, kPipe = 4 };   // LaunchCfg::flags (NETC_GPU_TUNE_*)
 
 struct LaunchCfg {
     int unroll = 4;            // U: 1 KiB spans per window (1, 2, 4, 8)

@@ -37,7 +37,16 @@ static constexpr uint64_t kInf = ~0ull;
 
 // waves per SIMD the register budget must allow: 8 (<= 64 VGPRs, full
 // occupancy) while the U in-flight vectors fit, 4 for U = 8
-constexpr int min_waves(int U) { return U >= 8 ? 4 : 8; }
+constexpr int min_waves(int U, int flags) {
+    return (U >= 8 || (U >= 4 && (flags & kPipe))) ? 4 : 8;
+}
+
+#ifdef NETC_MASK_STAMPS
+__device__ uint64_t* g_stamps;   // diagnostic build only: 2 x u64 per wavefront
+extern "C" int netc_gpu_debug_stamps(void* d_buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &d_buf, sizeof(d_buf));
+}
+#endif
 
 __device__ __forceinline__ uint32_t rotr8(uint32_t key, uint64_t r) {
     // rotate right by 8 * (r & 3) bits: v_alignbit_b32 key, key, sh
@@ -225,14 +234,28 @@ __device__ __forceinline__ void edge_vec(const Args& a, uint64_t P, u32x4 mask) 
 // One wavefront = one contiguous run of windows [w_begin, w_end); a window is U
 // spans of 1 KiB, one 16-B vector per lane per span.  The first window's loads
 // are issued before the frame search so the search latency hides under them.
-template <int U, bool SRC_ALIGNED, bool NT_LOAD, bool NT_STORE>
-__global__ __launch_bounds__(256, min_waves(U)) void mask_frames_kernel(Args a) {
+template <int U, bool SRC_ALIGNED, int FLAGS>
+__global__ __launch_bounds__(256, min_waves(U, FLAGS)) void mask_frames_kernel(Args a) {
+    constexpr bool NT_LOAD = FLAGS & kNtLoads, NT_STORE = FLAGS & kNtStores, PIPE = FLAGS & kPipe;
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / kWave);
     const uint64_t w_begin = wave * a.nwin / nwaves;
     const uint64_t w_end = (wave + 1) * a.nwin / nwaves;
     if (w_begin >= w_end) return;
+#ifdef NETC_MASK_STAMPS
+    // diagnostic build only (tools/): per-wave start / end wall clock (100 MHz)
+    const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
+    struct StampOnExit {
+        uint64_t w, s0;
+        __device__ ~StampOnExit() {
+            if ((threadIdx.x & 63) == 0 && g_stamps) {
+                g_stamps[2 * w] = s0;
+                g_stamps[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
+            }
+        }
+    } stamp_guard{wave, stamp0};
+#endif
 
     constexpr uint64_t kWin = kSpan * U;
     const uint64_t full_lo = a.mis ? 16 : 0;                       // first full vector's P
@@ -241,15 +264,23 @@ __global__ __launch_bounds__(256, min_waves(U)) void mask_frames_kernel(Args a) 
 
     uint64_t W0 = w_begin * kWin;
     u32x4 d[U];
+    auto load_window = [&](u32x4 (&dst)[U], uint64_t base) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint64_t P = W0 + (uint64_t)u * kSpan + 16ull * lane;
-        if (P >= full_lo && P < full_hi) d[u] = load_vec<SRC_ALIGNED, NT_LOAD>(a, P);
-    }
+        for (int u = 0; u < U; ++u) {
+            const uint64_t P = base + (uint64_t)u * kSpan + 16ull * lane;
+            if (P >= full_lo && P < full_hi) dst[u] = load_vec<SRC_ALIGNED, NT_LOAD>(a, P);
+        }
+    };
+    load_window(d, W0);
     Table t;
     table_load(a, t, locate(a, W0, lane), lane);
 
     for (uint64_t w = w_begin;;) {
+        // PIPE: the next window's loads are in flight while this window is masked and stored
+        u32x4 dn[PIPE ? U : 1];
+        if constexpr (PIPE) {
+            if (w + 1 < w_end) load_window(dn, W0 + kWin);
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t A0 = W0 + (uint64_t)u * kSpan;
@@ -264,10 +295,11 @@ __global__ __launch_bounds__(256, min_waves(U)) void mask_frames_kernel(Args a) 
         }
         if (++w >= w_end) break;
         W0 += kWin;
+        if constexpr (PIPE) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t P = W0 + (uint64_t)u * kSpan + 16ull * lane;
-            if (P >= full_lo && P < full_hi) d[u] = load_vec<SRC_ALIGNED, NT_LOAD>(a, P);
+            for (int u = 0; u < U; ++u) d[u] = dn[u];
+        } else {
+            load_window(d, W0);
         }
     }
 }
@@ -282,38 +314,41 @@ namespace netc_gpu {
 // (occupancy x CUs), cached per device.  The grid is sized to exactly one
 // resident round: every wavefront gets an equal contiguous share, so a second,
 // partial round of workgroups would only add a tail.
-template <int U, bool AL, bool NL, bool NS>
+template <int U, bool AL, int F>
 static int resident_blocks() {
     static int cache[64] = {0};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
     if (cache[dev] > 0) return cache[dev];
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mask_frames_kernel<U, AL, NL, NS>, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mask_frames_kernel<U, AL, F>, 256, 0) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 || cus <= 0)
         return 1024;
     cache[dev] = per_cu * cus;
     return cache[dev];
 }
 
-template <int U, bool AL, bool NL, bool NS>
+template <int U, bool AL, int F>
 static hipError_t launch_u(const Args& a, int max_blocks, hipStream_t s) {
-    const uint64_t cap = (uint64_t)(max_blocks > 0 ? max_blocks : resident_blocks<U, AL, NL, NS>());
+    const uint64_t cap = (uint64_t)(max_blocks > 0 ? max_blocks : resident_blocks<U, AL, F>());
     const uint64_t want = (a.nwin + 3) / 4;                   // one window per wavefront at most
     const int blocks = (int)(want < cap ? want : cap);
     if (blocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL((mask_frames_kernel<U, AL, NL, NS>), dim3(blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((mask_frames_kernel<U, AL, F>), dim3(blocks), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
-template <bool NL, bool NS>
-static hipError_t launch_nt(const Args& a, int U, bool aligned, int max_blocks, hipStream_t s) {
-    if (!aligned) return launch_u<4, false, NL, NS>(a, max_blocks, s);
-    switch (U) {
-        case 1: return launch_u<1, true, NL, NS>(a, max_blocks, s);
-        case 2: return launch_u<2, true, NL, NS>(a, max_blocks, s);
-        case 8: return launch_u<8, true, NL, NS>(a, max_blocks, s);
-        default: return launch_u<4, true, NL, NS>(a, max_blocks, s);
+template <int U>
+static hipError_t launch_flags(const Args& a, int flags, int max_blocks, hipStream_t s) {
+    switch (flags & (kNtLoads | kNtStores | kPipe)) {
+        case 0: return launch_u<U, true, 0>(a, max_blocks, s);
+        case 1: return launch_u<U, true, 1>(a, max_blocks, s);
+        case 2: return launch_u<U, true, 2>(a, max_blocks, s);
+        case 3: return launch_u<U, true, 3>(a, max_blocks, s);
+        case 4: return launch_u<U, true, 4>(a, max_blocks, s);
+        case 5: return launch_u<U, true, 5>(a, max_blocks, s);
+        case 6: return launch_u<U, true, 6>(a, max_blocks, s);
+        default: return launch_u<U, true, 7>(a, max_blocks, s);
     }
 }
 
@@ -333,12 +368,17 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
     const uint64_t win_vec = 64ull * (uint64_t)U;
     a.nwin = (nvec + win_vec - 1) / win_vec;
     if (a.nwin == 0) return hipSuccess;
-    const bool nl = cfg.flags & kNtLoads, ns = cfg.flags & kNtStores;
     const int mb = cfg.max_blocks;
-    if (nl && ns) return launch_nt<true, true>(a, U, aligned, mb, stream);
-    if (nl) return launch_nt<true, false>(a, U, aligned, mb, stream);
-    if (ns) return launch_nt<false, true>(a, U, aligned, mb, stream);
-    return launch_nt<false, false>(a, U, aligned, mb, stream);
+    if (!aligned) {   // src and dst differ mod 16: byte-assembled loads, one shape
+        return (cfg.flags & kNtStores) ? launch_u<4, false, kNtStores>(a, mb, stream)
+                                       : launch_u<4, false, 0>(a, mb, stream);
+    }
+    switch (U) {
+        case 1: return launch_flags<1>(a, cfg.flags, mb, stream);
+        case 2: return launch_flags<2>(a, cfg.flags, mb, stream);
+        case 8: return launch_flags<8>(a, cfg.flags, mb, stream);
+        default: return launch_flags<4>(a, cfg.flags, mb, stream);
+    }
 }
 
 }  // namespace netc_gpu

@@ -1,0 +1,139 @@
+"""ctypes mirrors of the netc WebSocket structs (include/ws/common.h) and socketpair drivers
+for the host framing library libnetc.so.  Test helpers only."""
+
+import ctypes
+import socket
+import threading
+
+from netc_amd import _lib
+
+
+class TcpClient(ctypes.Structure):          # include/tcp/server.h (reference include/tcp/server.h:17-41)
+    _fields_ = [("sockfd", ctypes.c_int), ("sockaddr", ctypes.c_void_p), ("listening", ctypes.c_int),
+                ("pfd", ctypes.c_int), ("data", ctypes.c_void_p), ("on_connect", ctypes.c_void_p),
+                ("on_data", ctypes.c_void_p), ("on_disconnect", ctypes.c_void_p)]
+
+
+class WebClientHead(ctypes.Structure):      # leading member of struct web_client (reference include/web/client.h:15)
+    _fields_ = [("tcp_client", ctypes.POINTER(TcpClient))]
+
+
+class WsFrame(ctypes.Structure):            # include/ws/common.h struct ws_frame
+    _fields_ = [("header", ctypes.c_uint8), ("mask", ctypes.c_bool), ("masking_key", ctypes.c_uint8 * 4),
+                ("payload_length", ctypes.c_uint64)]
+
+
+class WsMessage(ctypes.Structure):
+    _fields_ = [("opcode", ctypes.c_uint8), ("buffer", ctypes.c_void_p), ("payload_length", ctypes.c_size_t)]
+
+
+class Vector(ctypes.Structure):
+    _fields_ = [("size", ctypes.c_size_t), ("capacity", ctypes.c_size_t), ("element_size", ctypes.c_size_t),
+                ("elements", ctypes.c_void_p)]
+
+
+class ParseState(ctypes.Structure):         # struct ws_frame_parsing_state
+    _fields_ = [("parsing_state", ctypes.c_int), ("frame", WsFrame), ("message", WsMessage),
+                ("real_payload_length", ctypes.c_uint64), ("payload_data", Vector),
+                ("received_length", ctypes.c_size_t)]
+
+
+libc = ctypes.CDLL(None)
+libc.free.argtypes = [ctypes.c_void_p]
+
+
+class Endpoint:
+    """A web_client bound to one end of a socketpair."""
+
+    def __init__(self, sock: socket.socket):
+        self.sock = sock
+        self.tcp = TcpClient()
+        self.tcp.sockfd = sock.fileno()
+        self.client = WebClientHead()
+        self.client.tcp_client = ctypes.pointer(self.tcp)
+
+
+def pending(sock: socket.socket) -> int:
+    import fcntl
+    import struct
+    import termios
+
+    return struct.unpack("i", fcntl.ioctl(sock.fileno(), termios.FIONREAD, b"\0\0\0\0"))[0]
+
+
+def pair():
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
+    for s in (a, b):
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 1 << 22)
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 22)
+    return a, b
+
+
+def send_wire(payload: bytes, opcode: int, key, num_frames: int = 1):
+    """(return code, wire bytes) of libnetc's ws_send_message for one message."""
+    lib = _lib.host()
+    a, b = pair()
+    out = bytearray()
+
+    def reader():
+        while True:
+            d = b.recv(1 << 20)
+            if not d:
+                break
+            out.extend(d)
+
+    th = threading.Thread(target=reader)
+    th.start()
+    ep = Endpoint(a)
+    buf = ctypes.create_string_buffer(bytes(payload), len(payload) + 1)
+    msg = WsMessage()
+    lib.ws_build_message(ctypes.byref(msg), opcode, len(payload), buf)
+    kbuf = (ctypes.c_uint8 * 4)(*key) if key is not None else None
+    rc = lib.ws_send_message(ctypes.byref(ep.client), ctypes.byref(msg), kbuf, num_frames)
+    a.shutdown(socket.SHUT_WR)
+    th.join()
+    a.close()
+    b.close()
+    return rc, bytes(out)
+
+
+def parse_stream(wire: bytes, chunks=(), max_payload=(1 << 62)):
+    """Feed wire to libnetc's ws_parse_frame in chunks; returns (messages, last rc).
+
+    messages: list of (opcode, buffer bytes as delivered incl. the TEXT NUL)."""
+    lib = _lib.host()
+    a, b = pair()
+    b.setblocking(False)
+    ep = Endpoint(b)
+    st = ParseState()
+    msgs = []
+    rc = 1
+    pos = 0
+    sizes = list(chunks)
+    while pos < len(wire) or sizes:
+        n = sizes.pop(0) if sizes else len(wire) - pos
+        piece = wire[pos:pos + n]
+        pos += len(piece)
+        a.sendall(piece)
+        while True:   # level-triggered: call again while bytes are pending (src/tcp/server.c:35-75)
+            rc = lib.ws_parse_frame(ctypes.byref(ep.client), ctypes.byref(st), max_payload)
+            if rc == 0:
+                m = st.message
+                msgs.append((m.opcode, ctypes.string_at(m.buffer, m.payload_length)))
+                libc.free(m.buffer)
+                ctypes.memset(ctypes.byref(st), 0, ctypes.sizeof(st))   # as src/web/server.c:139-140
+                continue
+            if rc == 1 and pending(b) > 0:
+                continue
+            break
+        if rc < 0:
+            break
+        if pos >= len(wire) and not sizes:
+            break
+    idle = st.parsing_state in (-1, 0) and not st.payload_data.elements
+    if st.payload_data.elements:
+        libc.free(st.payload_data.elements)
+    a.close()
+    b.close()
+    # rc: a parse error if one occurred, else 0 when the stream ended between messages, else 1
+    return msgs, (rc if rc < 0 else (0 if idle else 1))

@@ -80,18 +80,22 @@ def main():
 
     variants = []
     for v in args.variants.split(","):
-        u, mb, fl = (int(x) for x in v.split(":"))
-        variants.append(("mask", u, mb, fl))
+        parts = [int(x) for x in v.split(":")]
+        u, mb, fl = parts[:3]
+        oop = parts[3] if len(parts) > 3 else 0
+        variants.append(("mask" if not oop else "mask_oop", u, mb, fl))
     variants += [("diag", 0, 2048, 0), ("diag", 0, 4096, 0), ("diag", 0, 2048, 1), ("copy", 0, 0, 0)]
     stream_counts = [int(x) for x in args.streams.split(",")]
     results = {}
     for rnd in range(args.rounds):
         for (kind, u, mb, fl), ns in itertools.product(variants, stream_counts):
-            if kind == "mask":
+            if kind in ("mask", "mask_oop"):
                 nm.tune(u, mb, fl)
+                oop = kind == "mask_oop"
 
-                def launch(p, s):
-                    rc = lib.netc_gpu_mask_batch(0, p, p, total, off_t.data_ptr(), keys_t.data_ptr(), n, s)
+                def launch(p, s, oop=oop):
+                    d = ptrs[(ptrs.index(p) + 1) % nb] if oop else p
+                    rc = lib.netc_gpu_mask_batch(0, d, p, total, off_t.data_ptr(), keys_t.data_ptr(), n, s)
                     assert rc == 0
             elif kind == "diag":
                 def launch(p, s, mb=mb, fl=fl):
