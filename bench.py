@@ -212,8 +212,8 @@ def main():
 
     from netc_amd import mask as nm
 
-    if args.unroll or args.max_blocks or args.nt_flags:
-        nm.tune(args.unroll or 4, args.max_blocks or 0, args.nt_flags or 0)
+    if args.unroll or args.max_blocks or args.nt_flags is not None:
+        nm.tune(args.unroll or 4, args.max_blocks or 0, -1 if args.nt_flags is None else args.nt_flags)
     nm.gpu_init(local)
     batches, total, nframes = make_batches(torch, args.workload, rank, args.rotation_bytes, device)
     stream = torch.cuda.current_stream(device)

@@ -109,7 +109,9 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags) {
     if (!(unroll == 1 || unroll == 2 || unroll == 4 || unroll == 8))
         return fail(NETC_GPU_EINVAL, "unroll must be 1, 2, 4 or 8 (got %d)", unroll);
     if (max_blocks < 0 || max_blocks > (1 << 24)) return fail(NETC_GPU_EINVAL, "max_blocks out of range");
-    if (flags & ~(NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES | NETC_GPU_TUNE_PIPELINE)) return fail(NETC_GPU_EINVAL, "unknown tune flags");
+    if (flags != NETC_GPU_TUNE_AUTO &&
+        (flags & ~(NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES | NETC_GPU_TUNE_PIPELINE)))
+        return fail(NETC_GPU_EINVAL, "unknown tune flags");
     g_cfg.unroll = unroll;
     g_cfg.max_blocks = max_blocks;
     g_cfg.flags = flags;

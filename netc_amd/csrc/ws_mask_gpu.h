@@ -25,7 +25,7 @@ enum : int { kNtLoads = 1, kNtStores = 2, kPipe = 4 };   // LaunchCfg::flags (NE
 struct LaunchCfg {
     int unroll = 4;            // U: 1 KiB spans per window (1, 2, 4, 8)
     int max_blocks = 0;        // cap on 256-thread workgroups; 0 = one resident round (occupancy x CUs)
-    int flags = 0;             // kNtLoads | kNtStores: non-temporal payload loads / stores
+    int flags = -1;            // kNtLoads | kNtStores | kPipe; -1 = chosen per batch (launch_mask_frames)
 };
 
 hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,

@@ -369,15 +369,24 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
     a.nwin = (nvec + win_vec - 1) / win_vec;
     if (a.nwin == 0) return hipSuccess;
     const int mb = cfg.max_blocks;
+    int flags = cfg.flags;
+    if (flags < 0) {
+        // auto: non-temporal payload stream always (it is touched once); keep the
+        // next window in flight (PIPE) when each wavefront has only a few windows
+        // -- small batches, where the wave's start-up latency is not amortised
+        // (tools/sweep.py on 64 MiB vs 1 GiB batches, DESIGN.md "Launch shape")
+        const uint64_t full_round_waves = 256ull * 32ull;   // 256 CUs x 32 waves at 8 waves / SIMD
+        flags = kNtLoads | kNtStores | (a.nwin <= 8 * full_round_waves ? kPipe : 0);
+    }
     if (!aligned) {   // src and dst differ mod 16: byte-assembled loads, one shape
-        return (cfg.flags & kNtStores) ? launch_u<4, false, kNtStores>(a, mb, stream)
-                                       : launch_u<4, false, 0>(a, mb, stream);
+        return (flags & kNtStores) ? launch_u<4, false, kNtStores>(a, mb, stream)
+                                   : launch_u<4, false, 0>(a, mb, stream);
     }
     switch (U) {
-        case 1: return launch_flags<1>(a, cfg.flags, mb, stream);
-        case 2: return launch_flags<2>(a, cfg.flags, mb, stream);
-        case 8: return launch_flags<8>(a, cfg.flags, mb, stream);
-        default: return launch_flags<4>(a, cfg.flags, mb, stream);
+        case 1: return launch_flags<1>(a, flags, mb, stream);
+        case 2: return launch_flags<2>(a, flags, mb, stream);
+        case 8: return launch_flags<8>(a, flags, mb, stream);
+        default: return launch_flags<4>(a, flags, mb, stream);
     }
 }
 

@@ -94,8 +94,12 @@ NETC_GPU_TUNE_NT_LOADS = 1
 NETC_GPU_TUNE_NT_STORES = 2
 
 
-def tune(unroll: int = 4, max_blocks: int = 0, flags: int = 0) -> None:
-    """netc_gpu_tune: process-wide launch shape (KiB per wave per trip, workgroup cap, NT flags)."""
+NETC_GPU_TUNE_AUTO = -1
+NETC_GPU_TUNE_PIPELINE = 4
+
+
+def tune(unroll: int = 4, max_blocks: int = 0, flags: int = NETC_GPU_TUNE_AUTO) -> None:
+    """netc_gpu_tune: process-wide launch shape (KiB per wave per trip, workgroup cap, cache/pipeline flags)."""
     _check(_lib.gpu().netc_gpu_tune(unroll, max_blocks, flags))
 
 

@@ -158,12 +158,15 @@ def test_one_huge_frame(torch_cuda):
 
 
 @pytest.mark.parametrize("unroll,max_blocks", [(1, 2048), (2, 64), (8, 0), (4, 1), (4, 100000), (4, 0)])
-def test_launch_shapes(torch_cuda, unroll, max_blocks):
+@pytest.mark.parametrize("flags", [-1, 0, 1, 2, 3, 4, 5, 6, 7])
+def test_launch_shapes(torch_cuda, unroll, max_blocks, flags):
+    """Every kernel instantiation (U x cache-hint / pipeline flags x grid cap) is bit-exact."""
     try:
-        nm.tune(unroll, max_blocks)
+        nm.tune(unroll, max_blocks, flags)
         off = synth.mixed_offsets(5 << 20, 1, 9000, seed=13)
         payload = synth.host_payload(int(off[-1]), 13)
         run_case(torch_cuda, payload, off, synth.random_keys(off.size - 1, 13), 4, 4)
+        run_case(torch_cuda, payload, off, synth.random_keys(off.size - 1, 14), 4, 9)   # src misaligned vs dst
     finally:
         nm.tune()
 

@@ -39,8 +39,9 @@ def main():
     dev = torch.device("cuda", 0)
     lib = _lib.gpu()
     diag = ctypes.CDLL(os.path.join(ROOT, "tools", "libdiag_stream.so"))
-    diag.diag_xor_const.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int,
-                                    ctypes.c_int, ctypes.c_void_p]
+    diag.diag_stream.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    sink = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
     off, keys, total = synth.config(args.workload)
     nb = max(2, -(-args.rotation_bytes // total))
     off_t = torch.from_numpy(off.view(np.int64)).to(dev)
@@ -84,7 +85,8 @@ def main():
         u, mb, fl = parts[:3]
         oop = parts[3] if len(parts) > 3 else 0
         variants.append(("mask" if not oop else "mask_oop", u, mb, fl))
-    variants += [("diag", 0, 2048, 0), ("diag", 0, 4096, 0), ("diag", 0, 2048, 1), ("copy", 0, 0, 0)]
+    # diag: in-place XOR, grid-stride (contig 0) / wave-contiguous (1), nt (flags 1) -- see tools/diag_stream.hip
+    variants += [("diag", 0, 0, 1), ("diag", 0, 1, 1), ("diag", 0, 0, 0)]
     stream_counts = [int(x) for x in args.streams.split(",")]
     results = {}
     for rnd in range(args.rounds):
@@ -98,8 +100,8 @@ def main():
                     rc = lib.netc_gpu_mask_batch(0, d, p, total, off_t.data_ptr(), keys_t.data_ptr(), n, s)
                     assert rc == 0
             elif kind == "diag":
-                def launch(p, s, mb=mb, fl=fl):
-                    diag.diag_xor_const(p, p, total, 0x5A5A5A5A, mb, fl, s)
+                def launch(p, s, contig=mb, nt=fl):
+                    diag.diag_stream(0, nt, contig, p, p, total, 0x5A5A5A5A, 2048, sink.data_ptr(), s)
             else:
                 def launch(p, s):
                     j = ptrs.index(p)
