@@ -57,6 +57,7 @@ def parse_args():
     p.add_argument("--max-blocks", type=int, default=None)
     p.add_argument("--nt-flags", type=int, default=None)
     p.add_argument("--no-copy-ceiling", action="store_true")
+    p.add_argument("--no-pipelined-probe", dest="pipelined_probe", action="store_false")
     return p.parse_args()
 
 
@@ -81,6 +82,18 @@ def make_batches(torch, workload: str, rank: int, rotation_bytes: int, device):
         k = synth.random_keys(keys.size, stream=300 + 1000 * rank + b)
         batches.append((payload, off_t, torch.from_numpy(k.view(np.int32)).to(device)))
     return batches, total, keys.size
+
+
+def traffic_per_launch(workload: str):
+    """HBM bytes per launch of the masking kernel from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, written by tools/summarize_prof.py from separate --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950 corrections applied), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        rec = json.load(open(path))[workload]
+        return rec["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def copy_ceiling(torch, device, nbytes=64 << 20, reps=64):
@@ -216,14 +229,26 @@ def main():
         nm.tune(args.unroll or 4, args.max_blocks or 0, -1 if args.nt_flags is None else args.nt_flags)
     nm.gpu_init(local)
     batches, total, nframes = make_batches(torch, args.workload, rank, args.rotation_bytes, device)
-    stream = torch.cuda.current_stream(device)
+    stream = torch.cuda.Stream(device)            # a dedicated (non-NULL) HIP stream for the hot path
+    torch.cuda.synchronize(device)                # batches were generated on the default stream
+    for p, o, k in batches[:1]:
+        nm.mask_batch(p, p, o, k, stream=stream)          # validated once through the Python mirror
+    # hot loop: the C-ABI entry itself, with the argument words prepared once
+    from netc_amd import _lib
 
-    def step(i):
-        p, o, k = batches[i % len(batches)]
-        nm.mask_batch(p, p, o, k, stream=stream)
+    entry = _lib.gpu().netc_gpu_mask_batch
+    prepared = [(p.data_ptr(), o.data_ptr(), k.data_ptr()) for p, o, k in batches]
+    nb = len(prepared)
 
+    def step(i, s_handle):
+        p, o, k = prepared[i % nb]
+        rc = entry(local, p, p, total, o, k, nframes, s_handle)
+        if rc != 0:
+            raise nm.NetcGpuError(rc, _lib.gpu().netc_gpu_strerror().decode())
+
+    sh = stream.cuda_stream
     for i in range(args.warmup):
-        step(i)
+        step(i, sh)
     torch.cuda.synchronize(device)
 
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -234,7 +259,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         starts[i].record(stream)
-        step(args.warmup + i)
+        step(args.warmup + i, sh)
         ends[i].record(stream)
     torch.cuda.synchronize(device)
     if world > 1:
@@ -242,13 +267,26 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = np.array([s.elapsed_time(e) for s, e in zip(starts, ends)])
 
+    # secondary figure: the same steps with two batches in flight on two HIP streams
+    # (independent batches, as a serving loop would pipeline them); not the headline
+    pipelined = None
+    if args.pipelined_probe:
+        s2 = [stream, torch.cuda.Stream(device)]
+        torch.cuda.synchronize(device)
+        if world > 1:
+            torch.distributed.barrier()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            step(i, s2[i % 2].cuda_stream)
+        torch.cuda.synchronize(device)
+        if world > 1:
+            torch.distributed.barrier()
+        pipelined = time.perf_counter() - t1
+
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, kern_ms.mean(), pipelined or 0.0], dtype=torch.float64, device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
-        km = torch.tensor([kern_ms.mean()], dtype=torch.float64, device=device)
-        torch.distributed.all_reduce(km, op=torch.distributed.ReduceOp.MAX)
-        kern_mean = float(km.item())
+        elapsed, kern_mean, pipelined = float(t[0]), float(t[1]), (float(t[2]) or None)
     else:
         kern_mean = float(kern_ms.mean())
 
@@ -293,13 +331,17 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": None,
+                "traffic": traffic_per_launch(args.workload),
                 "kernel_ms_mean": round(kern_mean, 5),
                 "kernel_ms_min": round(float(kern_ms.min()), 5),
                 "algorithmic_bytes_per_launch": 2 * total,
                 "copy_ceiling_GBps": round(ceiling, 1) if ceiling else None,
             },
             "cpu_baseline": cpu,
+            "pipelined_2stream": None if not pipelined else {
+                "value": round(float(total) * world * args.steps / pipelined / GIB, 3),
+                "ms_per_step": round(pipelined / args.steps * 1e3, 5),
+                "note": "same steps, two independent batches in flight on two HIP streams (not the headline)"},
         }
         print(json.dumps(line), flush=True)
     if world > 1:
