@@ -17,7 +17,8 @@ struct Args {
     const uint32_t* keys;      // n packed keys
     uint64_t n;                // frames
     uint64_t mis;              // dst & 15
-    uint64_t nwin;             // windows of U KiB covering [0, mis + total)
+    uint64_t nwin;             // windows (chunks) of U KiB covering [0, mis + total)
+    double density;            // n / total: frames per payload byte (table-base guesses)
 };
 
 enum : int { kNtLoads = 1, kNtStores = 2, kPipe = 4 };   // LaunchCfg::flags (NETC_GPU_TUNE_*)

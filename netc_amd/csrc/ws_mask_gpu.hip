@@ -35,11 +35,10 @@ static constexpr int kWave = 64;
 static constexpr uint64_t kSpan = 64ull * 16ull;          // bytes one wave-instruction moves
 static constexpr uint64_t kInf = ~0ull;
 
-// waves per SIMD the register budget must allow: 8 (<= 64 VGPRs, full
-// occupancy) while the U in-flight vectors fit, 4 for U = 8
-constexpr int min_waves(int U, int flags) {
-    return (U >= 8 || (U >= 4 && (flags & kPipe))) ? 4 : 8;
-}
+// waves per SIMD the register budget is sized for, by U (KiB per chunk): two
+// chunks of payload are live per wavefront (current + prefetched), 8 U VGPRs
+__device__ constexpr int kMinWaves[9] = {8, 8, 4, 4, 4, 4, 4, 4, 2};
+
 
 #ifdef NETC_MASK_STAMPS
 __device__ uint64_t* g_stamps;   // diagnostic build only: 2 x u64 per wavefront
@@ -98,11 +97,38 @@ __device__ __forceinline__ void frame_entry(const Args& a, int64_t v, uint64_t& 
     }
 }
 
-__device__ __forceinline__ void table_load(const Args& a, Table& t, int64_t kb, int lane) {
+// issue the table loads (frames kb .. kb+63, one per lane) without waiting for them
+__device__ __forceinline__ void table_issue(const Args& a, Table& t, int64_t kb, int lane) {
     t.kb = kb;
     frame_entry(a, kb + lane, t.start, t.key);
-    t.last = readlane64(t.start, kWave - 1);
     t.tail = kb + (kWave - 1) >= (int64_t)a.n;
+}
+
+__device__ __forceinline__ void table_finish(Table& t) { t.last = readlane64(t.start, kWave - 1); }
+
+__device__ __forceinline__ void table_load(const Args& a, Table& t, int64_t kb, int lane) {
+    table_issue(a, t, kb, lane);
+    table_finish(t);
+}
+
+// Does the table hold the frame containing P (entry 0 starts at or before P and a
+// later entry starts after it, or the open-ended tail frame is in the table)?
+__device__ __forceinline__ bool table_brackets(const Table& t, uint64_t P) {
+    const uint64_t m = __ballot(t.start <= P);
+    if (m == 0) return false;
+    return t.tail || m != ~0ull;
+}
+
+// Table base for the chunk at P guessed from a frame known to start at s_known
+// (index f_known) and the batch's mean frame density: frames are independent
+// draws, so the guess error grows only with the square root of the frames in
+// between; the window is biased forward so the chunk's later frames fit too.
+__device__ __forceinline__ int64_t guess_base(const Args& a, int64_t f_known, uint64_t s_known, uint64_t P) {
+    if (P < a.mis) return -1;
+    const double ahead = (double)(P - s_known) * a.density;
+    int64_t g = f_known + (int64_t)ahead - 24;
+    g = g < -1 ? -1 : g;
+    return g > (int64_t)a.n ? (int64_t)a.n : g;
 }
 
 // Virtual frame index L whose start is <= P and such that the frame containing
@@ -231,18 +257,21 @@ __device__ __forceinline__ void edge_vec(const Args& a, uint64_t P, u32x4 mask) 
     }
 }
 
-// One wavefront = one contiguous run of windows [w_begin, w_end); a window is U
-// spans of 1 KiB, one 16-B vector per lane per span.  The first window's loads
-// are issued before the frame search so the search latency hides under them.
-template <int U, bool SRC_ALIGNED, int FLAGS>
-__global__ __launch_bounds__(256, min_waves(U, FLAGS)) void mask_frames_kernel(Args a) {
-    constexpr bool NT_LOAD = FLAGS & kNtLoads, NT_STORE = FLAGS & kNtStores, PIPE = FLAGS & kPipe;
+// Chunk = one window of U spans (U KiB).  Wavefront w of W takes chunks w, w+W,
+// w+2W, ...: at any moment the resident wavefronts stream one compact region of
+// HBM (the order a grid-stride copy has), which measured 10-14 % faster than
+// each wavefront walking its own contiguous share (tools/order_probe.py).
+// Software pipeline per wavefront: the NEXT chunk's payload loads and its frame
+// table probe are in flight while the current chunk is masked and stored.  The
+// probe is a table load at a guessed base (exact for evenly sized frames); a
+// miss falls back to the search in locate().
+template <int U, bool SRC_ALIGNED, bool NT>
+__global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / kWave);
-    const uint64_t w_begin = wave * a.nwin / nwaves;
-    const uint64_t w_end = (wave + 1) * a.nwin / nwaves;
-    if (w_begin >= w_end) return;
+    uint64_t c = wave;
+    if (c >= a.nwin) return;
 #ifdef NETC_MASK_STAMPS
     // diagnostic build only (tools/): per-wave start / end wall clock (100 MHz)
     const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
@@ -262,45 +291,58 @@ __global__ __launch_bounds__(256, min_waves(U, FLAGS)) void mask_frames_kernel(A
     const uint64_t full_hi = (a.mis + a.total) & ~15ull;           // end of the last full vector
     const uint64_t vec_end = (a.mis + a.total + 15) & ~15ull;      // end of the last vector
 
-    uint64_t W0 = w_begin * kWin;
-    u32x4 d[U];
     auto load_window = [&](u32x4 (&dst)[U], uint64_t base) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t P = base + (uint64_t)u * kSpan + 16ull * lane;
-            if (P >= full_lo && P < full_hi) dst[u] = load_vec<SRC_ALIGNED, NT_LOAD>(a, P);
+            if (P >= full_lo && P < full_hi) dst[u] = load_vec<SRC_ALIGNED, NT>(a, P);
         }
     };
-    load_window(d, W0);
-    Table t;
-    table_load(a, t, locate(a, W0, lane), lane);
 
-    for (uint64_t w = w_begin;;) {
-        // PIPE: the next window's loads are in flight while this window is masked and stored
-        u32x4 dn[PIPE ? U : 1];
-        if constexpr (PIPE) {
-            if (w + 1 < w_end) load_window(dn, W0 + kWin);
+    u32x4 d[U];
+    uint64_t A = c * kWin;
+    load_window(d, A);
+    Table t;
+    table_issue(a, t, guess_base(a, 0, a.mis, A), lane);   // global guess: frame 0 starts near P = mis
+
+    for (;;) {
+        // resolve this chunk's table (its probe was issued one chunk ago)
+        table_finish(t);
+        if (!table_brackets(t, A)) table_load(a, t, locate(a, A, lane), lane);
+        const uint64_t m0 = __ballot(t.start <= A);
+        const int j0 = __popcll(m0) - 1;
+        const int64_t f0 = t.kb + j0;
+        const uint64_t s0 = readlane64(t.start, j0);
+
+        // prefetch the next chunk: payload loads + table probe guessed from f0
+        const uint64_t cn = c + nwaves;
+        const bool more = cn < a.nwin;
+        const uint64_t An = cn * kWin;
+        u32x4 dn[U];
+        Table tn;
+        if (more) {
+            load_window(dn, An);
+            table_issue(a, tn, guess_base(a, f0, s0, An), lane);
         }
+
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t A0 = W0 + (uint64_t)u * kSpan;
+            const uint64_t A0 = A + (uint64_t)u * kSpan;
             if (A0 >= vec_end) break;                               // wave-uniform
             const u32x4 m = span_mask(a, t, A0, lane);
             const uint64_t P = A0 + 16ull * lane;
             if (P >= full_lo && P < full_hi) {
-                store_vec<NT_STORE>(a, P, d[u] ^ m);
+                store_vec<NT>(a, P, d[u] ^ m);
             } else if (P < vec_end) {
                 edge_vec(a, P, m);
             }
         }
-        if (++w >= w_end) break;
-        W0 += kWin;
-        if constexpr (PIPE) {
+        if (!more) break;
+        c = cn;
+        A = An;
+        t = tn;
 #pragma unroll
-            for (int u = 0; u < U; ++u) d[u] = dn[u];
-        } else {
-            load_window(d, W0);
-        }
+        for (int u = 0; u < U; ++u) d[u] = dn[u];
     }
 }
 
@@ -311,45 +353,35 @@ __global__ __launch_bounds__(256, min_waves(U, FLAGS)) void mask_frames_kernel(A
 namespace netc_gpu {
 
 // Workgroups that fit on the device at once for one kernel instantiation
-// (occupancy x CUs), cached per device.  The grid is sized to exactly one
-// resident round: every wavefront gets an equal contiguous share, so a second,
-// partial round of workgroups would only add a tail.
-template <int U, bool AL, int F>
+// (occupancy x CUs), cached per device: the grid is exactly one resident round
+// and every wavefront strides over the chunks.
+template <int U, bool AL, bool NT>
 static int resident_blocks() {
     static int cache[64] = {0};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
     if (cache[dev] > 0) return cache[dev];
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mask_frames_kernel<U, AL, F>, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mask_frames_kernel<U, AL, NT>, 256, 0) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 || cus <= 0)
         return 1024;
     cache[dev] = per_cu * cus;
     return cache[dev];
 }
 
-template <int U, bool AL, int F>
+template <int U, bool AL, bool NT>
 static hipError_t launch_u(const Args& a, int max_blocks, hipStream_t s) {
-    const uint64_t cap = (uint64_t)(max_blocks > 0 ? max_blocks : resident_blocks<U, AL, F>());
-    const uint64_t want = (a.nwin + 3) / 4;                   // one window per wavefront at most
+    const uint64_t cap = (uint64_t)(max_blocks > 0 ? max_blocks : resident_blocks<U, AL, NT>());
+    const uint64_t want = (a.nwin + 3) / 4;                   // one chunk per wavefront at most
     const int blocks = (int)(want < cap ? want : cap);
     if (blocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL((mask_frames_kernel<U, AL, F>), dim3(blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((mask_frames_kernel<U, AL, NT>), dim3(blocks), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 template <int U>
-static hipError_t launch_flags(const Args& a, int flags, int max_blocks, hipStream_t s) {
-    switch (flags & (kNtLoads | kNtStores | kPipe)) {
-        case 0: return launch_u<U, true, 0>(a, max_blocks, s);
-        case 1: return launch_u<U, true, 1>(a, max_blocks, s);
-        case 2: return launch_u<U, true, 2>(a, max_blocks, s);
-        case 3: return launch_u<U, true, 3>(a, max_blocks, s);
-        case 4: return launch_u<U, true, 4>(a, max_blocks, s);
-        case 5: return launch_u<U, true, 5>(a, max_blocks, s);
-        case 6: return launch_u<U, true, 6>(a, max_blocks, s);
-        default: return launch_u<U, true, 7>(a, max_blocks, s);
-    }
+static hipError_t launch_nt(const Args& a, bool nt, int max_blocks, hipStream_t s) {
+    return nt ? launch_u<U, true, true>(a, max_blocks, s) : launch_u<U, true, false>(a, max_blocks, s);
 }
 
 hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,
@@ -368,25 +400,18 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
     const uint64_t win_vec = 64ull * (uint64_t)U;
     a.nwin = (nvec + win_vec - 1) / win_vec;
     if (a.nwin == 0) return hipSuccess;
+    a.density = total ? (double)n / (double)total : 0.0;
     const int mb = cfg.max_blocks;
-    int flags = cfg.flags;
-    if (flags < 0) {
-        // auto: non-temporal payload stream always (it is touched once); keep the
-        // next window in flight (PIPE) when each wavefront has only a few windows
-        // -- small batches, where the wave's start-up latency is not amortised
-        // (tools/sweep.py on 64 MiB vs 1 GiB batches, DESIGN.md "Launch shape")
-        const uint64_t full_round_waves = 256ull * 32ull;   // 256 CUs x 32 waves at 8 waves / SIMD
-        flags = kNtLoads | kNtStores | (a.nwin <= 8 * full_round_waves ? kPipe : 0);
-    }
+    // payload loads / stores non-temporal unless asked otherwise: every byte is touched once
+    const bool nt = cfg.flags < 0 || (cfg.flags & (kNtLoads | kNtStores));
     if (!aligned) {   // src and dst differ mod 16: byte-assembled loads, one shape
-        return (flags & kNtStores) ? launch_u<4, false, kNtStores>(a, mb, stream)
-                                   : launch_u<4, false, 0>(a, mb, stream);
+        return nt ? launch_u<4, false, true>(a, mb, stream) : launch_u<4, false, false>(a, mb, stream);
     }
     switch (U) {
-        case 1: return launch_flags<1>(a, flags, mb, stream);
-        case 2: return launch_flags<2>(a, flags, mb, stream);
-        case 8: return launch_flags<8>(a, flags, mb, stream);
-        default: return launch_flags<4>(a, flags, mb, stream);
+        case 1: return launch_nt<1>(a, nt, mb, stream);
+        case 2: return launch_nt<2>(a, nt, mb, stream);
+        case 8: return launch_nt<8>(a, nt, mb, stream);
+        default: return launch_nt<4>(a, nt, mb, stream);
     }
 }
 
