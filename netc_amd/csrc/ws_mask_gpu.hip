@@ -13,12 +13,16 @@
 //   * frames are [off[k], off[k+1]) in payload coordinates, i.e.
 //     [off[k]+mis, off[k+1]+mis) in P coordinates.  Two virtual frames with a
 //     zero key close the range: -1 = [0, off[0]+mis) and n = [off[n]+mis, inf).
-//   * every wavefront owns a contiguous run of windows (U spans of 64 vectors =
-//     U KiB) and keeps a 64-entry "frame table" in registers: lane j holds the
-//     start and key of virtual frame kb + j.  A span's frame is found with one
-//     ballot; the (rare) frame boundaries inside a span are applied with a
-//     wave-uniform loop; the table slides forward with one coalesced 768-byte
-//     reload whenever the window runs past it.
+//   * the batch is cut into chunks of U spans (a span = 64 vectors = 1 KiB, one
+//     wave-instruction); wavefront w of W takes chunks w, w+W, w+2W, ... so the
+//     resident wavefronts always stream one compact region of HBM.
+//   * per chunk a wavefront holds a 64-entry "frame table" in registers: lane j
+//     holds the start and key of virtual frame kb + j.  A span's frame is found
+//     with one ballot; the (rare) frame boundaries inside a span are applied with
+//     a wave-uniform loop; the table slides forward with one coalesced 768-byte
+//     reload if a chunk runs past it.  The table for the NEXT chunk is loaded at a
+//     guessed base while the current chunk is processed (exact for evenly sized
+//     frames, within a few frames otherwise); a miss falls back to locate().
 //   * the key stays in registers and is rotated per vector with v_alignbit
 //     (rotr by 8*((P - frame_start) & 3)); it is the same for the 4 dwords of a
 //     16-B vector, and the same for every lane of a span.
