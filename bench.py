@@ -215,13 +215,22 @@ def main():
     world, rank, local = dist_env()
     import torch
 
+    # NETC_BENCH_DEVICE / NETC_BENCH_BACKEND=gloo: rehearsal of the N-rank path on a
+    # one-GPU box (every rank on one device, timing collectives on the CPU); the
+    # real multi-GPU run uses one GPU per rank and RCCL ("nccl") for the barrier.
+    local = int(os.environ.get("NETC_BENCH_DEVICE", local))
+    backend = os.environ.get("NETC_BENCH_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    coll_dev = device if backend == "nccl" else torch.device("cpu")
 
     from netc_amd import mask as nm
 
@@ -289,7 +298,7 @@ def main():
         pipelined = time.perf_counter() - t1
 
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms.mean(), pipelined or 0.0], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, kern_ms.mean(), pipelined or 0.0], dtype=torch.float64, device=coll_dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed, kern_mean, pipelined = float(t[0]), float(t[1]), (float(t[2]) or None)
     else:
