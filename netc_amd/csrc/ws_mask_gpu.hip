@@ -35,6 +35,21 @@ namespace netc_gpu {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Every device buffer here is global memory.  Accesses go through explicit
+// address-space-1 pointers so the compiler emits global_* instructions: a flat_*
+// access (what a generic pointer becomes once its provenance is lost) completes
+// out of order and forces s_waitcnt vmcnt(0) lgkmcnt(0) at every use, which
+// drains the prefetched chunk and kills the software pipeline.
+#define NETC_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ const NETC_GLOBAL T* gptr(const T* p) {
+    return (const NETC_GLOBAL T*)p;
+}
+template <typename T>
+__device__ __forceinline__ NETC_GLOBAL T* gptr(T* p) {
+    return (NETC_GLOBAL T*)p;
+}
+
 static constexpr int kWave = 64;
 static constexpr uint64_t kSpan = 64ull * 16ull;          // bytes one wave-instruction moves
 static constexpr uint64_t kInf = ~0ull;
@@ -87,18 +102,20 @@ struct Table {
     bool tail;        // frame n (the open-ended pass-through frame) is in the table
 };
 
-// start / key of virtual frame v in P coordinates
+// start / key of virtual frame v in P coordinates.  Branch-free: both loads are
+// always issued at clamped (valid) indices and the virtual-frame values are
+// selected afterwards, so the loads stay straight-line code and the compiler can
+// count them in vmcnt instead of draining every outstanding load (a load under a
+// per-lane branch forces s_waitcnt vmcnt(0) at the next use).  With n == 0 the
+// host points keys at the offsets array, so keys[0] is always readable.
 __device__ __forceinline__ void frame_entry(const Args& a, int64_t v, uint64_t& s, uint32_t& k) {
-    if (v < 0) {
-        s = 0;
-        k = 0;
-    } else if ((uint64_t)v <= a.n) {
-        s = a.off[v] + a.mis;
-        k = (uint64_t)v < a.n ? a.keys[v] : 0u;
-    } else {
-        s = kInf;
-        k = 0;
-    }
+    const int64_t n = (int64_t)a.n;
+    const int64_t vo = v < 0 ? 0 : (v > n ? n : v);
+    const int64_t vk = v < 0 ? 0 : (v >= n ? (n > 0 ? n - 1 : 0) : v);
+    const uint64_t off = gptr(a.off)[vo];
+    const uint32_t key = gptr(a.keys)[vk];
+    s = v < 0 ? 0 : (v <= n ? off + a.mis : kInf);
+    k = (v >= 0 && v < n) ? key : 0u;
 }
 
 // issue the table loads (frames kb .. kb+63, one per lane) without waiting for them
@@ -156,7 +173,7 @@ __device__ int64_t locate(const Args& a, uint64_t P, int lane) {
         const int64_t base = g - 31 * kStride;
         const int64_t idx = base + (int64_t)lane * kStride;
         const bool valid = idx >= 0 && idx <= (int64_t)a.n;
-        const uint64_t val = valid ? a.off[idx] : 0;
+        const uint64_t val = valid ? gptr(a.off)[idx] : 0;
         const uint64_t le = __ballot(valid && val <= q);   // probes at or before q
         const uint64_t gt = __ballot(valid && val > q);    // probes after q
         if (le) {
@@ -175,7 +192,7 @@ __device__ int64_t locate(const Args& a, uint64_t P, int lane) {
         const int64_t step = (H - lo + kWave - 1) / kWave;   // probes lo, lo + step, ... cover [lo, H)
         const int64_t idx = lo + (int64_t)lane * step;
         const bool valid = idx < H;
-        const uint64_t val = valid ? a.off[idx] : kInf;
+        const uint64_t val = valid ? gptr(a.off)[idx] : kInf;
         const uint64_t le = __ballot(valid && val <= q);
         const uint64_t gt = __ballot(valid && val > q);
         if (le) L = lo + (int64_t)(63 - __builtin_clzll(le)) * step;
@@ -226,11 +243,11 @@ __device__ __forceinline__ u32x4 span_mask(const Args& a, Table& t, uint64_t A0,
 template <bool SRC_ALIGNED, bool NT>
 __device__ __forceinline__ u32x4 load_vec(const Args& a, uint64_t P) {
     if constexpr (SRC_ALIGNED) {
-        const u32x4* p = reinterpret_cast<const u32x4*>(a.src_base + P);
+        const NETC_GLOBAL u32x4* p = gptr(reinterpret_cast<const u32x4*>(a.src_base + P));
         if constexpr (NT) return __builtin_nontemporal_load(p);
         return *p;
     } else {
-        const uint8_t* p = a.src_base + P;
+        const NETC_GLOBAL uint8_t* p = gptr(a.src_base + P);
         u32x4 v;
 #pragma unroll
         for (int w = 0; w < 4; ++w)
@@ -242,7 +259,7 @@ __device__ __forceinline__ u32x4 load_vec(const Args& a, uint64_t P) {
 
 template <bool NT>
 __device__ __forceinline__ void store_vec(const Args& a, uint64_t P, u32x4 v) {
-    u32x4* p = reinterpret_cast<u32x4*>(a.dst_base + P);
+    NETC_GLOBAL u32x4* p = gptr(reinterpret_cast<u32x4*>(a.dst_base + P));
     if constexpr (NT) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
@@ -256,26 +273,62 @@ __device__ __forceinline__ void edge_vec(const Args& a, uint64_t P, u32x4 mask) 
         const uint64_t p = P + bi;
         if (p >= lo && p < hi) {
             const uint8_t mb = (uint8_t)(mask[bi >> 2] >> (8 * (bi & 3)));
-            a.dst_base[p] = a.src_base[p] ^ mb;
+            gptr(a.dst_base)[p] = gptr(a.src_base)[p] ^ mb;
         }
     }
 }
 
-// Chunk = one window of U spans (U KiB).  Wavefront w of W takes chunks w, w+W,
-// w+2W, ...: at any moment the resident wavefronts stream one compact region of
-// HBM (the order a grid-stride copy has), which measured 10-14 % faster than
-// each wavefront walking its own contiguous share (tools/order_probe.py).
+// A chunk that holds one of the two partial 16-B vectors at the ends of an
+// unaligned buffer (at most three chunks per batch): per-vector range checks,
+// a fresh frame search, no prefetch.
+template <int U, bool SRC_ALIGNED, bool NT>
+__device__ __forceinline__ void edge_chunk(const Args& a, uint64_t A, int lane) {
+    constexpr uint64_t kWin = kSpan * U;
+    const uint64_t full_lo = a.mis ? 16 : 0;
+    const uint64_t full_hi = (a.mis + a.total) & ~15ull;
+    const uint64_t vec_end = (a.mis + a.total + 15) & ~15ull;
+    u32x4 d[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t P = A + (uint64_t)u * kSpan + 16ull * lane;
+        if (P >= full_lo && P < full_hi) d[u] = load_vec<SRC_ALIGNED, NT>(a, P);
+    }
+    Table t;
+    table_load(a, t, locate(a, A, lane), lane);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t A0 = A + (uint64_t)u * kSpan;
+        if (A0 >= vec_end) break;                                   // wave-uniform
+        const u32x4 m = span_mask(a, t, A0, lane);
+        const uint64_t P = A0 + 16ull * lane;
+        if (P >= full_lo && P < full_hi) store_vec<NT>(a, P, d[u] ^ m);
+        else if (P < vec_end) edge_vec(a, P, m);
+    }
+    (void)kWin;
+}
+
+// Chunk = U spans (U KiB).  Wavefront w of W takes chunks w, w+W, w+2W, ...: at
+// any moment the resident wavefronts stream one compact region of HBM (the
+// order a grid-stride copy has), 10-14 % faster than each wavefront walking its
+// own contiguous share (tools/order_probe.py).  Giving each XCD (blocks
+// b % 8 == x) its own contiguous eighth of the chunks -- so its L2 would fetch
+// only an eighth of the frame descriptors -- measured 7 % slower.
+//
 // Software pipeline per wavefront: the NEXT chunk's payload loads and its frame
-// table probe are in flight while the current chunk is masked and stored.  The
-// probe is a table load at a guessed base (exact for evenly sized frames); a
-// miss falls back to the search in locate().
+// table load are in flight while the current chunk is masked and stored.  The
+// interior chunks (every vector full) run a straight-line body: unconditional
+// loads / stores, the prefetch issued every trip (the last chunk is peeled), so
+// the compiler waits with counted vmcnt(N) and the prefetch stays in flight.  The
+// table base of the next chunk is guessed from the frame known to hold this one
+// (exact for evenly sized frames); a miss falls back to locate().  The <= 3
+// partial chunks at the buffer ends go through edge_chunk().
 template <int U, bool SRC_ALIGNED, bool NT>
 __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) {
+    constexpr uint64_t kWin = kSpan * U;
     const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / kWave);
-    uint64_t c = wave;
-    if (c >= a.nwin) return;
+    const uint32_t wpb = blockDim.x / kWave;                     // wavefronts per block
+    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
+    const uint64_t wave = (uint64_t)blockIdx.x * wpb + (threadIdx.x / kWave);
 #ifdef NETC_MASK_STAMPS
     // diagnostic build only (tools/): per-wave start / end wall clock (100 MHz)
     const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
@@ -290,17 +343,38 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
     } stamp_guard{wave, stamp0};
 #endif
 
-    constexpr uint64_t kWin = kSpan * U;
-    const uint64_t full_lo = a.mis ? 16 : 0;                       // first full vector's P
-    const uint64_t full_hi = (a.mis + a.total) & ~15ull;           // end of the last full vector
-    const uint64_t vec_end = (a.mis + a.total + 15) & ~15ull;      // end of the last vector
+    // interior chunks [ci_lo, ci_hi): every 16-B vector inside the buffer
+    const uint64_t full_hi = (a.mis + a.total) & ~15ull;
+    const uint64_t ci_lo = a.mis ? 1 : 0;
+    uint64_t ci_hi = full_hi / kWin;
+    if (ci_hi < ci_lo) ci_hi = ci_lo;
+    // edge chunks: chunk 0 when the buffer start is unaligned, and [ci_hi, nwin)
+    if (a.mis && wave == 0) edge_chunk<U, SRC_ALIGNED, NT>(a, 0, lane);
+    for (uint64_t e = ci_hi; e < a.nwin; ++e)
+        if (e % nwaves == (wave + 1) % nwaves) edge_chunk<U, SRC_ALIGNED, NT>(a, e * kWin, lane);
+
+    uint64_t c = ci_lo + wave;
+    if (c >= ci_hi) return;
 
     auto load_window = [&](u32x4 (&dst)[U], uint64_t base) {
 #pragma unroll
+        for (int u = 0; u < U; ++u) dst[u] = load_vec<SRC_ALIGNED, NT>(a, base + (uint64_t)u * kSpan + 16ull * lane);
+    };
+    auto process = [&](const u32x4 (&src)[U], Table& t, uint64_t base) {
+#pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t P = base + (uint64_t)u * kSpan + 16ull * lane;
-            if (P >= full_lo && P < full_hi) dst[u] = load_vec<SRC_ALIGNED, NT>(a, P);
+            const uint64_t A0 = base + (uint64_t)u * kSpan;
+            const u32x4 m = span_mask(a, t, A0, lane);
+            store_vec<NT>(a, A0 + 16ull * lane, src[u] ^ m);
         }
+    };
+    // make t hold the frame containing A (its probe was issued a chunk ago)
+    auto resolve = [&](Table& t, uint64_t A, int64_t& f0, uint64_t& s0) {
+        table_finish(t);
+        if (!table_brackets(t, A)) table_load(a, t, locate(a, A, lane), lane);
+        const int j0 = __popcll(__ballot(t.start <= A)) - 1;
+        f0 = t.kb + j0;
+        s0 = readlane64(t.start, j0);
     };
 
     u32x4 d[U];
@@ -309,45 +383,25 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
     Table t;
     table_issue(a, t, guess_base(a, 0, a.mis, A), lane);   // global guess: frame 0 starts near P = mis
 
-    for (;;) {
-        // resolve this chunk's table (its probe was issued one chunk ago)
-        table_finish(t);
-        if (!table_brackets(t, A)) table_load(a, t, locate(a, A, lane), lane);
-        const uint64_t m0 = __ballot(t.start <= A);
-        const int j0 = __popcll(m0) - 1;
-        const int64_t f0 = t.kb + j0;
-        const uint64_t s0 = readlane64(t.start, j0);
-
-        // prefetch the next chunk: payload loads + table probe guessed from f0
-        const uint64_t cn = c + nwaves;
-        const bool more = cn < a.nwin;
+    for (uint64_t cn = c + nwaves; cn < ci_hi; cn += nwaves) {
+        int64_t f0;
+        uint64_t s0;
+        resolve(t, A, f0, s0);
         const uint64_t An = cn * kWin;
         u32x4 dn[U];
+        load_window(dn, An);
         Table tn;
-        if (more) {
-            load_window(dn, An);
-            table_issue(a, tn, guess_base(a, f0, s0, An), lane);
-        }
-
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t A0 = A + (uint64_t)u * kSpan;
-            if (A0 >= vec_end) break;                               // wave-uniform
-            const u32x4 m = span_mask(a, t, A0, lane);
-            const uint64_t P = A0 + 16ull * lane;
-            if (P >= full_lo && P < full_hi) {
-                store_vec<NT>(a, P, d[u] ^ m);
-            } else if (P < vec_end) {
-                edge_vec(a, P, m);
-            }
-        }
-        if (!more) break;
-        c = cn;
+        table_issue(a, tn, guess_base(a, f0, s0, An), lane);
+        process(d, t, A);
         A = An;
         t = tn;
 #pragma unroll
         for (int u = 0; u < U; ++u) d[u] = dn[u];
     }
+    int64_t f0;
+    uint64_t s0;
+    resolve(t, A, f0, s0);
+    process(d, t, A);
 }
 
 }  // namespace netc_gpu
@@ -396,7 +450,7 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
     a.src_base = src - a.mis;
     a.total = total;
     a.off = off;
-    a.keys = keys;
+    a.keys = n ? keys : reinterpret_cast<const uint32_t*>(off);   // frame_entry always reads keys[0]
     a.n = n;
     const bool aligned = (((uintptr_t)src ^ (uintptr_t)dst) & 15u) == 0;
     const int U = aligned ? cfg.unroll : 4;
