@@ -286,6 +286,8 @@ def main():
     pipelined = None
     if args.pipelined_probe:
         s2 = [stream, torch.cuda.Stream(device)]
+        for i in range(max(4, args.warmup)):      # first use of a stream pays a one-off set-up (~6 ms)
+            step(i, s2[i % 2].cuda_stream)
         torch.cuda.synchronize(device)
         if world > 1:
             torch.distributed.barrier()
