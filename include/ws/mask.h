@@ -94,16 +94,16 @@ int netc_gpu_init(int device);
 
 /**
  * Process-wide launch shape of the batch kernel (defaults: 4, 0, AUTO).
- * unroll: KiB each wavefront moves per loop trip (1, 2, 4 or 8); max_blocks:
- * cap on 256-thread workgroups, 0 = exactly the workgroups the device holds
- * at once (each wavefront walks an equal contiguous run); flags:
- * NETC_GPU_TUNE_AUTO (chosen per batch size) or an OR of the bits below.
- * Call before launching work; it is not synchronised with concurrent launches.
+ * unroll: KiB per chunk, the unit a wavefront masks per loop trip (1, 2, 4 or
+ * 8); max_blocks: cap on 256-thread workgroups, 0 = exactly the workgroups the
+ * device holds at once; flags: NETC_GPU_TUNE_AUTO (non-temporal payload stream)
+ * or 0 (plain loads / stores) or NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES
+ * (either bit selects the non-temporal stream).  Diagnostic knob: call before
+ * launching work; it is not synchronised with concurrent launches.
  */
 #define NETC_GPU_TUNE_AUTO     -1
 #define NETC_GPU_TUNE_NT_LOADS  1   /* non-temporal payload loads  */
 #define NETC_GPU_TUNE_NT_STORES 2   /* non-temporal payload stores */
-#define NETC_GPU_TUNE_PIPELINE  4   /* keep the next window's loads in flight while storing */
 int netc_gpu_tune(int unroll, int max_blocks, int flags);
 
 /** Message for the last failing netc_gpu_* call on this thread ("" if none). */

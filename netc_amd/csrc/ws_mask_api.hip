@@ -110,7 +110,7 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags) {
         return fail(NETC_GPU_EINVAL, "unroll must be 1, 2, 4 or 8 (got %d)", unroll);
     if (max_blocks < 0 || max_blocks > (1 << 24)) return fail(NETC_GPU_EINVAL, "max_blocks out of range");
     if (flags != NETC_GPU_TUNE_AUTO &&
-        (flags & ~(NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES | NETC_GPU_TUNE_PIPELINE)))
+        (flags & ~(NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES)))
         return fail(NETC_GPU_EINVAL, "unknown tune flags");
     g_cfg.unroll = unroll;
     g_cfg.max_blocks = max_blocks;

@@ -21,12 +21,12 @@ struct Args {
     double density;            // n / total: frames per payload byte (table-base guesses)
 };
 
-enum : int { kNtLoads = 1, kNtStores = 2, kPipe = 4 };   // LaunchCfg::flags (NETC_GPU_TUNE_*)
+enum : int { kNtLoads = 1, kNtStores = 2 };   // LaunchCfg::flags (NETC_GPU_TUNE_NT_*)
 
 struct LaunchCfg {
     int unroll = 4;            // U: 1 KiB spans per window (1, 2, 4, 8)
     int max_blocks = 0;        // cap on 256-thread workgroups; 0 = one resident round (occupancy x CUs)
-    int flags = -1;            // kNtLoads | kNtStores | kPipe; -1 = chosen per batch (launch_mask_frames)
+    int flags = -1;            // -1 (auto) or kNtLoads | kNtStores: non-temporal payload stream; 0 = plain
 };
 
 hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,

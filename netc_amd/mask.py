@@ -95,7 +95,6 @@ NETC_GPU_TUNE_NT_STORES = 2
 
 
 NETC_GPU_TUNE_AUTO = -1
-NETC_GPU_TUNE_PIPELINE = 4
 
 
 def tune(unroll: int = 4, max_blocks: int = 0, flags: int = NETC_GPU_TUNE_AUTO) -> None:

@@ -158,7 +158,7 @@ def test_one_huge_frame(torch_cuda):
 
 
 @pytest.mark.parametrize("unroll,max_blocks", [(1, 2048), (2, 64), (8, 0), (4, 1), (4, 100000), (4, 0)])
-@pytest.mark.parametrize("flags", [-1, 0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("flags", [-1, 0, 3])
 def test_launch_shapes(torch_cuda, unroll, max_blocks, flags):
     """Every kernel instantiation (U x cache-hint / pipeline flags x grid cap) is bit-exact."""
     try:
