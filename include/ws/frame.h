@@ -1,0 +1,75 @@
+#ifndef NETC_WS_FRAME_H
+#define NETC_WS_FRAME_H
+
+/*
+ * Send-side frame assembly for a batch of frames — the C-ABI of SURVEY.md §8(f)
+ * row 2, MI355X (gfx950) edition.
+ *
+ * The reference frames one message at a time (ws_send_message,
+ * src/ws/common.c:36-130): per frame it builds the 2-byte header (FIN | opcode,
+ * MASK | 7-bit length code, :55-67), the 16- or 64-bit big-endian extended
+ * length (:69-82), copies the payload and masks it (:96-107), and copies header,
+ * key and payload into one frame buffer (:112-119) before send().  This header
+ * turns that into ONE out-of-place device pass over a batch:
+ *
+ *   netc_ws_wire_size()       exact wire bytes of a batch (host)
+ *   netc_gpu_encode_frames()  headers + keys + masked payloads of every frame,
+ *                             back to back, into a device wire buffer
+ *
+ * Frames use the layout of include/ws/mask.h ("Frame layout", "Key packing"):
+ * frame k's payload is [offsets[k], offsets[k+1]) of the payload buffer.  Each
+ * frame also has its first header byte, header0[k] = FIN << 7 | RSV << 4 |
+ * opcode (e.g. 0x82 = final BINARY, 0x01 = first TEXT fragment, 0x80 = final
+ * continuation).  Header lengths follow the reference (:63): payloads of up to
+ * 125 bytes use the 7-bit code, up to 65535 the 16-bit form, longer the 64-bit
+ * form.  With masked != 0 every frame carries MASK and its 4 key bytes — also a
+ * frame with an empty payload (RFC 6455 §5.2; the reference omits the key
+ * there, defect B9 in DESIGN.md).  Errors as in include/ws/mask.h.
+ */
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/** Largest header (+ key) of one frame: 2 + 8 extended length + 4 key bytes. */
+#define NETC_WS_MAX_HEADER(masked) ((uint64_t)((masked) ? 14 : 10))
+
+/** Upper bound of the wire bytes of nframes frames holding total_bytes of payload. */
+#define NETC_WS_WIRE_BOUND(total_bytes, nframes, masked) \
+    ((uint64_t)(total_bytes) + (uint64_t)(nframes) * NETC_WS_MAX_HEADER(masked))
+
+/**
+ * Exact wire bytes of frames 0..nframes-1 (host offsets, nframes + 1 entries):
+ * the sum of header lengths and payload lengths.  Host only.
+ */
+uint64_t netc_ws_wire_size(const uint64_t *offsets, size_t nframes, int masked);
+
+/**
+ * Assemble the wire bytes of a device-resident batch of frames on `device`,
+ * asynchronously on `stream`.
+ *   d_wire            device output, wire_capacity bytes; must be at least
+ *                     NETC_WS_WIRE_BOUND(total_bytes, nframes, masked) and must
+ *                     not overlap the payload (out of place)
+ *   d_wire_offsets    device output, nframes + 1 uint64: frame k's header starts
+ *                     at wire byte d_wire_offsets[k]; d_wire_offsets[nframes] is
+ *                     the wire length
+ *   d_payload         device, total_bytes readable; frames as in mask.h
+ *   d_frame_offsets   device, nframes + 1 uint64
+ *   d_keys            device, nframes packed key32 words (ignored unless masked)
+ *   d_header0         device, nframes header bytes, or NULL for 0x82 (final BINARY)
+ * Wire bytes past d_wire_offsets[nframes] are not written.  Returns once the
+ * kernels are queued.
+ */
+int netc_gpu_encode_frames(int device, void *d_wire, size_t wire_capacity, uint64_t *d_wire_offsets,
+                           const void *d_payload, size_t total_bytes, const uint64_t *d_frame_offsets,
+                           const uint32_t *d_keys, const uint8_t *d_header0, size_t nframes, int masked,
+                           void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NETC_WS_FRAME_H */

@@ -44,6 +44,8 @@ def host() -> ctypes.CDLL:
             lib.netc_ws_mask.restype = None
             lib.netc_shard_frames.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]
             lib.netc_shard_frames.restype = ctypes.c_int
+            lib.netc_ws_wire_size.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+            lib.netc_ws_wire_size.restype = ctypes.c_uint64
             lib.ws_build_masking_key.argtypes = [ctypes.c_void_p]
             lib.ws_build_masking_key.restype = None
             lib.ws_build_message.argtypes = [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint64, ctypes.c_void_p]
@@ -85,5 +87,8 @@ def gpu() -> ctypes.CDLL:
             lib.netc_gpu_mask_stream_host.argtypes = [ctypes.c_int, vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t,
                                                       ctypes.c_size_t, ctypes.c_int]
             lib.netc_gpu_mask_stream_host.restype = ctypes.c_int
+            lib.netc_gpu_encode_frames.argtypes = [ctypes.c_int, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp, vp,
+                                                   vp, ctypes.c_size_t, ctypes.c_int, vp]
+            lib.netc_gpu_encode_frames.restype = ctypes.c_int
             _gpu = lib
         return _gpu

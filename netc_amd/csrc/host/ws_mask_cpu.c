@@ -11,6 +11,7 @@
  * same rotation because 8 is a multiple of the key period 4.
  */
 #include "../../../include/ws/mask.h"
+#include "../../../include/ws/frame.h"
 
 #include <stdint.h>
 #include <string.h>
@@ -73,4 +74,16 @@ int netc_shard_frames(const uint64_t *offsets, size_t nframes, size_t nshards, s
     }
     cuts[nshards] = nframes;
     return 0;
+}
+
+/* include/ws/frame.h: header lengths as src/ws/common.c:63,69-82 (+ 4 key bytes when masked) */
+uint64_t netc_ws_wire_size(const uint64_t *offsets, size_t nframes, int masked)
+{
+    uint64_t total = 0;
+    for (size_t k = 0; k < nframes; ++k)
+    {
+        const uint64_t len = offsets[k + 1] - offsets[k];
+        total += 2 + (len < 126 ? 0 : (len < 65536 ? 2 : 8)) + (masked ? 4 : 0) + len;
+    }
+    return total;
 }

@@ -14,6 +14,7 @@
 
 extern "C" {
 #include "../../include/ws/mask.h"
+#include "../../include/ws/frame.h"
 // netc's thread-local error side channel (include/utils/error.h:19-23, src/utils/error.c:5)
 extern __thread int netc_errno_reason;
 }
@@ -73,6 +74,12 @@ bool partial_overlap(const void* a, const void* b, size_t n) {
     const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
     if (x == y) return false;
     return x < y + n && y < x + n;
+}
+
+bool ranges_overlap(const void* a, size_t na, const void* b, size_t nb) {
+    const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+    if (na == 0 || nb == 0) return false;
+    return x < y + nb && y < x + na;
 }
 
 int mask_batch_on_current(void* d_dst, const void* d_src, size_t total, const uint64_t* d_off,
@@ -155,6 +162,36 @@ int netc_gpu_mask_batch_multi(int nshards, const int* devices, void* const* d_ds
             if (e != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipStreamSynchronize", e);
         }
     }
+    return 0;
+}
+
+int netc_gpu_encode_frames(int device, void* d_wire, size_t wire_capacity, uint64_t* d_wire_offsets,
+                           const void* d_payload, size_t total_bytes, const uint64_t* d_frame_offsets,
+                           const uint32_t* d_keys, const uint8_t* d_header0, size_t nframes, int masked,
+                           void* stream) {
+    if (int r = check_device(device)) return r;
+    if (!d_wire_offsets) return fail(NETC_GPU_EINVAL, "null wire offsets");
+    if (nframes && (!d_frame_offsets || !d_payload || !d_wire)) return fail(NETC_GPU_EINVAL, "null frame buffer");
+    if (masked && nframes && !d_keys) return fail(NETC_GPU_EINVAL, "masked frames need keys");
+    const uint64_t per = NETC_WS_MAX_HEADER(masked);
+    if (nframes > (UINT64_MAX - total_bytes) / per)
+        return fail(NETC_GPU_EINVAL, "wire size overflows (%zu frames)", nframes);
+    const uint64_t bound = NETC_WS_WIRE_BOUND(total_bytes, nframes, masked);
+    if (nframes && wire_capacity < bound)
+        return fail(NETC_GPU_EINVAL, "wire capacity %zu < bound %llu (payload + %llu B per frame)", wire_capacity,
+                    (unsigned long long)bound, (unsigned long long)per);
+    const size_t wo_bytes = (nframes + 1) * sizeof(uint64_t);
+    if (nframes && ranges_overlap(d_wire, bound, d_payload, total_bytes))
+        return fail(NETC_GPU_EINVAL, "wire and payload overlap (the assembly is out of place)");
+    if (nframes && (ranges_overlap(d_wire_offsets, wo_bytes, d_frame_offsets, wo_bytes) ||
+                    ranges_overlap(d_wire_offsets, wo_bytes, d_wire, bound)))
+        return fail(NETC_GPU_EINVAL, "wire offsets overlap the frame offsets or the wire");
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+    hipError_t e = netc_gpu::launch_encode_frames((uint8_t*)d_wire, bound, (const uint8_t*)d_payload, total_bytes,
+                                                  d_frame_offsets, d_keys, d_header0, nframes, masked != 0,
+                                                  d_wire_offsets, (hipStream_t)stream, g_cfg);
+    if (e != hipSuccess) return fail_hip(NETC_GPU_ELAUNCH, "frame assembly launch", e);
     return 0;
 }
 

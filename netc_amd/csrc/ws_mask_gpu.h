@@ -32,4 +32,11 @@ struct LaunchCfg {
 hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,
                               const uint32_t* keys, uint64_t n, hipStream_t stream, const LaunchCfg& cfg);
 
+// ws_frame_gpu.hip: wire offsets (n + 1 entries into wo), then the wire bytes of
+// every frame (header, key, masked payload) into wire.  wire_bound >= wo[n].
+hipError_t launch_wire_offsets(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream);
+hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_t* src, uint64_t src_total,
+                                const uint64_t* off, const uint32_t* keys, const uint8_t* b0, uint64_t n, bool masked,
+                                uint64_t* wo, hipStream_t stream, const LaunchCfg& cfg);
+
 }  // namespace netc_gpu

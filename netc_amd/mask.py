@@ -165,6 +165,52 @@ def mask_batch_multi(shards: Sequence[Tuple], streams: Optional[Sequence] = None
                                                 strs if streams else None, 1 if synchronize else 0))
 
 
+def wire_bound(total: int, nframes: int, masked: bool) -> int:
+    """NETC_WS_WIRE_BOUND: capacity netc_gpu_encode_frames needs for the wire buffer."""
+    return int(total) + int(nframes) * (14 if masked else 10)
+
+
+def wire_size(offsets: np.ndarray, masked: bool) -> int:
+    """netc_ws_wire_size: exact wire bytes of the frames described by host offsets."""
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    return int(_lib.host().netc_ws_wire_size(_ptr(off), off.size - 1, 1 if masked else 0))
+
+
+def encode_frames(wire, wire_offsets, src, offsets, keys=None, header0=None, masked: bool = True, stream=None,
+                  device: Optional[int] = None) -> None:
+    """netc_gpu_encode_frames: headers + keys + masked payloads of every frame into `wire` (device tensors).
+
+    wire: uint8, >= wire_bound(src.numel(), n, masked) bytes; wire_offsets: int64, n + 1 (output);
+    header0: uint8 per frame (FIN | RSV | opcode) or None for 0x82; keys: packed key32 (masked only).
+    """
+    import torch
+
+    n = offsets.numel() - 1
+    for name, t in (("wire", wire), ("wire_offsets", wire_offsets), ("src", src), ("offsets", offsets)):
+        if not isinstance(t, torch.Tensor) or not t.is_cuda or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous device tensor")
+    if wire.dtype != torch.uint8 or src.dtype != torch.uint8:
+        raise TypeError("wire and src must be uint8")
+    if offsets.dtype not in (torch.int64, torch.uint64) or wire_offsets.dtype not in (torch.int64, torch.uint64):
+        raise TypeError("offsets and wire_offsets must be int64")
+    if wire_offsets.numel() != n + 1:
+        raise ValueError("wire_offsets must have nframes + 1 entries")
+    kp = 0
+    if masked:
+        if keys is None or keys.numel() != n or keys.dtype not in (torch.int32, torch.uint32):
+            raise ValueError("masked frames need nframes int32 keys")
+        kp = keys.data_ptr()
+    hp = 0
+    if header0 is not None:
+        if header0.numel() != n or header0.dtype != torch.uint8:
+            raise ValueError("header0 must be nframes uint8")
+        hp = header0.data_ptr()
+    dev = src.device.index if device is None else device
+    _check(_lib.gpu().netc_gpu_encode_frames(dev, wire.data_ptr(), wire.numel(), wire_offsets.data_ptr(),
+                                             src.data_ptr(), src.numel(), offsets.data_ptr(), kp, hp, n,
+                                             1 if masked else 0, _stream_handle(stream)))
+
+
 def mask_stream_host(dst: np.ndarray, src: np.ndarray, offsets: np.ndarray, keys: np.ndarray,
                      slot_bytes: int = 256 << 20, nslots: int = 4, device: int = 0) -> None:
     """netc_gpu_mask_stream_host: host buffers through pinned slots on overlapped streams."""

@@ -39,6 +39,8 @@ def _load(name: str) -> ctypes.CDLL:
             lib.oracle_build_masking_key.argtypes = [vp, vp]
             lib.oracle_encode_frame.argtypes = [vp, ctypes.c_int, ctypes.c_uint8, vp, ctypes.c_uint64, vp]
             lib.oracle_encode_frame.restype = sz
+            lib.oracle_encode_batch.argtypes = [vp, vp, vp, vp, vp, vp, sz, ctypes.c_int]
+            lib.oracle_encode_batch.restype = sz
             lib.oracle_decode_message.argtypes = [vp, sz, vp, sz, vp, vp]
             lib.oracle_decode_message.restype = sz
         else:
@@ -107,6 +109,21 @@ def encode_frame(payload: bytes, opcode: int, key: Optional[bytes], fin: bool = 
     k = np.frombuffer(bytes(key), dtype=np.uint8).copy() if key is not None else None
     n = lib().oracle_encode_frame(_p(out), 1 if fin else 0, opcode, _p(p), p.size, _p(k) if k is not None else None)
     return out[:n].tobytes()
+
+
+def encode_batch(payload, offsets: np.ndarray, keys32: Optional[np.ndarray], header0: Optional[np.ndarray] = None,
+                 masked: bool = True, opt: str = "O2") -> Tuple[np.ndarray, np.ndarray]:
+    """oracle_encode_batch: (wire bytes, n + 1 wire offsets) of a frame batch (include/ws/frame.h)."""
+    p = _u8(payload)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = off.size - 1
+    k = np.ascontiguousarray(keys32, dtype=np.uint32) if masked else None
+    h = np.ascontiguousarray(header0, dtype=np.uint8) if header0 is not None else None
+    out = np.zeros(p.size + 14 * n + 1, dtype=np.uint8)
+    wo = np.zeros(n + 1, dtype=np.uint64)
+    w = lib(opt).oracle_encode_batch(_p(out), _p(wo), _p(p), _p(off), _p(k) if k is not None else None,
+                                     _p(h) if h is not None else None, n, 1 if masked else 0)
+    return out[:w], wo
 
 
 def decode_message(wire: bytes, cap: Optional[int] = None) -> Tuple[int, bytes, int]:

@@ -100,6 +100,39 @@ size_t oracle_encode_frame(uint8_t *out, int fin, uint8_t opcode, const uint8_t 
 }
 
 /*
+ * A batch of frames as include/ws/frame.h describes it: frame k is payload
+ * [off[k], off[k+1]) with first header byte header0[k] (FIN | RSV | opcode) and,
+ * when masked, key32 keys[k]; each frame is oracle_encode_frame (the reference's
+ * single-frame send, src/ws/common.c:53-125) and the frames are concatenated.
+ * One deliberate deviation, defect B9: a masked frame with an
+ * empty payload still carries its 4 key bytes (RFC 6455 §5.2); the reference
+ * sets MASK but omits the key (:84-89,119).  wire_off receives n + 1 offsets.
+ * Returns the wire length.
+ */
+size_t oracle_encode_batch(uint8_t *out, uint64_t *wire_off, const uint8_t *payload, const uint64_t *off,
+                           const uint32_t *keys, const uint8_t *header0, size_t nframes, int masked)
+{
+    size_t w = 0;
+    for (size_t k = 0; k < nframes; ++k)
+    {
+        const uint8_t b0 = header0 ? header0[k] : 0x82;
+        const uint8_t key[4] = {(uint8_t)(masked ? keys[k] : 0), (uint8_t)(masked ? keys[k] >> 8 : 0),
+                                (uint8_t)(masked ? keys[k] >> 16 : 0), (uint8_t)(masked ? keys[k] >> 24 : 0)};
+        const uint64_t len = off[k + 1] - off[k];
+        wire_off[k] = w;
+        w += oracle_encode_frame(out + w, b0 >> 7, (uint8_t)(b0 & 0x7F), payload + off[k], len,
+                                 masked ? key : NULL);
+        if (masked && len == 0)
+        {
+            memcpy(out + w, key, 4); /* B9: the key follows MASK */
+            w += 4;
+        }
+    }
+    wire_off[nframes] = w;
+    return w;
+}
+
+/*
  * src/ws/common.c:146-347 as a pure function over a complete byte stream:
  * decodes frames until one with FIN completes a message.  On success returns
  * the wire bytes consumed and writes the message (payload bytes, unmasked, no

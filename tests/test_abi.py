@@ -39,7 +39,8 @@ def exported(path):
 
 def test_every_declared_symbol_is_exported():
     decl = declared_functions()
-    assert {"netc_ws_mask", "netc_gpu_mask_batch", "ws_parse_frame", "ws_send_message"} <= decl
+    assert {"netc_ws_mask", "netc_gpu_mask_batch", "ws_parse_frame", "ws_send_message", "netc_gpu_encode_frames",
+            "netc_ws_wire_size"} <= decl
     have = exported(_lib.HOST_LIB) | exported(_lib.GPU_LIB)
     missing = sorted(decl - have)
     assert not missing, f"declared but not exported: {missing}"

@@ -1,0 +1,202 @@
+"""GPU parity: netc_gpu_encode_frames (send-side frame assembly, include/ws/frame.h) vs the oracle.
+
+The oracle (oracle_encode_batch) concatenates the reference's single-frame send
+(src/ws/common.c:53-125: header, extended length, key, payload masked with
+:104-107), with the key kept on empty masked frames (defect B9).  The bar: the
+wire bytes and wire offsets are bit-exact, and no byte past the wire length (or
+before the wire start) is written.
+"""
+
+import numpy as np
+import pytest
+
+from netc_amd import mask as nm
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+GUARD = 64
+SENTINEL = 0xEE
+
+
+def _dev(torch, a: np.ndarray):
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint64:
+        a = a.view(np.int64)
+    elif a.dtype == np.uint32:
+        a = a.view(np.int32)
+    return torch.from_numpy(a).cuda()
+
+
+def frames_from_sizes(sizes, start=0):
+    off = np.zeros(len(sizes) + 1, dtype=np.uint64)
+    off[0] = start
+    off[1:] = start + np.cumsum(np.asarray(sizes, dtype=np.uint64))
+    return off
+
+
+def run_encode(torch, payload, off, keys, header0=None, masked=True, wire_shift=0, src_shift=0, check=True):
+    total = payload.size
+    n = off.size - 1
+    src_buf = torch.full((total + 2 * GUARD,), 0x5A, dtype=torch.uint8, device="cuda")
+    src = src_buf[GUARD + src_shift: GUARD + src_shift + total]
+    src.copy_(torch.from_numpy(payload))
+    cap = nm.wire_bound(total, n, masked)
+    wire_buf = torch.full((cap + 2 * GUARD,), SENTINEL, dtype=torch.uint8, device="cuda")
+    wire = wire_buf[GUARD + wire_shift: GUARD + wire_shift + cap]
+    wo = torch.full((n + 1,), -1, dtype=torch.int64, device="cuda")
+    keys_t = _dev(torch, np.asarray(keys, dtype=np.uint32)) if masked else None
+    h_t = torch.from_numpy(np.ascontiguousarray(header0, dtype=np.uint8)).cuda() if header0 is not None else None
+    nm.encode_frames(wire, wo, src, _dev(torch, off), keys_t, h_t, masked=masked)
+    torch.cuda.synchronize()
+    exp_wire, exp_wo = orc.encode_batch(payload, off, keys if masked else None, header0, masked)
+    got_wo = wo.cpu().numpy().view(np.uint64)
+    assert np.array_equal(got_wo, exp_wo), f"wire offsets differ (first at {np.nonzero(got_wo != exp_wo)[0][:4]})"
+    assert int(exp_wo[-1]) == nm.wire_size(off, masked)
+    whole = wire_buf.cpu().numpy()
+    lo = GUARD + wire_shift
+    got = whole[lo: lo + exp_wire.size]
+    if check and not np.array_equal(got, exp_wire):
+        bad = np.nonzero(got != exp_wire)[0]
+        raise AssertionError(f"{bad.size} wire bytes differ, first at {bad[:8].tolist()} (n={n}, total={total}, "
+                             f"masked={masked}, shifts={wire_shift},{src_shift})")
+    assert (whole[:lo] == SENTINEL).all(), "write before the wire start"
+    assert (whole[lo + exp_wire.size:] == SENTINEL).all(), "write past the wire length"
+    return exp_wire
+
+
+EDGE_SIZES = [0, 1, 2, 3, 4, 5, 15, 16, 17, 124, 125, 126, 127, 128, 1000, 1023, 1024, 1025, 4096, 65535, 65536,
+              65537, 70000]
+
+
+def _payload(rng, n):
+    return rng.integers(0, 256, n, dtype=np.uint8)
+
+
+@pytest.mark.parametrize("masked", [True, False])
+def test_every_length_class(torch_cuda, masked):
+    rng = np.random.default_rng(11)
+    sizes = EDGE_SIZES + EDGE_SIZES[::-1]
+    off = frames_from_sizes(sizes)
+    payload = _payload(rng, int(off[-1]))
+    keys = rng.integers(0, 2**32, len(sizes), dtype=np.uint64).astype(np.uint32)
+    keys[:3] = [0, 0xFFFFFFFF, 0x00FF00FF]
+    run_encode(torch_cuda, payload, off, keys, masked=masked)
+
+
+@pytest.mark.parametrize("wire_shift", [0, 1, 3, 7, 8, 13, 15])
+@pytest.mark.parametrize("src_shift", [0, 5, 12])
+def test_alignments(torch_cuda, wire_shift, src_shift):
+    rng = np.random.default_rng(100 + wire_shift * 16 + src_shift)
+    sizes = rng.integers(0, 3000, 300)
+    off = frames_from_sizes(sizes)
+    payload = _payload(rng, int(off[-1]))
+    keys = rng.integers(0, 2**32, len(sizes), dtype=np.uint64).astype(np.uint32)
+    run_encode(torch_cuda, payload, off, keys, wire_shift=wire_shift, src_shift=src_shift)
+
+
+def test_header_bytes_and_fragmented_message(torch_cuda):
+    # one TEXT message in 4 fragments + a PING + a BINARY message: first-byte variants
+    rng = np.random.default_rng(5)
+    sizes = [300, 300, 300, 301, 0, 125, 70000]
+    header0 = np.array([0x01, 0x00, 0x00, 0x80, 0x89, 0x8A, 0x82], dtype=np.uint8)
+    off = frames_from_sizes(sizes)
+    payload = _payload(rng, int(off[-1]))
+    keys = rng.integers(0, 2**32, len(sizes), dtype=np.uint64).astype(np.uint32)
+    wire = run_encode(torch_cuda, payload, off, keys, header0=header0)
+    # the reference's receive path (oracle restatement of src/ws/common.c:146-347) decodes the message back
+    used, msg, opcode = orc.decode_message(wire.tobytes())
+    assert opcode == 1 and msg == payload[:1201].tobytes()
+
+
+def test_tiny_frames_many_per_span(torch_cuda):
+    # > 63 frame starts inside one 1 KiB span: the frame table slides mid-span
+    rng = np.random.default_rng(9)
+    sizes = rng.integers(0, 4, 5000)
+    off = frames_from_sizes(sizes)
+    payload = _payload(rng, int(off[-1]))
+    keys = rng.integers(0, 2**32, len(sizes), dtype=np.uint64).astype(np.uint32)
+    for masked in (True, False):
+        run_encode(torch_cuda, payload, off, keys, masked=masked, wire_shift=3)
+
+
+def test_payload_with_unframed_prefix(torch_cuda):
+    # frames need not start at payload byte 0: off[0] > 0 (bytes before it are not sent)
+    rng = np.random.default_rng(12)
+    sizes = rng.integers(0, 2000, 50)
+    off = frames_from_sizes(sizes, start=777)
+    payload = _payload(rng, int(off[-1]) + 100)
+    keys = rng.integers(0, 2**32, len(sizes), dtype=np.uint64).astype(np.uint32)
+    run_encode(torch_cuda, payload, off, keys)
+
+
+def test_single_frame_sizes(torch_cuda):
+    rng = np.random.default_rng(13)
+    for size in (0, 1, 17, 125, 126, 1024, 65535, 65536, 1 << 20):
+        off = frames_from_sizes([size])
+        payload = _payload(rng, size)
+        keys = np.array([0x3D21FA37], dtype=np.uint32)
+        run_encode(torch_cuda, payload, off, keys)
+
+
+def test_rfc6455_hello(torch_cuda):
+    # RFC 6455 §5.7: a single-frame masked text message "Hello" with key 37 fa 21 3d
+    torch = torch_cuda
+    payload = np.frombuffer(b"Hello", dtype=np.uint8).copy()
+    off = frames_from_sizes([5])
+    keys = nm.pack_keys(np.frombuffer(bytes.fromhex("37fa213d"), dtype=np.uint8))
+    wire = run_encode(torch, payload, off, keys, header0=np.array([0x81], dtype=np.uint8))
+    assert wire.tobytes() == bytes.fromhex("818537fa213d7f9f4d5158")
+    # and unmasked: 0x81 0x05 "Hello"
+    wire = run_encode(torch, payload, off, keys, header0=np.array([0x81], dtype=np.uint8), masked=False)
+    assert wire.tobytes() == bytes.fromhex("810548656c6c6f")
+
+
+def test_empty_batch(torch_cuda):
+    torch = torch_cuda
+    wo = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+    wire = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    src = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    off = torch.zeros(1, dtype=torch.int64, device="cuda")
+    keys = torch.zeros(0, dtype=torch.int32, device="cuda")
+    nm.encode_frames(wire, wo, src, off, keys)
+    torch.cuda.synchronize()
+    assert int(wo.cpu()[0]) == 0
+
+
+def test_c2_full_size(torch_cuda):
+    # config 2 shape: 65,536 x 1 KiB frames, independent keys
+    rng = np.random.default_rng(0x6E657463)
+    n = 65536
+    off = frames_from_sizes(np.full(n, 1024))
+    payload = _payload(rng, int(off[-1]))
+    keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    run_encode(torch_cuda, payload, off, keys)
+
+
+def test_mixed_64mib(torch_cuda):
+    # config 4 shape (sizes uniform in [256, 65536], unaligned), 64 MiB
+    rng = np.random.default_rng(44)
+    sizes = rng.integers(256, 65537, 4096)
+    off = frames_from_sizes(sizes)
+    payload = _payload(rng, int(off[-1]))
+    keys = rng.integers(0, 2**32, sizes.size, dtype=np.uint64).astype(np.uint32)
+    run_encode(torch_cuda, payload, off, keys, wire_shift=5, src_shift=3)
+
+
+def test_errors(torch_cuda):
+    torch = torch_cuda
+    src = torch.zeros(1000, dtype=torch.uint8, device="cuda")
+    off = torch.tensor([0, 500, 1000], dtype=torch.int64, device="cuda")
+    keys = torch.zeros(2, dtype=torch.int32, device="cuda")
+    wo = torch.zeros(3, dtype=torch.int64, device="cuda")
+    small = torch.zeros(1000 + 27, dtype=torch.uint8, device="cuda")   # bound is 1000 + 2 * 14
+    with pytest.raises(nm.NetcGpuError) as e:
+        nm.encode_frames(small, wo, src, off, keys)
+    assert e.value.code == nm.NETC_GPU_EINVAL
+    big = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    with pytest.raises(nm.NetcGpuError) as e:   # wire overlapping the payload
+        nm.encode_frames(big, wo, big[100:1100], off, keys)
+    assert e.value.code == nm.NETC_GPU_EINVAL
+    with pytest.raises(ValueError):
+        nm.encode_frames(big, wo, src, off, None, masked=True)

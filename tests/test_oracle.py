@@ -60,6 +60,29 @@ def test_encoder_matches_reference_sender(case):
     assert wire_matches(case["wire"], orc.encode_frame(p, case["opcode"], key))
 
 
+@pytest.mark.parametrize("masked", [True, False])
+def test_batch_encoder_matches_reference_sender(masked):
+    # oracle_encode_batch (the checker of netc_gpu_encode_frames) over every golden
+    # single-frame send of one kind, concatenated: each frame's slice of the batch
+    # wire equals the reference's wire for that frame (B9: an empty masked frame
+    # additionally carries its key, which the reference omits)
+    cases = [c for c in GOLDEN["send_single_frame"] if bool(c["key"]) == masked]
+    assert cases
+    payloads = [payload_of(c["payload"]) for c in cases]
+    off = np.zeros(len(cases) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(p) for p in payloads])
+    keys = np.array([int.from_bytes(bytes.fromhex(c["key"]), "little") if c["key"] else 0 for c in cases],
+                    dtype=np.uint32)
+    header0 = np.array([0x80 | c["opcode"] for c in cases], dtype=np.uint8)
+    wire, wo = orc.encode_batch(b"".join(payloads), off, keys, header0, masked)
+    for k, c in enumerate(cases):
+        w = wire[int(wo[k]): int(wo[k + 1])].tobytes()
+        if masked and not payloads[k]:
+            assert w[2:] == bytes.fromhex(c["key"])
+            w = w[:2]
+        assert wire_matches(c["wire"], w), c["name"]
+
+
 @pytest.mark.parametrize("case", GOLDEN["receive"], ids=lambda c: f"{len(payload_of(c['payload']))}B-{c['key']}")
 def test_decoder_matches_reference_receiver(case):
     p = payload_of(case["payload"])
