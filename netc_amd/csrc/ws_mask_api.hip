@@ -117,7 +117,8 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags) {
         return fail(NETC_GPU_EINVAL, "unroll must be 1, 2, 4 or 8 (got %d)", unroll);
     if (max_blocks < 0 || max_blocks > (1 << 24)) return fail(NETC_GPU_EINVAL, "max_blocks out of range");
     if (flags != NETC_GPU_TUNE_AUTO &&
-        (flags & ~(NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES)))
+        ((flags & ~(NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES | NETC_GPU_TUNE_TABLE64 | NETC_GPU_TUNE_TABLE16)) ||
+         (flags & NETC_GPU_TUNE_TABLE64 && flags & NETC_GPU_TUNE_TABLE16)))
         return fail(NETC_GPU_EINVAL, "unknown tune flags");
     g_cfg.unroll = unroll;
     g_cfg.max_blocks = max_blocks;

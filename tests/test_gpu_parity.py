@@ -158,15 +158,39 @@ def test_one_huge_frame(torch_cuda):
 
 
 @pytest.mark.parametrize("unroll,max_blocks", [(1, 2048), (2, 64), (8, 0), (4, 1), (4, 100000), (4, 0)])
-@pytest.mark.parametrize("flags", [-1, 0, 3])
+@pytest.mark.parametrize("flags", [-1, 0, 3, 3 | 4, 3 | 8])
 def test_launch_shapes(torch_cuda, unroll, max_blocks, flags):
-    """Every kernel instantiation (U x cache-hint / pipeline flags x grid cap) is bit-exact."""
+    """Every kernel instantiation (U x cache-hint flags x table size x grid cap) is bit-exact."""
     try:
         nm.tune(unroll, max_blocks, flags)
         off = synth.mixed_offsets(5 << 20, 1, 9000, seed=13)
         payload = synth.host_payload(int(off[-1]), 13)
         run_case(torch_cuda, payload, off, synth.random_keys(off.size - 1, 13), 4, 4)
         run_case(torch_cuda, payload, off, synth.random_keys(off.size - 1, 14), 4, 9)   # src misaligned vs dst
+    finally:
+        nm.tune()
+
+
+@pytest.mark.parametrize("flags", [-1, 3 | 8])
+def test_near_uniform_frames(torch_cuda, flags):
+    """Evenly sized frames with sparse irregular ones: the adaptive frame table drops to
+    16 entries while guesses are exact and must recover (64 entries / locate) after
+    each irregular frame shifts every later frame start."""
+    try:
+        nm.tune(4, 0, flags)
+        rng = np.random.default_rng(21)
+        sizes = np.full(40000, 1024, dtype=np.int64)
+        irregular = rng.choice(sizes.size, 40, replace=False)
+        sizes[irregular] = rng.integers(0, 20000, irregular.size)
+        off = frames_from_sizes(sizes)
+        payload = synth.host_payload(int(off[-1]), 21)
+        run_case(torch_cuda, payload, off, synth.random_keys(sizes.size, 21))
+        run_case(torch_cuda, payload, off, synth.random_keys(sizes.size, 22), 3, 3)
+        # dense frames (many per chunk): the 16-entry table slides within a span
+        sizes = np.full(30000, 40, dtype=np.int64)
+        off = frames_from_sizes(sizes)
+        payload = synth.host_payload(int(off[-1]), 23)
+        run_case(torch_cuda, payload, off, synth.random_keys(sizes.size, 23))
     finally:
         nm.tune()
 

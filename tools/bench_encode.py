@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Send-side frame assembly (netc_gpu_encode_frames) throughput, one GPU.
+
+Per step: the wire-offset scan + the assembly kernel over one batch (configs 2 and 4
+shapes: 65,536 x 1 KiB, and 1 GiB of 256 B..64 KiB frames), masked.  Algorithmic
+bytes = payload read + wire written (+ 8 B/frame offsets read, + 8 B/frame wire
+offsets written, reported, not counted).  GPU time from two events around K steps
+on one stream; batches rotate over >= 1 GiB of distinct payload.  One JSON line per
+workload.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workloads", default="c2,c4")
+    args = ap.parse_args()
+
+    import torch
+
+    from netc_amd import _lib, synth
+    from netc_amd import mask as nm
+
+    dev = torch.device("cuda", 0)
+    entry = _lib.gpu().netc_gpu_encode_frames
+    s = torch.cuda.Stream(dev)
+    sh = s.cuda_stream
+    for wl in args.workloads.split(","):
+        off, keys, total = synth.config(wl)
+        n = keys.size
+        nb = max(2, (1 << 30) // total)
+        srcs = [torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev) for _ in range(nb)]
+        cap = nm.wire_bound(total, n, True)
+        wires = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(2)]
+        wo = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        off_t = torch.from_numpy(off.view(np.int64)).to(dev)
+        keys_t = torch.from_numpy(keys.view(np.int32)).to(dev)
+        wire_len = nm.wire_size(off, True)
+        torch.cuda.synchronize()
+
+        def step(i):
+            rc = entry(0, wires[i % 2].data_ptr(), cap, wo.data_ptr(), srcs[i % nb].data_ptr(), total,
+                       off_t.data_ptr(), keys_t.data_ptr(), None, n, 1, sh)
+            if rc:
+                raise RuntimeError(nm._lib.gpu().netc_gpu_strerror())
+
+        K = args.steps if wl == "c2" else max(10, args.steps // 5)
+        with torch.cuda.stream(s):
+            for i in range(args.warmup):
+                step(i)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            for i in range(K):
+                step(i)
+            b.record(s)
+        torch.cuda.synchronize()
+        us = a.elapsed_time(b) / K * 1e3
+        # spot check the last step against the oracle on a few frames
+        from oracle import oracle as orc
+
+        last = (K - 1 + args.warmup) % 2
+        wire = wires[last][:wire_len].cpu().numpy()
+        wo_h = wo.cpu().numpy().view(np.uint64)
+        src_h = srcs[(args.warmup + K - 1) % nb].cpu().numpy()
+        bad = 0
+        for k in np.linspace(0, n - 1, 16).astype(np.int64):
+            lo, hi = int(off[k]), int(off[k + 1])
+            exp = orc.encode_frame(src_h[lo:hi].tobytes(), 2, int(keys[k]).to_bytes(4, "little"))
+            bad += wire[int(wo_h[k]): int(wo_h[k + 1])].tobytes() != exp
+        alg = total + wire_len
+        print(json.dumps({"workload": wl, "frames": int(n), "payload_bytes": int(total), "wire_bytes": int(wire_len),
+                          "us_per_step": round(us, 2), "achieved_GBps": round(alg / (us * 1e-6) / 1e9, 1),
+                          "frac_of_8TBps": round(alg / (us * 1e-6) / 8e12, 4),
+                          "payload_GiBps": round(total / (us * 1e-6) / 2**30, 1),
+                          "sampled_frames_wrong": int(bad)}), flush=True)
+        del srcs, wires
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
