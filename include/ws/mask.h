@@ -98,16 +98,12 @@ int netc_gpu_init(int device);
  * 8); max_blocks: cap on 256-thread workgroups, 0 = exactly the workgroups the
  * device holds at once; flags: NETC_GPU_TUNE_AUTO (non-temporal payload stream)
  * or 0 (plain loads / stores) or NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES
- * (either bit selects the non-temporal stream), optionally with one
- * NETC_GPU_TUNE_TABLE* bit pinning the per-wavefront frame table to 64 or 16
- * entries (AUTO and no bit: adaptive).  Diagnostic knob: call before launching
- * work; it is not synchronised with concurrent launches.
+ * (either bit selects the non-temporal stream).  Diagnostic knob: call before
+ * launching work; it is not synchronised with concurrent launches.
  */
 #define NETC_GPU_TUNE_AUTO     -1
 #define NETC_GPU_TUNE_NT_LOADS  1   /* non-temporal payload loads  */
 #define NETC_GPU_TUNE_NT_STORES 2   /* non-temporal payload stores */
-#define NETC_GPU_TUNE_TABLE64   4   /* always a 64-entry frame table */
-#define NETC_GPU_TUNE_TABLE16   8   /* always a 16-entry frame table */
 int netc_gpu_tune(int unroll, int max_blocks, int flags);
 
 /** Message for the last failing netc_gpu_* call on this thread ("" if none). */

@@ -11,9 +11,8 @@
 // reference omits it there, defect B9 in DESIGN.md).
 //
 // Two steps on the caller's stream:
-//   1. wire offsets: wo[j] = sum over k < j of (header_len(k) + len(k)), a scan
-//      over the frames (three small kernels, no scratch memory: the block sums
-//      live in wo[] itself until the last kernel overwrites them);
+//   1. wire offsets: wo[j] = sum over k < j of (header_len(k) + len(k)), a
+//      single-pass chained scan over the frames (one kernel, decoupled look-back);
 //   2. the assembly kernel, output-driven: the wire buffer is walked in 16-byte
 //      vectors aligned to the destination, chunk by chunk in grid-stride order
 //      as in ws_mask_gpu.hip; a 64-entry frame table in VGPRs (wire start,
@@ -25,6 +24,10 @@
 //      every frame they touch.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "gpu_util.h"
 #include "ws_mask_gpu.h"
@@ -65,42 +68,26 @@ __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total) {
     return before + inc - v;
 }
 
-// 1. per block: sum of extended-length bytes of its frames -> wo[block * kScanBlock]
-__global__ __launch_bounds__(kScanThreads) void wire_block_sums(const uint64_t* off, uint64_t n, uint64_t* wo) {
-    const uint64_t base = (uint64_t)blockIdx.x * kScanBlock;
-    uint64_t s = 0;
-#pragma unroll
-    for (int i = 0; i < kScanPer; ++i) {
-        const uint64_t j = base + (uint64_t)i * kScanThreads + threadIdx.x;
-        if (j < n) s += ext_len(gptr(off)[j + 1] - gptr(off)[j]);
-    }
-    uint64_t total;
-    (void)block_exclusive_scan(s, &total);
-    if (threadIdx.x == 0) gptr(wo)[base] = total;
+// Single-pass chained scan (decoupled look-back).  Tile b = frames
+// [b kScanBlock, (b + 1) kScanBlock); tiles cover frames 0 .. n inclusive, so the
+// tile holding frame n writes wo[n].  Each tile publishes one 64-bit status word:
+//   [63:62] flag (1 = tile aggregate, 2 = inclusive prefix) | [61:46] epoch | [45:0] value
+// value = extended-length bytes (<= 8 per frame, so n < 2^43).  The epoch (one per
+// call, per device) makes words left over from earlier calls read as "not yet
+// published", so the status array is never cleared between calls.  A tile only
+// waits on lower-numbered tiles, which are dispatched first.
+static constexpr uint64_t kValBits = 46;
+static constexpr uint64_t kValMask = (1ull << kValBits) - 1;
+
+__device__ __forceinline__ uint64_t status_word(uint64_t flag, uint32_t epoch, uint64_t v) {
+    return flag << 62 | (uint64_t)(epoch & 0xFFFF) << kValBits | (v & kValMask);
 }
 
-// 2. one block: exclusive scan of the nb block sums in place (stride kScanBlock)
-__global__ __launch_bounds__(kScanThreads) void wire_scan_sums(uint64_t nb, uint64_t* wo) {
-    uint64_t carry = 0;
-    for (uint64_t b0 = 0; b0 < nb; b0 += kScanThreads) {
-        const uint64_t b = b0 + threadIdx.x;
-        const uint64_t v = b < nb ? gptr(wo)[b * kScanBlock] : 0;
-        uint64_t total;
-        const uint64_t ex = block_exclusive_scan(v, &total);
-        if (b < nb) gptr(wo)[b * kScanBlock] = carry + ex;
-        carry += total;
-    }
-}
-
-// 3. per block: wo[j] = (off[j] - off[0]) + (2 + 4 masked) j + (extended-length
-//    bytes of frames < j); the block's last thread with frames also writes wo[n].
-__global__ __launch_bounds__(kScanThreads) void wire_offsets(const uint64_t* off, uint64_t n, uint32_t fixed,
-                                                             uint64_t* wo) {
-    __shared__ uint64_t block_prefix;
-    const uint64_t base = (uint64_t)blockIdx.x * kScanBlock;
-    if (threadIdx.x == 0) block_prefix = gptr(wo)[base];
-    __syncthreads();
-    const uint64_t first = base + (uint64_t)threadIdx.x * kScanPer;   // this thread's kScanPer frames
+__global__ __launch_bounds__(kScanThreads) void wire_offsets_chained(const uint64_t* off, uint64_t n, uint32_t fixed,
+                                                                     uint64_t* wo, uint64_t* status, uint32_t epoch) {
+    __shared__ uint64_t tile_prefix;
+    const uint64_t tile = blockIdx.x;
+    const uint64_t first = tile * kScanBlock + (uint64_t)threadIdx.x * kScanPer;   // this thread's frames
     uint32_t e[kScanPer];
     uint64_t s = 0;
 #pragma unroll
@@ -109,8 +96,32 @@ __global__ __launch_bounds__(kScanThreads) void wire_offsets(const uint64_t* off
         e[i] = j < n ? ext_len(gptr(off)[j + 1] - gptr(off)[j]) : 0u;
         s += e[i];
     }
-    uint64_t total;
-    uint64_t run = block_prefix + block_exclusive_scan(s, &total);
+    uint64_t agg;
+    const uint64_t ex = block_exclusive_scan(s, &agg);
+    if (threadIdx.x == 0) {
+        uint64_t prefix = 0;
+        if (tile == 0) {
+            __hip_atomic_store(&status[0], status_word(2, epoch, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&status[tile], status_word(1, epoch, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int64_t p = (int64_t)tile - 1; p >= 0;) {
+                const uint64_t w = __hip_atomic_load(&status[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t flag = w >> 62;
+                if (flag == 0 || ((w >> kValBits) & 0xFFFF) != (epoch & 0xFFFF)) {
+                    __builtin_amdgcn_s_sleep(1);   // predecessor not published yet
+                    continue;
+                }
+                prefix += w & kValMask;
+                if (flag == 2) break;
+                --p;
+            }
+            __hip_atomic_store(&status[tile], status_word(2, epoch, prefix + agg), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        tile_prefix = prefix;
+    }
+    __syncthreads();
+    uint64_t run = tile_prefix + ex;
     const uint64_t off0 = gptr(off)[0];
 #pragma unroll
     for (int i = 0; i < kScanPer; ++i) {
@@ -160,11 +171,17 @@ __device__ __forceinline__ void enc_entry(const EncArgs& a, int64_t v, EncTable&
     t.b0 = b0;
 }
 
-__device__ __forceinline__ void enc_table_load(const EncArgs& a, EncTable& t, int64_t kb, int lane) {
+__device__ __forceinline__ void enc_table_issue(const EncArgs& a, EncTable& t, int64_t kb, int lane) {
     t.kb = kb;
     enc_entry(a, kb + lane, t);
     t.tail = kb + (kWave - 1) >= (int64_t)a.n;
-    t.last = readlane64(t.start, kWave - 1);
+}
+
+__device__ __forceinline__ void enc_table_finish(EncTable& t) { t.last = readlane64(t.start, kWave - 1); }
+
+__device__ __forceinline__ void enc_table_load(const EncArgs& a, EncTable& t, int64_t kb, int lane) {
+    enc_table_issue(a, t, kb, lane);
+    enc_table_finish(t);
 }
 
 // Largest virtual frame L whose header starts at or before W (wave-uniform):
@@ -327,6 +344,70 @@ __device__ __forceinline__ void store_wire(const EncArgs& a, uint64_t W, u32x4 v
     }
 }
 
+// Wave-uniform description of the frame in table entry l (needs entry l + 1).
+struct FrameInfo {
+    uint64_t Ws, We, pw, o, len;   // wire start / end, payload start (W coords); payload offset, length
+    uint32_t key, b0;
+};
+
+__device__ __forceinline__ FrameInfo frame_info(const EncArgs& a, const EncTable& t, int l) {
+    FrameInfo f;
+    f.Ws = readlane64(t.start, l);
+    f.We = readlane64(t.start, l + 1);
+    f.o = readlane64(t.poff, l);
+    f.len = readlane64(t.poff, l + 1) - f.o;
+    f.key = readlane32(t.key, l);
+    f.b0 = readlane32(t.b0, l);
+    f.pw = f.Ws + 2 + ext_len(f.len) + (a.masked ? 4 : 0);
+    return f;
+}
+
+// One frame's payload as seen from a lane's 16-B vector at W.
+struct Slot {
+    int64_t s0;        // src offset of the vector's byte 0 (o + W - pw)
+    int32_t plo, phi;  // payload bytes [plo, phi) of the vector, clamped to [0, 16]
+    uint32_t rk;       // key rotated to the phase of byte 0 (W - pw)
+};
+
+__device__ __forceinline__ int32_t clamp16(int64_t x) { return x < 0 ? 0 : (x > 16 ? 16 : (int32_t)x); }
+
+__device__ __forceinline__ Slot slot_of(const FrameInfo& f, uint64_t W) {
+    Slot s;
+    s.s0 = (int64_t)f.o + (int64_t)(W - f.pw);
+    s.plo = clamp16((int64_t)(f.pw - W));
+    s.phi = clamp16((int64_t)(f.We - W));
+    s.rk = rotr8(f.key, W - f.pw);
+    return s;
+}
+
+__device__ __forceinline__ Slot select_slot(bool c, const Slot& x, const Slot& y) {
+    Slot s;
+    s.s0 = c ? x.s0 : y.s0;
+    s.plo = c ? x.plo : y.plo;
+    s.phi = c ? x.phi : y.phi;
+    s.rk = c ? x.rk : y.rk;
+    return s;
+}
+
+// OR the header bytes of frame f that fall into the lane's vector into v
+__device__ __forceinline__ u32x4 put_header(const EncArgs& a, const FrameInfo& f, uint64_t W, u32x4 v) {
+    const int64_t hs = (int64_t)(f.Ws - W), he = (int64_t)(f.pw - W);
+    if (he > 0 && hs < 16) {
+        uint64_t hl, hh;
+        build_header(f.b0, f.len, a.masked != 0, f.key, hl, hh);
+        v |= shift_bytes(hl, hh, (int)hs) & select_range(hs, he);
+    }
+    return v;
+}
+
+// Span kinds (wave-uniform): the whole span is payload of one frame; or every
+// vector holds bytes of at most two frames, from two unaligned loads plus header
+// bytes; or the general compose path (table edges, tiny frames, buffer edges).
+enum : int { kSpanFast = 0, kSpanSlots = 1, kSpanCompose = 2 };
+
+// Chunk = U spans.  Phase 1 plans every span of the chunk and issues all its
+// payload loads; phase 2 masks, places headers and stores.  The frame table of
+// the NEXT chunk is loaded (at a guessed base) while this chunk is processed.
 template <int U, bool NT>
 __global__ __launch_bounds__(256) void encode_frames_kernel(EncArgs a) {
     constexpr uint64_t kWin = kSpan * U;
@@ -337,53 +418,145 @@ __global__ __launch_bounds__(256) void encode_frames_kernel(EncArgs a) {
     const uint64_t wire_total = gptr(a.wo)[a.n];
     const uint64_t wlo = a.wmis, whi = a.wmis + wire_total;
     const uint64_t nwin = (whi + kWin - 1) / kWin;
+    const double density = wire_total ? (double)a.n / (double)wire_total : 0.0;   // frames per wire byte
 
+    uint64_t c = wave;
+    if (c >= nwin) return;
+    // table base for the chunk at A from a frame f_known starting at s_known,
+    // biased 24 frames back (the spread of independent random sizes)
+    auto guess = [&](int64_t f_known, uint64_t s_known, uint64_t A) -> int64_t {
+        if (A < a.wmis) return -1;
+        int64_t g = f_known + (int64_t)((double)(A - s_known) * density) - 24;
+        g = g < -1 ? -1 : g;
+        return g > (int64_t)a.n ? (int64_t)a.n : g;
+    };
+    uint64_t A = c * kWin;
     EncTable t;
-    t.kb = -2;   // no table yet
-    for (uint64_t c = wave; c < nwin; c += nwaves) {
-        const uint64_t A = c * kWin;
-        // table holding the frame that contains A
-        bool ok = false;
-        if (t.kb != -2) {
+    enc_table_issue(a, t, guess(0, a.wmis, A), lane);
+    for (;;) {
+        // resolve this chunk's table (issued a chunk ago)
+        enc_table_finish(t);
+        {
             const uint64_t m = __ballot(t.start <= A);
-            ok = m != 0 && (t.tail || m != ~0ull);
+            if (!(m != 0 && (t.tail || m != ~0ull))) enc_table_load(a, t, enc_locate(a, A, wire_total, lane), lane);
         }
-        if (!ok) enc_table_load(a, t, enc_locate(a, A, wire_total, lane), lane);
+        const int j0 = __popcll(__ballot(t.start <= A)) - 1;
+        const int64_t f_known = t.kb + j0;
+        const uint64_t s_known = readlane64(t.start, j0);
+        const uint64_t cn = c + nwaves;
+        EncTable tn;
+        if (cn < nwin) enc_table_issue(a, tn, guess(f_known, s_known, cn * kWin), lane);
+
+        // phase 1: plan each span, issue its loads
+        // per span and lane, what phase 2 needs: the two loads, the two rotated keys,
+        // and one packed word: plo1 | phi1 << 5 | plo2 << 10 | phi2 << 15 | two << 20 | slow << 21
+        int kind[U];
+        u32x4 d1[U], d2[U];
+        uint32_t rk1[U], rk2[U], pk[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t A0 = A + (uint64_t)u * kSpan;
+            const uint64_t A0 = A + (uint64_t)u * kSpan, Aend = A0 + kSpan;
+            const uint64_t W = A0 + 16ull * (uint64_t)lane;
+            kind[u] = kSpanCompose;
+            if (A0 >= whi) continue;
+            const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
+            const uint64_t bm = __ballot(t.start > A0 && t.start < Aend);
+            const int nb = __popcll(bm);
+            const bool covered = (t.tail || t.last >= Aend) && l0 + nb + 1 <= kWave - 1;
+            if (!covered || A0 < wlo || Aend > whi || t.kb + l0 < 0 || t.kb + l0 + nb >= (int64_t)a.n) continue;
+            const FrameInfo f0 = frame_info(a, t, l0);
+            if (nb == 0 && f0.pw <= A0 && Aend <= f0.We) {
+                kind[u] = kSpanFast;
+                const Slot sf = slot_of(f0, W);
+                rk1[u] = sf.rk;
+                d1[u] = load_u<NT>(a.src + sf.s0);
+                continue;
+            }
+            kind[u] = kSpanSlots;
+            Slot a1 = slot_of(f0, W), a2 = a1;
+            int cut = 0;   // frame starts inside (W, W + 15]
+            uint64_t b = bm;
+            while (b) {
+                const int l = __builtin_ctzll(b);
+                b &= b - 1;
+                const FrameInfo fj = frame_info(a, t, l);
+                const Slot sj = slot_of(fj, W);
+                a1 = select_slot(W >= fj.Ws, sj, a1);
+                a2 = select_slot(W + 15 >= fj.Ws, sj, a2);
+                cut += (fj.Ws > W && fj.Ws <= W + 15) ? 1 : 0;
+            }
+            const bool two = cut == 1;
+            bool slow = cut > 1;
+            // a load must stay inside [0, src_total): near the ends of the payload the
+            // compose path reads byte by byte
+            const bool need1 = a1.phi > a1.plo, need2 = two && a2.phi > a2.plo;
+            slow |= need1 && (a1.s0 < 0 || (uint64_t)a1.s0 + 16 > a.src_total);
+            slow |= need2 && (a2.s0 < 0 || (uint64_t)a2.s0 + 16 > a.src_total);
+            rk1[u] = a1.rk;
+            rk2[u] = a2.rk;
+            pk[u] = (uint32_t)a1.plo | (uint32_t)a1.phi << 5 | (uint32_t)a2.plo << 10 | (uint32_t)a2.phi << 15 |
+                    (two ? 1u << 20 : 0u) | (slow ? 1u << 21 : 0u);
+            if (need1 && !slow) d1[u] = load_u<NT>(a.src + a1.s0);
+            if (need2 && !slow) d2[u] = load_u<NT>(a.src + a2.s0);
+        }
+
+        // phase 2: mask, headers, store (lanes / spans needing the general path are
+        // left to phase 3, so the compose code is instantiated once, not per span)
+        uint32_t compose_spans = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t A0 = A + (uint64_t)u * kSpan, Aend = A0 + kSpan;
             if (A0 >= whi) break;
-            const uint64_t Aend = A0 + kSpan;
+            const uint64_t W = A0 + 16ull * (uint64_t)lane;
+            u32x4 v;
+            if (kind[u] == kSpanCompose) {
+                compose_spans |= 1u << u;
+                continue;
+            }
+            if (kind[u] == kSpanFast) {
+                const u32x4 kv = {rk1[u], rk1[u], rk1[u], rk1[u]};
+                v = d1[u] ^ kv;
+            } else if (kind[u] == kSpanSlots) {
+                const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
+                const uint32_t p = pk[u];
+                const u32x4 k1 = {rk1[u], rk1[u], rk1[u], rk1[u]};
+                const u32x4 k2 = {rk2[u], rk2[u], rk2[u], rk2[u]};
+                v = (d1[u] ^ k1) & select_range(p & 31, (p >> 5) & 31);
+                if (p & (1u << 20)) v |= (d2[u] ^ k2) & select_range((p >> 10) & 31, (p >> 15) & 31);
+                // headers: the span's first frame (if the span starts inside its
+                // header) and every frame starting inside the span
+                const FrameInfo f0 = frame_info(a, t, l0);
+                if (f0.pw > A0) v = put_header(a, f0, W, v);
+                uint64_t b = __ballot(t.start > A0 && t.start < Aend);
+                while (b) {
+                    const int l = __builtin_ctzll(b);
+                    b &= b - 1;
+                    v = put_header(a, frame_info(a, t, l), W, v);
+                }
+                if (__ballot((p >> 21) & 1)) compose_spans |= 1u << u;
+                if ((p >> 21) & 1) continue;   // this lane's vector: phase 3
+            }
+            store_wire<NT>(a, W, v, wlo, whi);
+        }
+        // phase 3: the general path, span by span (the table may slide here)
+        for (int u = 0; u < U; ++u) {
+            if (!((compose_spans >> u) & 1)) continue;
+            const uint64_t A0 = A + (uint64_t)u * kSpan, Aend = A0 + kSpan;
+            const uint64_t W = A0 + 16ull * (uint64_t)lane;
+            // a kSpanSlots span only recomposes its slow lanes
+            const bool mine = kind[u] == kSpanCompose || ((pk[u] >> 21) & 1);
             int l0 = __popcll(__ballot(t.start <= A0)) - 1;
             if (l0 >= kWave - 1 || (l0 > 0 && !t.tail && t.last < Aend)) {
                 enc_table_load(a, t, t.kb + l0, lane);
                 l0 = 0;
             }
-            const uint64_t W = A0 + 16ull * (uint64_t)lane;
-            const int64_t j0 = t.kb + l0;
-            bool fast = false;
-            uint64_t Ws = 0, We = 0, o0 = 0, pw = 0;
-            uint32_t key = 0;
-            if (j0 >= 0 && j0 < (int64_t)a.n && A0 >= wlo && Aend <= whi) {
-                Ws = readlane64(t.start, l0);
-                We = readlane64(t.start, l0 + 1);
-                o0 = readlane64(t.poff, l0);
-                const uint64_t o1 = readlane64(t.poff, l0 + 1);
-                key = readlane32(t.key, l0);
-                pw = Ws + 2 + ext_len(o1 - o0) + (a.masked ? 4 : 0);
-                fast = pw <= A0 && Aend <= We;
-            }
-            u32x4 v;
-            if (fast) {   // the whole span is payload of frame j0 (wave-uniform)
-                const uint64_t s = o0 + (W - pw);
-                const uint32_t rk = rotr8(key, A0 - pw);
-                const u32x4 kv = {rk, rk, rk, rk};
-                v = load_u<NT>(a.src + s) ^ kv;
-            } else {
-                v = compose_vec<NT>(a, t, l0, A0, W, lane);
-            }
-            store_wire<NT>(a, W, v, wlo, whi);
+            const u32x4 v = compose_vec<NT>(a, t, l0, A0, W, lane);
+            if (mine) store_wire<NT>(a, W, v, wlo, whi);
         }
+        if (cn >= nwin) break;
+        c = cn;
+        A = cn * kWin;
+        t = tn;
     }
 }
 
@@ -401,16 +574,64 @@ static int enc_resident_blocks() {
     return cache[dev];
 }
 
+// Scan scratch: one status word per tile, per (device, stream).  Scans queued on
+// one stream run one after another, so they can share an array (the epoch tells
+// their words apart); scans on different streams may run concurrently and get
+// different arrays.  Arrays grow geometrically and are never freed: an outgrown
+// one may still be read by scans queued before the growth.
+struct ScanScratch {
+    uint64_t* status = nullptr;
+    uint64_t tiles = 0;
+    uint32_t epoch = 0;
+};
+
 hipError_t launch_wire_offsets(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream) {
     if (n == 0) return hipMemsetAsync(wo, 0, sizeof(uint64_t), stream);
-    // blocks cover frames 0 .. n inclusive: every block base is <= n, so wo[base]
-    // can hold that block's sum, and some block writes wo[n]
-    const uint64_t nb = n / kScanBlock + 1;
-    if (nb > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(wire_block_sums, dim3((unsigned)nb), dim3(kScanThreads), 0, stream, off, n, wo);
-    hipLaunchKernelGGL(wire_scan_sums, dim3(1), dim3(kScanThreads), 0, stream, nb, wo);
-    hipLaunchKernelGGL(wire_offsets, dim3((unsigned)nb), dim3(kScanThreads), 0, stream, off, n,
-                       (uint32_t)(2 + (masked ? 4 : 0)), wo);
+    const uint64_t tiles = n / kScanBlock + 1;   // frames 0 .. n inclusive
+    if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    static std::map<std::pair<int, hipStream_t>, ScanScratch> scratch;
+    static std::mutex mu;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    uint64_t* status;
+    uint32_t epoch;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        ScanScratch& sc = scratch[{dev, stream}];
+        if (sc.tiles < tiles) {
+            uint64_t* p = nullptr;
+            uint64_t want = sc.tiles ? 2 * sc.tiles : 1024;
+            while (want < tiles) want *= 2;
+            if ((e = hipMalloc(&p, want * sizeof(uint64_t))) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(p, 0, want * sizeof(uint64_t), stream)) != hipSuccess) return e;
+            sc.status = p;
+            sc.tiles = want;
+            sc.epoch = 0;
+        }
+        sc.epoch = (sc.epoch + 1) & 0xFFFF;
+        if (sc.epoch == 0) {   // epochs wrapped: clear the words so no stale epoch can match
+            if ((e = hipMemsetAsync(sc.status, 0, sc.tiles * sizeof(uint64_t), stream)) != hipSuccess) return e;
+            sc.epoch = 1;
+        }
+        status = sc.status;
+        epoch = sc.epoch;
+    }
+    hipLaunchKernelGGL(wire_offsets_chained, dim3((unsigned)tiles), dim3(kScanThreads), 0, stream, off, n,
+                       (uint32_t)(2 + (masked ? 4 : 0)), wo, status, epoch);
+    return hipGetLastError();
+}
+
+template <int U>
+static hipError_t launch_enc_u(EncArgs a, uint64_t wire_bound, bool nt, int max_blocks, hipStream_t stream) {
+    a.nwin = (a.wmis + wire_bound + kSpan * U - 1) / (kSpan * U);
+    const uint64_t cap = (uint64_t)(max_blocks > 0 ? max_blocks
+                                                  : (nt ? enc_resident_blocks<U, true>() : enc_resident_blocks<U, false>()));
+    const uint64_t want = (a.nwin + 3) / 4;
+    const int blocks = (int)(want < cap ? want : cap);
+    if (blocks <= 0) return hipSuccess;
+    if (nt) hipLaunchKernelGGL((encode_frames_kernel<U, true>), dim3(blocks), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((encode_frames_kernel<U, false>), dim3(blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -419,7 +640,6 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
                                 uint64_t* wo, hipStream_t stream, const LaunchCfg& cfg) {
     hipError_t e = launch_wire_offsets(off, n, masked, wo, stream);
     if (e != hipSuccess || n == 0) return e;
-    constexpr int U = 4;
     EncArgs a;
     a.wmis = (uint64_t)(uintptr_t)wire & 15u;
     a.wire_base = wire - a.wmis;
@@ -431,16 +651,10 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     a.b0 = b0;
     a.n = n;
     a.masked = masked ? 1u : 0u;
-    a.nwin = (a.wmis + wire_bound + kSpan * U - 1) / (kSpan * U);
     const bool nt = cfg.flags < 0 || (cfg.flags & (kNtLoads | kNtStores));
-    const uint64_t cap = (uint64_t)(cfg.max_blocks > 0 ? cfg.max_blocks
-                                                       : (nt ? enc_resident_blocks<U, true>() : enc_resident_blocks<U, false>()));
-    const uint64_t want = (a.nwin + 3) / 4;
-    const int blocks = (int)(want < cap ? want : cap);
-    if (blocks <= 0) return hipSuccess;
-    if (nt) hipLaunchKernelGGL((encode_frames_kernel<U, true>), dim3(blocks), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((encode_frames_kernel<U, false>), dim3(blocks), dim3(256), 0, stream, a);
-    return hipGetLastError();
+    // U = 2 KiB chunks unless tuned to 4 (netc_gpu_tune's unroll; 1 and 8 map to 2 and 4)
+    if (cfg.unroll >= 4) return launch_enc_u<4>(a, wire_bound, nt, cfg.max_blocks, stream);
+    return launch_enc_u<2>(a, wire_bound, nt, cfg.max_blocks, stream);
 }
 
 }  // namespace netc_gpu

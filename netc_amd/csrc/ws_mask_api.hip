@@ -117,8 +117,7 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags) {
         return fail(NETC_GPU_EINVAL, "unroll must be 1, 2, 4 or 8 (got %d)", unroll);
     if (max_blocks < 0 || max_blocks > (1 << 24)) return fail(NETC_GPU_EINVAL, "max_blocks out of range");
     if (flags != NETC_GPU_TUNE_AUTO &&
-        ((flags & ~(NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES | NETC_GPU_TUNE_TABLE64 | NETC_GPU_TUNE_TABLE16)) ||
-         (flags & NETC_GPU_TUNE_TABLE64 && flags & NETC_GPU_TUNE_TABLE16)))
+        (flags & ~(NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES)))
         return fail(NETC_GPU_EINVAL, "unknown tune flags");
     g_cfg.unroll = unroll;
     g_cfg.max_blocks = max_blocks;
@@ -172,7 +171,8 @@ int netc_gpu_encode_frames(int device, void* d_wire, size_t wire_capacity, uint6
                            void* stream) {
     if (int r = check_device(device)) return r;
     if (!d_wire_offsets) return fail(NETC_GPU_EINVAL, "null wire offsets");
-    if (nframes && (!d_frame_offsets || !d_payload || !d_wire)) return fail(NETC_GPU_EINVAL, "null frame buffer");
+    if (nframes && (!d_frame_offsets || !d_wire)) return fail(NETC_GPU_EINVAL, "null frame buffer");
+    if (total_bytes && !d_payload) return fail(NETC_GPU_EINVAL, "null payload buffer");
     if (masked && nframes && !d_keys) return fail(NETC_GPU_EINVAL, "masked frames need keys");
     const uint64_t per = NETC_WS_MAX_HEADER(masked);
     if (nframes > (UINT64_MAX - total_bytes) / per)

@@ -19,11 +19,9 @@ struct Args {
     uint64_t mis;              // dst & 15
     uint64_t nwin;             // windows (chunks) of U KiB covering [0, mis + total)
     double density;            // n / total: frames per payload byte (table-base guesses)
-    int table_mode;            // 0: adaptive 16/64-entry frame table, 1: always 64, 2: always 16
-    int few_frames;            // a chunk holds <= 8 frames on average (16-entry table can suffice)
 };
 
-enum : int { kNtLoads = 1, kNtStores = 2, kTable64 = 4, kTable16 = 8 };   // LaunchCfg::flags (NETC_GPU_TUNE_*)
+enum : int { kNtLoads = 1, kNtStores = 2 };   // LaunchCfg::flags (NETC_GPU_TUNE_NT_*)
 
 struct LaunchCfg {
     int unroll = 4;            // U: 1 KiB spans per window (1, 2, 4, 8)

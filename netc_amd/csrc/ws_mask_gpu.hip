@@ -48,10 +48,9 @@ extern "C" int netc_gpu_debug_stamps(void* d_buf) {
 
 struct Table {
     int64_t kb;       // virtual frame index held by lane 0
-    uint64_t start;   // this lane's entry: start of frame kb + lane (P coords); inf past `size`
+    uint64_t start;   // this lane's entry: start of frame kb + lane (P coords)
     uint32_t key;     // this lane's entry: packed key of frame kb + lane
-    uint64_t last;    // start of frame kb + size - 1 (uniform)
-    int size;         // entries held: 64, or 16 while frame starts are predicted exactly
+    uint64_t last;    // start of frame kb + 63 (uniform)
     bool tail;        // frame n (the open-ended pass-through frame) is in the table
 };
 
@@ -71,23 +70,17 @@ __device__ __forceinline__ void frame_entry(const Args& a, int64_t v, uint64_t& 
     k = (v >= 0 && v < n) ? key : 0u;
 }
 
-// issue the table loads (frames kb .. kb+size-1, one per lane) without waiting for
-// them.  Lanes past `size` repeat the last entry's address (the same bytes: no extra
-// cache lines) and then read as "starts at infinity", so a 16-entry table costs a
-// quarter of the descriptor traffic of a 64-entry one.
-__device__ __forceinline__ void table_issue(const Args& a, Table& t, int64_t kb, int lane, int size) {
+// issue the table loads (frames kb .. kb+63, one per lane) without waiting for them
+__device__ __forceinline__ void table_issue(const Args& a, Table& t, int64_t kb, int lane) {
     t.kb = kb;
-    t.size = size;
-    const bool live = lane < size;
-    frame_entry(a, kb + (live ? lane : size - 1), t.start, t.key);
-    t.start = live ? t.start : kInf;
-    t.tail = kb + (size - 1) >= (int64_t)a.n;
+    frame_entry(a, kb + lane, t.start, t.key);
+    t.tail = kb + (kWave - 1) >= (int64_t)a.n;
 }
 
-__device__ __forceinline__ void table_finish(Table& t) { t.last = readlane64(t.start, t.size - 1); }
+__device__ __forceinline__ void table_finish(Table& t) { t.last = readlane64(t.start, kWave - 1); }
 
-__device__ __forceinline__ void table_load(const Args& a, Table& t, int64_t kb, int lane, int size) {
-    table_issue(a, t, kb, lane, size);
+__device__ __forceinline__ void table_load(const Args& a, Table& t, int64_t kb, int lane) {
+    table_issue(a, t, kb, lane);
     table_finish(t);
 }
 
@@ -96,22 +89,17 @@ __device__ __forceinline__ void table_load(const Args& a, Table& t, int64_t kb, 
 __device__ __forceinline__ bool table_brackets(const Table& t, uint64_t P) {
     const uint64_t m = __ballot(t.start <= P);
     if (m == 0) return false;
-    return t.tail || ((m >> (t.size - 1)) & 1) == 0;
+    return t.tail || m != ~0ull;
 }
 
 // Table base for the chunk at P guessed from a frame known to start at s_known
 // (index f_known) and the batch's mean frame density: frames are independent
 // draws, so the guess error grows only with the square root of the frames in
 // between; the window is biased forward so the chunk's later frames fit too.
-// Returns the unbiased guess; the table base is guess - bias (clamped by the caller).
-__device__ __forceinline__ int64_t guess_frame(const Args& a, int64_t f_known, uint64_t s_known, uint64_t P) {
+__device__ __forceinline__ int64_t guess_base(const Args& a, int64_t f_known, uint64_t s_known, uint64_t P) {
     if (P < a.mis) return -1;
     const double ahead = (double)(P - s_known) * a.density;
-    return f_known + (int64_t)ahead;
-}
-
-__device__ __forceinline__ int64_t table_base(const Args& a, int64_t guess, int64_t bias) {
-    int64_t g = guess - bias;
+    int64_t g = f_known + (int64_t)ahead - 24;
     g = g < -1 ? -1 : g;
     return g > (int64_t)a.n ? (int64_t)a.n : g;
 }
@@ -173,7 +161,7 @@ __device__ __forceinline__ u32x4 span_mask(const Args& a, Table& t, uint64_t A0,
     if (!t.tail && t.last < Aend) {
         const uint64_t m = __ballot(t.start <= A0);
         const int j0 = __popcll(m) - 1;
-        if (j0 > 0) table_load(a, t, t.kb + j0, lane, t.size);
+        if (j0 > 0) table_load(a, t, t.kb + j0, lane);
     }
     const uint64_t m0 = __ballot(t.start <= A0);
     const int j0 = __popcll(m0) - 1;
@@ -196,9 +184,9 @@ __device__ __forceinline__ u32x4 span_mask(const Args& a, Table& t, uint64_t A0,
             mask = (mask & ~sel) | (kv & sel);
         }
         if (t.tail || t.last >= Aend) break;
-        // more boundaries in one span than the table holds: advance the table past
-        // the last applied entry (re-applying entry 0 is idempotent) and continue
-        table_load(a, t, t.kb + (t.size - 1), lane, t.size);
+        // more than 63 boundaries in one span: advance the table past the last
+        // applied entry (re-applying entry 0 again is idempotent) and continue
+        table_load(a, t, t.kb + (kWave - 1), lane);
         b = __ballot(t.start > A0 && t.start < Aend);
     }
     return mask;
@@ -258,7 +246,7 @@ __device__ __forceinline__ void edge_chunk(const Args& a, uint64_t A, int lane) 
         if (P >= full_lo && P < full_hi) d[u] = load_vec<SRC_ALIGNED, NT>(a, P);
     }
     Table t;
-    table_load(a, t, locate(a, A, lane), lane, kWave);
+    table_load(a, t, locate(a, A, lane), lane);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t A0 = A + (uint64_t)u * kSpan;
@@ -335,41 +323,27 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
     // make t hold the frame containing A (its probe was issued a chunk ago)
     auto resolve = [&](Table& t, uint64_t A, int64_t& f0, uint64_t& s0) {
         table_finish(t);
-        if (!table_brackets(t, A)) table_load(a, t, locate(a, A, lane), lane, kWave);
+        if (!table_brackets(t, A)) table_load(a, t, locate(a, A, lane), lane);
         const int j0 = __popcll(__ballot(t.start <= A)) - 1;
         f0 = t.kb + j0;
         s0 = readlane64(t.start, j0);
     };
-    // Table size for the next chunk: 16 entries (bias 2) while the guesses land
-    // within one frame (evenly sized frames) and a chunk holds few frames, else 64
-    // (bias 24, covers the +-18-frame spread of independent random sizes).
-    auto next_size = [&](int64_t f0, int64_t guess) {
-        if (a.table_mode == 1) return kWave;
-        if (a.table_mode == 2) return 16;
-        const int64_t dev = f0 - guess;
-        return (a.few_frames && dev >= -1 && dev <= 1) ? 16 : kWave;
-    };
-    auto bias_of = [](int size) -> int64_t { return size == kWave ? 24 : 2; };
 
     u32x4 d[U];
     uint64_t A = c * kWin;
     load_window(d, A);
     Table t;
-    int tsz = a.table_mode == 2 ? 16 : kWave;
-    int64_t g = guess_frame(a, 0, a.mis, A);   // global guess: frame 0 starts near P = mis
-    table_issue(a, t, table_base(a, g, bias_of(tsz)), lane, tsz);
+    table_issue(a, t, guess_base(a, 0, a.mis, A), lane);   // global guess: frame 0 starts near P = mis
 
     for (uint64_t cn = c + nwaves; cn < ci_hi; cn += nwaves) {
         int64_t f0;
         uint64_t s0;
         resolve(t, A, f0, s0);
-        tsz = next_size(f0, g);
         const uint64_t An = cn * kWin;
         u32x4 dn[U];
         load_window(dn, An);
         Table tn;
-        g = guess_frame(a, f0, s0, An);
-        table_issue(a, tn, table_base(a, g, bias_of(tsz)), lane, tsz);
+        table_issue(a, tn, guess_base(a, f0, s0, An), lane);
         process(d, t, A);
         A = An;
         t = tn;
@@ -437,8 +411,6 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
     a.nwin = (nvec + win_vec - 1) / win_vec;
     if (a.nwin == 0) return hipSuccess;
     a.density = total ? (double)n / (double)total : 0.0;
-    a.table_mode = cfg.flags < 0 ? 0 : ((cfg.flags & kTable64) ? 1 : ((cfg.flags & kTable16) ? 2 : 0));
-    a.few_frames = a.density * (double)(kSpan * (uint64_t)U) <= 8.0 ? 1 : 0;
     const int mb = cfg.max_blocks;
     // payload loads / stores non-temporal unless asked otherwise: every byte is touched once
     const bool nt = cfg.flags < 0 || (cfg.flags & (kNtLoads | kNtStores));

@@ -200,3 +200,19 @@ def test_errors(torch_cuda):
     assert e.value.code == nm.NETC_GPU_EINVAL
     with pytest.raises(ValueError):
         nm.encode_frames(big, wo, src, off, None, masked=True)
+
+
+@pytest.mark.parametrize("unroll,max_blocks", [(4, 0), (2, 1), (4, 3)])
+def test_launch_shapes(torch_cuda, unroll, max_blocks):
+    # both chunk sizes, and grids far smaller than the work (long grid-stride walks)
+    try:
+        nm.tune(unroll, max_blocks)
+        rng = np.random.default_rng(31 + unroll)
+        sizes = np.concatenate([rng.integers(0, 3000, 400), rng.integers(0, 20, 400), np.full(300, 1024)])
+        off = frames_from_sizes(sizes)
+        payload = _payload(rng, int(off[-1]))
+        keys = rng.integers(0, 2**32, sizes.size, dtype=np.uint64).astype(np.uint32)
+        run_encode(torch_cuda, payload, off, keys, wire_shift=9, src_shift=2)
+        run_encode(torch_cuda, payload, off, keys, masked=False)
+    finally:
+        nm.tune()

@@ -158,9 +158,9 @@ def test_one_huge_frame(torch_cuda):
 
 
 @pytest.mark.parametrize("unroll,max_blocks", [(1, 2048), (2, 64), (8, 0), (4, 1), (4, 100000), (4, 0)])
-@pytest.mark.parametrize("flags", [-1, 0, 3, 3 | 4, 3 | 8])
+@pytest.mark.parametrize("flags", [-1, 0, 3])
 def test_launch_shapes(torch_cuda, unroll, max_blocks, flags):
-    """Every kernel instantiation (U x cache-hint flags x table size x grid cap) is bit-exact."""
+    """Every kernel instantiation (U x cache-hint flags x grid cap) is bit-exact."""
     try:
         nm.tune(unroll, max_blocks, flags)
         off = synth.mixed_offsets(5 << 20, 1, 9000, seed=13)
@@ -171,11 +171,11 @@ def test_launch_shapes(torch_cuda, unroll, max_blocks, flags):
         nm.tune()
 
 
-@pytest.mark.parametrize("flags", [-1, 3 | 8])
+@pytest.mark.parametrize("flags", [-1, 0])
 def test_near_uniform_frames(torch_cuda, flags):
-    """Evenly sized frames with sparse irregular ones: the adaptive frame table drops to
-    16 entries while guesses are exact and must recover (64 entries / locate) after
-    each irregular frame shifts every later frame start."""
+    """Evenly sized frames with sparse irregular ones: the table-base guesses are exact
+    until an irregular frame shifts every later frame start, then must recover
+    (locate) — and dense 40-byte frames make the table slide inside a span."""
     try:
         nm.tune(4, 0, flags)
         rng = np.random.default_rng(21)

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workloads", default="c2,c4")
+    ap.add_argument("--unroll", default="2,4", help="netc_gpu_tune unroll values to time (KiB per chunk)")
     args = ap.parse_args()
 
     import torch
@@ -55,35 +56,37 @@ def main():
             if rc:
                 raise RuntimeError(nm._lib.gpu().netc_gpu_strerror())
 
-        K = args.steps if wl == "c2" else max(10, args.steps // 5)
-        with torch.cuda.stream(s):
-            for i in range(args.warmup):
-                step(i)
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(s)
-            for i in range(K):
-                step(i)
-            b.record(s)
-        torch.cuda.synchronize()
-        us = a.elapsed_time(b) / K * 1e3
-        # spot check the last step against the oracle on a few frames
-        from oracle import oracle as orc
+        for unroll in [int(x) for x in args.unroll.split(",")]:
+            nm.tune(unroll)
+            K = args.steps if wl == "c2" else max(10, args.steps // 5)
+            with torch.cuda.stream(s):
+                for i in range(args.warmup):
+                    step(i)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(s)
+                for i in range(K):
+                    step(i)
+                b.record(s)
+            torch.cuda.synchronize()
+            us = a.elapsed_time(b) / K * 1e3
+            # spot check the last step against the oracle on a few frames
+            from oracle import oracle as orc
 
-        last = (K - 1 + args.warmup) % 2
-        wire = wires[last][:wire_len].cpu().numpy()
-        wo_h = wo.cpu().numpy().view(np.uint64)
-        src_h = srcs[(args.warmup + K - 1) % nb].cpu().numpy()
-        bad = 0
-        for k in np.linspace(0, n - 1, 16).astype(np.int64):
-            lo, hi = int(off[k]), int(off[k + 1])
-            exp = orc.encode_frame(src_h[lo:hi].tobytes(), 2, int(keys[k]).to_bytes(4, "little"))
-            bad += wire[int(wo_h[k]): int(wo_h[k + 1])].tobytes() != exp
-        alg = total + wire_len
-        print(json.dumps({"workload": wl, "frames": int(n), "payload_bytes": int(total), "wire_bytes": int(wire_len),
-                          "us_per_step": round(us, 2), "achieved_GBps": round(alg / (us * 1e-6) / 1e9, 1),
-                          "frac_of_8TBps": round(alg / (us * 1e-6) / 8e12, 4),
-                          "payload_GiBps": round(total / (us * 1e-6) / 2**30, 1),
-                          "sampled_frames_wrong": int(bad)}), flush=True)
+            wire = wires[(K - 1) % 2][:wire_len].cpu().numpy()   # the last timed step is step(K - 1)
+            wo_h = wo.cpu().numpy().view(np.uint64)
+            src_h = srcs[(K - 1) % nb].cpu().numpy()
+            bad = 0
+            for k in np.linspace(0, n - 1, 16).astype(np.int64):
+                lo, hi = int(off[k]), int(off[k + 1])
+                exp = orc.encode_frame(src_h[lo:hi].tobytes(), 2, int(keys[k]).to_bytes(4, "little"))
+                bad += wire[int(wo_h[k]): int(wo_h[k + 1])].tobytes() != exp
+            alg = total + wire_len
+            print(json.dumps({"workload": wl, "unroll": unroll, "frames": int(n), "payload_bytes": int(total), "wire_bytes": int(wire_len),
+                              "us_per_step": round(us, 2), "achieved_GBps": round(alg / (us * 1e-6) / 1e9, 1),
+                              "frac_of_8TBps": round(alg / (us * 1e-6) / 8e12, 4),
+                              "payload_GiBps": round(total / (us * 1e-6) / 2**30, 1),
+                              "sampled_frames_wrong": int(bad)}), flush=True)
+        nm.tune()
         del srcs, wires
         torch.cuda.empty_cache()
 
