@@ -41,6 +41,9 @@ def _load(name: str) -> ctypes.CDLL:
             lib.oracle_encode_frame.restype = sz
             lib.oracle_encode_batch.argtypes = [vp, vp, vp, vp, vp, vp, sz, ctypes.c_int]
             lib.oracle_encode_batch.restype = sz
+            lib.oracle_scan_frames.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, vp, vp, vp, sz,
+                                               vp, vp]
+            lib.oracle_scan_frames.restype = sz
             lib.oracle_decode_message.argtypes = [vp, sz, vp, sz, vp, vp]
             lib.oracle_decode_message.restype = sz
         else:
@@ -124,6 +127,21 @@ def encode_batch(payload, offsets: np.ndarray, keys32: Optional[np.ndarray], hea
     w = lib(opt).oracle_encode_batch(_p(out), _p(wo), _p(p), _p(off), _p(k) if k is not None else None,
                                      _p(h) if h is not None else None, n, 1 if masked else 0)
     return out[:w], wo
+
+
+def scan_frames(wire, start: int = 0, strict: bool = True, opt: str = "O2"):
+    """oracle_scan_frames: (header offsets, packed keys, byte 0s, consumed, error or None) of a byte stream."""
+    w = _u8(wire)
+    cap = max(1, w.size // 2 + 1)
+    hdr = np.zeros(cap, dtype=np.uint64)
+    keys = np.zeros(cap, dtype=np.uint32)
+    b0 = np.zeros(cap, dtype=np.uint8)
+    consumed = ctypes.c_uint64(0)
+    error = ctypes.c_uint64(0)
+    n = lib(opt).oracle_scan_frames(_p(w), w.size, start, 1 if strict else 0, _p(hdr), _p(keys), _p(b0), cap,
+                                    ctypes.addressof(consumed), ctypes.addressof(error))
+    err = None if error.value == (1 << 64) - 1 else int(error.value)
+    return hdr[:n], keys[:n], b0[:n], int(consumed.value), err
 
 
 def decode_message(wire: bytes, cap: Optional[int] = None) -> Tuple[int, bytes, int]:

@@ -133,6 +133,70 @@ size_t oracle_encode_batch(uint8_t *out, uint64_t *wire_off, const uint8_t *payl
 }
 
 /*
+ * The frame boundaries of a received byte stream (checker of the device frame
+ * scan, include/ws/frame.h): the header decode of src/ws/common.c:146-296 walked
+ * over wire[start, len) frame by frame —
+ *   byte 0: FIN | RSV1-3 | opcode (:157-161); byte 1: MASK | 7-bit length (:180-181);
+ *   126 → 16-bit, 127 → 64-bit big-endian extended length (:223-245);
+ *   MASK → 4 key bytes (:273-289); then the payload.
+ * For frame k it records the header offset, the packed key (0 if unmasked) and
+ * byte 0.  The walk stops at the first frame not complete inside the stream
+ * (*consumed = its header offset, or len when every byte was used) or, with
+ * strict != 0, at the first header RFC 6455 forbids from a client (*error =
+ * its offset, else UINT64_MAX): MASK clear, RSV set, a reserved opcode, or a
+ * control frame (opcode >= 8) fragmented or longer than 125 (§5.1, §5.2, §5.5),
+ * or a 64-bit length with its top bit set.  The reference checks none of these
+ * (it accepts any header; strict = 0 reproduces that).  Returns the frames
+ * found (at most cap are recorded).
+ */
+size_t oracle_scan_frames(const uint8_t *wire, uint64_t len, uint64_t start, int strict, uint64_t *hdr,
+                          uint32_t *keys, uint8_t *b0, size_t cap, uint64_t *consumed, uint64_t *error)
+{
+    size_t n = 0;
+    uint64_t p = start;
+    *error = UINT64_MAX;
+    for (;;)
+    {
+        if (p + 2 > len) break;
+        const uint8_t first = wire[p], second = wire[p + 1];
+        const uint8_t opcode = first & 0x0F, mask = second >> 7, code = second & 0x7F;
+        const uint64_t ext = code == 126 ? 2 : (code == 127 ? 8 : 0);
+        const uint64_t hl = 2 + ext + (mask ? 4 : 0);
+        if (p + 2 + ext > len) break;
+        uint64_t plen = code;
+        if (ext)
+        {
+            plen = 0;
+            for (uint64_t i = 0; i < ext; ++i) plen = plen << 8 | wire[p + 2 + i];
+        }
+        if (strict)
+        {
+            const int reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
+            const int control = opcode >= 8;
+            if (!mask || (first & 0x70) || reserved || (control && (!(first & 0x80) || plen > 125)) ||
+                (code == 127 && (plen >> 63)))
+            {
+                *error = p;
+                break;
+            }
+        }
+        if (p + hl > len || plen > len - (p + hl)) break;
+        if (n < cap)
+        {
+            hdr[n] = p;
+            keys[n] = mask ? ((uint32_t)wire[p + hl - 4] | (uint32_t)wire[p + hl - 3] << 8 |
+                              (uint32_t)wire[p + hl - 2] << 16 | (uint32_t)wire[p + hl - 1] << 24)
+                           : 0;
+            b0[n] = first;
+        }
+        ++n;
+        p += hl + plen;
+    }
+    *consumed = p;
+    return n;
+}
+
+/*
  * src/ws/common.c:146-347 as a pure function over a complete byte stream:
  * decodes frames until one with FIN completes a message.  On success returns
  * the wire bytes consumed and writes the message (payload bytes, unmasked, no
