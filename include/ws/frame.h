@@ -68,6 +68,41 @@ int netc_gpu_encode_frames(int device, void *d_wire, size_t wire_capacity, uint6
                            const uint32_t *d_keys, const uint8_t *d_header0, size_t nframes, int masked,
                            void *stream);
 
+/* ---------------------------------------------------------- receive side -- */
+
+/** netc_gpu_scan_frames flag: reject what RFC 6455 forbids from a client (see below). */
+#define NETC_WS_SCAN_STRICT 1
+
+/** d_result layout of netc_gpu_scan_frames. */
+#define NETC_WS_SCAN_FRAMES   0   /* complete frames found (may exceed max_frames)        */
+#define NETC_WS_SCAN_CONSUMED 1   /* offset of the first incomplete frame, or len        */
+#define NETC_WS_SCAN_ERROR    2   /* offset of the first rejected header, or UINT64_MAX  */
+
+/**
+ * The frame boundaries of a received byte stream, found on `device` —
+ * the header state machine of ws_parse_frame
+ * (src/ws/common.c:146-296) over a whole buffer, in parallel.
+ *   d_wire, len       device, the stream; the first header is at `start`
+ *   flags             0: accept every header, as the reference does;
+ *                     NETC_WS_SCAN_STRICT: stop at the first header with MASK
+ *                     clear, an RSV bit set, a reserved opcode, a control frame
+ *                     that is fragmented or longer than 125 bytes, or a 64-bit
+ *                     length with its top bit set (RFC 6455 §5.1, §5.2, §5.5)
+ *   d_hdr             device output, max_frames + 1 uint64: header offset of
+ *                     frame k; d_hdr[n] = the consumed offset (when n <= max_frames)
+ *   d_keys, d_b0      device outputs, max_frames each: packed key32 (0 when the
+ *                     frame is unmasked) and header byte 0 (FIN | RSV | opcode)
+ *   d_result          device output, 3 uint64 (NETC_WS_SCAN_*)
+ * A frame counts when its header and whole payload lie inside [start, len); the
+ * scan stops at the first frame that does not (its offset is CONSUMED — keep the
+ * bytes from there for the next call) or, in strict mode, at a rejected header
+ * (ERROR = CONSUMED = its offset).  Frames past max_frames are counted but not
+ * recorded.  Asynchronous on `stream`; read d_result after synchronising.
+ * Scratch memory is allocated on first use per (device, stream) and reused.
+ */
+int netc_gpu_scan_frames(int device, const void *d_wire, size_t len, uint64_t start, int flags, uint64_t *d_hdr,
+                         uint32_t *d_keys, uint8_t *d_b0, size_t max_frames, uint64_t *d_result, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -516,7 +516,7 @@ __global__ __launch_bounds__(256) void encode_frames_kernel(EncArgs a) {
             if (kind[u] == kSpanFast) {
                 const u32x4 kv = {rk1[u], rk1[u], rk1[u], rk1[u]};
                 v = d1[u] ^ kv;
-            } else if (kind[u] == kSpanSlots) {
+            } else {   // kSpanSlots
                 const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
                 const uint32_t p = pk[u];
                 const u32x4 k1 = {rk1[u], rk1[u], rk1[u], rk1[u]};

@@ -196,6 +196,23 @@ int netc_gpu_encode_frames(int device, void* d_wire, size_t wire_capacity, uint6
     return 0;
 }
 
+int netc_gpu_scan_frames(int device, const void* d_wire, size_t len, uint64_t start, int flags, uint64_t* d_hdr,
+                         uint32_t* d_keys, uint8_t* d_b0, size_t max_frames, uint64_t* d_result, void* stream) {
+    if (int r = check_device(device)) return r;
+    if (flags & ~NETC_WS_SCAN_STRICT) return fail(NETC_GPU_EINVAL, "unknown scan flags 0x%x", flags);
+    if (!d_hdr || !d_result || (max_frames && (!d_keys || !d_b0))) return fail(NETC_GPU_EINVAL, "null output");
+    if (len && !d_wire) return fail(NETC_GPU_EINVAL, "null stream");
+    if (start > len) return fail(NETC_GPU_EINVAL, "start %llu past the stream end %zu", (unsigned long long)start, len);
+    if (len >= (1ull << 60)) return fail(NETC_GPU_EINVAL, "stream too long");
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+    hipError_t e = netc_gpu::launch_scan_frames((const uint8_t*)d_wire, len, start, (flags & NETC_WS_SCAN_STRICT) != 0,
+                                                d_hdr, d_keys, d_b0, max_frames, d_result, (hipStream_t)stream);
+    if (e == hipErrorOutOfMemory) return fail_hip(NETC_GPU_ENOMEM, "frame scan scratch", e);
+    if (e != hipSuccess) return fail_hip(NETC_GPU_ELAUNCH, "frame scan launch", e);
+    return 0;
+}
+
 // ---------------------------------------------------------------------------
 // Host → device → host pipeline (BASELINE config 5).  Slots are fixed byte
 // ranges of the payload; a frame cut by a slot edge continues in the next slot

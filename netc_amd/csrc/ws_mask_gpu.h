@@ -35,6 +35,11 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
 // ws_frame_gpu.hip: wire offsets (n + 1 entries into wo), then the wire bytes of
 // every frame (header, key, masked payload) into wire.  wire_bound >= wo[n].
 hipError_t launch_wire_offsets(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream);
+// ws_scan_gpu.hip: frame boundaries of a received stream (include/ws/frame.h)
+hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start, bool strict, uint64_t* hdr,
+                              uint32_t* keys, uint8_t* b0, uint64_t max_frames, uint64_t* result,
+                              hipStream_t stream);
+
 hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_t* src, uint64_t src_total,
                                 const uint64_t* off, const uint32_t* keys, const uint8_t* b0, uint64_t n, bool masked,
                                 uint64_t* wo, hipStream_t stream, const LaunchCfg& cfg);

@@ -1,0 +1,439 @@
+// MI355X (gfx950 / CDNA4) frame-boundary scan — device kernels.
+//
+// Replaces the reference's header state machine (src/ws/common.c:146-296: byte 0
+// FIN | RSV | opcode, byte 1 MASK | 7-bit length, 16 / 64-bit big-endian extended
+// length, 4 key bytes) run over a received byte stream: it finds every frame of
+// the stream (header offset, key, byte 0) in parallel.
+//
+// Frame starts form a chain: the next header follows the current frame's payload.
+// Chunks of C bytes are processed independently, for EVERY byte position:
+//   K1 / K2  per chunk, in LDS: parse a header at each position p (invalid under
+//            the strict RFC checks -> DEAD; not complete inside the stream -> END),
+//            link p to the next header, and pointer-jump the links until each
+//            position knows where its chain leaves the chunk (EXIT at a position
+//            in a later chunk) or ends (END / DEAD).  K1 publishes each chunk's
+//            distinct exits as "candidate entries" of the chunk they land in (the
+//            true chain enters each chunk at one of them); K2 maps every candidate
+//            entry of its chunk to the candidate it exits to: a graph of a few
+//            nodes per chunk whose path from the stream start is the true chain,
+//            one node per chunk it enters.
+//   K3       binary lifting over that graph (log2(chunks) doubling passes);
+//   K4       per chunk: the true entry (by lifting from the start node), a walk of
+//            the chunk's frames in LDS to count them, a chained scan of the counts
+//            (decoupled look-back), and a second walk that writes the descriptors.
+// Garbage chains (payload bytes parsed as headers) die within a hop or two under
+// the strict checks, so chunks have few distinct exits; a stream whose exits
+// overflow the fixed capacities (adversarial payloads) is finished by a serial
+// walk in K4 instead — same results, slower.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <mutex>
+#include <utility>
+
+#include "gpu_util.h"
+#include "ws_mask_gpu.h"
+
+namespace netc_gpu {
+
+static constexpr uint64_t kChunk = 4096;        // bytes per chunk (LDS: bytes + 8 B link per byte)
+static constexpr int kScanT = 256;              // threads per K1 / K2 block
+static constexpr int kPer = (int)(kChunk / kScanT);
+static constexpr int kCand = 8;                 // candidate entries per chunk
+static constexpr int kSet = 64;                 // distinct exits per chunk
+static constexpr uint64_t kTerm = 1ull << 63;   // link is terminal
+static constexpr uint64_t kPosMask = (1ull << 61) - 1;
+enum : uint64_t { kExit = 0, kEnd = 1, kDead = 2 };
+
+__device__ __forceinline__ uint64_t term(uint64_t type, uint64_t pos) { return kTerm | type << 61 | pos; }
+__device__ __forceinline__ uint64_t term_type(uint64_t v) { return (v >> 61) & 3; }
+__device__ __forceinline__ uint64_t term_pos(uint64_t v) { return v & kPosMask; }
+
+struct ScanArgs {
+    const uint8_t* wire;
+    uint64_t len;          // stream bytes
+    uint64_t start;        // offset of the first header
+    uint64_t nc;           // chunks (the last one, index nc, is virtual: positions >= len)
+    int strict;
+    uint32_t* ccount;      // nc + 1 candidate counters (zeroed per call)
+    uint64_t* cand;        // (nc + 1) * kCand candidate positions
+    int32_t* link;         // (nc + 1) * kCand: node -> next node, -1 = chain ends
+    uint64_t* nterm;       // (nc + 1) * kCand: the terminal where the chain ends (END / DEAD)
+    int32_t* lift;         // levels x (nc + 1) * kCand
+    int levels;
+    uint32_t* flags;       // [0] overflow, [1] root node
+    uint64_t* status;      // chained-scan status words (nc + 1)
+    uint32_t epoch;
+    uint64_t* hdr;         // outputs
+    uint32_t* keys;
+    uint8_t* b0;
+    uint64_t max_frames;
+    uint64_t* result;      // [0] frames, [1] consumed, [2] error offset or ~0
+};
+
+// One header at stream position p (bytes b[0..13] from p; bytes past len unused).
+// Returns the link: the next header position, or a terminal.
+template <typename Bytes>
+__device__ __forceinline__ uint64_t parse_at(const ScanArgs& a, uint64_t p, const Bytes& b, uint32_t* key_out,
+                                             uint8_t* b0_out) {
+    if (p + 2 > a.len) return term(kEnd, p);
+    const uint32_t first = b[0], second = b[1];
+    const uint32_t code = second & 0x7F, mask = second >> 7, opcode = first & 0x0F;
+    const uint64_t ext = code == 126 ? 2 : (code == 127 ? 8 : 0);
+    if (p + 2 + ext > a.len) return term(kEnd, p);
+    uint64_t plen = code;
+    if (ext == 2) plen = (uint64_t)b[2] << 8 | b[3];
+    if (ext == 8) {
+        plen = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) plen = plen << 8 | b[2 + i];
+    }
+    if (a.strict) {
+        const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
+        const bool control = opcode >= 8;
+        if (!mask || (first & 0x70) || reserved || (control && (!(first & 0x80) || plen > 125)) || (plen >> 63))
+            return term(kDead, p);
+    }
+    const uint64_t hl = 2 + ext + (mask ? 4 : 0);
+    if (p + hl > a.len || plen > a.len - (p + hl)) return term(kEnd, p);
+    if (key_out) {   // key bytes at 2 + ext (constant offsets: no dynamic indexing)
+        auto rd = [&](int o) {
+            return (uint32_t)b[o] | (uint32_t)b[o + 1] << 8 | (uint32_t)b[o + 2] << 16 | (uint32_t)b[o + 3] << 24;
+        };
+        *key_out = mask ? (ext == 0 ? rd(2) : (ext == 2 ? rd(4) : rd(10))) : 0u;
+        *b0_out = (uint8_t)first;
+    }
+    return p + hl + plen;
+}
+
+// K1 / K2 common part: chunk bytes into LDS, link every position, pointer-jump.
+// After it, lk[i] is terminal for every i: EXIT(x) with x >= chunk end, END(p) or DEAD(p).
+__device__ void chunk_links(const ScanArgs& a, uint64_t B, uint8_t* bytes, uint64_t* lk) {
+    const int tid = threadIdx.x;
+    // bytes [B, B + kChunk + 16), zero past len
+    for (uint64_t i = tid; i < kChunk + 16; i += kScanT) {
+        const uint64_t p = B + i;
+        bytes[i] = p < a.len ? gptr(a.wire)[p] : 0;
+    }
+    __syncthreads();
+    const uint64_t Bend = B + kChunk;
+#pragma unroll 4
+    for (int k = 0; k < kPer; ++k) {
+        const int i = k * kScanT + tid;
+        const uint64_t p = B + i;
+        uint64_t v;
+        if (p < a.start) {
+            v = term(kDead, p);   // before the first header: never on the chain
+        } else {
+            uint8_t hb[14];
+#pragma unroll
+            for (int j = 0; j < 14; ++j) hb[j] = bytes[i + j];
+            v = parse_at(a, p, hb, nullptr, nullptr);
+            if (!(v & kTerm)) v = v < Bend ? v - B : term(kExit, v);
+        }
+        lk[i] = v;
+    }
+    __syncthreads();
+    for (;;) {
+        int changed = 0;
+        for (int k = 0; k < kPer; ++k) {
+            const int i = k * kScanT + tid;
+            const uint64_t v = lk[i];
+            if (!(v & kTerm)) {
+                const uint64_t w = lk[v];
+                lk[i] = w;
+                changed |= !(w & kTerm);
+            }
+        }
+        if (!__syncthreads_or(changed)) break;
+    }
+}
+
+// K1: distinct exits of each chunk, appended to the candidate lists of the chunks
+// they land in; the stream start is the candidate (root) of its chunk.
+__global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
+    __shared__ uint8_t bytes[kChunk + 16];
+    __shared__ uint64_t lk[kChunk];
+    __shared__ unsigned long long set[kSet];
+    __shared__ int overflow;
+    const uint64_t chunk = blockIdx.x;
+    const uint64_t B = chunk * kChunk;
+    const int tid = threadIdx.x;
+    if (tid < kSet) set[tid] = ~0ull;
+    if (tid == 0) overflow = 0;
+    chunk_links(a, B, bytes, lk);
+    // dedup: a wave retires one distinct value per round (exits repeat a lot)
+    for (int k = 0; k < kPer; ++k) {
+        const uint64_t v = lk[k * kScanT + tid];
+        bool pending = (v & kTerm) && term_type(v) == kExit;
+        uint64_t x = term_pos(v);
+        while (__ballot(pending)) {
+            const int leader = __builtin_ctzll(__ballot(pending));
+            const uint64_t x0 = readlane64(x, leader);
+            if (pending && x == x0) pending = false;
+            if ((tid & (kWave - 1)) == leader) {
+                uint32_t h = (uint32_t)((x0 * 0x9E3779B97F4A7C15ull) >> 58);
+                int tries = 0;
+                for (; tries < kSet; ++tries, h = (h + 1) & (kSet - 1)) {
+                    const unsigned long long cur = set[h];
+                    if (cur == x0) break;
+                    if (cur == ~0ull) {
+                        const unsigned long long prev = atomicCAS(&set[h], ~0ull, (unsigned long long)x0);
+                        if (prev == ~0ull || prev == x0) break;
+                    }
+                }
+                if (tries == kSet) overflow = 1;
+            }
+        }
+    }
+    __syncthreads();
+    auto append = [&](uint64_t x) {
+        const uint64_t t = x / kChunk;   // x <= len: t <= nc
+        const uint32_t slot = atomicAdd(&a.ccount[t], 1u);
+        if (slot < (uint32_t)kCand) a.cand[t * kCand + slot] = x;
+        else atomicOr(&a.flags[0], 1u);
+    };
+    if (tid < kSet && set[tid] != ~0ull) append(set[tid]);
+    if (tid == 0) {
+        if (overflow) atomicOr(&a.flags[0], 1u);
+        if (a.start / kChunk == chunk) append(a.start);
+    }
+}
+
+// K2: for each candidate entry of the chunk, the candidate its chain exits to.
+__global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
+    __shared__ uint8_t bytes[kChunk + 16];
+    __shared__ uint64_t lk[kChunk];
+    const uint64_t chunk = blockIdx.x;
+    const uint64_t B = chunk * kChunk;
+    const uint32_t nc_here = min(a.ccount[chunk], (uint32_t)kCand);
+    if (nc_here == 0) return;   // uniform per block
+    chunk_links(a, B, bytes, lk);
+    const int tid = threadIdx.x;
+    if (tid < (int)nc_here) {
+        const uint64_t node = chunk * kCand + tid;
+        const uint64_t x = a.cand[node];
+        if (x == a.start) a.flags[1] = (uint32_t)node;
+        const uint64_t v = x - B < kChunk ? lk[x - B] : term(kEnd, x);   // x == len on a chunk edge
+        int32_t next = -1;
+        if (term_type(v) == kExit) {
+            const uint64_t y = term_pos(v), t = y / kChunk;
+            const uint32_t cnt = min(a.ccount[t], (uint32_t)kCand);
+            for (uint32_t i = 0; i < cnt; ++i)
+                if (a.cand[t * kCand + i] == y) next = (int32_t)(t * kCand + i);
+            if (next < 0) atomicOr(&a.flags[0], 1u);   // its bucket overflowed
+        }
+        a.link[node] = next;
+        a.nterm[node] = v;
+    }
+}
+
+// K3: lift[k+1][v] = lift[k][lift[k][v]]   (lift[0] = link)
+__global__ void scan_lift(const int32_t* src, int32_t* dst, uint64_t nodes) {
+    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nodes) return;
+    const int32_t u = src[v];
+    dst[v] = u < 0 ? -1 : src[u];
+}
+
+// Walk the true frames of a chunk from its entry e (in LDS bytes), calling emit
+// for each complete frame; returns the terminal where the walk left the chunk.
+template <typename F>
+__device__ uint64_t walk_chunk(const ScanArgs& a, uint64_t B, const uint8_t* bytes, uint64_t e, F&& emit) {
+    uint64_t p = e;
+    const uint64_t Bend = B + kChunk;
+    while (p < Bend) {
+        uint32_t key;
+        uint8_t b0;
+        const uint64_t v = parse_at(a, p, bytes + (p - B), &key, &b0);   // LDS, 16 bytes of lookahead
+        if (v & kTerm) return v;
+        emit(p, key, b0);
+        p = v;
+    }
+    return term(kExit, p);
+}
+
+__device__ __forceinline__ uint64_t cand_pos(const ScanArgs& a, int32_t node) { return a.cand[node]; }
+
+// K4: one wavefront per chunk.
+__global__ __launch_bounds__(64) void scan_emit(ScanArgs a) {
+    __shared__ uint8_t bytes[kChunk + 16];
+    const uint64_t chunk = blockIdx.x;
+    const uint64_t B = chunk * kChunk;
+    const int lane = threadIdx.x;
+    const bool overflow = __hip_atomic_load(&a.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (overflow) {
+        // serial fallback: wavefront 0 walks the whole stream from global memory
+        if (chunk != 0) return;
+        if (lane == 0) {
+            uint64_t p = a.start, n = 0, err = ~0ull;
+            for (;;) {
+                uint8_t hb[14];
+#pragma unroll
+                for (int j = 0; j < 14; ++j) hb[j] = p + j < a.len ? a.wire[p + j] : 0;
+                uint32_t key;
+                uint8_t b0;
+                const uint64_t v = parse_at(a, p, hb, &key, &b0);
+                if (v & kTerm) {
+                    if (term_type(v) == kDead) err = p;
+                    break;
+                }
+                if (n < a.max_frames) {
+                    a.hdr[n] = p;
+                    a.keys[n] = key;
+                    a.b0[n] = b0;
+                }
+                ++n;
+                p = v;
+            }
+            if (n <= a.max_frames) a.hdr[n] = p;
+            a.result[0] = n;
+            a.result[1] = p;
+            a.result[2] = err;
+        }
+        return;
+    }
+    // the true entry of this chunk: last node of the chain from the root before the chunk end
+    int64_t entry = -1;
+    {
+        int32_t v = (int32_t)a.flags[1];
+        const uint64_t bound = B + kChunk;
+        if (cand_pos(a, v) < bound) {
+            for (int k = a.levels - 1; k >= 0; --k) {
+                const int32_t u = a.lift[(uint64_t)k * (a.nc + 1) * kCand + v];
+                if (u >= 0 && cand_pos(a, u) < bound) v = u;
+            }
+            if (cand_pos(a, v) >= B) entry = (int64_t)cand_pos(a, v);
+        }
+    }
+    uint64_t count = 0;
+    uint64_t stop = 0;
+    if (entry >= 0) {
+        for (uint64_t i = lane; i < kChunk + 16; i += 64) bytes[i] = B + i < a.len ? gptr(a.wire)[B + i] : 0;
+        __syncthreads();
+        if (lane == 0) stop = walk_chunk(a, B, bytes, (uint64_t)entry, [&](uint64_t, uint32_t, uint8_t) { ++count; });
+    }
+    // chained scan of the frame counts (lane 0 publishes and looks back)
+    uint64_t base = 0;
+    if (lane == 0) {
+        const uint64_t kV = (1ull << 46) - 1;
+        auto word = [&](uint64_t flag, uint64_t v) { return flag << 62 | (uint64_t)(a.epoch & 0xFFFF) << 46 | (v & kV); };
+        if (chunk == 0) {
+            __hip_atomic_store(&a.status[0], word(2, count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&a.status[chunk], word(1, count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int64_t p = (int64_t)chunk - 1; p >= 0;) {
+                const uint64_t w = __hip_atomic_load(&a.status[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((w >> 62) == 0 || ((w >> 46) & 0xFFFF) != (a.epoch & 0xFFFF)) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                base += w & kV;
+                if ((w >> 62) == 2) break;
+                --p;
+            }
+            __hip_atomic_store(&a.status[chunk], word(2, base + count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (chunk == a.nc) a.result[0] = base + count;
+        if (entry >= 0) {
+            uint64_t k = base;
+            walk_chunk(a, B, bytes, (uint64_t)entry, [&](uint64_t p, uint32_t key, uint8_t b0) {
+                if (k < a.max_frames) {
+                    a.hdr[k] = p;
+                    a.keys[k] = key;
+                    a.b0[k] = b0;
+                }
+                ++k;
+            });
+            if (term_type(stop) != kExit) {   // the chain ends in this chunk
+                const uint64_t end = term_pos(stop);
+                a.result[1] = end;
+                a.result[2] = term_type(stop) == kDead ? end : ~0ull;
+                if (k <= a.max_frames) a.hdr[k] = end;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ launch --
+
+struct ScanScratchSet {
+    void* mem = nullptr;
+    uint64_t bytes = 0;
+    uint32_t epoch = 0;
+};
+
+hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start, bool strict, uint64_t* hdr,
+                              uint32_t* keys, uint8_t* b0, uint64_t max_frames, uint64_t* result,
+                              hipStream_t stream) {
+    ScanArgs a;
+    a.wire = wire;
+    a.len = len;
+    a.start = start;
+    a.strict = strict ? 1 : 0;
+    a.nc = (len + kChunk - 1) / kChunk;   // real chunks 0 .. nc-1; chunk nc is virtual (positions >= len)
+    const uint64_t chunks = a.nc + 1, nodes = chunks * kCand;
+    int levels = 1;
+    while ((1ull << levels) < chunks + 1) ++levels;
+    a.levels = levels;
+    a.hdr = hdr;
+    a.keys = keys;
+    a.b0 = b0;
+    a.max_frames = max_frames;
+    a.result = result;
+    // scratch layout, per (device, stream)
+    const uint64_t need = chunks * 4 + nodes * 8 + nodes * 4 + nodes * 8 + (uint64_t)levels * nodes * 4 + 16 +
+                          chunks * 8 + 64 * 5;
+    static std::map<std::pair<int, hipStream_t>, ScanScratchSet> scratch;
+    static std::mutex mu;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    uint8_t* m;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        ScanScratchSet& s = scratch[{dev, stream}];
+        if (s.bytes < need) {
+            void* p = nullptr;
+            uint64_t want = s.bytes ? 2 * s.bytes : (1ull << 20);
+            while (want < need) want *= 2;
+            if ((e = hipMalloc(&p, want)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(p, 0, want, stream)) != hipSuccess) return e;   // status words: epoch 0
+            s.mem = p;
+            s.bytes = want;
+            s.epoch = 0;
+        }
+        s.epoch = (s.epoch + 1) & 0xFFFF;
+        m = (uint8_t*)s.mem;
+        auto align = [](uint64_t x) { return (x + 63) & ~63ull; };
+        uint64_t o = 0;
+        a.ccount = (uint32_t*)(m + o); o = align(o + chunks * 4);
+        a.flags = (uint32_t*)(m + o); o = align(o + 16);
+        a.cand = (uint64_t*)(m + o); o = align(o + nodes * 8);
+        a.link = (int32_t*)(m + o); o = align(o + nodes * 4);
+        a.nterm = (uint64_t*)(m + o); o = align(o + nodes * 8);
+        a.status = (uint64_t*)(m + o); o = align(o + chunks * 8);
+        a.lift = (int32_t*)(m + o);
+        if (s.epoch == 0) {   // epochs wrapped: clear the status words
+            if ((e = hipMemsetAsync(a.status, 0, chunks * 8, stream)) != hipSuccess) return e;
+            s.epoch = 1;
+        }
+        a.epoch = s.epoch;
+    }
+    // counters + flags, and the default results (no frames, nothing consumed past start)
+    if ((e = hipMemsetAsync(a.ccount, 0, chunks * 4, stream)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.flags, 0, 16, stream)) != hipSuccess) return e;
+    hipLaunchKernelGGL(scan_exits, dim3((unsigned)chunks), dim3(kScanT), 0, stream, a);
+    hipLaunchKernelGGL(scan_links, dim3((unsigned)chunks), dim3(kScanT), 0, stream, a);
+    // lift[0] = link, then doublings
+    if ((e = hipMemcpyAsync(a.lift, a.link, nodes * 4, hipMemcpyDeviceToDevice, stream)) != hipSuccess) return e;
+    const unsigned lb = (unsigned)((nodes + 255) / 256);
+    for (int k = 0; k + 1 < levels; ++k)
+        hipLaunchKernelGGL(scan_lift, dim3(lb), dim3(256), 0, stream, a.lift + (uint64_t)k * nodes,
+                           a.lift + (uint64_t)(k + 1) * nodes, nodes);
+    hipLaunchKernelGGL(scan_emit, dim3((unsigned)chunks), dim3(64), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace netc_gpu

@@ -211,6 +211,26 @@ def encode_frames(wire, wire_offsets, src, offsets, keys=None, header0=None, mas
                                              1 if masked else 0, _stream_handle(stream)))
 
 
+NETC_WS_SCAN_STRICT = 1
+
+
+def scan_frames(wire, hdr, keys, b0, result, start: int = 0, strict: bool = True, length: Optional[int] = None,
+                stream=None, device: Optional[int] = None) -> None:
+    """netc_gpu_scan_frames: frame boundaries of the device stream `wire` (uint8 tensor).
+
+    hdr: int64 (max_frames + 1), keys: int32 (max_frames), b0: uint8 (max_frames), result: int64 (3)
+    receives [frames, consumed, error offset or -1 (UINT64_MAX)].  Asynchronous on `stream`.
+    """
+    n = wire.numel() if length is None else int(length)
+    max_frames = hdr.numel() - 1
+    if keys.numel() < max_frames or b0.numel() < max_frames or result.numel() < 3:
+        raise ValueError("output tensors too small")
+    dev = wire.device.index if device is None else device
+    _check(_lib.gpu().netc_gpu_scan_frames(dev, wire.data_ptr(), n, start, NETC_WS_SCAN_STRICT if strict else 0,
+                                           hdr.data_ptr(), keys.data_ptr(), b0.data_ptr(), max_frames,
+                                           result.data_ptr(), _stream_handle(stream)))
+
+
 def mask_stream_host(dst: np.ndarray, src: np.ndarray, offsets: np.ndarray, keys: np.ndarray,
                      slot_bytes: int = 256 << 20, nslots: int = 4, device: int = 0) -> None:
     """netc_gpu_mask_stream_host: host buffers through pinned slots on overlapped streams."""

@@ -1,0 +1,157 @@
+"""GPU parity: netc_gpu_scan_frames (device frame-boundary scan, include/ws/frame.h) vs the oracle.
+
+The checker is oracle_scan_frames (the header decode of src/ws/common.c:146-296
+walked over the stream; pinned in tests/test_scan_oracle.py by the reference's
+golden wire and its compiled receiver).  The bar: identical header offsets, keys,
+header bytes, frame count, consumed offset and error offset.
+"""
+
+import numpy as np
+import pytest
+
+from netc_amd import mask as nm
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def frames_from_sizes(sizes, start=0):
+    off = np.zeros(len(sizes) + 1, dtype=np.uint64)
+    off[0] = start
+    off[1:] = start + np.cumsum(np.asarray(sizes, dtype=np.uint64))
+    return off
+
+
+def run_scan(torch, wire: np.ndarray, start=0, strict=True, max_frames=None):
+    exp_hdr, exp_keys, exp_b0, exp_consumed, exp_err = orc.scan_frames(wire, start=start, strict=strict)
+    n = exp_hdr.size
+    cap = n if max_frames is None else max_frames
+    w = torch.from_numpy(np.ascontiguousarray(wire)).cuda() if wire.size else torch.zeros(1, dtype=torch.uint8,
+                                                                                          device="cuda")
+    hdr = torch.full((cap + 1,), -7, dtype=torch.int64, device="cuda")
+    keys = torch.zeros(max(cap, 1), dtype=torch.int32, device="cuda")
+    b0 = torch.zeros(max(cap, 1), dtype=torch.uint8, device="cuda")
+    res = torch.full((3,), -7, dtype=torch.int64, device="cuda")
+    nm.scan_frames(w, hdr, keys, b0, res, start=start, strict=strict, length=wire.size)
+    torch.cuda.synchronize()
+    r = res.cpu().numpy().view(np.uint64)
+    assert int(r[0]) == n, f"frames {int(r[0])} != {n}"
+    assert int(r[1]) == exp_consumed, f"consumed {int(r[1])} != {exp_consumed}"
+    assert (None if int(r[2]) == (1 << 64) - 1 else int(r[2])) == exp_err
+    k = min(n, cap)
+    got_hdr = hdr.cpu().numpy().view(np.uint64)
+    assert np.array_equal(got_hdr[:k], exp_hdr[:k]), f"header offsets differ at {np.nonzero(got_hdr[:k] != exp_hdr[:k])[0][:4]}"
+    assert np.array_equal(keys.cpu().numpy().view(np.uint32)[:k], exp_keys[:k])
+    assert np.array_equal(b0.cpu().numpy()[:k], exp_b0[:k])
+    if n <= cap:
+        assert int(got_hdr[n]) == exp_consumed
+    return n
+
+
+def _stream(rng, sizes, masked=True, b0=None):
+    off = frames_from_sizes(sizes)
+    payload = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    keys = rng.integers(0, 2**32, len(sizes), dtype=np.uint64).astype(np.uint32)
+    wire, wo = orc.encode_batch(payload, off, keys, b0, masked)
+    return wire, wo
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_mixed_sizes(torch_cuda, seed):
+    rng = np.random.default_rng(seed)
+    sizes = np.concatenate([rng.integers(0, 5000, 300), rng.integers(0, 130, 300), [65535, 65536, 200000]])
+    rng.shuffle(sizes)
+    wire, _ = _stream(rng, sizes)
+    assert run_scan(torch_cuda, wire) == sizes.size
+
+
+def test_c2_shape(torch_cuda):
+    rng = np.random.default_rng(2)
+    wire, _ = _stream(rng, np.full(65536, 1024))
+    assert run_scan(torch_cuda, wire) == 65536
+
+
+def test_c4_shape_64mib(torch_cuda):
+    rng = np.random.default_rng(4)
+    wire, _ = _stream(rng, rng.integers(256, 65537, 2000))
+    assert run_scan(torch_cuda, wire) == 2000
+
+
+def test_tiny_frames(torch_cuda):
+    # 6-byte wire frames (empty masked payloads) and 1-3 byte payloads: long chains inside a chunk
+    rng = np.random.default_rng(5)
+    wire, _ = _stream(rng, rng.integers(0, 4, 20000))
+    assert run_scan(torch_cuda, wire) == 20000
+
+
+def test_truncated_streams(torch_cuda):
+    rng = np.random.default_rng(6)
+    wire, wo = _stream(rng, rng.integers(0, 9000, 200))
+    for cut in [0, 1, 2, 5, int(wo[50]) - 1, int(wo[50]), int(wo[50]) + 1, int(wo[50]) + 3, int(wo[120]) + 7,
+                wire.size - 1, wire.size]:
+        run_scan(torch_cuda, wire[:cut])
+
+
+def test_start_offset(torch_cuda):
+    rng = np.random.default_rng(7)
+    wire, wo = _stream(rng, rng.integers(0, 9000, 200))
+    for s in (int(wo[1]), int(wo[77]), int(wo[199]), wire.size):
+        run_scan(torch_cuda, wire, start=s)
+
+
+def test_unmasked_and_non_strict(torch_cuda):
+    rng = np.random.default_rng(8)
+    wire, _ = _stream(rng, rng.integers(0, 3000, 300), masked=False)
+    assert run_scan(torch_cuda, wire, strict=False) == 300
+    assert run_scan(torch_cuda, wire, strict=True) == 0   # the first unmasked header is rejected
+
+
+def test_strict_errors_mid_stream(torch_cuda):
+    rng = np.random.default_rng(9)
+    good, _ = _stream(rng, rng.integers(0, 6000, 100))
+    for bad in (bytes.fromhex("8105") + b"Hello", bytes.fromhex("c185") + bytes(9), bytes.fromhex("0980") + bytes(4),
+                bytes.fromhex("83850000000048656c6c6f")):
+        wire = np.concatenate([good, np.frombuffer(bad, dtype=np.uint8), good])
+        run_scan(torch_cuda, wire, strict=True)
+        run_scan(torch_cuda, wire, strict=False)
+
+
+def test_header_byte_variants(torch_cuda):
+    rng = np.random.default_rng(10)
+    sizes = rng.integers(0, 125, 500)
+    b0 = rng.choice(np.array([0x81, 0x82, 0x01, 0x00, 0x80, 0x89, 0x8A, 0x88], dtype=np.uint8), 500)
+    wire, _ = _stream(rng, sizes, b0=b0)
+    assert run_scan(torch_cuda, wire) == 500
+
+
+def test_max_frames_cap(torch_cuda):
+    rng = np.random.default_rng(11)
+    wire, _ = _stream(rng, rng.integers(0, 2000, 400))
+    run_scan(torch_cuda, wire, max_frames=100)
+    run_scan(torch_cuda, wire, max_frames=0)
+
+
+def test_adversarial_payload_falls_back(torch_cuda):
+    # a big frame masked with the zero key whose payload is a run of valid-looking
+    # 8-byte headers (16-bit lengths 5000..5996) that each jump to a different place:
+    # hundreds of distinct exits per chunk (capacity overflow -> the serial walk)
+    rng = np.random.default_rng(12)
+    rec = b"".join(bytes.fromhex("82fe") + (5000 + i % 997).to_bytes(2, "big") + bytes(4) for i in range(997))
+    inner = np.tile(np.frombuffer(rec, dtype=np.uint8), 40)
+    off = np.array([0, inner.size, inner.size + 10], dtype=np.uint64)
+    payload = np.concatenate([inner, rng.integers(0, 256, 10, dtype=np.uint8)])
+    wire, _ = orc.encode_batch(payload, off, np.array([0, 0x01020304], dtype=np.uint32), None, True)
+    assert run_scan(torch_cuda, wire) == 2
+
+
+def test_empty(torch_cuda):
+    run_scan(torch_cuda, np.zeros(0, dtype=np.uint8))
+    run_scan(torch_cuda, np.zeros(1, dtype=np.uint8))
+
+
+def test_repeat_calls_same_stream(torch_cuda):
+    # the chained scan's status words are reused across calls (epochs)
+    rng = np.random.default_rng(13)
+    for i in range(5):
+        wire, _ = _stream(rng, rng.integers(0, 4000, 300 + 50 * i))
+        run_scan(torch_cuda, wire)
