@@ -129,10 +129,10 @@ def encode_batch(payload, offsets: np.ndarray, keys32: Optional[np.ndarray], hea
     return out[:w], wo
 
 
-def scan_frames(wire, start: int = 0, strict: bool = True, opt: str = "O2"):
+def scan_frames(wire, start: int = 0, strict: bool = True, opt: str = "O2", cap: Optional[int] = None):
     """oracle_scan_frames: (header offsets, packed keys, byte 0s, consumed, error or None) of a byte stream."""
     w = _u8(wire)
-    cap = max(1, w.size // 2 + 1)
+    cap = max(1, w.size // 2 + 1) if cap is None else max(1, cap)
     hdr = np.zeros(cap, dtype=np.uint64)
     keys = np.zeros(cap, dtype=np.uint32)
     b0 = np.zeros(cap, dtype=np.uint8)
