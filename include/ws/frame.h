@@ -103,6 +103,17 @@ int netc_gpu_encode_frames(int device, void *d_wire, size_t wire_capacity, uint6
 int netc_gpu_scan_frames(int device, const void *d_wire, size_t len, uint64_t start, int flags, uint64_t *d_hdr,
                          uint32_t *d_keys, uint8_t *d_b0, size_t max_frames, uint64_t *d_result, void *stream);
 
+/**
+ * Unmask, in place, the payloads of the frames a netc_gpu_scan_frames call found
+ * in d_wire (the reference's unmask loop, src/ws/common.c:317-323, for every
+ * frame of the stream at once); header bytes and bytes past the last recorded
+ * frame are left as they are.  d_hdr / d_keys / max_frames / d_result are that
+ * call's outputs, read on the device: queue this on the same stream right after
+ * the scan, no synchronisation needed.  Frames beyond max_frames are not unmasked.
+ */
+int netc_gpu_unmask_frames(int device, void *d_wire, size_t len, const uint64_t *d_hdr, const uint32_t *d_keys,
+                           size_t max_frames, const uint64_t *d_result, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -213,6 +213,21 @@ int netc_gpu_scan_frames(int device, const void* d_wire, size_t len, uint64_t st
     return 0;
 }
 
+int netc_gpu_unmask_frames(int device, void* d_wire, size_t len, const uint64_t* d_hdr, const uint32_t* d_keys,
+                           size_t max_frames, const uint64_t* d_result, void* stream) {
+    if (int r = check_device(device)) return r;
+    if (!d_hdr || !d_result || (max_frames && !d_keys)) return fail(NETC_GPU_EINVAL, "null scan output");
+    if (len == 0) return 0;
+    if (!d_wire) return fail(NETC_GPU_EINVAL, "null stream");
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+    hipError_t e = netc_gpu::launch_unmask_scanned((uint8_t*)d_wire, len, d_hdr, d_keys, max_frames, d_result,
+                                                   (hipStream_t)stream, g_cfg);
+    if (e == hipErrorOutOfMemory) return fail_hip(NETC_GPU_ENOMEM, "unmask view scratch", e);
+    if (e != hipSuccess) return fail_hip(NETC_GPU_ELAUNCH, "unmask launch", e);
+    return 0;
+}
+
 // ---------------------------------------------------------------------------
 // Host → device → host pipeline (BASELINE config 5).  Slots are fixed byte
 // ranges of the payload; a frame cut by a slot edge continues in the next slot

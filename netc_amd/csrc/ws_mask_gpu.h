@@ -19,6 +19,7 @@ struct Args {
     uint64_t mis;              // dst & 15
     uint64_t nwin;             // windows (chunks) of U KiB covering [0, mis + total)
     double density;            // n / total: frames per payload byte (table-base guesses)
+    const uint64_t* n_dev;     // if set: the frame count is read from device memory at kernel start
 };
 
 enum : int { kNtLoads = 1, kNtStores = 2 };   // LaunchCfg::flags (NETC_GPU_TUNE_NT_*)
@@ -30,7 +31,8 @@ struct LaunchCfg {
 };
 
 hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,
-                              const uint32_t* keys, uint64_t n, hipStream_t stream, const LaunchCfg& cfg);
+                              const uint32_t* keys, uint64_t n, hipStream_t stream, const LaunchCfg& cfg,
+                              const uint64_t* n_dev = nullptr);
 
 // ws_frame_gpu.hip: wire offsets (n + 1 entries into wo), then the wire bytes of
 // every frame (header, key, masked payload) into wire.  wire_bound >= wo[n].
@@ -39,6 +41,9 @@ hipError_t launch_wire_offsets(const uint64_t* off, uint64_t n, bool masked, uin
 hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start, bool strict, uint64_t* hdr,
                               uint32_t* keys, uint8_t* b0, uint64_t max_frames, uint64_t* result,
                               hipStream_t stream);
+hipError_t launch_unmask_scanned(uint8_t* wire, uint64_t len, const uint64_t* hdr, const uint32_t* keys,
+                                 uint64_t max_frames, const uint64_t* result, hipStream_t stream,
+                                 const LaunchCfg& cfg);
 
 hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_t* src, uint64_t src_total,
                                 const uint64_t* off, const uint32_t* keys, const uint8_t* b0, uint64_t n, bool masked,

@@ -281,6 +281,10 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
     const uint32_t wpb = blockDim.x / kWave;                     // wavefronts per block
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     const uint64_t wave = (uint64_t)blockIdx.x * wpb + (threadIdx.x / kWave);
+    if (a.n_dev) {   // frame count produced on the device by an earlier kernel (scan -> unmask)
+        a.n = *gptr(a.n_dev);
+        a.density = a.total ? (double)a.n / (double)a.total : 0.0;
+    }
 #ifdef NETC_MASK_STAMPS
     // diagnostic build only (tools/): per-wave start / end wall clock (100 MHz)
     const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
@@ -395,14 +399,17 @@ static hipError_t launch_nt(const Args& a, bool nt, int max_blocks, hipStream_t 
 }
 
 hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,
-                              const uint32_t* keys, uint64_t n, hipStream_t stream, const LaunchCfg& cfg) {
+                              const uint32_t* keys, uint64_t n, hipStream_t stream, const LaunchCfg& cfg,
+                              const uint64_t* n_dev) {
+    // n_dev: n is only an upper bound here (keys must then always be readable)
     Args a;
+    a.n_dev = n_dev;
     a.mis = (uint64_t)(uintptr_t)dst & 15u;
     a.dst_base = dst - a.mis;
     a.src_base = src - a.mis;
     a.total = total;
     a.off = off;
-    a.keys = n ? keys : reinterpret_cast<const uint32_t*>(off);   // frame_entry always reads keys[0]
+    a.keys = (n || n_dev) ? keys : reinterpret_cast<const uint32_t*>(off);   // frame_entry always reads keys[0]
     a.n = n;
     const bool aligned = (((uintptr_t)src ^ (uintptr_t)dst) & 15u) == 0;
     const int U = aligned ? cfg.unroll : 4;

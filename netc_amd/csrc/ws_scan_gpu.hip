@@ -356,6 +356,75 @@ __global__ __launch_bounds__(64) void scan_emit(ScanArgs a) {
     }
 }
 
+// In-place unmask of scanned frames: the "mask view" of the stream as the batch
+// kernel takes it -- 2 n frames alternating header (key 0, passed through) and
+// payload (the frame's key), closed at the last payload's end.  n is read from the
+// scan's result on the device, so scan -> view -> mask needs no host round trip.
+__global__ void scan_view(const uint8_t* wire, const uint64_t* hdr, const uint32_t* keys, uint64_t max_frames,
+                          const uint64_t* result, uint64_t* voff, uint32_t* vkey, uint64_t* vn) {
+    const uint64_t n = min(result[0], max_frames);
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 0) {
+        *vn = 2 * n;
+        if (n == 0) voff[0] = 0;
+    }
+    if (k >= n) return;
+    const uint64_t p = hdr[k];
+    const uint32_t second = wire[p + 1];
+    const uint32_t code = second & 0x7F, mask = second >> 7;
+    const uint64_t ext = code == 126 ? 2 : (code == 127 ? 8 : 0);
+    uint64_t plen = code;
+    if (ext) {
+        plen = 0;
+        for (uint64_t i = 0; i < ext; ++i) plen = plen << 8 | wire[p + 2 + i];
+    }
+    const uint64_t ps = p + 2 + ext + (mask ? 4 : 0);
+    voff[2 * k] = p;
+    voff[2 * k + 1] = ps;
+    vkey[2 * k] = 0;
+    vkey[2 * k + 1] = keys[k];
+    if (k == n - 1) voff[2 * n] = ps + plen;
+}
+
+struct ViewScratch {
+    uint64_t* voff = nullptr;
+    uint32_t* vkey = nullptr;
+    uint64_t* vn = nullptr;
+    uint64_t frames = 0;
+};
+
+hipError_t launch_unmask_scanned(uint8_t* wire, uint64_t len, const uint64_t* hdr, const uint32_t* keys,
+                                 uint64_t max_frames, const uint64_t* result, hipStream_t stream,
+                                 const LaunchCfg& cfg) {
+    static std::map<std::pair<int, hipStream_t>, ViewScratch> scratch;
+    static std::mutex mu;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    ViewScratch v;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        ViewScratch& s = scratch[{dev, stream}];
+        if (s.frames < max_frames || !s.voff) {
+            uint64_t want = s.frames ? 2 * s.frames : 4096;
+            while (want < max_frames) want *= 2;
+            void *a = nullptr, *b = nullptr;
+            if ((e = hipMalloc(&a, (2 * want + 2) * sizeof(uint64_t))) != hipSuccess) return e;
+            if ((e = hipMalloc(&b, (2 * want + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+            s.voff = (uint64_t*)a;
+            s.vn = s.voff + 2 * want + 1;
+            s.vkey = (uint32_t*)b;
+            s.frames = want;
+        }
+        v = s;
+    }
+    const uint64_t threads = max_frames ? max_frames : 1;
+    hipLaunchKernelGGL(scan_view, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, wire, hdr, keys,
+                       max_frames, result, v.voff, v.vkey, v.vn);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return launch_mask_frames(wire, wire, len, v.voff, v.vkey, 2 * max_frames, stream, cfg, v.vn);
+}
+
 // ------------------------------------------------------------------ launch --
 
 struct ScanScratchSet {

@@ -231,6 +231,15 @@ def scan_frames(wire, hdr, keys, b0, result, start: int = 0, strict: bool = True
                                            result.data_ptr(), _stream_handle(stream)))
 
 
+def unmask_frames(wire, hdr, keys, result, length: Optional[int] = None, stream=None,
+                  device: Optional[int] = None) -> None:
+    """netc_gpu_unmask_frames: unmask in place the payloads scan_frames found (outputs read on the device)."""
+    n = wire.numel() if length is None else int(length)
+    dev = wire.device.index if device is None else device
+    _check(_lib.gpu().netc_gpu_unmask_frames(dev, wire.data_ptr(), n, hdr.data_ptr(), keys.data_ptr(),
+                                             hdr.numel() - 1, result.data_ptr(), _stream_handle(stream)))
+
+
 def mask_stream_host(dst: np.ndarray, src: np.ndarray, offsets: np.ndarray, keys: np.ndarray,
                      slot_bytes: int = 256 << 20, nslots: int = 4, device: int = 0) -> None:
     """netc_gpu_mask_stream_host: host buffers through pinned slots on overlapped streams."""

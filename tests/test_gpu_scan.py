@@ -149,6 +149,40 @@ def test_empty(torch_cuda):
     run_scan(torch_cuda, np.zeros(1, dtype=np.uint8))
 
 
+@pytest.mark.parametrize("cut", [None, -3])
+def test_scan_then_unmask_in_place(torch_cuda, cut):
+    # the whole receive path on the device: scan -> unmask, no host round trip;
+    # every payload byte equals the plaintext, every header byte (and the partial
+    # frame at the end) is untouched
+    torch = torch_cuda
+    rng = np.random.default_rng(14)
+    sizes = np.concatenate([rng.integers(0, 3000, 500), [0, 1, 125, 126, 65536]])
+    off = frames_from_sizes(sizes)
+    plain = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    keys = rng.integers(0, 2**32, sizes.size, dtype=np.uint64).astype(np.uint32)
+    wire, wo = orc.encode_batch(plain, off, keys, None, True)
+    if cut is not None:
+        wire = wire[:cut]
+    n = sizes.size
+    w = torch.from_numpy(wire.copy()).cuda()
+    hdr = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    kk = torch.zeros(n, dtype=torch.int32, device="cuda")
+    b0 = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    res = torch.zeros(3, dtype=torch.int64, device="cuda")
+    nm.scan_frames(w, hdr, kk, b0, res)
+    nm.unmask_frames(w, hdr, kk, res)
+    torch.cuda.synchronize()
+    got = w.cpu().numpy()
+    found = int(res.cpu()[0])
+    assert found == (n if cut is None else n - 1)
+    expect = wire.copy()
+    for k in range(found):   # payload region of frame k = its last len bytes before the next header
+        lo, hi = int(off[k]), int(off[k + 1])
+        p_end = int(wo[k + 1])
+        expect[p_end - (hi - lo): p_end] = plain[lo:hi]
+    assert np.array_equal(got, expect)
+
+
 def test_repeat_calls_same_stream(torch_cuda):
     # the chained scan's status words are reused across calls (epochs)
     rng = np.random.default_rng(13)
