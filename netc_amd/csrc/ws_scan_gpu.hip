@@ -107,6 +107,16 @@ __device__ __forceinline__ uint64_t parse_at(const ScanArgs& a, uint64_t p, cons
     return p + hl + plen;
 }
 
+// Strict mode: can a header start at x at all?  (The two first bytes fail the
+// checks.)  A chain reaching such an x dies there: DEAD(x).
+__device__ __forceinline__ bool quick_reject(const ScanArgs& a, uint64_t x) {
+    if (!a.strict || x + 2 > a.len) return false;
+    const uint32_t first = gptr(a.wire)[x], second = gptr(a.wire)[x + 1];
+    const uint32_t opcode = first & 0x0F;
+    const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
+    return !(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80));
+}
+
 // K1 / K2 common part: chunk bytes into LDS, link every position, pointer-jump.
 // After it, lk[i] is terminal for every i: EXIT(x) with x >= chunk end, END(p) or DEAD(p).
 __device__ void chunk_links(const ScanArgs& a, uint64_t B, uint8_t* bytes, uint64_t* lk) {
@@ -194,7 +204,11 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
         if (slot < (uint32_t)kCand) a.cand[t * kCand + slot] = x;
         else atomicOr(&a.flags[0], 1u);
     };
-    if (tid < kSet && set[tid] != ~0ull) append(set[tid]);
+    // Strict mode prunes exits that cannot start a frame (2 header bytes fail the
+    // checks): payload bytes parsed as a chain land on random positions, and a
+    // random position passes with ~2 % odds, while the true chain always lands on
+    // a real header.  This keeps the candidate lists at about one entry per chunk.
+    if (tid < kSet && set[tid] != ~0ull && !quick_reject(a, set[tid])) append(set[tid]);
     if (tid == 0) {
         if (overflow) atomicOr(&a.flags[0], 1u);
         if (a.start / kChunk == chunk) append(a.start);
@@ -208,9 +222,11 @@ __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
     const uint64_t chunk = blockIdx.x;
     const uint64_t B = chunk * kChunk;
     const uint32_t nc_here = min(a.ccount[chunk], (uint32_t)kCand);
+    const int tid = threadIdx.x;
+    // unused node slots hold stale values from earlier calls: make them dead ends
+    if (tid >= (int)nc_here && tid < kCand) a.link[chunk * kCand + tid] = -1;
     if (nc_here == 0) return;   // uniform per block
     chunk_links(a, B, bytes, lk);
-    const int tid = threadIdx.x;
     if (tid < (int)nc_here) {
         const uint64_t node = chunk * kCand + tid;
         const uint64_t x = a.cand[node];
@@ -222,7 +238,8 @@ __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
             const uint32_t cnt = min(a.ccount[t], (uint32_t)kCand);
             for (uint32_t i = 0; i < cnt; ++i)
                 if (a.cand[t * kCand + i] == y) next = (int32_t)(t * kCand + i);
-            if (next < 0) atomicOr(&a.flags[0], 1u);   // its bucket overflowed
+            // not a candidate: pruned by K1 (the chain dies at y), or its bucket overflowed
+            if (next < 0 && !quick_reject(a, y)) atomicOr(&a.flags[0], 1u);
         }
         a.link[node] = next;
         a.nterm[node] = v;
@@ -234,7 +251,7 @@ __global__ void scan_lift(const int32_t* src, int32_t* dst, uint64_t nodes) {
     const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= nodes) return;
     const int32_t u = src[v];
-    dst[v] = u < 0 ? -1 : src[u];
+    dst[v] = (u < 0 || (uint64_t)u >= nodes) ? -1 : src[u];   // (range check: defence in depth)
 }
 
 // Walk the true frames of a chunk from its entry e (in LDS bytes), calling emit
@@ -346,7 +363,9 @@ __global__ __launch_bounds__(64) void scan_emit(ScanArgs a) {
                 }
                 ++k;
             });
-            if (term_type(stop) != kExit) {   // the chain ends in this chunk
+            // the chain ends in this chunk, or leaves it onto a header K1 pruned
+            if (term_type(stop) == kExit && quick_reject(a, term_pos(stop))) stop = term(kDead, term_pos(stop));
+            if (term_type(stop) != kExit) {
                 const uint64_t end = term_pos(stop);
                 a.result[1] = end;
                 a.result[2] = term_type(stop) == kDead ? end : ~0ull;
@@ -453,7 +472,7 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.result = result;
     // scratch layout, per (device, stream)
     const uint64_t need = chunks * 4 + nodes * 8 + nodes * 4 + nodes * 8 + (uint64_t)levels * nodes * 4 + 16 +
-                          chunks * 8 + 64 * 5;
+                          chunks * 8 + 64 * 8;   // + alignment padding of the 7 regions
     static std::map<std::pair<int, hipStream_t>, ScanScratchSet> scratch;
     static std::mutex mu;
     int dev = 0;
