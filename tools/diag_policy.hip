@@ -39,3 +39,30 @@ extern "C" int diag_policy(int laux, int saux, void* dst, const void* src, uint6
     CASE(16, 2) CASE(3, 3)
     return -1;
 }
+
+// Unaligned-source stream: dst (16-B aligned) <- src + shift (any byte shift), 16-B
+// loads at byte granularity (global_load_dwordx4 on an unaligned address), NT.
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+__global__ __launch_bounds__(256) void shift_kernel(uint8_t* dst, const uint8_t* src, uint64_t nchunks, uint32_t key) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t W = (uint64_t)gridDim.x * 4;
+    const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const u32x4 k = {key, key, key, key};
+    for (uint64_t c = w; c < nchunks; c += W) {
+        u32x4 d[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            d[u] = __builtin_nontemporal_load(
+                (const __attribute__((address_space(1))) u32x4u*)(src + c * 4096 + u * 1024 + lane * 16));
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            __builtin_nontemporal_store(d[u] ^ k, (__attribute__((address_space(1))) u32x4*)(dst + c * 4096 + u * 1024 + lane * 16));
+    }
+}
+
+extern "C" int diag_shift(void* dst, const void* src, uint64_t nbytes, int shift, uint32_t key, int blocks,
+                          void* stream) {
+    hipLaunchKernelGGL(shift_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (uint8_t*)dst,
+                       (const uint8_t*)src + shift, nbytes / 4096 - 1, key);
+    return (int)hipGetLastError();
+}
