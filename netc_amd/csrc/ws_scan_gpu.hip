@@ -117,29 +117,61 @@ __device__ __forceinline__ bool quick_reject(const ScanArgs& a, uint64_t x) {
     return !(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80));
 }
 
-// K1 / K2 common part: chunk bytes into LDS, link every position, pointer-jump.
-// After it, lk[i] is terminal for every i: EXIT(x) with x >= chunk end, END(p) or DEAD(p).
-__device__ void chunk_links(const ScanArgs& a, uint64_t B, uint8_t* bytes, uint64_t* lk) {
-    const int tid = threadIdx.x;
-    // bytes [B, B + kChunk + 16), zero past len
-    for (uint64_t i = tid; i < kChunk + 16; i += kScanT) {
-        const uint64_t p = B + i;
-        bytes[i] = p < a.len ? gptr(a.wire)[p] : 0;
+// 16 stream bytes from LDS position i as 4 dwords (5 dword reads + v_alignbyte),
+// indexed with constant byte offsets once the parse is unrolled.
+struct Win {
+    uint32_t d[4];
+    __device__ __forceinline__ uint32_t operator[](int j) const { return (d[j >> 2] >> (8 * (j & 3))) & 0xFF; }
+};
+
+__device__ __forceinline__ Win window_at(const uint32_t* words, int i) {
+    const int q = i >> 2;
+    const uint32_t r = (uint32_t)(i & 3) * 8;
+    uint32_t w[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) w[k] = words[q + k];
+    Win x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x.d[k] = (uint32_t)((((uint64_t)w[k + 1] << 32) | w[k]) >> r);
+    return x;
+}
+
+// LDS copy of the chunk: stream bytes [B, B + kChunk + 32), zero past len.
+static constexpr int kWords = (int)((kChunk + 32) / 4);
+
+__device__ void load_chunk(const ScanArgs& a, uint64_t B, uint32_t* words) {
+    typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (B + kChunk + 32 <= a.len) {
+        for (int v = tid; v < kWords / 4; v += nt) {   // 16-B loads (any alignment of the stream)
+            const u32x4 x = *(const NETC_GLOBAL u32x4u*)(a.wire + B + 16 * (uint64_t)v);
+            words[4 * v] = x[0];
+            words[4 * v + 1] = x[1];
+            words[4 * v + 2] = x[2];
+            words[4 * v + 3] = x[3];
+        }
+    } else {
+        uint8_t* bytes = (uint8_t*)words;
+        for (int i = tid; i < kWords * 4; i += nt) bytes[i] = B + i < a.len ? gptr(a.wire)[B + i] : 0;
     }
     __syncthreads();
+}
+
+// Link every position of the chunk (local index, or a terminal) and pointer-jump
+// until every link is terminal: EXIT(x) with x >= chunk end, END(p) or DEAD(p).
+__device__ void chunk_links(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t* lk) {
+    const int tid = threadIdx.x;
     const uint64_t Bend = B + kChunk;
 #pragma unroll 4
     for (int k = 0; k < kPer; ++k) {
         const int i = k * kScanT + tid;
         const uint64_t p = B + i;
         uint64_t v;
+        const Win w = window_at(words, i);
         if (p < a.start) {
             v = term(kDead, p);   // before the first header: never on the chain
         } else {
-            uint8_t hb[14];
-#pragma unroll
-            for (int j = 0; j < 14; ++j) hb[j] = bytes[i + j];
-            v = parse_at(a, p, hb, nullptr, nullptr);
+            v = parse_at(a, p, w, nullptr, nullptr);
             if (!(v & kTerm)) v = v < Bend ? v - B : term(kExit, v);
         }
         lk[i] = v;
@@ -160,10 +192,24 @@ __device__ void chunk_links(const ScanArgs& a, uint64_t B, uint8_t* bytes, uint6
     }
 }
 
+// Walk one chain from x inside the chunk for at most `hops` frames: its terminal,
+// or 0 if the hop budget ran out.
+__device__ uint64_t walk_exit(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t x, int hops) {
+    const uint64_t Bend = B + kChunk;
+    uint64_t p = x;
+    for (int h = 0; h < hops; ++h) {
+        if (p >= Bend) return term(kExit, p);
+        const uint64_t v = parse_at(a, p, window_at(words, (int)(p - B)), nullptr, nullptr);
+        if (v & kTerm) return v;
+        p = v;
+    }
+    return p >= Bend ? term(kExit, p) : 0;
+}
+
 // K1: distinct exits of each chunk, appended to the candidate lists of the chunks
 // they land in; the stream start is the candidate (root) of its chunk.
 __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
-    __shared__ uint8_t bytes[kChunk + 16];
+    __shared__ uint32_t words[kWords];
     __shared__ uint64_t lk[kChunk];
     __shared__ unsigned long long set[kSet];
     __shared__ int overflow;
@@ -172,7 +218,8 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     const int tid = threadIdx.x;
     if (tid < kSet) set[tid] = ~0ull;
     if (tid == 0) overflow = 0;
-    chunk_links(a, B, bytes, lk);
+    load_chunk(a, B, words);
+    chunk_links(a, B, words, lk);
     // dedup: a wave retires one distinct value per round (exits repeat a lot)
     for (int k = 0; k < kPer; ++k) {
         const uint64_t v = lk[k * kScanT + tid];
@@ -217,8 +264,9 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
 
 // K2: for each candidate entry of the chunk, the candidate its chain exits to.
 __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
-    __shared__ uint8_t bytes[kChunk + 16];
+    __shared__ uint32_t words[kWords];
     __shared__ uint64_t lk[kChunk];
+    __shared__ int long_chain;
     const uint64_t chunk = blockIdx.x;
     const uint64_t B = chunk * kChunk;
     const uint32_t nc_here = min(a.ccount[chunk], (uint32_t)kCand);
@@ -226,12 +274,25 @@ __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
     // unused node slots hold stale values from earlier calls: make them dead ends
     if (tid >= (int)nc_here && tid < kCand) a.link[chunk * kCand + tid] = -1;
     if (nc_here == 0) return;   // uniform per block
-    chunk_links(a, B, bytes, lk);
+    if (tid == 0) long_chain = 0;
+    load_chunk(a, B, words);
+    // each candidate walks its chain directly (a few frames per chunk); only if a
+    // chain runs longer (tiny frames) does the block pointer-jump the whole chunk
+    uint64_t v = 0;
+    uint64_t x = 0;
+    if (tid < (int)nc_here) {
+        x = a.cand[chunk * kCand + tid];
+        v = x - B < kChunk ? walk_exit(a, B, words, x, 64) : term(kEnd, x);   // x == len on a chunk edge
+        if (v == 0) long_chain = 1;
+    }
+    __syncthreads();
+    if (long_chain) {
+        chunk_links(a, B, words, lk);
+        if (tid < (int)nc_here && v == 0) v = lk[x - B];
+    }
     if (tid < (int)nc_here) {
         const uint64_t node = chunk * kCand + tid;
-        const uint64_t x = a.cand[node];
         if (x == a.start) a.flags[1] = (uint32_t)node;
-        const uint64_t v = x - B < kChunk ? lk[x - B] : term(kEnd, x);   // x == len on a chunk edge
         int32_t next = -1;
         if (term_type(v) == kExit) {
             const uint64_t y = term_pos(v), t = y / kChunk;
@@ -257,13 +318,13 @@ __global__ void scan_lift(const int32_t* src, int32_t* dst, uint64_t nodes) {
 // Walk the true frames of a chunk from its entry e (in LDS bytes), calling emit
 // for each complete frame; returns the terminal where the walk left the chunk.
 template <typename F>
-__device__ uint64_t walk_chunk(const ScanArgs& a, uint64_t B, const uint8_t* bytes, uint64_t e, F&& emit) {
+__device__ uint64_t walk_chunk(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t e, F&& emit) {
     uint64_t p = e;
     const uint64_t Bend = B + kChunk;
     while (p < Bend) {
         uint32_t key;
         uint8_t b0;
-        const uint64_t v = parse_at(a, p, bytes + (p - B), &key, &b0);   // LDS, 16 bytes of lookahead
+        const uint64_t v = parse_at(a, p, window_at(words, (int)(p - B)), &key, &b0);
         if (v & kTerm) return v;
         emit(p, key, b0);
         p = v;
@@ -275,7 +336,7 @@ __device__ __forceinline__ uint64_t cand_pos(const ScanArgs& a, int32_t node) { 
 
 // K4: one wavefront per chunk.
 __global__ __launch_bounds__(64) void scan_emit(ScanArgs a) {
-    __shared__ uint8_t bytes[kChunk + 16];
+    __shared__ uint32_t words[kWords];
     const uint64_t chunk = blockIdx.x;
     const uint64_t B = chunk * kChunk;
     const int lane = threadIdx.x;
@@ -327,9 +388,8 @@ __global__ __launch_bounds__(64) void scan_emit(ScanArgs a) {
     uint64_t count = 0;
     uint64_t stop = 0;
     if (entry >= 0) {
-        for (uint64_t i = lane; i < kChunk + 16; i += 64) bytes[i] = B + i < a.len ? gptr(a.wire)[B + i] : 0;
-        __syncthreads();
-        if (lane == 0) stop = walk_chunk(a, B, bytes, (uint64_t)entry, [&](uint64_t, uint32_t, uint8_t) { ++count; });
+        load_chunk(a, B, words);
+        if (lane == 0) stop = walk_chunk(a, B, words, (uint64_t)entry, [&](uint64_t, uint32_t, uint8_t) { ++count; });
     }
     // chained scan of the frame counts (lane 0 publishes and looks back)
     uint64_t base = 0;
@@ -355,7 +415,7 @@ __global__ __launch_bounds__(64) void scan_emit(ScanArgs a) {
         if (chunk == a.nc) a.result[0] = base + count;
         if (entry >= 0) {
             uint64_t k = base;
-            walk_chunk(a, B, bytes, (uint64_t)entry, [&](uint64_t p, uint32_t key, uint8_t b0) {
+            walk_chunk(a, B, words, (uint64_t)entry, [&](uint64_t p, uint32_t key, uint8_t b0) {
                 if (k < a.max_frames) {
                     a.hdr[k] = p;
                     a.keys[k] = key;
