@@ -17,8 +17,9 @@
 //            entry of its chunk to the candidate it exits to: a graph of a few
 //            nodes per chunk whose path from the stream start is the true chain,
 //            one node per chunk it enters.
-//   K3       binary lifting over that graph (log2(chunks) doubling passes);
-//   K4       per chunk: the true entry (by lifting from the start node), a walk of
+//   K3       pointer doubling over that graph, marking the nodes reachable from
+//            the start node (log2(chunks) passes);
+//   K4       per chunk: the true entry (its marked node), a walk of
 //            the chunk's frames in LDS to count them, a chained scan of the counts
 //            (decoupled look-back), and a second walk that writes the descriptors.
 // Garbage chains (payload bytes parsed as headers) die within a hop or two under
@@ -60,8 +61,7 @@ struct ScanArgs {
     uint64_t* cand;        // (nc + 1) * kCand candidate positions
     int32_t* link;         // (nc + 1) * kCand: node -> next node, -1 = chain ends
     uint64_t* nterm;       // (nc + 1) * kCand: the terminal where the chain ends (END / DEAD)
-    int32_t* lift;         // levels x (nc + 1) * kCand
-    int levels;
+    uint8_t* mark;         // (nc + 1) * kCand: node is on the chain from the stream start
     uint32_t* flags;       // [0] overflow, [1] root node
     uint64_t* status;      // chained-scan status words (nc + 1)
     uint32_t epoch;
@@ -162,18 +162,32 @@ __device__ void load_chunk(const ScanArgs& a, uint64_t B, uint32_t* words) {
 __device__ void chunk_links(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t* lk) {
     const int tid = threadIdx.x;
     const uint64_t Bend = B + kChunk;
-#pragma unroll 4
-    for (int k = 0; k < kPer; ++k) {
-        const int i = k * kScanT + tid;
-        const uint64_t p = B + i;
-        uint64_t v;
-        const Win w = window_at(words, i);
-        if (p < a.start) {
-            v = term(kDead, p);   // before the first header: never on the chain
-        } else {
-            v = parse_at(a, p, w, nullptr, nullptr);
-            if (!(v & kTerm)) v = v < Bend ? v - B : term(kExit, v);
-        }
+    // every link starts DEAD (coalesced); only positions that can start a header are parsed
+    const uint64_t kDeadLink = term(kDead, 0);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) lk[k * kScanT + tid] = kDeadLink;
+    // this thread's kPer consecutive positions: bytes [kPer tid, kPer tid + kPer + 14) in 8 dwords
+    const int i0 = kPer * tid;
+    uint32_t w[kPer / 4 + 4];
+#pragma unroll
+    for (int k = 0; k < kPer / 4 + 4; ++k) w[k] = words[i0 / 4 + k];
+    auto byte_at = [&](int j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
+    // strict quick check on bytes 0-1 of each position (~98 % of payload positions fail it)
+    uint32_t cand = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t first = byte_at(j), second = byte_at(j + 1), opcode = first & 0x0F;
+        const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
+        const bool reject = a.strict && (!(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80)));
+        if (!reject && B + i0 + j >= a.start) cand |= 1u << j;
+    }
+    __syncthreads();   // DEAD fill done before the scattered writes
+    while (cand) {
+        const int j = __builtin_ctz(cand);
+        cand &= cand - 1;
+        const int i = i0 + j;
+        uint64_t v = parse_at(a, B + i, window_at(words, i), nullptr, nullptr);
+        if (!(v & kTerm)) v = v < Bend ? v - B : term(kExit, v);
         lk[i] = v;
     }
     __syncthreads();
@@ -292,7 +306,10 @@ __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
     }
     if (tid < (int)nc_here) {
         const uint64_t node = chunk * kCand + tid;
-        if (x == a.start) a.flags[1] = (uint32_t)node;
+        if (x == a.start) {
+            a.flags[1] = (uint32_t)node;
+            a.mark[node] = 1;
+        }
         int32_t next = -1;
         if (term_type(v) == kExit) {
             const uint64_t y = term_pos(v), t = y / kChunk;
@@ -307,12 +324,19 @@ __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
     }
 }
 
-// K3: lift[k+1][v] = lift[k][lift[k][v]]   (lift[0] = link)
-__global__ void scan_lift(const int32_t* src, int32_t* dst, uint64_t nodes) {
+// K3, pass k: src = J_k (the 2^k-th successor; J_0 = link).  Builds J_{k+1} =
+// J_k o J_k into dst (unless last) and marks the J_k-successor of every marked
+// node: after pass k every node within 2^(k+1) - 1 steps of the start is marked,
+// so after log2(chunks) passes exactly the chain's nodes are (one per chunk it
+// enters).  Marks set during a pass may be followed in the same pass: they are
+// on the chain too.
+__global__ void scan_lift(const int32_t* src, int32_t* dst, uint8_t* mark, uint64_t nodes) {
     const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= nodes) return;
-    const int32_t u = src[v];
-    dst[v] = (u < 0 || (uint64_t)u >= nodes) ? -1 : src[u];   // (range check: defence in depth)
+    int32_t u = src[v];
+    if (u >= 0 && (uint64_t)u >= nodes) u = -1;   // (range check: defence in depth)
+    if (dst) dst[v] = u < 0 ? -1 : src[u];
+    if (u >= 0 && mark[v]) mark[u] = 1;
 }
 
 // Walk the true frames of a chunk from its entry e (in LDS bytes), calling emit
@@ -372,18 +396,12 @@ __global__ __launch_bounds__(64) void scan_emit(ScanArgs a) {
         }
         return;
     }
-    // the true entry of this chunk: last node of the chain from the root before the chunk end
+    // the true entry of this chunk: its candidate node on the chain (at most one)
     int64_t entry = -1;
     {
-        int32_t v = (int32_t)a.flags[1];
-        const uint64_t bound = B + kChunk;
-        if (cand_pos(a, v) < bound) {
-            for (int k = a.levels - 1; k >= 0; --k) {
-                const int32_t u = a.lift[(uint64_t)k * (a.nc + 1) * kCand + v];
-                if (u >= 0 && cand_pos(a, u) < bound) v = u;
-            }
-            if (cand_pos(a, v) >= B) entry = (int64_t)cand_pos(a, v);
-        }
+        const uint32_t cnt = min(a.ccount[chunk], (uint32_t)kCand);
+        for (uint32_t i = 0; i < cnt; ++i)
+            if (a.mark[chunk * kCand + i]) entry = (int64_t)cand_pos(a, (int32_t)(chunk * kCand + i));
     }
     uint64_t count = 0;
     uint64_t stop = 0;
@@ -522,23 +540,23 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.strict = strict ? 1 : 0;
     a.nc = (len + kChunk - 1) / kChunk;   // real chunks 0 .. nc-1; chunk nc is virtual (positions >= len)
     const uint64_t chunks = a.nc + 1, nodes = chunks * kCand;
-    int levels = 1;
+    int levels = 1;   // doubling passes: 2^levels - 1 >= chunks steps along the chain
     while ((1ull << levels) < chunks + 1) ++levels;
-    a.levels = levels;
     a.hdr = hdr;
     a.keys = keys;
     a.b0 = b0;
     a.max_frames = max_frames;
     a.result = result;
     // scratch layout, per (device, stream)
-    const uint64_t need = chunks * 4 + nodes * 8 + nodes * 4 + nodes * 8 + (uint64_t)levels * nodes * 4 + 16 +
-                          chunks * 8 + 64 * 8;   // + alignment padding of the 7 regions
+    const uint64_t need = chunks * 4 + nodes * 8 + nodes * 4 + nodes * 8 + 2 * nodes * 4 + nodes + 16 +
+                          chunks * 8 + 64 * 9;   // + alignment padding of the 9 regions
     static std::map<std::pair<int, hipStream_t>, ScanScratchSet> scratch;
     static std::mutex mu;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     uint8_t* m;
+    int32_t *jp, *jq;   // ping-pong doubling tables
     {
         std::lock_guard<std::mutex> g(mu);
         ScanScratchSet& s = scratch[{dev, stream}];
@@ -562,7 +580,9 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         a.link = (int32_t*)(m + o); o = align(o + nodes * 4);
         a.nterm = (uint64_t*)(m + o); o = align(o + nodes * 8);
         a.status = (uint64_t*)(m + o); o = align(o + chunks * 8);
-        a.lift = (int32_t*)(m + o);
+        jp = (int32_t*)(m + o); o = align(o + nodes * 4);
+        jq = (int32_t*)(m + o); o = align(o + nodes * 4);
+        a.mark = m + o;
         if (s.epoch == 0) {   // epochs wrapped: clear the status words
             if ((e = hipMemsetAsync(a.status, 0, chunks * 8, stream)) != hipSuccess) return e;
             s.epoch = 1;
@@ -572,14 +592,16 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     // counters + flags, and the default results (no frames, nothing consumed past start)
     if ((e = hipMemsetAsync(a.ccount, 0, chunks * 4, stream)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(a.flags, 0, 16, stream)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.mark, 0, nodes, stream)) != hipSuccess) return e;
     hipLaunchKernelGGL(scan_exits, dim3((unsigned)chunks), dim3(kScanT), 0, stream, a);
     hipLaunchKernelGGL(scan_links, dim3((unsigned)chunks), dim3(kScanT), 0, stream, a);
-    // lift[0] = link, then doublings
-    if ((e = hipMemcpyAsync(a.lift, a.link, nodes * 4, hipMemcpyDeviceToDevice, stream)) != hipSuccess) return e;
     const unsigned lb = (unsigned)((nodes + 255) / 256);
-    for (int k = 0; k + 1 < levels; ++k)
-        hipLaunchKernelGGL(scan_lift, dim3(lb), dim3(256), 0, stream, a.lift + (uint64_t)k * nodes,
-                           a.lift + (uint64_t)(k + 1) * nodes, nodes);
+    const int32_t* src = a.link;
+    for (int k = 0; k < levels; ++k) {
+        int32_t* dst = k + 1 < levels ? ((k & 1) ? jq : jp) : nullptr;
+        hipLaunchKernelGGL(scan_lift, dim3(lb), dim3(256), 0, stream, src, dst, a.mark, nodes);
+        src = dst;
+    }
     hipLaunchKernelGGL(scan_emit, dim3((unsigned)chunks), dim3(64), 0, stream, a);
     return hipGetLastError();
 }
