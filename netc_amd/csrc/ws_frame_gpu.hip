@@ -10,23 +10,27 @@
 // key always follows the MASK bit, also for an empty payload (RFC 6455 §5.2; the
 // reference omits it there, defect B9 in DESIGN.md).
 //
-// Two steps on the caller's stream:
+// Three kernels on the caller's stream:
 //   1. wire offsets: wo[j] = sum over k < j of (header_len(k) + len(k)), a
-//      single-pass chained scan over the frames (one kernel, decoupled look-back);
+//      single-pass chained scan over the frames (decoupled look-back, 64
+//      predecessors inspected at once);
 //   2. the assembly kernel, output-driven: the wire buffer is walked in 16-byte
-//      vectors aligned to the destination, chunk by chunk in grid-stride order
-//      as in ws_mask_gpu.hip; a 64-entry frame table in VGPRs (wire start,
-//      payload offset, key, header byte of 64 consecutive frames) places each
-//      vector.  A vector inside one frame's payload is one unaligned 16-B load
-//      of the payload, one XOR with the key rotated to its phase, one aligned
-//      store; vectors holding a header or a frame edge are composed from the
-//      header (built once per frame, wave-uniform) and the masked payload of
-//      every frame they touch.
+//      vectors aligned to the destination, chunk by chunk in grid-stride order as
+//      in ws_mask_gpu.hip.  A 64-entry frame table in VGPRs (wire start, payload
+//      offset, key, header byte of 64 consecutive frames) places each vector.  A
+//      vector inside one frame's payload is one unaligned 16-B load, one XOR with
+//      the key rotated to its phase, one aligned store; a vector holding a frame
+//      edge takes two loads and the header bytes (built once per frame,
+//      wave-uniform).  Software pipeline: while chunk c is stored, chunk c+W's
+//      loads and chunk c+2W's frame table are in flight.  Spans outside those two
+//      shapes (frames under 16 B, the buffer edges) are queued;
+//   3. the queued spans, composed byte-exactly from every frame they touch.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <map>
 #include <mutex>
+#include <type_traits>
 #include <utility>
 
 #include "gpu_util.h"
@@ -43,7 +47,7 @@ __device__ __forceinline__ uint32_t ext_len(uint64_t len) { return len < 126 ? 0
 
 static constexpr int kScanThreads = 256;
 static constexpr int kScanPer = 16;
-static constexpr uint64_t kScanBlock = (uint64_t)kScanThreads * kScanPer;   // frames per block
+static constexpr uint64_t kScanBlock = (uint64_t)kScanThreads * kScanPer;   // frames per tile
 
 // exclusive prefix sum over the block (kScanThreads threads); returns the block total in *total
 __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total) {
@@ -68,13 +72,21 @@ __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total) {
     return before + inc - v;
 }
 
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+    for (int d = kWave / 2; d > 0; d >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, d, kWave);
+    return v;
+}
+
 // Single-pass chained scan (decoupled look-back).  Tile b = frames
 // [b kScanBlock, (b + 1) kScanBlock); tiles cover frames 0 .. n inclusive, so the
 // tile holding frame n writes wo[n].  Each tile publishes one 64-bit status word:
 //   [63:62] flag (1 = tile aggregate, 2 = inclusive prefix) | [61:46] epoch | [45:0] value
 // value = extended-length bytes (<= 8 per frame, so n < 2^43).  The epoch (one per
-// call, per device) makes words left over from earlier calls read as "not yet
-// published", so the status array is never cleared between calls.  A tile only
+// call and stream) makes words left from earlier calls read as "not yet
+// published", so the status array is never cleared between calls.  The look-back
+// reads 64 predecessors at once: it sums their aggregates back to the nearest
+// inclusive prefix, so tiles do not wait on each other one by one.  A tile only
 // waits on lower-numbered tiles, which are dispatched first.
 static constexpr uint64_t kValBits = 46;
 static constexpr uint64_t kValMask = (1ull << kValBits) - 1;
@@ -83,11 +95,39 @@ __device__ __forceinline__ uint64_t status_word(uint64_t flag, uint32_t epoch, u
     return flag << 62 | (uint64_t)(epoch & 0xFFFF) << kValBits | (v & kValMask);
 }
 
+__device__ uint64_t look_back(uint64_t* status, int64_t tile, uint32_t epoch, int lane) {
+    uint64_t prefix = 0;
+    for (int64_t top = tile - 1; top >= 0;) {
+        const int64_t idx = top - lane;
+        uint64_t v = 0;
+        bool ok = true, incl = idx < 0;   // before tile 0: an inclusive prefix of 0
+        if (idx >= 0) {
+            const uint64_t w = __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (w >> 62) != 0 && ((w >> kValBits) & 0xFFFF) == (epoch & 0xFFFF);
+            incl = ok && (w >> 62) == 2;
+            v = w & kValMask;
+        }
+        const uint64_t im = __ballot(incl);
+        const int stop = im ? __builtin_ctzll(im) : kWave;   // nearest inclusive prefix
+        const uint64_t need = stop >= kWave - 1 ? ~0ull : ((2ull << stop) - 1);
+        if ((__ballot(ok) & need) != need) {
+            __builtin_amdgcn_s_sleep(1);   // a predecessor has not published yet
+            continue;
+        }
+        prefix += wave_sum(lane <= stop ? v : 0);
+        if (stop < kWave) break;
+        top -= kWave;
+    }
+    return prefix;
+}
+
 __global__ __launch_bounds__(kScanThreads) void wire_offsets_chained(const uint64_t* off, uint64_t n, uint32_t fixed,
-                                                                     uint64_t* wo, uint64_t* status, uint32_t epoch) {
+                                                                     uint64_t* wo, uint64_t* status, uint32_t epoch,
+                                                                     uint32_t* defer_count) {
     __shared__ uint64_t tile_prefix;
     const uint64_t tile = blockIdx.x;
     const uint64_t first = tile * kScanBlock + (uint64_t)threadIdx.x * kScanPer;   // this thread's frames
+    if (tile == 0 && threadIdx.x == 0) *defer_count = 0;   // the assembly kernel's queue (runs after)
     uint32_t e[kScanPer];
     uint64_t s = 0;
 #pragma unroll
@@ -98,27 +138,17 @@ __global__ __launch_bounds__(kScanThreads) void wire_offsets_chained(const uint6
     }
     uint64_t agg;
     const uint64_t ex = block_exclusive_scan(s, &agg);
-    if (threadIdx.x == 0) {
-        uint64_t prefix = 0;
-        if (tile == 0) {
-            __hip_atomic_store(&status[0], status_word(2, epoch, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(&status[tile], status_word(1, epoch, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int64_t p = (int64_t)tile - 1; p >= 0;) {
-                const uint64_t w = __hip_atomic_load(&status[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t flag = w >> 62;
-                if (flag == 0 || ((w >> kValBits) & 0xFFFF) != (epoch & 0xFFFF)) {
-                    __builtin_amdgcn_s_sleep(1);   // predecessor not published yet
-                    continue;
-                }
-                prefix += w & kValMask;
-                if (flag == 2) break;
-                --p;
-            }
-            __hip_atomic_store(&status[tile], status_word(2, epoch, prefix + agg), __ATOMIC_RELAXED,
+    if (threadIdx.x < kWave) {
+        const int lane = threadIdx.x;
+        if (lane == 0)
+            __hip_atomic_store(&status[tile], status_word(tile == 0 ? 2 : 1, epoch, agg), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t prefix = tile == 0 ? 0 : look_back(status, (int64_t)tile, epoch, lane);
+        if (lane == 0) {
+            if (tile) __hip_atomic_store(&status[tile], status_word(2, epoch, prefix + agg), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+            tile_prefix = prefix;
         }
-        tile_prefix = prefix;
     }
     __syncthreads();
     uint64_t run = tile_prefix + ex;
@@ -143,8 +173,10 @@ struct EncArgs {
     const uint8_t* b0;         // n header bytes (FIN | RSV | opcode), or null: 0x82
     uint64_t n;
     uint64_t wmis;             // wire & 15
-    uint64_t nwin;             // chunks covering the wire upper bound
     uint32_t masked;
+    uint64_t* defer;           // queued span starts (W coordinates), capacity defer_cap
+    uint32_t* defer_count;
+    uint64_t defer_cap;
 };
 
 // Frame table: lane l holds virtual frame kb + l.  W coordinates = wire byte + wmis.
@@ -218,6 +250,13 @@ __device__ int64_t enc_locate(const EncArgs& a, uint64_t W, uint64_t wire_total,
     return L;
 }
 
+// make t hold the frame containing W (wave-uniform): keep it if it does, else search
+__device__ __forceinline__ void enc_resolve(const EncArgs& a, EncTable& t, uint64_t W, uint64_t wire_total,
+                                            int lane) {
+    const uint64_t m = __ballot(t.start <= W);
+    if (!(m != 0 && (t.tail || m != ~0ull))) enc_table_load(a, t, enc_locate(a, W, wire_total, lane), lane);
+}
+
 // The frame header as 16 little-endian bytes (h <= 14 used), wave-uniform:
 // b0 | MASK, length code | extended length, big-endian | key bytes.
 __device__ __forceinline__ void build_header(uint32_t b0, uint64_t len, bool masked, uint32_t key, uint64_t& lo,
@@ -281,56 +320,6 @@ __device__ __forceinline__ u32x4 load_guarded(const EncArgs& a, int64_t s0, int 
     return v;
 }
 
-// Wire vector of this lane for the span at A0 (general path: header bytes and any
-// number of frame edges).  Frames are taken from the table from entry l0 on.
-template <bool NT>
-__device__ u32x4 compose_vec(const EncArgs& a, EncTable& t, int l0, uint64_t A0, uint64_t W, int lane) {
-    const uint64_t Aend = A0 + kSpan;
-    u32x4 out = {0, 0, 0, 0};
-    int l = l0;
-    for (;;) {
-        if (l >= kWave - 1) {   // entry l needs entry l + 1: slide the table
-            enc_table_load(a, t, t.kb + l, lane);
-            l = 0;
-        }
-        const int64_t j = t.kb + l;
-        if (j >= (int64_t)a.n) break;
-        const uint64_t Ws = readlane64(t.start, l);
-        if (Ws >= Aend) break;
-        if (j < 0) {
-            ++l;
-            continue;
-        }
-        const uint64_t We = readlane64(t.start, l + 1);
-        const uint64_t o0 = readlane64(t.poff, l), o1 = readlane64(t.poff, l + 1);
-        const uint32_t key = readlane32(t.key, l), b0 = readlane32(t.b0, l);
-        const uint64_t len = o1 - o0;
-        const uint64_t pw = Ws + 2 + ext_len(len) + (a.masked ? 4 : 0);   // payload start (W)
-        // header bytes [Ws, pw) of this vector
-        const int64_t hlo = (int64_t)(Ws - W), hhi = (int64_t)(pw - W);
-        if (hhi > 0 && hlo < 16) {
-            uint64_t hl, hh;
-            build_header(b0, len, a.masked != 0, key, hl, hh);
-            const u32x4 sel = select_range(hlo, hhi);
-            out = (out & ~sel) | (shift_bytes(hl, hh, (int)hlo) & sel);
-        }
-        // payload bytes [pw, We) of this vector
-        const int64_t plo = (int64_t)(pw - W), phi = (int64_t)(We - W);
-        if (phi > 0 && plo < 16 && phi > plo) {
-            const int64_t s0 = (int64_t)o0 - plo;   // src offset of the vector's byte 0
-            u32x4 v;
-            if (s0 >= 0 && (uint64_t)s0 + 16 <= a.src_total) v = load_u<false>(a.src + s0);
-            else v = load_guarded(a, s0, plo < 0 ? 0 : (int)plo, phi > 16 ? 16 : (int)phi);
-            const uint32_t rk = rotr8(key, (uint64_t)(-plo));   // phase of byte 0: W - pw
-            const u32x4 kv = {rk, rk, rk, rk};
-            const u32x4 sel = select_range(plo, phi);
-            out = (out & ~sel) | ((v ^ kv) & sel);
-        }
-        ++l;
-    }
-    return out;
-}
-
 template <bool NT>
 __device__ __forceinline__ void store_wire(const EncArgs& a, uint64_t W, u32x4 v, uint64_t wlo, uint64_t whi) {
     if (W >= wlo && W + 16 <= whi) {
@@ -362,6 +351,54 @@ __device__ __forceinline__ FrameInfo frame_info(const EncArgs& a, const EncTable
     return f;
 }
 
+// OR the header bytes of frame f that fall into the lane's vector into v
+__device__ __forceinline__ u32x4 put_header(const EncArgs& a, const FrameInfo& f, uint64_t W, u32x4 v) {
+    const int64_t hs = (int64_t)(f.Ws - W), he = (int64_t)(f.pw - W);
+    if (he > 0 && hs < 16) {
+        uint64_t hl, hh;
+        build_header(f.b0, f.len, a.masked != 0, f.key, hl, hh);
+        v |= shift_bytes(hl, hh, (int)hs) & select_range(hs, he);
+    }
+    return v;
+}
+
+// Wire vector of this lane for the span at A0, composed from every frame touching
+// it (header bytes and any number of frame edges), starting at table entry l0; the
+// table slides forward as needed.
+__device__ u32x4 compose_vec(const EncArgs& a, EncTable& t, int l0, uint64_t A0, uint64_t W, int lane) {
+    const uint64_t Aend = A0 + kSpan;
+    u32x4 out = {0, 0, 0, 0};
+    int l = l0;
+    for (;;) {
+        if (l >= kWave - 1) {   // entry l needs entry l + 1: slide the table
+            enc_table_load(a, t, t.kb + l, lane);
+            l = 0;
+        }
+        const int64_t j = t.kb + l;
+        if (j >= (int64_t)a.n) break;
+        if (j < 0) {
+            ++l;
+            continue;
+        }
+        const FrameInfo f = frame_info(a, t, l);
+        if (f.Ws >= Aend) break;
+        out = put_header(a, f, W, out);
+        // payload bytes [pw, We) of this vector
+        const int64_t plo = (int64_t)(f.pw - W), phi = (int64_t)(f.We - W);
+        if (phi > 0 && plo < 16 && phi > plo) {
+            const int64_t s0 = (int64_t)f.o - plo;   // src offset of the vector's byte 0
+            u32x4 v;
+            if (s0 >= 0 && (uint64_t)s0 + 16 <= a.src_total) v = load_u<false>(a.src + s0);
+            else v = load_guarded(a, s0, plo < 0 ? 0 : (int)plo, phi > 16 ? 16 : (int)phi);
+            const uint32_t rk = rotr8(f.key, (uint64_t)(-plo));   // phase of byte 0: W - pw
+            const u32x4 kv = {rk, rk, rk, rk};
+            out |= (v ^ kv) & select_range(plo, phi);
+        }
+        ++l;
+    }
+    return out;
+}
+
 // One frame's payload as seen from a lane's 16-B vector at W.
 struct Slot {
     int64_t s0;        // src offset of the vector's byte 0 (o + W - pw)
@@ -389,25 +426,147 @@ __device__ __forceinline__ Slot select_slot(bool c, const Slot& x, const Slot& y
     return s;
 }
 
-// OR the header bytes of frame f that fall into the lane's vector into v
-__device__ __forceinline__ u32x4 put_header(const EncArgs& a, const FrameInfo& f, uint64_t W, u32x4 v) {
-    const int64_t hs = (int64_t)(f.Ws - W), he = (int64_t)(f.pw - W);
-    if (he > 0 && hs < 16) {
-        uint64_t hl, hh;
-        build_header(f.b0, f.len, a.masked != 0, f.key, hl, hh);
-        v |= shift_bytes(hl, hh, (int)hs) & select_range(hs, he);
+// Span kinds (wave-uniform): the whole span is payload of one frame; or every
+// vector holds bytes of at most two frames (two unaligned loads plus header
+// bytes); or anything else (table edges, frames under 16 B, buffer edges), which
+// is queued for the compose kernel.
+enum : int { kSpanFast = 0, kSpanSlots = 1, kSpanQueued = 2, kSpanNone = 3 };
+
+// What phase 2 needs for one span of a chunk: the loads, the rotated keys, and one
+// packed word per lane: plo1 | phi1 << 5 | plo2 << 10 | phi2 << 15 | two << 20.
+struct SpanPlan {
+    int kind;
+    u32x4 d1, d2;
+    uint32_t rk1, rk2, pk;
+};
+template <int U>
+struct Plan {
+    SpanPlan s[U];
+};
+
+// f(integral_constant<int, I>) for I = 0 .. N-1, unrolled at compile time: span
+// state stays in registers (a runtime-indexed span array lands in scratch, and
+// every load then waits on vmcnt(0) to be stored there)
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
     }
-    return v;
 }
 
-// Span kinds (wave-uniform): the whole span is payload of one frame; or every
-// vector holds bytes of at most two frames, from two unaligned loads plus header
-// bytes; or the general compose path (table edges, tiny frames, buffer edges).
-enum : int { kSpanFast = 0, kSpanSlots = 1, kSpanCompose = 2 };
+template <int U, bool NT>
+__device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, uint64_t A, uint64_t wlo,
+                                           uint64_t whi, int lane, Plan<U>& P) {
+    static_for<0, U>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        SpanPlan& sp = P.s[u];
+        const uint64_t A0 = A + (uint64_t)u * kSpan, Aend = A0 + kSpan;
+        const uint64_t W = A0 + 16ull * (uint64_t)lane;
+        // the span is classified first; its two loads are then issued unconditionally
+        // at the end (one exit path: loads under branches end up staged through
+        // scratch with full vmcnt drains)
+        int kind = kSpanNone;
+        int64_t ad1 = 0, ad2 = 0;
+        uint32_t rk1 = 0, rk2 = 0, pk = 0;
+        do {
+            if (A0 >= whi) break;
+            kind = kSpanQueued;
+            const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
+            const uint64_t bm = __ballot(t.start > A0 && t.start < Aend);
+            const int nb = __popcll(bm);
+            const bool covered = (t.tail || t.last >= Aend) && l0 + nb + 1 <= kWave - 1;
+            if (!covered || A0 < wlo || Aend > whi || t.kb + l0 < 0 || t.kb + l0 + nb >= (int64_t)a.n) break;
+            const FrameInfo f0 = frame_info(a, t, l0);
+            if (nb == 0 && f0.pw <= A0 && Aend <= f0.We) {
+                kind = kSpanFast;
+                const Slot sf = slot_of(f0, W);
+                rk1 = sf.rk;
+                ad1 = ad2 = sf.s0;
+                break;
+            }
+            Slot a1 = slot_of(f0, W), a2 = a1;
+            int cut = 0;   // frame starts inside (W, W + 15]
+            uint64_t b = bm;
+            while (b) {
+                const int l = __builtin_ctzll(b);
+                b &= b - 1;
+                const FrameInfo fj = frame_info(a, t, l);
+                const Slot sj = slot_of(fj, W);
+                a1 = select_slot(W >= fj.Ws, sj, a1);
+                a2 = select_slot(W + 15 >= fj.Ws, sj, a2);
+                cut += (fj.Ws > W && fj.Ws <= W + 15) ? 1 : 0;
+            }
+            const bool two = cut == 1;
+            const bool need1 = a1.phi > a1.plo, need2 = two && a2.phi > a2.plo;
+            // three frames in one vector, or a load leaving [0, src_total): the compose kernel
+            bool slow = cut > 1;
+            slow |= need1 && (a1.s0 < 0 || (uint64_t)a1.s0 + 16 > a.src_total);
+            slow |= need2 && (a2.s0 < 0 || (uint64_t)a2.s0 + 16 > a.src_total);
+            if (__ballot(slow)) break;   // the whole span is queued
+            kind = kSpanSlots;
+            rk1 = a1.rk;
+            rk2 = a2.rk;
+            pk = (uint32_t)a1.plo | (uint32_t)a1.phi << 5 | (uint32_t)a2.plo << 10 | (uint32_t)a2.phi << 15 |
+                 (two ? 1u << 20 : 0u);
+            ad1 = need1 ? a1.s0 : 0;   // unused bytes are masked off in phase 2
+            ad2 = need2 ? a2.s0 : ad1;
+        } while (false);
+        if (a.src_total < 16) ad1 = ad2 = 0;   // (tiny payload buffers: every span is queued anyway)
+        sp.kind = kind;
+        sp.rk1 = rk1;
+        sp.rk2 = rk2;
+        sp.pk = pk;
+        sp.d1 = load_u<NT>(a.src + ad1);
+        sp.d2 = load_u<NT>(a.src + ad2);
+    });
+}
 
-// Chunk = U spans.  Phase 1 plans every span of the chunk and issues all its
-// payload loads; phase 2 masks, places headers and stores.  The frame table of
-// the NEXT chunk is loaded (at a guessed base) while this chunk is processed.
+template <int U, bool NT>
+__device__ __forceinline__ void finish_chunk(const EncArgs& a, const EncTable& t, uint64_t A, uint64_t wlo,
+                                             uint64_t whi, int lane, const Plan<U>& P) {
+    static_for<0, U>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        const SpanPlan& sp = P.s[u];
+        const uint64_t A0 = A + (uint64_t)u * kSpan, Aend = A0 + kSpan;
+        const uint64_t W = A0 + 16ull * (uint64_t)lane;
+        if (sp.kind == kSpanNone) return;
+        if (sp.kind == kSpanQueued) {
+            if (lane == 0) {
+                const uint32_t slot = atomicAdd(a.defer_count, 1u);
+                if (slot < a.defer_cap) a.defer[slot] = A0;   // capacity covers every span
+            }
+            return;
+        }
+        u32x4 v;
+        if (sp.kind == kSpanFast) {
+            const u32x4 kv = {sp.rk1, sp.rk1, sp.rk1, sp.rk1};
+            v = sp.d1 ^ kv;
+        } else {
+            const uint32_t p = sp.pk;
+            const u32x4 k1 = {sp.rk1, sp.rk1, sp.rk1, sp.rk1};
+            const u32x4 k2 = {sp.rk2, sp.rk2, sp.rk2, sp.rk2};
+            v = (sp.d1 ^ k1) & select_range(p & 31, (p >> 5) & 31);
+            if (p & (1u << 20)) v |= (sp.d2 ^ k2) & select_range((p >> 10) & 31, (p >> 15) & 31);
+            // headers: the span's first frame (if the span starts inside its header)
+            // and every frame starting inside the span
+            const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
+            const FrameInfo f0 = frame_info(a, t, l0);
+            if (f0.pw > A0) v = put_header(a, f0, W, v);
+            uint64_t b = __ballot(t.start > A0 && t.start < Aend);
+            while (b) {
+                const int l = __builtin_ctzll(b);
+                b &= b - 1;
+                v = put_header(a, frame_info(a, t, l), W, v);
+            }
+        }
+        store_wire<NT>(a, W, v, wlo, whi);
+    });
+}
+
+// Chunk = U spans.  Wavefront w of W takes chunks w, w+W, ...  Per trip: the table
+// of chunk c+W (issued a trip ago) is resolved and chunk c+W's loads are issued,
+// chunk c+2W's table is issued, then chunk c (loaded a trip ago) is stored.
 template <int U, bool NT>
 __global__ __launch_bounds__(256) void encode_frames_kernel(EncArgs a) {
     constexpr uint64_t kWin = kSpan * U;
@@ -430,133 +589,59 @@ __global__ __launch_bounds__(256) void encode_frames_kernel(EncArgs a) {
         g = g < -1 ? -1 : g;
         return g > (int64_t)a.n ? (int64_t)a.n : g;
     };
+    auto known = [&](const EncTable& t, uint64_t A, int64_t& f, uint64_t& s) {
+        const int j = __popcll(__ballot(t.start <= A)) - 1;
+        f = t.kb + j;
+        s = readlane64(t.start, j);
+    };
+    int64_t f;
+    uint64_t s;
+    EncTable tc, tn;
+    Plan<U> pc, pn;
     uint64_t A = c * kWin;
-    EncTable t;
-    enc_table_issue(a, t, guess(0, a.wmis, A), lane);
+    enc_table_issue(a, tc, guess(0, a.wmis, A), lane);
+    enc_table_finish(tc);
+    enc_resolve(a, tc, A, wire_total, lane);
+    plan_chunk<U, NT>(a, tc, A, wlo, whi, lane, pc);
+    known(tc, A, f, s);
+    uint64_t cn = c + nwaves;
+    if (cn < nwin) enc_table_issue(a, tn, guess(f, s, cn * kWin), lane);
     for (;;) {
-        // resolve this chunk's table (issued a chunk ago)
-        enc_table_finish(t);
-        {
-            const uint64_t m = __ballot(t.start <= A);
-            if (!(m != 0 && (t.tail || m != ~0ull))) enc_table_load(a, t, enc_locate(a, A, wire_total, lane), lane);
+        EncTable tnn;
+        if (cn < nwin) {
+            const uint64_t An = cn * kWin;
+            enc_table_finish(tn);
+            enc_resolve(a, tn, An, wire_total, lane);
+            plan_chunk<U, NT>(a, tn, An, wlo, whi, lane, pn);
+            known(tn, An, f, s);
+            if (cn + nwaves < nwin) enc_table_issue(a, tnn, guess(f, s, (cn + nwaves) * kWin), lane);
         }
-        const int j0 = __popcll(__ballot(t.start <= A)) - 1;
-        const int64_t f_known = t.kb + j0;
-        const uint64_t s_known = readlane64(t.start, j0);
-        const uint64_t cn = c + nwaves;
-        EncTable tn;
-        if (cn < nwin) enc_table_issue(a, tn, guess(f_known, s_known, cn * kWin), lane);
-
-        // phase 1: plan each span, issue its loads
-        // per span and lane, what phase 2 needs: the two loads, the two rotated keys,
-        // and one packed word: plo1 | phi1 << 5 | plo2 << 10 | phi2 << 15 | two << 20 | slow << 21
-        int kind[U];
-        u32x4 d1[U], d2[U];
-        uint32_t rk1[U], rk2[U], pk[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t A0 = A + (uint64_t)u * kSpan, Aend = A0 + kSpan;
-            const uint64_t W = A0 + 16ull * (uint64_t)lane;
-            kind[u] = kSpanCompose;
-            if (A0 >= whi) continue;
-            const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
-            const uint64_t bm = __ballot(t.start > A0 && t.start < Aend);
-            const int nb = __popcll(bm);
-            const bool covered = (t.tail || t.last >= Aend) && l0 + nb + 1 <= kWave - 1;
-            if (!covered || A0 < wlo || Aend > whi || t.kb + l0 < 0 || t.kb + l0 + nb >= (int64_t)a.n) continue;
-            const FrameInfo f0 = frame_info(a, t, l0);
-            if (nb == 0 && f0.pw <= A0 && Aend <= f0.We) {
-                kind[u] = kSpanFast;
-                const Slot sf = slot_of(f0, W);
-                rk1[u] = sf.rk;
-                d1[u] = load_u<NT>(a.src + sf.s0);
-                continue;
-            }
-            kind[u] = kSpanSlots;
-            Slot a1 = slot_of(f0, W), a2 = a1;
-            int cut = 0;   // frame starts inside (W, W + 15]
-            uint64_t b = bm;
-            while (b) {
-                const int l = __builtin_ctzll(b);
-                b &= b - 1;
-                const FrameInfo fj = frame_info(a, t, l);
-                const Slot sj = slot_of(fj, W);
-                a1 = select_slot(W >= fj.Ws, sj, a1);
-                a2 = select_slot(W + 15 >= fj.Ws, sj, a2);
-                cut += (fj.Ws > W && fj.Ws <= W + 15) ? 1 : 0;
-            }
-            const bool two = cut == 1;
-            bool slow = cut > 1;
-            // a load must stay inside [0, src_total): near the ends of the payload the
-            // compose path reads byte by byte
-            const bool need1 = a1.phi > a1.plo, need2 = two && a2.phi > a2.plo;
-            slow |= need1 && (a1.s0 < 0 || (uint64_t)a1.s0 + 16 > a.src_total);
-            slow |= need2 && (a2.s0 < 0 || (uint64_t)a2.s0 + 16 > a.src_total);
-            rk1[u] = a1.rk;
-            rk2[u] = a2.rk;
-            pk[u] = (uint32_t)a1.plo | (uint32_t)a1.phi << 5 | (uint32_t)a2.plo << 10 | (uint32_t)a2.phi << 15 |
-                    (two ? 1u << 20 : 0u) | (slow ? 1u << 21 : 0u);
-            if (need1 && !slow) d1[u] = load_u<NT>(a.src + a1.s0);
-            if (need2 && !slow) d2[u] = load_u<NT>(a.src + a2.s0);
-        }
-
-        // phase 2: mask, headers, store (lanes / spans needing the general path are
-        // left to phase 3, so the compose code is instantiated once, not per span)
-        uint32_t compose_spans = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t A0 = A + (uint64_t)u * kSpan, Aend = A0 + kSpan;
-            if (A0 >= whi) break;
-            const uint64_t W = A0 + 16ull * (uint64_t)lane;
-            u32x4 v;
-            if (kind[u] == kSpanCompose) {
-                compose_spans |= 1u << u;
-                continue;
-            }
-            if (kind[u] == kSpanFast) {
-                const u32x4 kv = {rk1[u], rk1[u], rk1[u], rk1[u]};
-                v = d1[u] ^ kv;
-            } else {   // kSpanSlots
-                const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
-                const uint32_t p = pk[u];
-                const u32x4 k1 = {rk1[u], rk1[u], rk1[u], rk1[u]};
-                const u32x4 k2 = {rk2[u], rk2[u], rk2[u], rk2[u]};
-                v = (d1[u] ^ k1) & select_range(p & 31, (p >> 5) & 31);
-                if (p & (1u << 20)) v |= (d2[u] ^ k2) & select_range((p >> 10) & 31, (p >> 15) & 31);
-                // headers: the span's first frame (if the span starts inside its
-                // header) and every frame starting inside the span
-                const FrameInfo f0 = frame_info(a, t, l0);
-                if (f0.pw > A0) v = put_header(a, f0, W, v);
-                uint64_t b = __ballot(t.start > A0 && t.start < Aend);
-                while (b) {
-                    const int l = __builtin_ctzll(b);
-                    b &= b - 1;
-                    v = put_header(a, frame_info(a, t, l), W, v);
-                }
-                if (__ballot((p >> 21) & 1)) compose_spans |= 1u << u;
-                if ((p >> 21) & 1) continue;   // this lane's vector: phase 3
-            }
-            store_wire<NT>(a, W, v, wlo, whi);
-        }
-        // phase 3: the general path, span by span (the table may slide here)
-        for (int u = 0; u < U; ++u) {
-            if (!((compose_spans >> u) & 1)) continue;
-            const uint64_t A0 = A + (uint64_t)u * kSpan, Aend = A0 + kSpan;
-            const uint64_t W = A0 + 16ull * (uint64_t)lane;
-            // a kSpanSlots span only recomposes its slow lanes
-            const bool mine = kind[u] == kSpanCompose || ((pk[u] >> 21) & 1);
-            int l0 = __popcll(__ballot(t.start <= A0)) - 1;
-            if (l0 >= kWave - 1 || (l0 > 0 && !t.tail && t.last < Aend)) {
-                enc_table_load(a, t, t.kb + l0, lane);
-                l0 = 0;
-            }
-            const u32x4 v = compose_vec<NT>(a, t, l0, A0, W, lane);
-            if (mine) store_wire<NT>(a, W, v, wlo, whi);
-        }
+        finish_chunk<U, NT>(a, tc, A, wlo, whi, lane, pc);
         if (cn >= nwin) break;
-        c = cn;
         A = cn * kWin;
-        t = tn;
+        tc = tn;
+        tn = tnn;
+        pc = pn;
+        cn += nwaves;
+    }
+}
+
+// The queued spans: each wavefront takes queue entries in turn and composes them.
+__global__ __launch_bounds__(256) void encode_queued_kernel(EncArgs a) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / kWave);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+    const uint64_t count = min((uint64_t)*a.defer_count, a.defer_cap);
+    const uint64_t wire_total = gptr(a.wo)[a.n];
+    const uint64_t wlo = a.wmis, whi = a.wmis + wire_total;
+    for (uint64_t q = wave; q < count; q += nwaves) {
+        const uint64_t A0 = a.defer[q];
+        EncTable t;
+        enc_table_load(a, t, enc_locate(a, A0, wire_total, lane), lane);
+        const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
+        const uint64_t W = A0 + 16ull * (uint64_t)lane;
+        const u32x4 v = compose_vec(a, t, l0, A0, W, lane);
+        if (W < whi) store_wire<false>(a, W, v, wlo, whi);
     }
 }
 
@@ -574,74 +659,104 @@ static int enc_resident_blocks() {
     return cache[dev];
 }
 
-// Scan scratch: one status word per tile, per (device, stream).  Scans queued on
-// one stream run one after another, so they can share an array (the epoch tells
-// their words apart); scans on different streams may run concurrently and get
-// different arrays.  Arrays grow geometrically and are never freed: an outgrown
-// one may still be read by scans queued before the growth.
-struct ScanScratch {
+// Per (device, stream) scratch: the scan's status words (one per tile) and the
+// span queue.  Work queued on one stream runs in order, so it can share them (the
+// epoch tells scans apart); streams may run concurrently and get their own.
+// Arrays grow geometrically and are never freed: an outgrown one may still be
+// read by work queued before the growth.
+struct EncScratch {
     uint64_t* status = nullptr;
     uint64_t tiles = 0;
     uint32_t epoch = 0;
+    uint64_t* defer = nullptr;   // defer[0 .. cap), then the counter word
+    uint64_t defer_cap = 0;
 };
 
-hipError_t launch_wire_offsets(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream) {
-    if (n == 0) return hipMemsetAsync(wo, 0, sizeof(uint64_t), stream);
-    const uint64_t tiles = n / kScanBlock + 1;   // frames 0 .. n inclusive
-    if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    static std::map<std::pair<int, hipStream_t>, ScanScratch> scratch;
-    static std::mutex mu;
+static std::map<std::pair<int, hipStream_t>, EncScratch> g_scratch;
+static std::mutex g_scratch_mu;
+
+static hipError_t scratch_for(hipStream_t stream, uint64_t tiles, uint64_t spans, EncScratch& out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    uint64_t* status;
-    uint32_t epoch;
-    {
-        std::lock_guard<std::mutex> g(mu);
-        ScanScratch& sc = scratch[{dev, stream}];
-        if (sc.tiles < tiles) {
-            uint64_t* p = nullptr;
-            uint64_t want = sc.tiles ? 2 * sc.tiles : 1024;
-            while (want < tiles) want *= 2;
-            if ((e = hipMalloc(&p, want * sizeof(uint64_t))) != hipSuccess) return e;
-            if ((e = hipMemsetAsync(p, 0, want * sizeof(uint64_t), stream)) != hipSuccess) return e;
-            sc.status = p;
-            sc.tiles = want;
-            sc.epoch = 0;
-        }
-        sc.epoch = (sc.epoch + 1) & 0xFFFF;
-        if (sc.epoch == 0) {   // epochs wrapped: clear the words so no stale epoch can match
-            if ((e = hipMemsetAsync(sc.status, 0, sc.tiles * sizeof(uint64_t), stream)) != hipSuccess) return e;
-            sc.epoch = 1;
-        }
-        status = sc.status;
-        epoch = sc.epoch;
+    std::lock_guard<std::mutex> g(g_scratch_mu);
+    EncScratch& sc = g_scratch[{dev, stream}];
+    if (sc.tiles < tiles) {
+        uint64_t* p = nullptr;
+        uint64_t want = sc.tiles ? 2 * sc.tiles : 1024;
+        while (want < tiles) want *= 2;
+        if ((e = hipMalloc(&p, want * sizeof(uint64_t))) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(p, 0, want * sizeof(uint64_t), stream)) != hipSuccess) return e;
+        sc.status = p;
+        sc.tiles = want;
+        sc.epoch = 0;
     }
+    if (sc.defer_cap < spans) {
+        uint64_t* p = nullptr;
+        uint64_t want = sc.defer_cap ? 2 * sc.defer_cap : 4096;
+        while (want < spans) want *= 2;
+        if ((e = hipMalloc(&p, (want + 1) * sizeof(uint64_t))) != hipSuccess) return e;
+        sc.defer = p;
+        sc.defer_cap = want;
+    }
+    sc.epoch = (sc.epoch + 1) & 0xFFFF;
+    if (sc.epoch == 0) {   // epochs wrapped: clear the words so no stale epoch can match
+        if ((e = hipMemsetAsync(sc.status, 0, sc.tiles * sizeof(uint64_t), stream)) != hipSuccess) return e;
+        sc.epoch = 1;
+    }
+    out = sc;
+    return hipSuccess;
+}
+
+static hipError_t launch_scan(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream,
+                              const EncScratch& sc) {
+    const uint64_t tiles = n / kScanBlock + 1;   // frames 0 .. n inclusive
     hipLaunchKernelGGL(wire_offsets_chained, dim3((unsigned)tiles), dim3(kScanThreads), 0, stream, off, n,
-                       (uint32_t)(2 + (masked ? 4 : 0)), wo, status, epoch);
+                       (uint32_t)(2 + (masked ? 4 : 0)), wo, sc.status, sc.epoch,
+                       (uint32_t*)(sc.defer + sc.defer_cap));
     return hipGetLastError();
+}
+
+hipError_t launch_wire_offsets(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream) {
+    if (n == 0) return hipMemsetAsync(wo, 0, sizeof(uint64_t), stream);
+    const uint64_t tiles = n / kScanBlock + 1;
+    if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    EncScratch sc;
+    hipError_t e = scratch_for(stream, tiles, 1, sc);
+    if (e != hipSuccess) return e;
+    return launch_scan(off, n, masked, wo, stream, sc);
 }
 
 template <int U>
 static hipError_t launch_enc_u(EncArgs a, uint64_t wire_bound, bool nt, int max_blocks, hipStream_t stream) {
-    a.nwin = (a.wmis + wire_bound + kSpan * U - 1) / (kSpan * U);
+    const uint64_t nwin = (a.wmis + wire_bound + kSpan * U - 1) / (kSpan * U);
     const uint64_t cap = (uint64_t)(max_blocks > 0 ? max_blocks
                                                   : (nt ? enc_resident_blocks<U, true>() : enc_resident_blocks<U, false>()));
-    const uint64_t want = (a.nwin + 3) / 4;
+    const uint64_t want = (nwin + 3) / 4;
     const int blocks = (int)(want < cap ? want : cap);
     if (blocks <= 0) return hipSuccess;
     if (nt) hipLaunchKernelGGL((encode_frames_kernel<U, true>), dim3(blocks), dim3(256), 0, stream, a);
     else hipLaunchKernelGGL((encode_frames_kernel<U, false>), dim3(blocks), dim3(256), 0, stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(encode_queued_kernel, dim3(256), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_t* src, uint64_t src_total,
                                 const uint64_t* off, const uint32_t* keys, const uint8_t* b0, uint64_t n, bool masked,
                                 uint64_t* wo, hipStream_t stream, const LaunchCfg& cfg) {
-    hipError_t e = launch_wire_offsets(off, n, masked, wo, stream);
-    if (e != hipSuccess || n == 0) return e;
+    if (n == 0) return hipMemsetAsync(wo, 0, sizeof(uint64_t), stream);
+    const uint64_t tiles = n / kScanBlock + 1;
+    if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    const uint64_t wmis = (uint64_t)(uintptr_t)wire & 15u;
+    const uint64_t spans = (wmis + wire_bound + kSpan - 1) / kSpan + 8;   // every span could be queued
+    EncScratch sc;
+    hipError_t e = scratch_for(stream, tiles, spans, sc);
+    if (e != hipSuccess) return e;
+    if ((e = launch_scan(off, n, masked, wo, stream, sc)) != hipSuccess) return e;
     EncArgs a;
-    a.wmis = (uint64_t)(uintptr_t)wire & 15u;
+    a.wmis = wmis;
     a.wire_base = wire - a.wmis;
     a.src = src;
     a.src_total = src_total;
@@ -651,6 +766,9 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     a.b0 = b0;
     a.n = n;
     a.masked = masked ? 1u : 0u;
+    a.defer = sc.defer;
+    a.defer_count = (uint32_t*)(sc.defer + sc.defer_cap);
+    a.defer_cap = sc.defer_cap;
     const bool nt = cfg.flags < 0 || (cfg.flags & (kNtLoads | kNtStores));
     // U = 2 KiB chunks unless tuned to 4 (netc_gpu_tune's unroll; 1 and 8 map to 2 and 4)
     if (cfg.unroll >= 4) return launch_enc_u<4>(a, wire_bound, nt, cfg.max_blocks, stream);
