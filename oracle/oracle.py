@@ -44,6 +44,10 @@ def _load(name: str) -> ctypes.CDLL:
             lib.oracle_scan_frames.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, vp, vp, vp, sz,
                                                vp, vp]
             lib.oracle_scan_frames.restype = sz
+            lib.oracle_utf8_valid.argtypes = [vp, sz]
+            lib.oracle_utf8_valid.restype = ctypes.c_int
+            lib.oracle_validate_batch.argtypes = [vp, vp, vp, sz, vp]
+            lib.oracle_validate_batch.restype = None
             lib.oracle_decode_message.argtypes = [vp, sz, vp, sz, vp, vp]
             lib.oracle_decode_message.restype = sz
         else:
@@ -142,6 +146,22 @@ def scan_frames(wire, start: int = 0, strict: bool = True, opt: str = "O2", cap:
                                     ctypes.addressof(consumed), ctypes.addressof(error))
     err = None if error.value == (1 << 64) - 1 else int(error.value)
     return hdr[:n], keys[:n], b0[:n], int(consumed.value), err
+
+
+def utf8_valid(data) -> bool:
+    """oracle_utf8_valid: RFC 3629 validity of a byte string."""
+    b = _u8(data)
+    return bool(lib().oracle_utf8_valid(_p(b) if b.size else None, b.size))
+
+
+def validate_batch(payload, offsets: np.ndarray, header0: np.ndarray) -> np.ndarray:
+    """oracle_validate_batch: per-frame TEXT-message verdicts (0 on the last frame of an invalid message)."""
+    p = _u8(payload)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    h = np.ascontiguousarray(header0, dtype=np.uint8)
+    out = np.zeros(max(1, off.size - 1), dtype=np.uint8)
+    lib().oracle_validate_batch(_p(p) if p.size else None, _p(off), _p(h), off.size - 1, _p(out))
+    return out[: off.size - 1]
 
 
 def decode_message(wire: bytes, cap: Optional[int] = None) -> Tuple[int, bytes, int]:

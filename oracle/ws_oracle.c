@@ -197,6 +197,103 @@ size_t oracle_scan_frames(const uint8_t *wire, uint64_t len, uint64_t start, int
 }
 
 /*
+ * UTF-8 validity (RFC 3629 §3-4: shortest form, no surrogates D800-DFFF, nothing
+ * above U+10FFFF) — what RFC 6455 §8.1 requires of a TEXT message and the
+ * reference never checks (src/ws/common.c:342 only appends a NUL).  A plain
+ * byte-at-a-time decoder, the checker of the fused unmask + validate kernel.
+ * Returns 1 if s[0, n) is valid UTF-8.
+ */
+int oracle_utf8_valid(const uint8_t *s, size_t n)
+{
+    size_t i = 0;
+    while (i < n)
+    {
+        const uint8_t c = s[i];
+        size_t need;
+        uint32_t cp;
+        if (c < 0x80)
+        {
+            ++i;
+            continue;
+        }
+        else if (c >= 0xC2 && c <= 0xDF)
+        {
+            need = 1;
+            cp = c & 0x1F;
+        }
+        else if (c >= 0xE0 && c <= 0xEF)
+        {
+            need = 2;
+            cp = c & 0x0F;
+        }
+        else if (c >= 0xF0 && c <= 0xF4)
+        {
+            need = 3;
+            cp = c & 0x07;
+        }
+        else
+            return 0; /* continuation byte, C0 / C1, F5..FF */
+        if (n - i - 1 < need) return 0; /* truncated sequence */
+        for (size_t k = 1; k <= need; ++k)
+        {
+            if ((s[i + k] & 0xC0) != 0x80) return 0;
+            cp = cp << 6 | (s[i + k] & 0x3F);
+        }
+        if ((need == 2 && cp < 0x800) || (need == 3 && cp < 0x10000)) return 0; /* overlong */
+        if (cp >= 0xD800 && cp <= 0xDFFF) return 0;                            /* surrogate */
+        if (cp > 0x10FFFF) return 0;
+        i += need + 1;
+    }
+    return 1;
+}
+
+/*
+ * The TEXT-message verdicts of a frame batch (include/ws/mask.h layout, payload
+ * already unmasked, header0[k] = FIN | RSV | opcode): a TEXT message is a frame
+ * with opcode 1 and the continuation frames (opcode 0) after it up to the first
+ * with FIN set; control frames (opcode >= 8) in between are not part of it (RFC
+ * 6455 §5.4).  valid[k] = 0 for the last frame of a TEXT message whose payload
+ * bytes, concatenated, are not valid UTF-8; 1 everywhere else (other frames,
+ * other messages, a message still open at the end of the batch, or abandoned by a
+ * new data frame before its FIN).
+ */
+#include <stdlib.h>
+void oracle_validate_batch(const uint8_t *payload, const uint64_t *off, const uint8_t *header0, size_t nframes,
+                           uint8_t *valid)
+{
+    uint8_t *msg = NULL;
+    size_t len = 0, cap = 0;
+    int open = 0; /* a TEXT message is being collected */
+    for (size_t k = 0; k < nframes; ++k)
+    {
+        valid[k] = 1;
+        const uint8_t op = header0[k] & 0x0F, fin = header0[k] >> 7;
+        if (op >= 8) continue; /* control frame */
+        if (op != 0) open = 0; /* a new message starts (an open one is abandoned) */
+        if (op == 1)
+        {
+            open = 1;
+            len = 0;
+        }
+        if (!open) continue;
+        const size_t n = (size_t)(off[k + 1] - off[k]);
+        if (len + n > cap)
+        {
+            cap = (len + n) * 2 + 16;
+            msg = (uint8_t *)realloc(msg, cap);
+        }
+        memcpy(msg + len, payload + off[k], n);
+        len += n;
+        if (fin)
+        {
+            valid[k] = (uint8_t)oracle_utf8_valid(msg, len);
+            open = 0;
+        }
+    }
+    free(msg);
+}
+
+/*
  * src/ws/common.c:146-347 as a pure function over a complete byte stream:
  * decodes frames until one with FIN completes a message.  On success returns
  * the wire bytes consumed and writes the message (payload bytes, unmasked, no
