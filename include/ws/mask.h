@@ -124,6 +124,25 @@ int netc_gpu_mask_batch(int device, void *d_dst, const void *d_src, size_t total
                         void *stream);
 
 /**
+ * netc_gpu_mask_batch plus, in the same pass over the bytes, the UTF-8 check RFC
+ * 6455 §8.1 requires of TEXT messages (RFC 3629: shortest form, no surrogates,
+ * nothing above U+10FFFF) — SURVEY.md §8(f) row 3; the reference never checks
+ * (src/ws/common.c:342 only appends a NUL).
+ *   d_header0   device, nframes bytes: header byte 0 of each frame (FIN | RSV | opcode)
+ *   d_valid     device output, nframes bytes
+ * A TEXT message is a frame with opcode 1 and the continuation frames (opcode 0)
+ * after it up to the first with FIN; control frames between them (opcode >= 8)
+ * are not part of it.  d_valid[k] = 0 on the FIN frame of a TEXT message whose
+ * unmasked payload, concatenated over its frames, is not valid UTF-8 (a code point
+ * may be split between frames); 1 everywhere else — other messages, and a message
+ * the batch does not finish.  d_dst receives the unmasked payload as with
+ * netc_gpu_mask_batch.  Scratch of nframes bytes is kept per (device, stream).
+ */
+int netc_gpu_unmask_validate(int device, void *d_dst, const void *d_src, size_t total_bytes,
+                             const uint64_t *d_frame_offsets, const uint32_t *d_keys, const uint8_t *d_header0,
+                             size_t nframes, uint8_t *d_valid, void *stream);
+
+/**
  * One shard per device, already resident: shard i lives on devices[i] and is
  * described exactly as for netc_gpu_mask_batch (offsets rebased to the shard's
  * own payload start).  All shards are launched before any is waited for; with

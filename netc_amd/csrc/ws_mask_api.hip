@@ -8,6 +8,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "ws_mask_gpu.h"
@@ -132,6 +134,45 @@ int netc_gpu_mask_batch(int device, void* d_dst, const void* d_src, size_t total
     if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
     return mask_batch_on_current(d_dst, d_src, total_bytes, d_frame_offsets, d_keys, nframes,
                                  (hipStream_t)stream);
+}
+
+int netc_gpu_unmask_validate(int device, void* d_dst, const void* d_src, size_t total_bytes,
+                             const uint64_t* d_frame_offsets, const uint32_t* d_keys, const uint8_t* d_header0,
+                             size_t nframes, uint8_t* d_valid, void* stream) {
+    if (int r = check_device(device)) return r;
+    if (nframes == 0) return 0;
+    if (!d_frame_offsets || !d_keys || !d_header0 || !d_valid) return fail(NETC_GPU_EINVAL, "null frame array");
+    if (total_bytes && (!d_dst || !d_src)) return fail(NETC_GPU_EINVAL, "null payload buffer");
+    if (partial_overlap(d_dst, d_src, total_bytes)) return fail(NETC_GPU_EINVAL, "dst and src partially overlap");
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+    // per (device, stream) flag scratch, grown geometrically, never freed (queued work may still use it)
+    static std::mutex mu;
+    static std::vector<std::pair<std::pair<int, void*>, std::pair<uint8_t*, size_t>>> scratch;
+    uint8_t* verr = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = std::find_if(scratch.begin(), scratch.end(),
+                               [&](const auto& e) { return e.first.first == device && e.first.second == stream; });
+        if (it == scratch.end()) {
+            scratch.push_back({{device, stream}, {nullptr, 0}});
+            it = scratch.end() - 1;
+        }
+        if (it->second.second < nframes) {
+            size_t want = it->second.second ? 2 * it->second.second : 65536;
+            while (want < nframes) want *= 2;
+            void* p = nullptr;
+            hipError_t e = hipMalloc(&p, want);
+            if (e != hipSuccess) return fail_hip(NETC_GPU_ENOMEM, "validation scratch", e);
+            it->second = {(uint8_t*)p, want};
+        }
+        verr = it->second.first;
+    }
+    hipError_t e = netc_gpu::launch_mask_validate((uint8_t*)d_dst, (const uint8_t*)d_src, total_bytes,
+                                                  d_frame_offsets, d_keys, d_header0, nframes, verr, d_valid,
+                                                  (hipStream_t)stream, g_cfg);
+    if (e != hipSuccess) return fail_hip(NETC_GPU_ELAUNCH, "unmask + validate launch", e);
+    return 0;
 }
 
 int netc_gpu_mask_batch_multi(int nshards, const int* devices, void* const* d_dst, const void* const* d_src,

@@ -233,7 +233,101 @@ __device__ __forceinline__ void edge_vec(const Args& a, uint64_t P, u32x4 mask) 
 // A chunk that holds one of the two partial 16-B vectors at the ends of an
 // unaligned buffer (at most three chunks per batch): per-vector range checks,
 // a fresh frame search, no prefetch.
-template <int U, bool SRC_ALIGNED, bool NT>
+// ------------------------------------------------------ UTF-8 validation --
+// RFC 3629 checked byte by byte from the byte and the 3 before it (the local
+// rules of the "lookup" validators): a byte must be a continuation exactly when a
+// lead 1-3 bytes back asks for one; C0, C1 and F5..FF never occur; the byte after
+// E0 / ED / F0 / F4 is limited (shortest form, surrogates, U+10FFFF).  Four bytes
+// at a time in a dword (SWAR); bit 7 of each byte of the result flags an error.
+__device__ __forceinline__ uint32_t sw_ge(uint32_t y, uint32_t c) {   // byte >= c, for c in [0x80, 0xFF]
+    return y & ((y & 0x7F7F7F7Fu) + (0x100u - c) * 0x01010101u) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t sw_eq(uint32_t y, uint32_t c) {   // byte == c
+    const uint32_t z = y ^ (c * 0x01010101u);
+    return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t utf8_err_word(uint32_t x, uint32_t prev) {
+    const uint32_t hi = 0x80808080u;
+    const uint32_t p1 = __builtin_amdgcn_alignbyte(x, prev, 3);   // the byte before each byte of x
+    const uint32_t p2 = __builtin_amdgcn_alignbyte(x, prev, 2);
+    const uint32_t p3 = __builtin_amdgcn_alignbyte(x, prev, 1);
+    if (((x | p3) & hi) == 0) return 0;   // all ASCII, nothing pending
+    const uint32_t cont = x & ~(x << 1) & hi;
+    const uint32_t need = ((p1 & (p1 << 1)) | (p2 & (p2 << 1) & (p2 << 2)) | (p3 & (p3 << 1) & (p3 << 2) & (p3 << 3))) & hi;
+    uint32_t err = need ^ cont;
+    err |= sw_ge(x, 0xF5) | (sw_ge(x, 0xC0) & ~sw_ge(x, 0xC2));
+    if (sw_ge(p1, 0xE0)) {
+        const uint32_t geA0 = sw_ge(x, 0xA0), ge90 = sw_ge(x, 0x90);
+        err |= (sw_eq(p1, 0xE0) & ~geA0) | (sw_eq(p1, 0xED) & geA0) | (sw_eq(p1, 0xF0) & ~ge90) | (sw_eq(p1, 0xF4) & ge90);
+    }
+    return err & hi;
+}
+
+// Phase A of the TEXT check, per span: flag the frames holding a byte that breaks
+// the local rules.  out = this lane's unmasked 16 bytes, prevd = the 4 bytes before
+// them.  The first 3 bytes of every frame are skipped (their rule reaches into the
+// previous frame of the message; utf8_messages() checks them), so are bytes in no
+// frame.  Errors are rare: their frame lookup is a slow path.
+__device__ __forceinline__ void validate_span(const Args& a, const Table& t, uint64_t A0, u32x4 out, uint32_t prevd,
+                                              int lane) {
+    const uint64_t W = A0 + 16ull * (uint64_t)lane;
+    u32x4 e;
+    e[0] = utf8_err_word(out[0], prevd);
+    e[1] = utf8_err_word(out[1], out[0]);
+    e[2] = utf8_err_word(out[2], out[1]);
+    e[3] = utf8_err_word(out[3], out[2]);
+    if (!__ballot((e[0] | e[1] | e[2] | e[3]) != 0)) return;
+    // drop bytes within 3 of a frame start: the span's first frame (if it starts
+    // less than 3 bytes before A0) and every frame starting inside the span
+    const uint64_t Aend = A0 + kSpan;
+    const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
+    const uint64_t s0 = readlane64(t.start, l0);
+    if (s0 + 3 > A0) e &= ~(select_from((int64_t)(s0 - W)) & ~select_from((int64_t)(s0 + 3 - W)));
+    uint64_t b = __ballot(t.start > A0 && t.start < Aend);
+    while (b) {
+        const int j = __builtin_ctzll(b);
+        b &= b - 1;
+        const uint64_t sj = readlane64(t.start, j);
+        e &= ~(select_from((int64_t)(sj - W)) & ~select_from((int64_t)(sj + 3 - W)));
+    }
+    const uint32_t any = e[0] | e[1] | e[2] | e[3];
+    if (!__ballot(any != 0)) return;
+    if (any) {
+        for (int k = 0; k < 16; ++k) {
+            if (!((e[k >> 2] >> (8 * (k & 3) + 7)) & 1)) continue;
+            const uint64_t p = W + k;
+            int64_t f = -2;   // frame holding p: the last table entry starting at or before it
+            for (int l = 0; l < kWave; ++l) {
+                const uint64_t sl = __builtin_amdgcn_readlane((int)(uint32_t)t.start, l) |
+                                    ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(t.start >> 32), l) << 32);
+                if (sl <= p) f = t.kb + l;
+            }
+            if (f >= 0 && f < (int64_t)a.n) a.verr[f] = 1;
+        }
+    }
+}
+
+// the 4 unmasked bytes before chunk position A (P coordinates), for the span check:
+// bytes of the frame holding A-1 carry its key; bytes of an earlier frame only
+// feed rules that validate_span drops anyway
+template <bool SRC_ALIGNED>
+__device__ __forceinline__ uint32_t chunk_prev_dword(const Args& a, const Table& t, uint64_t A, uint32_t raw) {
+    if (A < 4) return 0;
+    const int l0 = __popcll(__ballot(t.start <= A - 1)) - 1;
+    if (l0 < 0) return 0;
+    const uint64_t s0 = readlane64(t.start, l0);
+    return raw ^ rotr8(readlane32(t.key, l0), (A - 4) - s0);
+}
+
+template <bool SRC_ALIGNED>
+__device__ __forceinline__ uint32_t load_prev_raw(const Args& a, uint64_t A) {
+    if (A < 4) return 0;
+    const NETC_GLOBAL uint8_t* p = gptr(a.src_base + A - 4);
+    if constexpr (SRC_ALIGNED) return *(const NETC_GLOBAL uint32_t*)p;
+    return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+
+template <int U, bool SRC_ALIGNED, bool NT, bool VAL>
 __device__ __forceinline__ void edge_chunk(const Args& a, uint64_t A, int lane) {
     constexpr uint64_t kWin = kSpan * U;
     const uint64_t full_lo = a.mis ? 16 : 0;
@@ -247,6 +341,17 @@ __device__ __forceinline__ void edge_chunk(const Args& a, uint64_t A, int lane) 
     }
     Table t;
     table_load(a, t, locate(a, A, lane), lane);
+    uint32_t carry = 0;
+    if constexpr (VAL) {
+        // bytes before A inside the buffer, unmasked (zero outside it)
+        const uint64_t lo = a.mis, hi = a.mis + a.total;
+        uint32_t raw = 0;
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t q = A - 4 + k;
+            if (A >= 4 && q >= lo && q < hi) raw |= (uint32_t)gptr(a.src_base)[q] << (8 * k);
+        }
+        carry = chunk_prev_dword<SRC_ALIGNED>(a, t, A, raw);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t A0 = A + (uint64_t)u * kSpan;
@@ -255,6 +360,23 @@ __device__ __forceinline__ void edge_chunk(const Args& a, uint64_t A, int lane) 
         const uint64_t P = A0 + 16ull * lane;
         if (P >= full_lo && P < full_hi) store_vec<NT>(a, P, d[u] ^ m);
         else if (P < vec_end) edge_vec(a, P, m);
+        if constexpr (VAL) {
+            // the unmasked vector; bytes outside the buffer read as 0
+            u32x4 out = {0, 0, 0, 0};
+            if (P >= full_lo && P < full_hi) {
+                out = d[u] ^ m;
+            } else {
+                const uint64_t lo = a.mis, hi = a.mis + a.total;
+#pragma unroll
+                for (int bi = 0; bi < 16; ++bi)
+                    if (P + bi >= lo && P + bi < hi)
+                        out[bi >> 2] |= (uint32_t)(gptr(a.src_base)[P + bi] ^ (uint8_t)(m[bi >> 2] >> (8 * (bi & 3))))
+                                        << (8 * (bi & 3));
+            }
+            const uint32_t up = (uint32_t)__shfl_up((int)out[3], 1, kWave);
+            validate_span(a, t, A0, out, lane ? up : carry, lane);
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1);
+        }
     }
     (void)kWin;
 }
@@ -274,7 +396,7 @@ __device__ __forceinline__ void edge_chunk(const Args& a, uint64_t A, int lane) 
 // table base of the next chunk is guessed from the frame known to hold this one
 // (exact for evenly sized frames); a miss falls back to locate().  The <= 3
 // partial chunks at the buffer ends go through edge_chunk().
-template <int U, bool SRC_ALIGNED, bool NT>
+template <int U, bool SRC_ALIGNED, bool NT, bool VAL = false>
 __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) {
     constexpr uint64_t kWin = kSpan * U;
     const int lane = threadIdx.x & (kWave - 1);
@@ -305,9 +427,9 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
     uint64_t ci_hi = full_hi / kWin;
     if (ci_hi < ci_lo) ci_hi = ci_lo;
     // edge chunks: chunk 0 when the buffer start is unaligned, and [ci_hi, nwin)
-    if (a.mis && wave == 0) edge_chunk<U, SRC_ALIGNED, NT>(a, 0, lane);
+    if (a.mis && wave == 0) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, 0, lane);
     for (uint64_t e = ci_hi; e < a.nwin; ++e)
-        if (e % nwaves == (wave + 1) % nwaves) edge_chunk<U, SRC_ALIGNED, NT>(a, e * kWin, lane);
+        if (e % nwaves == (wave + 1) % nwaves) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, e * kWin, lane);
 
     uint64_t c = ci_lo + wave;
     if (c >= ci_hi) return;
@@ -316,12 +438,20 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
 #pragma unroll
         for (int u = 0; u < U; ++u) dst[u] = load_vec<SRC_ALIGNED, NT>(a, base + (uint64_t)u * kSpan + 16ull * lane);
     };
-    auto process = [&](const u32x4 (&src)[U], Table& t, uint64_t base) {
+    auto process = [&](const u32x4 (&src)[U], Table& t, uint64_t base, uint32_t prev_raw) {
+        uint32_t carry = 0;
+        if constexpr (VAL) carry = chunk_prev_dword<SRC_ALIGNED>(a, t, base, prev_raw);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t A0 = base + (uint64_t)u * kSpan;
             const u32x4 m = span_mask(a, t, A0, lane);
-            store_vec<NT>(a, A0 + 16ull * lane, src[u] ^ m);
+            const u32x4 out = src[u] ^ m;
+            store_vec<NT>(a, A0 + 16ull * lane, out);
+            if constexpr (VAL) {
+                const uint32_t up = (uint32_t)__shfl_up((int)out[3], 1, kWave);
+                validate_span(a, t, A0, out, lane ? up : carry, lane);
+                carry = (uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1);
+            }
         }
     };
     // make t hold the frame containing A (its probe was issued a chunk ago)
@@ -336,6 +466,8 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
     u32x4 d[U];
     uint64_t A = c * kWin;
     load_window(d, A);
+    uint32_t pr = 0;
+    if constexpr (VAL) pr = load_prev_raw<SRC_ALIGNED>(a, A);
     Table t;
     table_issue(a, t, guess_base(a, 0, a.mis, A), lane);   // global guess: frame 0 starts near P = mis
 
@@ -346,10 +478,13 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
         const uint64_t An = cn * kWin;
         u32x4 dn[U];
         load_window(dn, An);
+        uint32_t prn = 0;
+        if constexpr (VAL) prn = load_prev_raw<SRC_ALIGNED>(a, An);
         Table tn;
         table_issue(a, tn, guess_base(a, f0, s0, An), lane);
-        process(d, t, A);
+        process(d, t, A, pr);
         A = An;
+        pr = prn;
         t = tn;
 #pragma unroll
         for (int u = 0; u < U; ++u) d[u] = dn[u];
@@ -357,8 +492,9 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
     int64_t f0;
     uint64_t s0;
     resolve(t, A, f0, s0);
-    process(d, t, A);
+    process(d, t, A, pr);
 }
+
 
 }  // namespace netc_gpu
 
@@ -404,6 +540,7 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
     // n_dev: n is only an upper bound here (keys must then always be readable)
     Args a;
     a.n_dev = n_dev;
+    a.verr = nullptr;
     a.mis = (uint64_t)(uintptr_t)dst & 15u;
     a.dst_base = dst - a.mis;
     a.src_base = src - a.mis;
@@ -430,6 +567,107 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
         case 8: return launch_nt<8>(a, nt, mb, stream);
         default: return launch_nt<4>(a, nt, mb, stream);
     }
+}
+
+
+// Phase B of the TEXT check: one thread per frame; the thread of a data frame with
+// FIN walks back to its message's first frame and, for a TEXT message, forward
+// again over its data frames (control frames skipped): any frame flagged by
+// phase A fails it; the first 3 bytes of every frame are checked here with the 3
+// bytes before them in the message; the message must not end inside a sequence.
+__device__ __forceinline__ bool utf8_rule(uint32_t b3, uint32_t b2, uint32_t b1, uint32_t b0) {
+    const bool need = b1 >= 0xC0 || b2 >= 0xE0 || b3 >= 0xF0;
+    const bool cont = (b0 & 0xC0) == 0x80;
+    if (need != cont) return true;
+    if (b0 >= 0xF5 || b0 == 0xC0 || b0 == 0xC1) return true;
+    if ((b1 == 0xE0 && b0 < 0xA0) || (b1 == 0xED && b0 >= 0xA0) || (b1 == 0xF0 && b0 < 0x90) ||
+        (b1 == 0xF4 && b0 >= 0x90))
+        return true;
+    return false;
+}
+
+__global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uint8_t* h0, uint64_t n,
+                              const uint8_t* verr, uint8_t* valid) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    uint8_t verdict = 1;
+    const uint32_t opk = h0[k] & 0x0F;
+    if (opk <= 2 && (h0[k] & 0x80)) {
+        // the message's first frame
+        int64_t first = -1;
+        for (int64_t j = (int64_t)k; j >= 0; --j) {
+            const uint32_t op = h0[j] & 0x0F;
+            if (op >= 8) continue;                              // control frame inside the message
+            if (op != 0) {
+                first = j;
+                break;
+            }
+            if (j != (int64_t)k && (h0[j] & 0x80)) break;       // a finished message: orphan continuation
+        }
+        if (first >= 0 && (h0[first] & 0x0F) == 1) {
+            uint32_t h1 = 0, h2 = 0, h3 = 0;   // the last 3 bytes of the message so far (h1 = last)
+            bool bad = false;
+            for (uint64_t j = (uint64_t)first; j <= k && !bad; ++j) {
+                if ((h0[j] & 0x0F) >= 8) continue;
+                if (verr[j]) bad = true;
+                const uint64_t lo = off[j], hi = off[j + 1];
+                for (uint64_t p = lo; p < hi && p < lo + 3; ++p) {
+                    const uint32_t b = dst[p];
+                    bad |= utf8_rule(h3, h2, h1, b);
+                    h3 = h2;
+                    h2 = h1;
+                    h1 = b;
+                }
+                if (hi - lo > 3) {   // the frame's own last 3 bytes become the history
+                    h3 = dst[hi - 3];
+                    h2 = dst[hi - 2];
+                    h1 = dst[hi - 1];
+                }
+            }
+            if (h1 >= 0xC0 || h2 >= 0xE0 || h3 >= 0xF0) bad = true;   // ends inside a sequence
+            verdict = bad ? 0 : 1;
+        }
+    }
+    valid[k] = verdict;
+}
+
+template <bool AL>
+static hipError_t launch_val(const Args& a, hipStream_t s) {
+    const uint64_t cap = (uint64_t)resident_blocks<4, AL, true>();
+    const uint64_t want = (a.nwin + 3) / 4;
+    const int blocks = (int)(want < cap ? want : cap);
+    if (blocks > 0) hipLaunchKernelGGL((mask_frames_kernel<4, AL, true, true>), dim3(blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_mask_validate(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,
+                                const uint32_t* keys, const uint8_t* header0, uint64_t n, uint8_t* verr,
+                                uint8_t* valid, hipStream_t stream, const LaunchCfg& cfg) {
+    (void)cfg;
+    if (n == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(verr, 0, n, stream);
+    if (e != hipSuccess) return e;
+    Args a;
+    a.n_dev = nullptr;
+    a.verr = verr;
+    a.mis = (uint64_t)(uintptr_t)dst & 15u;
+    a.dst_base = dst - a.mis;
+    a.src_base = src - a.mis;
+    a.total = total;
+    a.off = off;
+    a.keys = keys;
+    a.n = n;
+    a.density = total ? (double)n / (double)total : 0.0;
+    const uint64_t nvec = (a.mis + total + 15) / 16;
+    a.nwin = (nvec + 255) / 256;   // U = 4 chunks of 64 vectors x 4
+    if (a.nwin) {
+        const bool aligned = (((uintptr_t)src ^ (uintptr_t)dst) & 15u) == 0;
+        e = aligned ? launch_val<true>(a, stream) : launch_val<false>(a, stream);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(utf8_messages, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dst, off, header0, n,
+                       verr, valid);
+    return hipGetLastError();
 }
 
 }  // namespace netc_gpu

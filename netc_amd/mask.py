@@ -144,6 +144,20 @@ def mask_batch(dst, src, offsets, keys, stream=None, device: Optional[int] = Non
                                           keys.data_ptr(), n, _stream_handle(stream)))
 
 
+def unmask_validate(dst, src, offsets, keys, header0, valid, stream=None, device: Optional[int] = None) -> None:
+    """netc_gpu_unmask_validate: mask_batch plus per-frame UTF-8 verdicts of the TEXT messages (valid: uint8, n)."""
+    import torch
+
+    total, n = _check_batch(dst, src, offsets, keys)
+    for name, t in (("header0", header0), ("valid", valid)):
+        if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype != torch.uint8 or t.numel() != n:
+            raise ValueError(f"{name} must be a device uint8 tensor of nframes entries")
+    dev = src.device.index if device is None else device
+    _check(_lib.gpu().netc_gpu_unmask_validate(dev, dst.data_ptr(), src.data_ptr(), total, offsets.data_ptr(),
+                                               keys.data_ptr(), header0.data_ptr(), n, valid.data_ptr(),
+                                               _stream_handle(stream)))
+
+
 def mask_batch_multi(shards: Sequence[Tuple], streams: Optional[Sequence] = None, synchronize: bool = True) -> None:
     """netc_gpu_mask_batch_multi: shards = [(dst, src, offsets, keys), ...], each on its own device."""
     k = len(shards)

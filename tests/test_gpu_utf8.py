@@ -1,0 +1,175 @@
+"""GPU parity: netc_gpu_unmask_validate (fused unmask + UTF-8 check of TEXT messages) vs the oracle.
+
+Checkers: oracle_mask_batch (the reference's unmask expression, src/ws/common.c:321)
+for the bytes, oracle_validate_batch (RFC 3629 decoder pinned by
+tests/test_utf8_oracle.py) for the per-frame verdicts.  The bar: identical bytes,
+identical verdicts.
+"""
+
+import numpy as np
+import pytest
+
+from netc_amd import mask as nm
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+GUARD = 64
+
+
+def _dev(torch, a):
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint64:
+        a = a.view(np.int64)
+    elif a.dtype == np.uint32:
+        a = a.view(np.int32)
+    return torch.from_numpy(a).cuda()
+
+
+def text_bytes(rng, n):
+    """~n bytes of UTF-8 text: mostly ASCII, code points near every encoding boundary."""
+    pool = [0x7F, 0x80, 0xE9, 0x7FF, 0x800, 0x20AC, 0xD7FF, 0xE000, 0xFFFD, 0xFFFF, 0x10000, 0x1F600, 0x10FFFF]
+    out = bytearray()
+    while len(out) < n:
+        c = int(rng.choice(pool)) if rng.random() < 0.15 else int(rng.integers(0x20, 0x7F))
+        out += chr(c).encode("utf-8")
+    return bytes(out)
+
+
+def corrupt(rng, b: bytes) -> bytes:
+    b = bytearray(b)
+    kind = rng.integers(0, 5)
+    if not b:
+        return bytes([0xC3])
+    i = int(rng.integers(0, len(b)))
+    if kind == 0:
+        b[i] = 0xFF
+    elif kind == 1:
+        b.insert(i, 0x80)                    # stray continuation
+    elif kind == 2:
+        b[i:i] = b"\xed\xa0\x80"             # surrogate
+    elif kind == 3:
+        b[i:i] = b"\xe0\x80\xaf"             # overlong
+    else:
+        b += b"\xf0\x9f\x98"                 # truncated at the end
+    return bytes(b)
+
+
+def build_batch(rng, n_msgs, max_len, bad_frac=0.3, control_frac=0.1, binary_frac=0.1):
+    """Frames (header byte, payload) of whole messages, fragments split at random byte offsets."""
+    frames = []
+    for _ in range(n_msgs):
+        r = rng.random()
+        if r < binary_frac:
+            body = rng.integers(0, 256, int(rng.integers(0, max_len)), dtype=np.uint8).tobytes()
+            op = 2
+        else:
+            body = text_bytes(rng, int(rng.integers(0, max_len)))
+            if rng.random() < bad_frac:
+                body = corrupt(rng, body)
+            op = 1
+        parts = int(rng.integers(1, 5))
+        cuts = sorted(int(x) for x in rng.integers(0, len(body) + 1, parts - 1))
+        pieces = [body[a:b] for a, b in zip([0] + cuts, cuts + [len(body)])]
+        for i, piece in enumerate(pieces):
+            frames.append(((0x80 if i == len(pieces) - 1 else 0) | (op if i == 0 else 0), piece))
+            if rng.random() < control_frac:
+                frames.append((0x89, rng.integers(0, 256, int(rng.integers(0, 20)), dtype=np.uint8).tobytes()))
+    return frames
+
+
+def run_validate(torch, frames, shift=0, inplace=True):
+    payload = np.frombuffer(b"".join(p for _, p in frames), dtype=np.uint8)
+    n = len(frames)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(p) for _, p in frames])
+    h0 = np.array([h for h, _ in frames], dtype=np.uint8)
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    masked = orc.mask_batch(payload, off, keys)            # the wire payload (masking is an involution)
+    total = masked.size
+    buf = torch.zeros(total + 2 * GUARD, dtype=torch.uint8, device="cuda")
+    src = buf[GUARD + shift: GUARD + shift + total]
+    src.copy_(torch.from_numpy(masked))
+    if inplace:
+        dst = src
+    else:
+        dbuf = torch.zeros(total + 2 * GUARD, dtype=torch.uint8, device="cuda")
+        dst = dbuf[GUARD + shift + 3: GUARD + shift + 3 + total]
+    valid = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    nm.unmask_validate(dst, src, _dev(torch, off), _dev(torch, keys), torch.from_numpy(h0).cuda(), valid)
+    torch.cuda.synchronize()
+    assert np.array_equal(dst.cpu().numpy(), payload), "unmasked bytes differ"
+    exp = orc.validate_batch(payload, off, h0)
+    got = valid.cpu().numpy()
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"verdicts differ at frames {bad[:8].tolist()} (got {got[bad[:8]].tolist()})"
+    return exp
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_mixed_messages(torch_cuda, seed):
+    rng = np.random.default_rng(seed)
+    exp = run_validate(torch_cuda, build_batch(rng, 300, 3000))
+    assert 0 < (exp == 0).sum()   # some messages are invalid
+
+
+@pytest.mark.parametrize("shift", [1, 7, 13])
+def test_alignments_and_out_of_place(torch_cuda, shift):
+    rng = np.random.default_rng(40 + shift)
+    run_validate(torch_cuda, build_batch(rng, 200, 2000), shift=shift)
+    run_validate(torch_cuda, build_batch(rng, 200, 2000), shift=shift, inplace=False)
+
+
+def test_tiny_fragments(torch_cuda):
+    # fragments of 0-3 bytes: every code point split across frames
+    rng = np.random.default_rng(50)
+    frames = []
+    for _ in range(200):
+        body = text_bytes(rng, int(rng.integers(0, 40)))
+        if rng.random() < 0.3:
+            body = corrupt(rng, body)
+        pieces, i = [], 0
+        while i < len(body):
+            k = int(rng.integers(0, 4))
+            pieces.append(body[i:i + k])
+            i += k
+        pieces = pieces or [b""]
+        for j, p in enumerate(pieces):
+            frames.append(((0x80 if j == len(pieces) - 1 else 0) | (1 if j == 0 else 0), p))
+    run_validate(torch_cuda, frames)
+
+
+def test_errors_at_every_boundary(torch_cuda):
+    # one long valid TEXT frame per case with an error at a vector / span / chunk edge
+    rng = np.random.default_rng(60)
+    base = text_bytes(rng, 20000)
+    base = base[: base.rfind(b" ") if b" " in base else len(base)]
+    frames = []
+    for pos in (0, 1, 2, 3, 15, 16, 17, 1023, 1024, 1025, 4093, 4094, 4095, 4096, 4097, 8191, 8192):
+        for bad in (b"\x80", b"\xff", b"\xc3\x28", b"\xed\xa0\x80", b"\xe0\x80\xaf"):
+            cut = base[:pos]
+            while cut and (cut[-1] & 0xC0) == 0x80:   # keep the prefix itself valid
+                cut = cut[:-1]
+            if cut and cut[-1] >= 0xC0:
+                cut = cut[:-1]
+            frames.append((0x81, cut + bad + b"tail"))
+    frames.append((0x81, base))   # and a valid one
+    exp = run_validate(torch_cuda, frames)
+    assert (exp[:-1] == 0).all() and exp[-1] == 1
+
+
+def test_large_text_batch(torch_cuda):
+    # ~64 MiB of 1 KiB TEXT frames (config 2 shape), 1 % corrupted
+    rng = np.random.default_rng(70)
+    chunk = text_bytes(rng, 1 << 20)
+    frames = []
+    pos = 0
+    for i in range(65536):
+        p = chunk[pos: pos + 1024]
+        pos = (pos + 1024) % (len(chunk) - 1024)
+        if i % 100 == 7:
+            p = corrupt(rng, p)
+        frames.append((0x81, p))
+    exp = run_validate(torch_cuda, frames)
+    assert (exp == 0).sum() > 300
