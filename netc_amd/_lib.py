@@ -14,6 +14,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIBDIR = os.path.join(_HERE, "lib")
 HOST_LIB = os.path.join(LIBDIR, "libnetc.so")
 GPU_LIB = os.path.join(LIBDIR, "libnetc_ws_gpu.so")
+# diagnostics only (tools/): an instrumented build of the same library
+if os.environ.get("NETC_GPU_LIB"):
+    GPU_LIB = os.path.abspath(os.environ["NETC_GPU_LIB"])
 
 _lock = threading.Lock()
 _host = None

@@ -300,6 +300,27 @@ __device__ __forceinline__ u32x4 shift_bytes(uint64_t lo, uint64_t hi, int sh) {
     return r;
 }
 
+#ifdef NETC_ENC_CHECKS
+// diagnostic build only (tools/): range checks that record the first violation
+// (site, value, limit, count) instead of making the access
+__device__ unsigned long long g_enc_fault[4];
+extern "C" int netc_gpu_debug_encode_faults(unsigned long long* out4) {
+    return (int)hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_enc_fault), 4 * sizeof(unsigned long long));
+}
+__device__ __forceinline__ bool enc_ok(int site, uint64_t v, uint64_t limit) {
+    if (v <= limit) return true;
+    if (atomicAdd(&g_enc_fault[3], 1ull) == 0) {
+        g_enc_fault[0] = (unsigned long long)site;
+        g_enc_fault[1] = v;
+        g_enc_fault[2] = limit;
+    }
+    return false;
+}
+#define ENC_OK(site, v, limit) enc_ok(site, (uint64_t)(v), (uint64_t)(limit))
+#else
+#define ENC_OK(site, v, limit) true
+#endif
+
 template <bool NT>
 __device__ __forceinline__ u32x4 load_u(const uint8_t* p) {
     const NETC_GLOBAL u32x4u* q = (const NETC_GLOBAL u32x4u*)p;
@@ -517,8 +538,9 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
         sp.rk1 = rk1;
         sp.rk2 = rk2;
         sp.pk = pk;
-        sp.d1 = load_u<NT>(a.src + ad1);
-        sp.d2 = load_u<NT>(a.src + ad2);
+        sp.d1 = sp.d2 = u32x4{0, 0, 0, 0};
+        if (ENC_OK(1, ad1, a.src_total - 16)) sp.d1 = load_u<NT>(a.src + ad1);
+        if (ENC_OK(2, ad2, a.src_total - 16)) sp.d2 = load_u<NT>(a.src + ad2);
     });
 }
 
@@ -636,6 +658,7 @@ __global__ __launch_bounds__(256) void encode_queued_kernel(EncArgs a) {
     const uint64_t wlo = a.wmis, whi = a.wmis + wire_total;
     for (uint64_t q = wave; q < count; q += nwaves) {
         const uint64_t A0 = a.defer[q];
+        if (!ENC_OK(3, A0, whi)) continue;
         EncTable t;
         enc_table_load(a, t, enc_locate(a, A0, wire_total, lane), lane);
         const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
