@@ -59,4 +59,54 @@ __device__ __forceinline__ u32x4 select_from(int64_t t) {
 // Bytes [lo, hi) of a vector selected (both clamped to [0, 16]).
 __device__ __forceinline__ u32x4 select_range(int64_t lo, int64_t hi) { return select_from(lo) & ~select_from(hi); }
 
+// ---------------------------------------------------- chained scans (shared) --
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+    for (int d = kWave / 2; d > 0; d >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, d, kWave);
+    return v;
+}
+
+// Single-pass chained scans (decoupled look-back) over tiles: each tile publishes
+// one 64-bit status word
+//   [63:62] flag (1 = tile aggregate, 2 = inclusive prefix) | [61:46] epoch | [45:0] value
+// The epoch (one per call and stream) makes words left from earlier calls read as
+// "not yet published", so a status array is never cleared between calls.  The
+// look-back (one wavefront) reads 64 predecessors at once and sums their
+// aggregates back to the nearest inclusive prefix, so tiles do not wait on each
+// other one by one.  A tile only waits on lower-numbered tiles, which are
+// dispatched first.
+static constexpr uint64_t kValBits = 46;
+static constexpr uint64_t kValMask = (1ull << kValBits) - 1;
+
+__device__ __forceinline__ uint64_t status_word(uint64_t flag, uint32_t epoch, uint64_t v) {
+    return flag << 62 | (uint64_t)(epoch & 0xFFFF) << kValBits | (v & kValMask);
+}
+
+// exclusive prefix of tile `tile` (every lane of the calling wavefront takes part)
+__device__ inline uint64_t look_back(uint64_t* status, int64_t tile, uint32_t epoch, int lane) {
+    uint64_t prefix = 0;
+    for (int64_t top = tile - 1; top >= 0;) {
+        const int64_t idx = top - lane;
+        uint64_t v = 0;
+        bool ok = true, incl = idx < 0;   // before tile 0: an inclusive prefix of 0
+        if (idx >= 0) {
+            const uint64_t w = __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (w >> 62) != 0 && ((w >> kValBits) & 0xFFFF) == (epoch & 0xFFFF);
+            incl = ok && (w >> 62) == 2;
+            v = w & kValMask;
+        }
+        const uint64_t im = __ballot(incl);
+        const int stop = im ? __builtin_ctzll(im) : kWave;   // nearest inclusive prefix
+        const uint64_t need = stop >= kWave - 1 ? ~0ull : ((2ull << stop) - 1);
+        if ((__ballot(ok) & need) != need) {
+            __builtin_amdgcn_s_sleep(1);   // a predecessor has not published yet
+            continue;
+        }
+        prefix += wave_sum(lane <= stop ? v : 0);
+        if (stop < kWave) break;
+        top -= kWave;
+    }
+    return prefix;
+}
+
 }  // namespace netc_gpu

@@ -72,55 +72,6 @@ __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total) {
     return before + inc - v;
 }
 
-__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
-#pragma unroll
-    for (int d = kWave / 2; d > 0; d >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, d, kWave);
-    return v;
-}
-
-// Single-pass chained scan (decoupled look-back).  Tile b = frames
-// [b kScanBlock, (b + 1) kScanBlock); tiles cover frames 0 .. n inclusive, so the
-// tile holding frame n writes wo[n].  Each tile publishes one 64-bit status word:
-//   [63:62] flag (1 = tile aggregate, 2 = inclusive prefix) | [61:46] epoch | [45:0] value
-// value = extended-length bytes (<= 8 per frame, so n < 2^43).  The epoch (one per
-// call and stream) makes words left from earlier calls read as "not yet
-// published", so the status array is never cleared between calls.  The look-back
-// reads 64 predecessors at once: it sums their aggregates back to the nearest
-// inclusive prefix, so tiles do not wait on each other one by one.  A tile only
-// waits on lower-numbered tiles, which are dispatched first.
-static constexpr uint64_t kValBits = 46;
-static constexpr uint64_t kValMask = (1ull << kValBits) - 1;
-
-__device__ __forceinline__ uint64_t status_word(uint64_t flag, uint32_t epoch, uint64_t v) {
-    return flag << 62 | (uint64_t)(epoch & 0xFFFF) << kValBits | (v & kValMask);
-}
-
-__device__ uint64_t look_back(uint64_t* status, int64_t tile, uint32_t epoch, int lane) {
-    uint64_t prefix = 0;
-    for (int64_t top = tile - 1; top >= 0;) {
-        const int64_t idx = top - lane;
-        uint64_t v = 0;
-        bool ok = true, incl = idx < 0;   // before tile 0: an inclusive prefix of 0
-        if (idx >= 0) {
-            const uint64_t w = __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = (w >> 62) != 0 && ((w >> kValBits) & 0xFFFF) == (epoch & 0xFFFF);
-            incl = ok && (w >> 62) == 2;
-            v = w & kValMask;
-        }
-        const uint64_t im = __ballot(incl);
-        const int stop = im ? __builtin_ctzll(im) : kWave;   // nearest inclusive prefix
-        const uint64_t need = stop >= kWave - 1 ? ~0ull : ((2ull << stop) - 1);
-        if ((__ballot(ok) & need) != need) {
-            __builtin_amdgcn_s_sleep(1);   // a predecessor has not published yet
-            continue;
-        }
-        prefix += wave_sum(lane <= stop ? v : 0);
-        if (stop < kWave) break;
-        top -= kWave;
-    }
-    return prefix;
-}
-
 __global__ __launch_bounds__(kScanThreads) void wire_offsets_chained(const uint64_t* off, uint64_t n, uint32_t fixed,
                                                                      uint64_t* wo, uint64_t* status, uint32_t epoch,
                                                                      uint32_t* defer_count) {

@@ -409,27 +409,17 @@ __global__ __launch_bounds__(64) void scan_emit(ScanArgs a) {
         load_chunk(a, B, words);
         if (lane == 0) stop = walk_chunk(a, B, words, (uint64_t)entry, [&](uint64_t, uint32_t, uint8_t) { ++count; });
     }
-    // chained scan of the frame counts (lane 0 publishes and looks back)
-    uint64_t base = 0;
+    // chained scan of the frame counts: lane 0 publishes, the wavefront looks back
+    count = (uint64_t)__builtin_amdgcn_readfirstlane((int)count) |
+            ((uint64_t)__builtin_amdgcn_readfirstlane((int)(count >> 32)) << 32);
+    if (lane == 0)
+        __hip_atomic_store(&a.status[chunk], status_word(chunk == 0 ? 2 : 1, a.epoch, count), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t base = chunk == 0 ? 0 : look_back(a.status, (int64_t)chunk, a.epoch, lane);
     if (lane == 0) {
-        const uint64_t kV = (1ull << 46) - 1;
-        auto word = [&](uint64_t flag, uint64_t v) { return flag << 62 | (uint64_t)(a.epoch & 0xFFFF) << 46 | (v & kV); };
-        if (chunk == 0) {
-            __hip_atomic_store(&a.status[0], word(2, count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(&a.status[chunk], word(1, count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int64_t p = (int64_t)chunk - 1; p >= 0;) {
-                const uint64_t w = __hip_atomic_load(&a.status[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((w >> 62) == 0 || ((w >> 46) & 0xFFFF) != (a.epoch & 0xFFFF)) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                base += w & kV;
-                if ((w >> 62) == 2) break;
-                --p;
-            }
-            __hip_atomic_store(&a.status[chunk], word(2, base + count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (chunk)
+            __hip_atomic_store(&a.status[chunk], status_word(2, a.epoch, base + count), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         if (chunk == a.nc) a.result[0] = base + count;
         if (entry >= 0) {
             uint64_t k = base;
