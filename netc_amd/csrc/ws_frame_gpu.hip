@@ -484,14 +484,17 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
             ad1 = need1 ? a1.s0 : 0;   // unused bytes are masked off in phase 2
             ad2 = need2 ? a2.s0 : ad1;
         } while (false);
-        if (a.src_total < 16) ad1 = ad2 = 0;   // (tiny payload buffers: every span is queued anyway)
         sp.kind = kind;
         sp.rk1 = rk1;
         sp.rk2 = rk2;
         sp.pk = pk;
         sp.d1 = sp.d2 = u32x4{0, 0, 0, 0};
-        if (ENC_OK(1, ad1, a.src_total - 16)) sp.d1 = load_u<NT>(a.src + ad1);
-        if (ENC_OK(2, ad2, a.src_total - 16)) sp.d2 = load_u<NT>(a.src + ad2);
+        // a payload buffer under 16 bytes (possibly NULL when empty) is never read
+        // here: every span is queued then, and the compose kernel reads byte-wise
+        if (a.src_total >= 16) {   // kernel-uniform
+            if (ENC_OK(1, ad1, a.src_total - 16)) sp.d1 = load_u<NT>(a.src + ad1);
+            if (ENC_OK(2, ad2, a.src_total - 16)) sp.d2 = load_u<NT>(a.src + ad2);
+        }
     });
 }
 
