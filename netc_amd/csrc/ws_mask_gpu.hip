@@ -265,17 +265,22 @@ __device__ __forceinline__ uint32_t utf8_err_word(uint32_t x, uint32_t prev) {
 
 // Phase A of the TEXT check, per span: flag the frames holding a byte that breaks
 // the local rules.  out = this lane's unmasked 16 bytes, prevd = the 4 bytes before
-// them.  The first 3 bytes of every frame are skipped (their rule reaches into the
-// previous frame of the message; utf8_messages() checks them), so are bytes in no
-// frame.  Errors are rare: their frame lookup is a slow path.
+// them (from the neighbouring lane / the previous span of the chunk).  Skipped here:
+// the first 3 bytes of every frame (their rule reaches into the previous frame of
+// the message; utf8_messages() checks them), bytes in no frame, and, with seam set
+// (a chunk's first span), the chunk's first 3 bytes: the bytes before them belong to
+// another wavefront's chunk, which in place may already hold unmasked or still
+// masked bytes -- utf8_seams() checks them once the whole batch is unmasked.
+// Errors are rare: their frame lookup is a slow path.
 __device__ __forceinline__ void validate_span(const Args& a, const Table& t, uint64_t A0, u32x4 out, uint32_t prevd,
-                                              int lane) {
+                                              bool seam, int lane) {
     const uint64_t W = A0 + 16ull * (uint64_t)lane;
     u32x4 e;
     e[0] = utf8_err_word(out[0], prevd);
     e[1] = utf8_err_word(out[1], out[0]);
     e[2] = utf8_err_word(out[2], out[1]);
     e[3] = utf8_err_word(out[3], out[2]);
+    if (seam && lane == 0) e[0] &= ~0x00FFFFFFu;
     if (!__ballot((e[0] | e[1] | e[2] | e[3]) != 0)) return;
     // drop bytes within 3 of a frame start: the span's first frame (if it starts
     // less than 3 bytes before A0) and every frame starting inside the span
@@ -307,29 +312,8 @@ __device__ __forceinline__ void validate_span(const Args& a, const Table& t, uin
     }
 }
 
-// the 4 unmasked bytes before chunk position A (P coordinates), for the span check:
-// bytes of the frame holding A-1 carry its key; bytes of an earlier frame only
-// feed rules that validate_span drops anyway
-template <bool SRC_ALIGNED>
-__device__ __forceinline__ uint32_t chunk_prev_dword(const Args& a, const Table& t, uint64_t A, uint32_t raw) {
-    if (A < 4) return 0;
-    const int l0 = __popcll(__ballot(t.start <= A - 1)) - 1;
-    if (l0 < 0) return 0;
-    const uint64_t s0 = readlane64(t.start, l0);
-    return raw ^ rotr8(readlane32(t.key, l0), (A - 4) - s0);
-}
-
-template <bool SRC_ALIGNED>
-__device__ __forceinline__ uint32_t load_prev_raw(const Args& a, uint64_t A) {
-    if (A < 4) return 0;
-    const NETC_GLOBAL uint8_t* p = gptr(a.src_base + A - 4);
-    if constexpr (SRC_ALIGNED) return *(const NETC_GLOBAL uint32_t*)p;
-    return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
-}
-
 template <int U, bool SRC_ALIGNED, bool NT, bool VAL>
 __device__ __forceinline__ void edge_chunk(const Args& a, uint64_t A, int lane) {
-    constexpr uint64_t kWin = kSpan * U;
     const uint64_t full_lo = a.mis ? 16 : 0;
     const uint64_t full_hi = (a.mis + a.total) & ~15ull;
     const uint64_t vec_end = (a.mis + a.total + 15) & ~15ull;
@@ -341,28 +325,16 @@ __device__ __forceinline__ void edge_chunk(const Args& a, uint64_t A, int lane) 
     }
     Table t;
     table_load(a, t, locate(a, A, lane), lane);
-    uint32_t carry = 0;
-    if constexpr (VAL) {
-        // bytes before A inside the buffer, unmasked (zero outside it)
-        const uint64_t lo = a.mis, hi = a.mis + a.total;
-        uint32_t raw = 0;
-        for (int k = 0; k < 4; ++k) {
-            const uint64_t q = A - 4 + k;
-            if (A >= 4 && q >= lo && q < hi) raw |= (uint32_t)gptr(a.src_base)[q] << (8 * k);
-        }
-        carry = chunk_prev_dword<SRC_ALIGNED>(a, t, A, raw);
-    }
+    uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t A0 = A + (uint64_t)u * kSpan;
         if (A0 >= vec_end) break;                                   // wave-uniform
         const u32x4 m = span_mask(a, t, A0, lane);
         const uint64_t P = A0 + 16ull * lane;
-        if (P >= full_lo && P < full_hi) store_vec<NT>(a, P, d[u] ^ m);
-        else if (P < vec_end) edge_vec(a, P, m);
+        u32x4 out = {0, 0, 0, 0};   // VAL: the unmasked vector, bytes outside the buffer 0
         if constexpr (VAL) {
-            // the unmasked vector; bytes outside the buffer read as 0
-            u32x4 out = {0, 0, 0, 0};
+            // read before the store below: in place, the store overwrites these bytes
             if (P >= full_lo && P < full_hi) {
                 out = d[u] ^ m;
             } else {
@@ -373,12 +345,15 @@ __device__ __forceinline__ void edge_chunk(const Args& a, uint64_t A, int lane) 
                         out[bi >> 2] |= (uint32_t)(gptr(a.src_base)[P + bi] ^ (uint8_t)(m[bi >> 2] >> (8 * (bi & 3))))
                                         << (8 * (bi & 3));
             }
+        }
+        if (P >= full_lo && P < full_hi) store_vec<NT>(a, P, d[u] ^ m);
+        else if (P < vec_end) edge_vec(a, P, m);
+        if constexpr (VAL) {
             const uint32_t up = (uint32_t)__shfl_up((int)out[3], 1, kWave);
-            validate_span(a, t, A0, out, lane ? up : carry, lane);
+            validate_span(a, t, A0, out, lane ? up : carry, u == 0, lane);
             carry = (uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1);
         }
     }
-    (void)kWin;
 }
 
 // Chunk = U spans (U KiB).  Wavefront w of W takes chunks w, w+W, w+2W, ...: at
@@ -438,9 +413,8 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
 #pragma unroll
         for (int u = 0; u < U; ++u) dst[u] = load_vec<SRC_ALIGNED, NT>(a, base + (uint64_t)u * kSpan + 16ull * lane);
     };
-    auto process = [&](const u32x4 (&src)[U], Table& t, uint64_t base, uint32_t prev_raw) {
-        uint32_t carry = 0;
-        if constexpr (VAL) carry = chunk_prev_dword<SRC_ALIGNED>(a, t, base, prev_raw);
+    auto process = [&](const u32x4 (&src)[U], Table& t, uint64_t base) {
+        uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t A0 = base + (uint64_t)u * kSpan;
@@ -449,7 +423,7 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
             store_vec<NT>(a, A0 + 16ull * lane, out);
             if constexpr (VAL) {
                 const uint32_t up = (uint32_t)__shfl_up((int)out[3], 1, kWave);
-                validate_span(a, t, A0, out, lane ? up : carry, lane);
+                validate_span(a, t, A0, out, lane ? up : carry, u == 0, lane);
                 carry = (uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1);
             }
         }
@@ -466,8 +440,6 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
     u32x4 d[U];
     uint64_t A = c * kWin;
     load_window(d, A);
-    uint32_t pr = 0;
-    if constexpr (VAL) pr = load_prev_raw<SRC_ALIGNED>(a, A);
     Table t;
     table_issue(a, t, guess_base(a, 0, a.mis, A), lane);   // global guess: frame 0 starts near P = mis
 
@@ -478,13 +450,10 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
         const uint64_t An = cn * kWin;
         u32x4 dn[U];
         load_window(dn, An);
-        uint32_t prn = 0;
-        if constexpr (VAL) prn = load_prev_raw<SRC_ALIGNED>(a, An);
         Table tn;
         table_issue(a, tn, guess_base(a, f0, s0, An), lane);
-        process(d, t, A, pr);
+        process(d, t, A);
         A = An;
-        pr = prn;
         t = tn;
 #pragma unroll
         for (int u = 0; u < U; ++u) d[u] = dn[u];
@@ -492,7 +461,7 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
     int64_t f0;
     uint64_t s0;
     resolve(t, A, f0, s0);
-    process(d, t, A, pr);
+    process(d, t, A);
 }
 
 
@@ -586,6 +555,31 @@ __device__ __forceinline__ bool utf8_rule(uint32_t b3, uint32_t b2, uint32_t b1,
     return false;
 }
 
+// Phase A of the TEXT check for the bytes validate_span skips at chunk seams: the
+// first 3 bytes of every chunk (win bytes apart in P coordinates), checked once the
+// whole batch is unmasked -- one thread per seam, a binary search for its frame.
+__global__ void utf8_seams(const uint8_t* dst, uint64_t total, const uint64_t* off, uint64_t n, uint64_t mis,
+                           uint64_t win, uint64_t nseams, uint8_t* verr) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+    if (c > nseams || n == 0) return;
+    const uint64_t q = c * win - mis;   // payload coordinate of the seam (c * win >= 4096 > mis)
+    if (q >= total || off[0] > q) return;
+    uint64_t lo = 0, hi = n;   // the last frame starting at or before q: off[lo] <= q
+    while (hi - lo > 1) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (off[mid] <= q) lo = mid;
+        else hi = mid;
+    }
+    const uint64_t fs = off[lo], fe = off[lo + 1];
+    for (uint64_t p = q; p < q + 3 && p < fe; ++p) {
+        if (p - fs < 3) continue;   // within 3 of the frame start: utf8_messages checks it
+        if (utf8_rule(dst[p - 3], dst[p - 2], dst[p - 1], dst[p])) {
+            verr[lo] = 1;
+            break;
+        }
+    }
+}
+
 __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uint8_t* h0, uint64_t n,
                               const uint8_t* verr, uint8_t* valid) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -664,6 +658,13 @@ hipError_t launch_mask_validate(uint8_t* dst, const uint8_t* src, uint64_t total
         const bool aligned = (((uintptr_t)src ^ (uintptr_t)dst) & 15u) == 0;
         e = aligned ? launch_val<true>(a, stream) : launch_val<false>(a, stream);
         if (e != hipSuccess) return e;
+    }
+    const uint64_t win = kSpan * 4;                    // the VAL kernel's chunk (U = 4)
+    const uint64_t nseams = (a.mis + total) / win;     // chunk starts c * win, c = 1 .. nseams
+    if (nseams) {
+        hipLaunchKernelGGL(utf8_seams, dim3((unsigned)((nseams + 255) / 256)), dim3(256), 0, stream, dst, total, off, n,
+                           a.mis, win, nseams, verr);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(utf8_messages, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dst, off, header0, n,
                        verr, valid);
