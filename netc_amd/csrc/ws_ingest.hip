@@ -1,0 +1,421 @@
+// Socket ingest into a pinned ring, framed and unmasked on the GPU:
+// include/ws/ingest.h.
+//
+// The reference reads a frame field by field with one recv() per header field and
+// the payload last (src/ws/common.c:149,172,237,283,306), then unmasks it byte by
+// byte (:317-323).  Here the bytes of a connection land, with recv() calls as large
+// as a slot, in page-locked host memory; per slot, on the slot's own HIP stream:
+//
+//   H2D     the slot's stream bytes: the carry of the previous slot + the new bytes
+//   scan    netc_gpu_scan_frames' kernels -> header offsets, keys, byte 0s, result
+//   D2H     the 3-word result (frames, consumed, error), then event "scanned"
+//   unmask  every frame the scan found, in place (the batch kernel reads the frame
+//           count on the device: no host round trip between scan and unmask)
+//   D2H     the stream back into the same pinned slot, then event "done"
+//
+// The host needs one number per slot before the NEXT slot can go: where the last
+// complete frame ends (the carry point).  It waits for the previous slot's
+// "scanned" event only when the next slot is submitted -- by then the scan has
+// long finished, a slot takes far longer to arrive on a socket than to scan.  The
+// carried bytes (the incomplete frame at the slot's end) are still raw in the
+// previous slot's pinned buffer: the unmask leaves bytes past the last complete
+// frame as they are, so the copy back writes them unchanged.  They are copied in
+// front of the next slot's received bytes (each slot keeps max-frame headroom in
+// front for that), so every H2D is one contiguous range and every frame is whole.
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdint.h>
+#include <string.h>
+#include <sys/socket.h>
+
+#include <new>
+
+#include "ws_mask_gpu.h"
+
+extern "C" {
+#include "../../include/ws/mask.h"
+#include "../../include/ws/frame.h"
+#include "../../include/ws/ingest.h"
+extern __thread int netc_errno_reason;   // include/utils/error.h
+}
+
+using netc_gpu::api_fail;
+using netc_gpu::api_fail_hip;
+
+namespace {
+
+constexpr int kBadRecv = 10;   // netc's BADRECV reason (include/utils/error.h)
+
+enum SlotState : int { kFree = 0, kFilling, kInflight, kTaken };
+
+struct IngestSlot {
+    uint8_t* h_buf = nullptr;    // pinned: [0, carry_cap) carry room, then slot_bytes received; D2H target too
+    uint8_t* d_buf = nullptr;    // device copy of the slot's stream
+    uint64_t* d_hdr = nullptr;   // scan outputs (max_frames + 1 / max_frames / max_frames / 3)
+    uint32_t* d_keys = nullptr;
+    uint8_t* d_b0 = nullptr;
+    uint64_t* d_res = nullptr;
+    uint64_t* h_hdr = nullptr;   // pinned descriptor copies
+    uint32_t* h_keys = nullptr;
+    uint8_t* h_b0 = nullptr;
+    uint64_t* h_res = nullptr;   // pinned: frames, consumed, error
+    hipStream_t stream = nullptr;
+    hipEvent_t scanned = nullptr, done = nullptr;
+    int state = kFree;
+    uint64_t fill = 0;           // received bytes, at h_buf + carry_cap
+    uint64_t carry = 0;          // carried bytes in front of them, at h_buf + carry_cap - carry
+    uint64_t pos = 0;            // stream position of the slot's first byte
+    bool resolved = false;       // scan result read: frames and carry point known, descriptors queued
+    uint64_t frames = 0;
+    uint64_t cut = 0;            // end of the last complete frame (slot coordinates)
+    uint64_t err = ~0ull;        // offset of a rejected header (strict), or ~0
+};
+
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int device) {
+        err = hipGetDevice(&prev);
+        if (err == hipSuccess && prev != device) err = hipSetDevice(device);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+struct netc_ws_ingest {
+    int device = 0;
+    int strict = 0;
+    int nslots = 0;
+    uint64_t slot_bytes = 0, carry_cap = 0, cap = 0, max_frames = 0;
+    IngestSlot* slots = nullptr;
+    int cur = -1;          // slot being filled, -1 = none
+    int next_fill = 0;     // the slot to fill next (ring order)
+    int prev = -1;         // the last submitted slot: its carry goes in front of the next
+    int fifo[16] = {0};    // submitted slots not yet handed out, in stream order
+    int head = 0, count = 0;
+    int sticky = 0;        // a stream error (TOO_BIG / PROTOCOL): reported from then on
+    int sticky_after = -1; // ... once the batch of this slot has been handed out (-1: now)
+};
+
+namespace {
+
+void free_slot(IngestSlot& s) {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.h_buf) (void)hipHostFree(s.h_buf);
+    if (s.h_hdr) (void)hipHostFree(s.h_hdr);
+    if (s.h_keys) (void)hipHostFree(s.h_keys);
+    if (s.h_b0) (void)hipHostFree(s.h_b0);
+    if (s.h_res) (void)hipHostFree(s.h_res);
+    if (s.d_buf) (void)hipFree(s.d_buf);
+    if (s.d_hdr) (void)hipFree(s.d_hdr);
+    if (s.d_keys) (void)hipFree(s.d_keys);
+    if (s.d_b0) (void)hipFree(s.d_b0);
+    if (s.d_res) (void)hipFree(s.d_res);
+    if (s.scanned) (void)hipEventDestroy(s.scanned);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s = IngestSlot();
+}
+
+int alloc_slot(const netc_ws_ingest* g, IngestSlot& s) {
+    hipError_t e;
+    const uint64_t mf = g->max_frames;
+    if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&s.scanned, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess)
+        return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: stream / event create", e);
+    if ((e = hipHostMalloc((void**)&s.h_buf, g->cap, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&s.h_hdr, (mf + 1) * sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&s.h_keys, mf * sizeof(uint32_t), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&s.h_b0, mf, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&s.h_res, 3 * sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess)
+        return api_fail_hip(NETC_GPU_ENOMEM, "ingest: pinned host allocation", e);
+    if ((e = hipMalloc((void**)&s.d_buf, g->cap)) != hipSuccess ||
+        (e = hipMalloc((void**)&s.d_hdr, (mf + 1) * sizeof(uint64_t))) != hipSuccess ||
+        (e = hipMalloc((void**)&s.d_keys, mf * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc((void**)&s.d_b0, mf)) != hipSuccess ||
+        (e = hipMalloc((void**)&s.d_res, 3 * sizeof(uint64_t))) != hipSuccess)
+        return api_fail_hip(NETC_GPU_ENOMEM, "ingest: device allocation", e);
+    return 0;
+}
+
+// Wait for a submitted slot's scan result; fix its frames and carry point and
+// queue the copy of its descriptors behind the unmask (the "done" event is
+// recorded again after them).  Idempotent.
+int resolve(netc_ws_ingest* g, IngestSlot& s) {
+    if (s.resolved) return 0;
+    hipError_t e = hipEventSynchronize(s.scanned);
+    if (e != hipSuccess) return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: scan wait", e);
+    const uint64_t n = s.h_res[0], consumed = s.h_res[1], len = s.carry + s.fill;
+    // max_frames is sized so that every frame of a slot is recorded (>= 2 or 6 bytes each)
+    if (n + 1 > g->max_frames || consumed > len)
+        return api_fail(NETC_GPU_ERUNTIME, "ingest: scan result out of range (%llu frames, consumed %llu of %llu)",
+                        (unsigned long long)n, (unsigned long long)consumed, (unsigned long long)len);
+    s.frames = n;
+    s.cut = consumed;
+    s.err = s.h_res[2];
+    if ((e = hipMemcpyAsync(s.h_hdr, s.d_hdr, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream)) !=
+            hipSuccess ||
+        (n && (e = hipMemcpyAsync(s.h_keys, s.d_keys, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream)) !=
+                  hipSuccess) ||
+        (n && (e = hipMemcpyAsync(s.h_b0, s.d_b0, n, hipMemcpyDeviceToHost, s.stream)) != hipSuccess) ||
+        (e = hipEventRecord(s.done, s.stream)) != hipSuccess)
+        return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: descriptor copy", e);
+    s.resolved = true;
+    return 0;
+}
+
+int set_sticky(netc_ws_ingest* g, int code, int after_slot) {
+    if (!g->sticky) {
+        g->sticky = code;
+        g->sticky_after = after_slot;
+    }
+    if (code == NETC_WS_INGEST_TOO_BIG)
+        return api_fail(code, "ingest: a frame is longer than the %llu-byte limit",
+                        (unsigned long long)(g->carry_cap - 14));
+    return api_fail(code, "ingest: strict mode rejected a frame header (RFC 6455 §5.1-5.5)");
+}
+
+// the sticky error, once it is due (after the batch holding the frames before it)
+int sticky_now(const netc_ws_ingest* g) {
+    if (!g->sticky) return 0;
+    if (g->sticky_after >= 0) {
+        for (int i = 0; i < g->count; ++i)
+            if (g->fifo[(g->head + i) % 16] == g->sticky_after) return 0;
+    }
+    return g->sticky;
+}
+
+// Queue the filling slot on the GPU (see the file comment).
+int submit_cur(netc_ws_ingest* g) {
+    if (g->cur < 0) return 0;
+    IngestSlot& s = g->slots[g->cur];
+    if (s.fill == 0) return 0;   // nothing new: the carry alone cannot complete a frame
+    uint64_t carry = 0, pos = 0;
+    const uint8_t* carry_src = nullptr;
+    if (g->prev >= 0) {
+        IngestSlot& p = g->slots[g->prev];
+        if (int r = resolve(g, p)) return r;
+        if (p.err != ~0ull) return set_sticky(g, NETC_WS_INGEST_PROTOCOL, g->prev);
+        carry = p.carry + p.fill - p.cut;
+        carry_src = p.h_buf + (g->carry_cap - p.carry) + p.cut;
+        pos = p.pos + p.cut;
+    }
+    if (carry > g->carry_cap) return set_sticky(g, NETC_WS_INGEST_TOO_BIG, g->prev);
+    // the carried bytes are raw in the previous slot (the unmask stops at its last
+    // complete frame, its copy back rewrites them unchanged)
+    uint8_t* h = s.h_buf + (g->carry_cap - carry);
+    if (carry) memmove(h, carry_src, carry);
+    s.carry = carry;
+    s.pos = pos;
+    s.resolved = false;
+    s.frames = s.cut = 0;
+    s.err = ~0ull;
+    const uint64_t len = carry + s.fill;
+    hipError_t e;
+    if ((e = hipMemcpyAsync(s.d_buf, h, len, hipMemcpyHostToDevice, s.stream)) != hipSuccess)
+        return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: H2D copy", e);
+    if ((e = netc_gpu::launch_scan_frames(s.d_buf, len, 0, g->strict != 0, s.d_hdr, s.d_keys, s.d_b0, g->max_frames,
+                                          s.d_res, s.stream)) != hipSuccess)
+        return api_fail_hip(e == hipErrorOutOfMemory ? NETC_GPU_ENOMEM : NETC_GPU_ELAUNCH, "ingest: frame scan", e);
+    if ((e = hipMemcpyAsync(s.h_res, s.d_res, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
+        (e = hipEventRecord(s.scanned, s.stream)) != hipSuccess)
+        return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: result copy", e);
+    if ((e = netc_gpu::launch_unmask_scanned(s.d_buf, len, s.d_hdr, s.d_keys, g->max_frames, s.d_res, s.stream,
+                                             netc_gpu::api_cfg())) != hipSuccess)
+        return api_fail_hip(e == hipErrorOutOfMemory ? NETC_GPU_ENOMEM : NETC_GPU_ELAUNCH, "ingest: unmask", e);
+    if ((e = hipMemcpyAsync(h, s.d_buf, len, hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
+        (e = hipEventRecord(s.done, s.stream)) != hipSuccess)
+        return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: D2H copy", e);
+    s.state = kInflight;
+    g->fifo[(g->head + g->count) % 16] = g->cur;
+    ++g->count;
+    g->prev = g->cur;
+    g->cur = -1;
+    return 0;
+}
+
+// make a slot the filling one (ring order); NETC_WS_INGEST_FULL if it is still in use
+int acquire(netc_ws_ingest* g) {
+    if (g->cur >= 0) return 0;
+    IngestSlot& s = g->slots[g->next_fill];
+    if (s.state != kFree) return api_fail(NETC_WS_INGEST_FULL, "ingest: no free slot (take and release batches)");
+    s.state = kFilling;
+    s.fill = 0;
+    g->cur = g->next_fill;
+    g->next_fill = (g->next_fill + 1) % g->nslots;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int netc_ws_ingest_create(struct netc_ws_ingest** out, int device, size_t slot_bytes, int nslots,
+                          size_t max_frame_bytes, int flags) {
+    if (!out) return api_fail(NETC_GPU_EINVAL, "ingest: null output pointer");
+    *out = nullptr;
+    if (int r = netc_gpu::api_check_device(device)) return r;
+    if (flags & ~NETC_WS_INGEST_STRICT) return api_fail(NETC_GPU_EINVAL, "ingest: unknown flags 0x%x", flags);
+    if (!slot_bytes) slot_bytes = 16u << 20;
+    if (!nslots) nslots = 4;
+    if (!max_frame_bytes) max_frame_bytes = 65536;
+    if (slot_bytes < 4096 || slot_bytes > (1ull << 40) || nslots < 2 || nslots > 16 || max_frame_bytes > (1ull << 40))
+        return api_fail(NETC_GPU_EINVAL, "ingest: need 4096 <= slot_bytes <= 2^40, 2 <= nslots <= 16, "
+                                         "max_frame_bytes <= 2^40");
+    DeviceGuard dg(device);
+    if (dg.err != hipSuccess) return api_fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", dg.err);
+    netc_ws_ingest* g = new (std::nothrow) netc_ws_ingest();
+    if (!g) return api_fail(NETC_GPU_ENOMEM, "ingest: host allocation");
+    g->device = device;
+    g->strict = (flags & NETC_WS_INGEST_STRICT) ? 1 : 0;
+    g->nslots = nslots;
+    g->slot_bytes = slot_bytes;
+    g->carry_cap = max_frame_bytes + 14;   // one whole frame: payload + the longest masked header
+    g->cap = g->carry_cap + slot_bytes;
+    // every frame is >= 6 bytes under the strict checks (masked), >= 2 otherwise
+    g->max_frames = g->cap / (g->strict ? 6 : 2) + 2;
+    g->slots = new (std::nothrow) IngestSlot[nslots];
+    if (!g->slots) {
+        delete g;
+        return api_fail(NETC_GPU_ENOMEM, "ingest: host allocation");
+    }
+    for (int i = 0; i < nslots; ++i) {
+        if (int r = alloc_slot(g, g->slots[i])) {
+            for (int j = 0; j <= i; ++j) free_slot(g->slots[j]);
+            delete[] g->slots;
+            delete g;
+            return r;
+        }
+    }
+    *out = g;
+    return 0;
+}
+
+void netc_ws_ingest_destroy(struct netc_ws_ingest* g) {
+    if (!g) return;
+    DeviceGuard dg(g->device);
+    for (int i = 0; i < g->nslots; ++i) free_slot(g->slots[i]);
+    delete[] g->slots;
+    delete g;
+}
+
+long netc_ws_ingest_recv(struct netc_ws_ingest* g, int fd) {
+    if (!g) return api_fail(NETC_GPU_EINVAL, "ingest: null ingest");
+    if (g->sticky) return sticky_now(g) ? g->sticky : api_fail(g->sticky, "ingest: the stream has ended (error)");
+    DeviceGuard dg(g->device);
+    if (dg.err != hipSuccess) return api_fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", dg.err);
+    if (int r = acquire(g)) return r;
+    IngestSlot& s = g->slots[g->cur];
+    uint8_t* dst = s.h_buf + g->carry_cap + s.fill;
+    const size_t room = (size_t)(g->slot_bytes - s.fill);
+    ssize_t r;
+    do r = recv(fd, dst, room, 0);
+    while (r < 0 && errno == EINTR);
+    if (r < 0) {
+        if (errno == EAGAIN || errno == EWOULDBLOCK) return 0;
+        const int saved = errno;
+        api_fail(NETC_WS_INGEST_ERECV, "ingest: recv: %s", strerror(saved));
+        netc_errno_reason = kBadRecv;
+        errno = saved;
+        return NETC_WS_INGEST_ERECV;
+    }
+    if (r == 0) {   // the peer closed: what it sent goes to the GPU
+        if (int e = submit_cur(g)) return e;
+        return api_fail(NETC_WS_INGEST_CLOSED, "ingest: the peer closed the connection");
+    }
+    s.fill += (uint64_t)r;
+    if (s.fill == g->slot_bytes) {
+        if (int e = submit_cur(g)) return e;
+    }
+    return (long)r;
+}
+
+long netc_ws_ingest_write(struct netc_ws_ingest* g, const void* data, size_t len) {
+    if (!g || (len && !data)) return api_fail(NETC_GPU_EINVAL, "ingest: null argument");
+    if (g->sticky) return api_fail(g->sticky, "ingest: the stream has ended (error)");
+    DeviceGuard dg(g->device);
+    if (dg.err != hipSuccess) return api_fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", dg.err);
+    const uint8_t* p = (const uint8_t*)data;
+    size_t taken = 0;
+    while (taken < len) {
+        if (int r = acquire(g)) return taken ? (long)taken : r;
+        IngestSlot& s = g->slots[g->cur];
+        const size_t room = (size_t)(g->slot_bytes - s.fill);
+        const size_t k = len - taken < room ? len - taken : room;
+        memcpy(s.h_buf + g->carry_cap + s.fill, p + taken, k);
+        s.fill += k;
+        taken += k;
+        if (s.fill == g->slot_bytes) {
+            if (int e = submit_cur(g)) return e;
+        }
+    }
+    return (long)taken;
+}
+
+int netc_ws_ingest_submit(struct netc_ws_ingest* g) {
+    if (!g) return api_fail(NETC_GPU_EINVAL, "ingest: null ingest");
+    if (g->sticky) return 0;
+    DeviceGuard dg(g->device);
+    if (dg.err != hipSuccess) return api_fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", dg.err);
+    return submit_cur(g);
+}
+
+int netc_ws_ingest_next(struct netc_ws_ingest* g, struct netc_ws_batch* out, int wait) {
+    if (!g || !out) return api_fail(NETC_GPU_EINVAL, "ingest: null argument");
+    if (g->count == 0) {
+        const int st = sticky_now(g);
+        return st ? api_fail(st, "ingest: the stream has ended (error)") : 0;
+    }
+    DeviceGuard dg(g->device);
+    if (dg.err != hipSuccess) return api_fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", dg.err);
+    const int i = g->fifo[g->head];
+    IngestSlot& s = g->slots[i];
+    if (!wait) {
+        const hipError_t q = hipEventQuery(s.done);
+        if (q == hipErrorNotReady) return 0;
+        if (q != hipSuccess) return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: event query", q);
+    }
+    if (int r = resolve(g, s)) return r;
+    hipError_t e = hipEventSynchronize(s.done);
+    if (e != hipSuccess) return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: batch wait", e);
+    out->wire = s.h_buf + (g->carry_cap - s.carry);
+    out->len = s.cut;
+    out->hdr = s.h_hdr;
+    out->keys = s.h_keys;
+    out->b0 = s.h_b0;
+    out->nframes = s.frames;
+    out->stream_offset = s.pos;
+    out->slot = i;
+    s.state = kTaken;
+    g->head = (g->head + 1) % 16;
+    --g->count;
+    if (s.err != ~0ull) set_sticky(g, NETC_WS_INGEST_PROTOCOL, i);   // reported from the next call on
+    return 1;
+}
+
+int netc_ws_ingest_release(struct netc_ws_ingest* g, const struct netc_ws_batch* b) {
+    if (!g || !b || b->slot < 0 || b->slot >= g->nslots || g->slots[b->slot].state != kTaken)
+        return api_fail(NETC_GPU_EINVAL, "ingest: not a batch handed out by this ingest");
+    g->slots[b->slot].state = kFree;
+    return 0;
+}
+
+int netc_ws_batch_payload(const struct netc_ws_batch* b, uint64_t k, uint64_t* offset, uint64_t* length) {
+    if (!b || !offset || !length || k >= b->nframes) return NETC_GPU_EINVAL;
+    // header bytes are as received (the unmask touches payloads only)
+    const uint64_t h = b->hdr[k];
+    const uint8_t second = b->wire[h + 1];
+    const uint64_t code = second & 0x7F;
+    const uint64_t hl = 2 + (code == 126 ? 2 : (code == 127 ? 8 : 0)) + ((second & 0x80) ? 4 : 0);
+    *offset = h + hl;
+    *length = b->hdr[k + 1] - (h + hl);
+    return 0;
+}
+
+}  // extern "C"

@@ -99,6 +99,21 @@ int mask_batch_on_current(void* d_dst, const void* d_src, size_t total, const ui
 
 }  // namespace
 
+// error / config helpers shared with the other C-ABI files (ws_ingest.hip)
+namespace netc_gpu {
+int api_fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    netc_errno_reason = NETC_REASON_GPU;
+    return code;
+}
+int api_fail_hip(int code, const char* what, hipError_t e) { return fail_hip(code, what, e); }
+int api_check_device(int device) { return check_device(device); }
+const LaunchCfg& api_cfg() { return g_cfg; }
+}  // namespace netc_gpu
+
 extern "C" {
 
 int netc_gpu_device_count(void) { return cached_device_count(); }

@@ -52,6 +52,12 @@ hipError_t launch_unmask_scanned(uint8_t* wire, uint64_t len, const uint64_t* hd
                                  uint64_t max_frames, const uint64_t* result, hipStream_t stream,
                                  const LaunchCfg& cfg);
 
+// ws_mask_api.hip: the C-ABI's error side channel and process-wide launch shape
+int api_fail(int code, const char* fmt, ...);                 // sets the message + netc_errno_reason, returns code
+int api_fail_hip(int code, const char* what, hipError_t e);
+int api_check_device(int device);                            // 0 or NETC_GPU_ENODEV (message set)
+const LaunchCfg& api_cfg();
+
 hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_t* src, uint64_t src_total,
                                 const uint64_t* off, const uint32_t* keys, const uint8_t* b0, uint64_t n, bool masked,
                                 uint64_t* wo, hipStream_t stream, const LaunchCfg& cfg);

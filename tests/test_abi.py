@@ -89,3 +89,17 @@ def test_struct_layout_is_the_reference_layout():
     ref = "/root/reference/include"
     if os.path.isdir(ref):
         assert layout(ref) == golden
+
+
+def test_ingest_without_gpu_fails_loudly():
+    """No device here: creating an ingest ring reports NETC_GPU_ENODEV (there is no CPU fallback)."""
+    import torch
+
+    from netc_amd import ingest as ni
+    from netc_amd.mask import NETC_GPU_ENODEV, NetcGpuError
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    with pytest.raises(NetcGpuError) as e:
+        ni.Ingest(0)
+    assert e.value.code == NETC_GPU_ENODEV
