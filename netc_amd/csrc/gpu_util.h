@@ -43,6 +43,14 @@ __device__ __forceinline__ uint32_t readlane32(uint32_t x, int lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, lane);
 }
 
+// x of lane `src` (per-lane source; every lane of the wave must execute it)
+__device__ __forceinline__ uint64_t bperm64(uint64_t x, int src) {
+    const int addr = src << 2;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)x);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // Bytes [t, 16) of a vector selected, as 4 dword masks; t is clamped to [0, 16].
 __device__ __forceinline__ u32x4 select_from(int64_t t) {
     t = t < 0 ? 0 : (t > 16 ? 16 : t);

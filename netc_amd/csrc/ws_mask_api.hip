@@ -161,30 +161,52 @@ int netc_gpu_unmask_validate(int device, void* d_dst, const void* d_src, size_t 
     if (partial_overlap(d_dst, d_src, total_bytes)) return fail(NETC_GPU_EINVAL, "dst and src partially overlap");
     DeviceGuard g(device);
     if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
-    // per (device, stream) flag scratch, grown geometrically, never freed (queued work may still use it)
+    // per (device, stream) flag scratch, grown geometrically, never freed (queued work
+    // may still use it).  A call flags frames with its own tag (1..255), so the flags
+    // need clearing only when the scratch is new and when the tags wrap.
+    struct FlagScratch {
+        int device;
+        void* stream;
+        uint8_t* p;
+        size_t cap;
+        uint8_t tag;
+    };
     static std::mutex mu;
-    static std::vector<std::pair<std::pair<int, void*>, std::pair<uint8_t*, size_t>>> scratch;
+    static std::vector<FlagScratch> scratch;
     uint8_t* verr = nullptr;
+    uint8_t tag = 0;
+    bool clear = false;
     {
         std::lock_guard<std::mutex> lk(mu);
         auto it = std::find_if(scratch.begin(), scratch.end(),
-                               [&](const auto& e) { return e.first.first == device && e.first.second == stream; });
+                               [&](const FlagScratch& f) { return f.device == device && f.stream == stream; });
         if (it == scratch.end()) {
-            scratch.push_back({{device, stream}, {nullptr, 0}});
+            scratch.push_back({device, stream, nullptr, 0, 0});
             it = scratch.end() - 1;
         }
-        if (it->second.second < nframes) {
-            size_t want = it->second.second ? 2 * it->second.second : 65536;
+        if (it->cap < nframes) {
+            size_t want = it->cap ? 2 * it->cap : 65536;
             while (want < nframes) want *= 2;
             void* p = nullptr;
             hipError_t e = hipMalloc(&p, want);
             if (e != hipSuccess) return fail_hip(NETC_GPU_ENOMEM, "validation scratch", e);
-            it->second = {(uint8_t*)p, want};
+            it->p = (uint8_t*)p;
+            it->cap = want;
+            it->tag = 0;
         }
-        verr = it->second.first;
+        if (it->tag == 0xFF || it->tag == 0) {
+            it->tag = 0;
+            clear = true;
+        }
+        tag = ++it->tag;
+        verr = it->p;
+        if (clear) {
+            hipError_t e = hipMemsetAsync(verr, 0, it->cap, (hipStream_t)stream);
+            if (e != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "validation scratch clear", e);
+        }
     }
     hipError_t e = netc_gpu::launch_mask_validate((uint8_t*)d_dst, (const uint8_t*)d_src, total_bytes,
-                                                  d_frame_offsets, d_keys, d_header0, nframes, verr, d_valid,
+                                                  d_frame_offsets, d_keys, d_header0, nframes, verr, tag, d_valid,
                                                   (hipStream_t)stream, g_cfg);
     if (e != hipSuccess) return fail_hip(NETC_GPU_ELAUNCH, "unmask + validate launch", e);
     return 0;

@@ -21,6 +21,7 @@ struct Args {
     double density;            // n / total: frames per payload byte (table-base guesses)
     const uint64_t* n_dev;     // if set: the frame count is read from device memory at kernel start
     uint8_t* verr;             // TEXT validation (VAL kernels): per-frame "local UTF-8 rule broken" flags
+    uint8_t vtag;              // ... written as this call's tag (verr[f] == vtag: flagged by this call)
 };
 
 enum : int { kNtLoads = 1, kNtStores = 2 };   // LaunchCfg::flags (NETC_GPU_TUNE_NT_*)
@@ -36,9 +37,10 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
                               const uint64_t* n_dev = nullptr);
 
 // Unmask + UTF-8 verdicts of the batch's TEXT messages (include/ws/mask.h,
-// netc_gpu_unmask_validate): verr is n bytes of scratch, valid the n-byte output.
+// netc_gpu_unmask_validate): verr is n bytes of scratch holding no byte equal to
+// tag (flags of earlier calls carry other tags), valid the n-byte output.
 hipError_t launch_mask_validate(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,
-                                const uint32_t* keys, const uint8_t* header0, uint64_t n, uint8_t* verr,
+                                const uint32_t* keys, const uint8_t* header0, uint64_t n, uint8_t* verr, uint8_t tag,
                                 uint8_t* valid, hipStream_t stream, const LaunchCfg& cfg);
 
 // ws_frame_gpu.hip: wire offsets (n + 1 entries into wo), then the wire bytes of

@@ -263,6 +263,22 @@ __device__ __forceinline__ uint32_t utf8_err_word(uint32_t x, uint32_t prev) {
     return err & hi;
 }
 
+// The frame holding position P (P coordinates), or -1: a binary search over the
+// offsets array (the UTF-8 check's rare path).
+__device__ int64_t frame_of(const Args& a, uint64_t P) {
+    if (P < a.mis || a.n == 0) return -1;
+    const uint64_t q = P - a.mis;
+    const NETC_GLOBAL uint64_t* off = gptr(a.off);
+    if (off[0] > q) return -1;
+    uint64_t lo = 0, hi = a.n;   // off[lo] <= q
+    while (hi - lo > 1) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (off[mid] <= q) lo = mid;
+        else hi = mid;
+    }
+    return q < off[lo + 1] ? (int64_t)lo : -1;
+}
+
 // Phase A of the TEXT check, per span: flag the frames holding a byte that breaks
 // the local rules.  out = this lane's unmasked 16 bytes, prevd = the 4 bytes before
 // them (from the neighbouring lane / the previous span of the chunk).  Skipped here:
@@ -282,32 +298,63 @@ __device__ __forceinline__ void validate_span(const Args& a, const Table& t, uin
     e[3] = utf8_err_word(out[3], out[2]);
     if (seam && lane == 0) e[0] &= ~0x00FFFFFFu;
     if (!__ballot((e[0] | e[1] | e[2] | e[3]) != 0)) return;
+    // one bit per broken byte of the lane's vector
+    uint32_t bits = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t m = (e[w] >> 7) & 0x01010101u;
+        bits |= ((m | m >> 7 | m >> 14 | m >> 21) & 0xFu) << (4 * w);
+    }
+    if (readlane64(t.start, 0) > A0) {
+        // more than 63 frames start inside this span, so the table holds only its last
+        // ones (span_mask slid it): each broken byte's frame from the offsets array
+        while (bits) {
+            const int k = __builtin_ctz(bits);
+            bits &= bits - 1;
+            const int64_t f = frame_of(a, W + (uint64_t)k);
+            if (f >= 0 && W + (uint64_t)k >= gptr(a.off)[f] + a.mis + 3) a.verr[f] = a.vtag;
+        }
+        return;
+    }
     // drop bytes within 3 of a frame start: the span's first frame (if it starts
     // less than 3 bytes before A0) and every frame starting inside the span
     const uint64_t Aend = A0 + kSpan;
     const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
     const uint64_t s0 = readlane64(t.start, l0);
-    if (s0 + 3 > A0) e &= ~(select_from((int64_t)(s0 - W)) & ~select_from((int64_t)(s0 + 3 - W)));
+    u32x4 drop = {0, 0, 0, 0};
+    if (s0 + 3 > A0) drop = select_from((int64_t)(s0 - W)) & ~select_from((int64_t)(s0 + 3 - W));
     uint64_t b = __ballot(t.start > A0 && t.start < Aend);
     while (b) {
         const int j = __builtin_ctzll(b);
         b &= b - 1;
         const uint64_t sj = readlane64(t.start, j);
-        e &= ~(select_from((int64_t)(sj - W)) & ~select_from((int64_t)(sj + 3 - W)));
+        drop |= select_from((int64_t)(sj - W)) & ~select_from((int64_t)(sj + 3 - W));
     }
-    const uint32_t any = e[0] | e[1] | e[2] | e[3];
-    if (!__ballot(any != 0)) return;
-    if (any) {
-        for (int k = 0; k < 16; ++k) {
-            if (!((e[k >> 2] >> (8 * (k & 3) + 7)) & 1)) continue;
-            const uint64_t p = W + k;
-            int64_t f = -2;   // frame holding p: the last table entry starting at or before it
-            for (int l = 0; l < kWave; ++l) {
-                const uint64_t sl = __builtin_amdgcn_readlane((int)(uint32_t)t.start, l) |
-                                    ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(t.start >> 32), l) << 32);
-                if (sl <= p) f = t.kb + l;
-            }
-            if (f >= 0 && f < (int64_t)a.n) a.verr[f] = 1;
+    uint32_t dbits = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t m = (drop[w] >> 7) & 0x01010101u;
+        dbits |= ((m | m >> 7 | m >> 14 | m >> 21) & 0xFu) << (4 * w);
+    }
+    bits &= ~dbits;
+    // The frame of a broken byte p: the last table entry starting at or before it,
+    // by a binary search over the 64 entries (ds_bpermute: each lane reads the entry
+    // its own search is at; every lane takes part, so the loop is wave-uniform).
+    // The lane's bytes before the next frame start are then done: one search per
+    // frame touched.  Entry 0 starts at or before A0 <= p (checked above).
+    while (__ballot(bits != 0)) {
+        const uint64_t p = W + (uint64_t)(bits ? __builtin_ctz(bits) : 0);
+        int idx = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1)
+            if (bperm64(t.start, idx + step) <= p) idx += step;
+        const uint64_t next = bperm64(t.start, idx < kWave - 1 ? idx + 1 : idx);
+        if (bits) {
+            const int64_t f = t.kb + idx;
+            if (f >= 0 && f < (int64_t)a.n) a.verr[f] = a.vtag;
+            // entry 63 is the last: the table covers the span (span_mask), so no later frame starts here
+            const int64_t keep = idx < kWave - 1 ? (int64_t)(next - W) : 16;
+            bits &= keep >= 16 ? 0u : (keep <= 0 ? ~0u : (~0u << keep));
         }
     }
 }
@@ -555,33 +602,8 @@ __device__ __forceinline__ bool utf8_rule(uint32_t b3, uint32_t b2, uint32_t b1,
     return false;
 }
 
-// Phase A of the TEXT check for the bytes validate_span skips at chunk seams: the
-// first 3 bytes of every chunk (win bytes apart in P coordinates), checked once the
-// whole batch is unmasked -- one thread per seam, a binary search for its frame.
-__global__ void utf8_seams(const uint8_t* dst, uint64_t total, const uint64_t* off, uint64_t n, uint64_t mis,
-                           uint64_t win, uint64_t nseams, uint8_t* verr) {
-    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
-    if (c > nseams || n == 0) return;
-    const uint64_t q = c * win - mis;   // payload coordinate of the seam (c * win >= 4096 > mis)
-    if (q >= total || off[0] > q) return;
-    uint64_t lo = 0, hi = n;   // the last frame starting at or before q: off[lo] <= q
-    while (hi - lo > 1) {
-        const uint64_t mid = lo + (hi - lo) / 2;
-        if (off[mid] <= q) lo = mid;
-        else hi = mid;
-    }
-    const uint64_t fs = off[lo], fe = off[lo + 1];
-    for (uint64_t p = q; p < q + 3 && p < fe; ++p) {
-        if (p - fs < 3) continue;   // within 3 of the frame start: utf8_messages checks it
-        if (utf8_rule(dst[p - 3], dst[p - 2], dst[p - 1], dst[p])) {
-            verr[lo] = 1;
-            break;
-        }
-    }
-}
-
 __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uint8_t* h0, uint64_t n,
-                              const uint8_t* verr, uint8_t* valid) {
+                              const uint8_t* verr, uint8_t tag, uint64_t mis, uint64_t win, uint8_t* valid) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     uint8_t verdict = 1;
@@ -603,7 +625,7 @@ __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uin
             bool bad = false;
             for (uint64_t j = (uint64_t)first; j <= k && !bad; ++j) {
                 if ((h0[j] & 0x0F) >= 8) continue;
-                if (verr[j]) bad = true;
+                if (verr[j] == tag) bad = true;
                 const uint64_t lo = off[j], hi = off[j + 1];
                 for (uint64_t p = lo; p < hi && p < lo + 3; ++p) {
                     const uint32_t b = dst[p];
@@ -611,6 +633,12 @@ __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uin
                     h3 = h2;
                     h2 = h1;
                     h1 = b;
+                }
+                // the first 3 bytes of every chunk inside the frame, which phase A skips
+                // (in place, another wavefront's chunk held the bytes before them)
+                for (uint64_t c = (lo + 3 + mis + win - 1) / win * win; c < hi + mis && !bad; c += win) {
+                    for (uint64_t p = c - mis; p < c - mis + 3 && p < hi; ++p)
+                        if (p >= lo + 3) bad |= utf8_rule(dst[p - 3], dst[p - 2], dst[p - 1], dst[p]);
                 }
                 if (hi - lo > 3) {   // the frame's own last 3 bytes become the history
                     h3 = dst[hi - 3];
@@ -635,15 +663,14 @@ static hipError_t launch_val(const Args& a, hipStream_t s) {
 }
 
 hipError_t launch_mask_validate(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,
-                                const uint32_t* keys, const uint8_t* header0, uint64_t n, uint8_t* verr,
+                                const uint32_t* keys, const uint8_t* header0, uint64_t n, uint8_t* verr, uint8_t tag,
                                 uint8_t* valid, hipStream_t stream, const LaunchCfg& cfg) {
     (void)cfg;
     if (n == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(verr, 0, n, stream);
-    if (e != hipSuccess) return e;
     Args a;
     a.n_dev = nullptr;
     a.verr = verr;
+    a.vtag = tag;
     a.mis = (uint64_t)(uintptr_t)dst & 15u;
     a.dst_base = dst - a.mis;
     a.src_base = src - a.mis;
@@ -654,20 +681,14 @@ hipError_t launch_mask_validate(uint8_t* dst, const uint8_t* src, uint64_t total
     a.density = total ? (double)n / (double)total : 0.0;
     const uint64_t nvec = (a.mis + total + 15) / 16;
     a.nwin = (nvec + 255) / 256;   // U = 4 chunks of 64 vectors x 4
+    hipError_t e;
     if (a.nwin) {
         const bool aligned = (((uintptr_t)src ^ (uintptr_t)dst) & 15u) == 0;
         e = aligned ? launch_val<true>(a, stream) : launch_val<false>(a, stream);
         if (e != hipSuccess) return e;
     }
-    const uint64_t win = kSpan * 4;                    // the VAL kernel's chunk (U = 4)
-    const uint64_t nseams = (a.mis + total) / win;     // chunk starts c * win, c = 1 .. nseams
-    if (nseams) {
-        hipLaunchKernelGGL(utf8_seams, dim3((unsigned)((nseams + 255) / 256)), dim3(256), 0, stream, dst, total, off, n,
-                           a.mis, win, nseams, verr);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
     hipLaunchKernelGGL(utf8_messages, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dst, off, header0, n,
-                       verr, valid);
+                       verr, tag, a.mis, kSpan * 4, valid);
     return hipGetLastError();
 }
 
