@@ -238,29 +238,55 @@ __device__ __forceinline__ void edge_vec(const Args& a, uint64_t P, u32x4 mask) 
 // rules of the "lookup" validators): a byte must be a continuation exactly when a
 // lead 1-3 bytes back asks for one; C0, C1 and F5..FF never occur; the byte after
 // E0 / ED / F0 / F4 is limited (shortest form, surrogates, U+10FFFF).  Four bytes
-// at a time in a dword (SWAR); bit 7 of each byte of the result flags an error.
-__device__ __forceinline__ uint32_t sw_ge(uint32_t y, uint32_t c) {   // byte >= c, for c in [0x80, 0xFF]
-    return y & ((y & 0x7F7F7F7Fu) + (0x100u - c) * 0x01010101u) & 0x80808080u;
+// at a time in a dword (SWAR; bit 7 of each byte of the result flags an error),
+// about 45 VALU operations per dword: the lead flags of a dword are computed once
+// and carried to the next, and the four second-byte rules are two nibble lookups
+// (v_perm_b32 over a 16-byte table) ANDed with a lookup on the byte's own high
+// nibble.  tools/ and DESIGN.md §10.3: checked exhaustively against the scalar rule
+// (utf8_rule below) over every 4-byte context of 31 boundary byte values.
+struct Utf8Carry {
+    uint32_t x, l2, l3, l4;   // the previous dword and its lead flags (bytes >= C0 / E0 / F0, bit 7)
+};
+
+__device__ __forceinline__ Utf8Carry utf8_carry(uint32_t prev) {
+    const uint32_t l2 = prev & (prev << 1) & 0x80808080u;
+    const uint32_t l3 = l2 & (prev << 2);
+    return {prev, l2, l3, l3 & (prev << 3)};
 }
-__device__ __forceinline__ uint32_t sw_eq(uint32_t y, uint32_t c) {   // byte == c
-    const uint32_t z = y ^ (c * 0x01010101u);
-    return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
+
+// t[idx] for each byte's nibble idx (0..15) of a 16-entry byte table held in 4 dwords
+__device__ __forceinline__ uint32_t nibble_lookup(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3, uint32_t idx) {
+    const uint32_t i7 = idx & 0x07070707u;
+    const uint32_t lo = __builtin_amdgcn_perm(t1, t0, i7);   // entries 0..7
+    const uint32_t hi = __builtin_amdgcn_perm(t3, t2, i7);   // entries 8..15
+    const uint32_t m = ((idx & 0x08080808u) >> 3) * 0xFFu;
+    return (m & hi) | (~m & lo);
 }
-__device__ __forceinline__ uint32_t utf8_err_word(uint32_t x, uint32_t prev) {
-    const uint32_t hi = 0x80808080u;
-    const uint32_t p1 = __builtin_amdgcn_alignbyte(x, prev, 3);   // the byte before each byte of x
-    const uint32_t p2 = __builtin_amdgcn_alignbyte(x, prev, 2);
-    const uint32_t p3 = __builtin_amdgcn_alignbyte(x, prev, 1);
-    if (((x | p3) & hi) == 0) return 0;   // all ASCII, nothing pending
-    const uint32_t cont = x & ~(x << 1) & hi;
-    const uint32_t need = ((p1 & (p1 << 1)) | (p2 & (p2 << 1) & (p2 << 2)) | (p3 & (p3 << 1) & (p3 << 2) & (p3 << 3))) & hi;
+
+__device__ __forceinline__ uint32_t utf8_err_word(uint32_t x, Utf8Carry& c) {
+    const uint32_t H = 0x80808080u;
+    const uint32_t s1 = x << 1;
+    const uint32_t l2 = x & s1 & H;          // byte >= C0: a lead of 2+ bytes
+    const uint32_t l3 = l2 & (x << 2);       // byte >= E0
+    const uint32_t l4 = l3 & (x << 3);       // byte >= F0
+    const uint32_t cont = x & ~s1 & H;       // 80..BF
+    const uint32_t need = __builtin_amdgcn_alignbyte(l2, c.l2, 3) | __builtin_amdgcn_alignbyte(l3, c.l3, 2) |
+                          __builtin_amdgcn_alignbyte(l4, c.l4, 1);
     uint32_t err = need ^ cont;
-    err |= sw_ge(x, 0xF5) | (sw_ge(x, 0xC0) & ~sw_ge(x, 0xC2));
-    if (sw_ge(p1, 0xE0)) {
-        const uint32_t geA0 = sw_ge(x, 0xA0), ge90 = sw_ge(x, 0x90);
-        err |= (sw_eq(p1, 0xE0) & ~geA0) | (sw_eq(p1, 0xED) & geA0) | (sw_eq(p1, 0xF0) & ~ge90) | (sw_eq(p1, 0xF4) & ge90);
-    }
-    return err & hi;
+    const uint32_t z = (x & 0xFEFEFEFEu) ^ 0xC0C0C0C0u;            // C0 / C1
+    err |= ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & H;
+    err |= ((x & 0x7F7F7F7Fu) + 0x0B0B0B0Bu) & x & H;               // F5..FF
+    // the byte after E0 / ED / F0 / F4: bits 0-3 = rule broken after E0 / F0 / ED / F4
+    const uint32_t p1 = __builtin_amdgcn_alignbyte(x, c.x, 3);      // the byte before each byte of x
+    const uint32_t lead3 = __builtin_amdgcn_alignbyte(l3, c.l3, 3);  // ... is >= E0
+    // by p1's low nibble: 0 -> E0 or F0, 4 -> F4, D -> ED
+    const uint32_t t1 = nibble_lookup(0x00000003u, 0x00000008u, 0x00000000u, 0x00000400u, p1 & 0x0F0F0F0Fu);
+    const uint32_t sel = ((p1 & 0x10101010u) >> 4) * 5u + 0x05050505u;   // E lead: E0 | ED bits, F lead: F0 | F4
+    // by x's high nibble 8..B (others are not continuations, flagged above)
+    const uint32_t t2 = __builtin_amdgcn_perm(0u, 0x0C0C0903u, (x >> 4) & 0x07070707u);
+    err |= ((t1 & sel & t2) + 0x7F7F7F7Fu) & lead3;
+    c = {x, l2, l3, l4};
+    return err & H;
 }
 
 // The frame holding position P (P coordinates), or -1: a binary search over the
@@ -292,10 +318,13 @@ __device__ __forceinline__ void validate_span(const Args& a, const Table& t, uin
                                               bool seam, int lane) {
     const uint64_t W = A0 + 16ull * (uint64_t)lane;
     u32x4 e;
-    e[0] = utf8_err_word(out[0], prevd);
-    e[1] = utf8_err_word(out[1], out[0]);
-    e[2] = utf8_err_word(out[2], out[1]);
-    e[3] = utf8_err_word(out[3], out[2]);
+    // all ASCII across the wave (the common case for text): nothing to check
+    if (!__ballot(((out[0] | out[1] | out[2] | out[3] | prevd) & 0x80808080u) != 0)) return;
+    Utf8Carry c = utf8_carry(prevd);
+    e[0] = utf8_err_word(out[0], c);
+    e[1] = utf8_err_word(out[1], c);
+    e[2] = utf8_err_word(out[2], c);
+    e[3] = utf8_err_word(out[3], c);
     if (seam && lane == 0) e[0] &= ~0x00FFFFFFu;
     if (!__ballot((e[0] | e[1] | e[2] | e[3]) != 0)) return;
     // one bit per broken byte of the lane's vector
