@@ -371,45 +371,58 @@ __device__ u32x4 compose_vec(const EncArgs& a, EncTable& t, int l0, uint64_t A0,
     return out;
 }
 
-// One frame's payload as seen from a lane's 16-B vector at W.
-struct Slot {
-    int64_t s0;        // src offset of the vector's byte 0 (o + W - pw)
-    int32_t plo, phi;  // payload bytes [plo, phi) of the vector, clamped to [0, 16]
-    uint32_t rk;       // key rotated to the phase of byte 0 (W - pw)
+// ------------------------------------------------------------ fast spans --
+// A frame's payload follows the previous frame's payload in the source (frames are
+// [off[k], off[k+1])), so the wire is the source with the headers inserted.  For a
+// lane's wire vector at W, take the frame l holding W (header start S <= W < next
+// header start Sn): one unaligned 16-B load at s = W + (off[l] - pw_l) (pw = wire
+// payload start) gives byte i = the payload byte of frame l at wire W + i, and for
+// the next frame (whose header starts at cut c = Sn - W < 16) byte i - hl_n.  So a
+// vector is the load XOR frame l's key, with at most two header insertions (frame
+// l's, if W is inside it, and frame l+1's at the cut) and the tail after the cut
+// shifted up by the next header's length -- the last two only in the lane or two a
+// header touches.  A span takes this path when every frame ending inside it has at
+// least 16 wire bytes (one cut per vector) and every load stays inside the payload
+// buffer; any other span is queued for the compose kernel.
+
+// per-lane frame data from the table (ds_bpermute: every lane of the wave executes it)
+struct LaneFrames {
+    uint64_t S, Sn;         // wire header starts of frames l and l + 1 (W coordinates)
+    uint64_t P, Pn, Pnn;    // payload offsets of frames l, l + 1, l + 2
+    uint32_t K, Kn, B, Bn;  // keys and header bytes of frames l and l + 1
 };
 
-__device__ __forceinline__ int32_t clamp16(int64_t x) { return x < 0 ? 0 : (x > 16 ? 16 : (int32_t)x); }
-
-__device__ __forceinline__ Slot slot_of(const FrameInfo& f, uint64_t W) {
-    Slot s;
-    s.s0 = (int64_t)f.o + (int64_t)(W - f.pw);
-    s.plo = clamp16((int64_t)(f.pw - W));
-    s.phi = clamp16((int64_t)(f.We - W));
-    s.rk = rotr8(f.key, W - f.pw);
-    return s;
+__device__ __forceinline__ uint32_t bperm32(uint32_t x, int src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)x);
 }
 
-__device__ __forceinline__ Slot select_slot(bool c, const Slot& x, const Slot& y) {
-    Slot s;
-    s.s0 = c ? x.s0 : y.s0;
-    s.plo = c ? x.plo : y.plo;
-    s.phi = c ? x.phi : y.phi;
-    s.rk = c ? x.rk : y.rk;
-    return s;
+__device__ __forceinline__ LaneFrames lane_frames(const EncTable& t, int l) {
+    LaneFrames f;
+    f.S = bperm64(t.start, l);
+    f.Sn = bperm64(t.start, l + 1);
+    f.P = bperm64(t.poff, l);
+    f.Pn = bperm64(t.poff, l + 1);
+    f.Pnn = bperm64(t.poff, l + 2);
+    f.K = bperm32(t.key, l);
+    f.Kn = bperm32(t.key, l + 1);
+    f.B = bperm32(t.b0, l);
+    f.Bn = bperm32(t.b0, l + 1);
+    return f;
 }
 
-// Span kinds (wave-uniform): the whole span is payload of one frame; or every
-// vector holds bytes of at most two frames (two unaligned loads plus header
-// bytes); or anything else (table edges, frames under 16 B, buffer edges), which
-// is queued for the compose kernel.
-enum : int { kSpanFast = 0, kSpanSlots = 1, kSpanQueued = 2, kSpanNone = 3 };
+__device__ __forceinline__ uint64_t header_len(uint64_t len, bool masked) {
+    return 2 + ext_len(len) + (masked ? 4 : 0);
+}
 
-// What phase 2 needs for one span of a chunk: the loads, the rotated keys, and one
-// packed word per lane: plo1 | phi1 << 5 | plo2 << 10 | phi2 << 15 | two << 20.
+enum : int { kSpanFast = 0, kSpanQueued = 2, kSpanNone = 3 };
+
+// What the store phase needs for one span: the load, the rotated key, and per lane
+// the table entry of its frame (bits 0-5) | W inside that frame's header (bit 6) |
+// the next frame's header starts inside the vector (bit 7).
 struct SpanPlan {
     int kind;
-    u32x4 d1, d2;
-    uint32_t rk1, rk2, pk;
+    u32x4 d;
+    uint32_t rk, info;
 };
 template <int U>
 struct Plan {
@@ -430,70 +443,49 @@ __device__ __forceinline__ void static_for(F&& f) {
 template <int U, bool NT>
 __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, uint64_t A, uint64_t wlo,
                                            uint64_t whi, int lane, Plan<U>& P) {
+    const bool masked = a.masked != 0;
     static_for<0, U>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
         SpanPlan& sp = P.s[u];
         const uint64_t A0 = A + (uint64_t)u * kSpan, Aend = A0 + kSpan;
         const uint64_t W = A0 + 16ull * (uint64_t)lane;
-        // the span is classified first; its two loads are then issued unconditionally
-        // at the end (one exit path: loads under branches end up staged through
-        // scratch with full vmcnt drains)
+        // classified first (wave-uniform); the load is then issued unconditionally at
+        // the end (one exit path: loads under branches end up staged through scratch
+        // with full vmcnt drains)
         int kind = kSpanNone;
-        int64_t ad1 = 0, ad2 = 0;
-        uint32_t rk1 = 0, rk2 = 0, pk = 0;
+        int64_t ad = 0;
+        uint32_t rk = 0, info = 0;
         do {
             if (A0 >= whi) break;
             kind = kSpanQueued;
             const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
             const uint64_t bm = __ballot(t.start > A0 && t.start < Aend);
             const int nb = __popcll(bm);
-            const bool covered = (t.tail || t.last >= Aend) && l0 + nb + 1 <= kWave - 1;
+            const bool covered = (t.tail || t.last >= Aend) && l0 >= 0 && l0 + nb + 2 <= kWave - 1;
             if (!covered || A0 < wlo || Aend > whi || t.kb + l0 < 0 || t.kb + l0 + nb >= (int64_t)a.n) break;
-            const FrameInfo f0 = frame_info(a, t, l0);
-            if (nb == 0 && f0.pw <= A0 && Aend <= f0.We) {
-                kind = kSpanFast;
-                const Slot sf = slot_of(f0, W);
-                rk1 = sf.rk;
-                ad1 = ad2 = sf.s0;
-                break;
-            }
-            Slot a1 = slot_of(f0, W), a2 = a1;
-            int cut = 0;   // frame starts inside (W, W + 15]
-            uint64_t b = bm;
-            while (b) {
-                const int l = __builtin_ctzll(b);
-                b &= b - 1;
-                const FrameInfo fj = frame_info(a, t, l);
-                const Slot sj = slot_of(fj, W);
-                a1 = select_slot(W >= fj.Ws, sj, a1);
-                a2 = select_slot(W + 15 >= fj.Ws, sj, a2);
-                cut += (fj.Ws > W && fj.Ws <= W + 15) ? 1 : 0;
-            }
-            const bool two = cut == 1;
-            const bool need1 = a1.phi > a1.plo, need2 = two && a2.phi > a2.plo;
-            // three frames in one vector, or a load leaving [0, src_total): the compose kernel
-            bool slow = cut > 1;
-            slow |= need1 && (a1.s0 < 0 || (uint64_t)a1.s0 + 16 > a.src_total);
-            slow |= need2 && (a2.s0 < 0 || (uint64_t)a2.s0 + 16 > a.src_total);
-            if (__ballot(slow)) break;   // the whole span is queued
-            kind = kSpanSlots;
-            rk1 = a1.rk;
-            rk2 = a2.rk;
-            pk = (uint32_t)a1.plo | (uint32_t)a1.phi << 5 | (uint32_t)a2.plo << 10 | (uint32_t)a2.phi << 15 |
-                 (two ? 1u << 20 : 0u);
-            ad1 = need1 ? a1.s0 : 0;   // unused bytes are masked off in phase 2
-            ad2 = need2 ? a2.s0 : ad1;
+            // every frame ending inside the span has >= 16 wire bytes: one cut per vector
+            const uint64_t nxt = bperm64(t.start, lane < kWave - 1 ? lane + 1 : lane);
+            if (__ballot(lane >= l0 && lane < l0 + nb && nxt - t.start < 16)) break;
+            // this lane's frame: the entries starting at or before W
+            int l = l0;
+            for (uint64_t b = bm; b; b &= b - 1) l += readlane64(t.start, __builtin_ctzll(b)) <= W ? 1 : 0;
+            const LaneFrames f = lane_frames(t, l);
+            const uint64_t pw = f.S + header_len(f.Pn - f.P, masked);
+            const int64_t s0 = (int64_t)(W + f.P - pw);   // source offset of the vector's byte 0
+            if (__ballot(s0 < 0 || (uint64_t)s0 + 16 > a.src_total)) break;
+            kind = kSpanFast;
+            ad = s0;
+            rk = rotr8(f.K, W - pw);
+            info = (uint32_t)l | (W < pw ? 64u : 0u) | (f.Sn < W + 16 ? 128u : 0u);
         } while (false);
         sp.kind = kind;
-        sp.rk1 = rk1;
-        sp.rk2 = rk2;
-        sp.pk = pk;
-        sp.d1 = sp.d2 = u32x4{0, 0, 0, 0};
+        sp.rk = rk;
+        sp.info = info;
+        sp.d = u32x4{0, 0, 0, 0};
         // a payload buffer under 16 bytes (possibly NULL when empty) is never read
         // here: every span is queued then, and the compose kernel reads byte-wise
         if (a.src_total >= 16) {   // kernel-uniform
-            if (ENC_OK(1, ad1, a.src_total - 16)) sp.d1 = load_u<NT>(a.src + ad1);
-            if (ENC_OK(2, ad2, a.src_total - 16)) sp.d2 = load_u<NT>(a.src + ad2);
+            if (ENC_OK(1, ad, a.src_total - 16)) sp.d = load_u<NT>(a.src + ad);
         }
     });
 }
@@ -501,10 +493,11 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
 template <int U, bool NT>
 __device__ __forceinline__ void finish_chunk(const EncArgs& a, const EncTable& t, uint64_t A, uint64_t wlo,
                                              uint64_t whi, int lane, const Plan<U>& P) {
+    const bool masked = a.masked != 0;
     static_for<0, U>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
         const SpanPlan& sp = P.s[u];
-        const uint64_t A0 = A + (uint64_t)u * kSpan, Aend = A0 + kSpan;
+        const uint64_t A0 = A + (uint64_t)u * kSpan;
         const uint64_t W = A0 + 16ull * (uint64_t)lane;
         if (sp.kind == kSpanNone) return;
         if (sp.kind == kSpanQueued) {
@@ -514,26 +507,31 @@ __device__ __forceinline__ void finish_chunk(const EncArgs& a, const EncTable& t
             }
             return;
         }
-        u32x4 v;
-        if (sp.kind == kSpanFast) {
-            const u32x4 kv = {sp.rk1, sp.rk1, sp.rk1, sp.rk1};
-            v = sp.d1 ^ kv;
-        } else {
-            const uint32_t p = sp.pk;
-            const u32x4 k1 = {sp.rk1, sp.rk1, sp.rk1, sp.rk1};
-            const u32x4 k2 = {sp.rk2, sp.rk2, sp.rk2, sp.rk2};
-            v = (sp.d1 ^ k1) & select_range(p & 31, (p >> 5) & 31);
-            if (p & (1u << 20)) v |= (sp.d2 ^ k2) & select_range((p >> 10) & 31, (p >> 15) & 31);
-            // headers: the span's first frame (if the span starts inside its header)
-            // and every frame starting inside the span
-            const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
-            const FrameInfo f0 = frame_info(a, t, l0);
-            if (f0.pw > A0) v = put_header(a, f0, W, v);
-            uint64_t b = __ballot(t.start > A0 && t.start < Aend);
-            while (b) {
-                const int l = __builtin_ctzll(b);
-                b &= b - 1;
-                v = put_header(a, frame_info(a, t, l), W, v);
+        const u32x4 kv = {sp.rk, sp.rk, sp.rk, sp.rk};
+        u32x4 v = sp.d ^ kv;
+        if (__ballot(sp.info >= 64)) {   // a header touches some lane's vector (wave-uniform)
+            const LaneFrames f = lane_frames(t, (int)(sp.info & 63));
+            const uint64_t len = f.Pn - f.P, hl = header_len(len, masked);
+            if (sp.info & 64) {   // W inside frame l's header: its bytes from S - W to pw - W
+                const int64_t hs = (int64_t)(f.S - W), he = hs + (int64_t)hl;
+                uint64_t lo, hi;
+                build_header(f.B, len, masked, f.K, lo, hi);
+                const u32x4 m = select_range(hs, he);
+                v = (v & ~m) | (shift_bytes(lo, hi, (int)hs) & m);
+            }
+            if (sp.info & 128) {   // frame l + 1 starts at c: its header, then its payload shifted by hn
+                const int64_t c = (int64_t)(f.Sn - W);
+                const uint64_t lenn = f.Pnn - f.Pn, hn = header_len(lenn, masked);
+                const uint64_t pwn = f.Sn + hn;
+                uint64_t lo, hi;
+                build_header(f.Bn, lenn, masked, f.Kn, lo, hi);
+                const uint64_t dlo = (uint64_t)sp.d[0] | (uint64_t)sp.d[1] << 32;
+                const uint64_t dhi = (uint64_t)sp.d[2] | (uint64_t)sp.d[3] << 32;
+                const uint32_t rkn = rotr8(f.Kn, W - pwn);
+                const u32x4 kn = {rkn, rkn, rkn, rkn};
+                const u32x4 tail = shift_bytes(dlo, dhi, (int)hn) ^ kn;
+                const u32x4 mh = select_range(c, c + (int64_t)hn), mt = select_from(c + (int64_t)hn);
+                v = (v & ~(mh | mt)) | (shift_bytes(lo, hi, (int)c) & mh) | (tail & mt);
             }
         }
         store_wire<NT>(a, W, v, wlo, whi);
