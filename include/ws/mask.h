@@ -98,8 +98,10 @@ int netc_gpu_init(int device);
  * 8); max_blocks: cap on 256-thread workgroups, 0 = exactly the workgroups the
  * device holds at once; flags: NETC_GPU_TUNE_AUTO (non-temporal payload stream)
  * or 0 (plain loads / stores) or NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES
- * (either bit selects the non-temporal stream).  Diagnostic knob: call before
- * launching work; it is not synchronised with concurrent launches.
+ * (either bit selects the non-temporal stream).  The frame assembly of
+ * include/ws/frame.h reads the same knob: unroll 8 selects 4 KiB chunks there,
+ * anything else 2 KiB.  Diagnostic knob: call before launching work; it is not
+ * synchronised with concurrent launches.
  */
 #define NETC_GPU_TUNE_AUTO     -1
 #define NETC_GPU_TUNE_NT_LOADS  1   /* non-temporal payload loads  */

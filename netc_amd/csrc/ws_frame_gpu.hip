@@ -410,6 +410,29 @@ __device__ __forceinline__ LaneFrames lane_frames(const EncTable& t, int l) {
     return f;
 }
 
+// The same for a span holding at most one frame start (nb <= 1): entries l0 .. l0 + 3
+// read once for the wave (readlane), each lane picks frame l0 or l0 + 1.
+__device__ __forceinline__ LaneFrames frames_near(const EncTable& t, int l0, int nb, uint64_t W, int l) {
+    if (nb > 1) return lane_frames(t, l);
+    const uint64_t S0 = readlane64(t.start, l0), S1 = readlane64(t.start, l0 + 1), S2 = readlane64(t.start, l0 + 2);
+    const uint64_t P0 = readlane64(t.poff, l0), P1 = readlane64(t.poff, l0 + 1), P2 = readlane64(t.poff, l0 + 2);
+    const uint64_t P3 = readlane64(t.poff, l0 + 3 < kWave ? l0 + 3 : kWave - 1);
+    const uint32_t K0 = readlane32(t.key, l0), K1 = readlane32(t.key, l0 + 1), K2 = readlane32(t.key, l0 + 2);
+    const uint32_t B0 = readlane32(t.b0, l0), B1 = readlane32(t.b0, l0 + 1), B2 = readlane32(t.b0, l0 + 2);
+    const bool in1 = nb == 1 && W >= S1;
+    LaneFrames f;
+    f.S = in1 ? S1 : S0;
+    f.Sn = in1 ? S2 : S1;
+    f.P = in1 ? P1 : P0;
+    f.Pn = in1 ? P2 : P1;
+    f.Pnn = in1 ? P3 : P2;
+    f.K = in1 ? K1 : K0;
+    f.Kn = in1 ? K2 : K1;
+    f.B = in1 ? B1 : B0;
+    f.Bn = in1 ? B2 : B1;
+    return f;
+}
+
 __device__ __forceinline__ uint64_t header_len(uint64_t len, bool masked) {
     return 2 + ext_len(len) + (masked ? 4 : 0);
 }
@@ -420,7 +443,7 @@ enum : int { kSpanFast = 0, kSpanQueued = 2, kSpanNone = 3 };
 // the table entry of its frame (bits 0-5) | W inside that frame's header (bit 6) |
 // the next frame's header starts inside the vector (bit 7).
 struct SpanPlan {
-    int kind;
+    int kind, l0, nb;   // kind; the span's first table entry and frame starts inside it (uniform)
     u32x4 d;
     uint32_t rk, info;
 };
@@ -452,24 +475,40 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
         // classified first (wave-uniform); the load is then issued unconditionally at
         // the end (one exit path: loads under branches end up staged through scratch
         // with full vmcnt drains)
-        int kind = kSpanNone;
+        int kind = kSpanNone, l0 = 0, nb = 0;
         int64_t ad = 0;
         uint32_t rk = 0, info = 0;
         do {
             if (A0 >= whi) break;
             kind = kSpanQueued;
-            const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
+            l0 = __popcll(__ballot(t.start <= A0)) - 1;
             const uint64_t bm = __ballot(t.start > A0 && t.start < Aend);
-            const int nb = __popcll(bm);
+            nb = __popcll(bm);
             const bool covered = (t.tail || t.last >= Aend) && l0 >= 0 && l0 + nb + 2 <= kWave - 1;
             if (!covered || A0 < wlo || Aend > whi || t.kb + l0 < 0 || t.kb + l0 + nb >= (int64_t)a.n) break;
+            if (nb == 0) {
+                // one frame covers the span: everything is wave-uniform
+                const uint64_t S0 = readlane64(t.start, l0), P0 = readlane64(t.poff, l0);
+                const uint64_t pw = S0 + header_len(readlane64(t.poff, l0 + 1) - P0, masked);
+                const int64_t delta = (int64_t)(P0 - pw);   // source offset = W + delta
+                if ((int64_t)A0 + delta < 0 || (int64_t)Aend + delta > (int64_t)a.src_total) break;
+                kind = kSpanFast;
+                ad = (int64_t)W + delta;
+                rk = rotr8(readlane32(t.key, l0), A0 - pw);
+                info = (uint32_t)l0 | (W < pw ? 64u : 0u);
+                break;
+            }
             // every frame ending inside the span has >= 16 wire bytes: one cut per vector
-            const uint64_t nxt = bperm64(t.start, lane < kWave - 1 ? lane + 1 : lane);
-            if (__ballot(lane >= l0 && lane < l0 + nb && nxt - t.start < 16)) break;
+            if (nb == 1) {
+                if (readlane64(t.start, l0 + 1) - readlane64(t.start, l0) < 16) break;
+            } else {
+                const uint64_t nxt = bperm64(t.start, lane < kWave - 1 ? lane + 1 : lane);
+                if (__ballot(lane >= l0 && lane < l0 + nb && nxt - t.start < 16)) break;
+            }
             // this lane's frame: the entries starting at or before W
             int l = l0;
             for (uint64_t b = bm; b; b &= b - 1) l += readlane64(t.start, __builtin_ctzll(b)) <= W ? 1 : 0;
-            const LaneFrames f = lane_frames(t, l);
+            const LaneFrames f = frames_near(t, l0, nb, W, l);
             const uint64_t pw = f.S + header_len(f.Pn - f.P, masked);
             const int64_t s0 = (int64_t)(W + f.P - pw);   // source offset of the vector's byte 0
             if (__ballot(s0 < 0 || (uint64_t)s0 + 16 > a.src_total)) break;
@@ -478,6 +517,8 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
             rk = rotr8(f.K, W - pw);
             info = (uint32_t)l | (W < pw ? 64u : 0u) | (f.Sn < W + 16 ? 128u : 0u);
         } while (false);
+        sp.l0 = l0;
+        sp.nb = nb;
         sp.kind = kind;
         sp.rk = rk;
         sp.info = info;
@@ -510,7 +551,7 @@ __device__ __forceinline__ void finish_chunk(const EncArgs& a, const EncTable& t
         const u32x4 kv = {sp.rk, sp.rk, sp.rk, sp.rk};
         u32x4 v = sp.d ^ kv;
         if (__ballot(sp.info >= 64)) {   // a header touches some lane's vector (wave-uniform)
-            const LaneFrames f = lane_frames(t, (int)(sp.info & 63));
+            const LaneFrames f = frames_near(t, sp.l0, sp.nb, W, (int)(sp.info & 63));
             const uint64_t len = f.Pn - f.P, hl = header_len(len, masked);
             if (sp.info & 64) {   // W inside frame l's header: its bytes from S - W to pw - W
                 const int64_t hs = (int64_t)(f.S - W), he = hs + (int64_t)hl;
@@ -568,35 +609,29 @@ __global__ __launch_bounds__(256) void encode_frames_kernel(EncArgs a) {
         f = t.kb + j;
         s = readlane64(t.start, j);
     };
-    int64_t f;
-    uint64_t s;
-    EncTable tc, tn;
-    Plan<U> pc, pn;
+    // Per trip: the table of this chunk (issued a trip ago) is resolved, the chunk's
+    // loads are issued, the next chunk's table is issued, then this chunk is stored.
+    // No payload prefetch across trips: the state stays small (one plan, two tables)
+    // so that 4+ wavefronts per SIMD keep the loads in flight instead.
+    EncTable tc;
     uint64_t A = c * kWin;
     enc_table_issue(a, tc, guess(0, a.wmis, A), lane);
-    enc_table_finish(tc);
-    enc_resolve(a, tc, A, wire_total, lane);
-    plan_chunk<U, NT>(a, tc, A, wlo, whi, lane, pc);
-    known(tc, A, f, s);
-    uint64_t cn = c + nwaves;
-    if (cn < nwin) enc_table_issue(a, tn, guess(f, s, cn * kWin), lane);
     for (;;) {
-        EncTable tnn;
-        if (cn < nwin) {
-            const uint64_t An = cn * kWin;
-            enc_table_finish(tn);
-            enc_resolve(a, tn, An, wire_total, lane);
-            plan_chunk<U, NT>(a, tn, An, wlo, whi, lane, pn);
-            known(tn, An, f, s);
-            if (cn + nwaves < nwin) enc_table_issue(a, tnn, guess(f, s, (cn + nwaves) * kWin), lane);
-        }
+        enc_table_finish(tc);
+        enc_resolve(a, tc, A, wire_total, lane);
+        Plan<U> pc;
+        plan_chunk<U, NT>(a, tc, A, wlo, whi, lane, pc);
+        int64_t f;
+        uint64_t s;
+        known(tc, A, f, s);
+        const uint64_t cn = c + nwaves;
+        EncTable tn;
+        if (cn < nwin) enc_table_issue(a, tn, guess(f, s, cn * kWin), lane);
         finish_chunk<U, NT>(a, tc, A, wlo, whi, lane, pc);
         if (cn >= nwin) break;
+        c = cn;
         A = cn * kWin;
         tc = tn;
-        tn = tnn;
-        pc = pn;
-        cn += nwaves;
     }
 }
 
@@ -745,8 +780,9 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     a.defer_count = (uint32_t*)(sc.defer + sc.defer_cap);
     a.defer_cap = sc.defer_cap;
     const bool nt = cfg.flags < 0 || (cfg.flags & (kNtLoads | kNtStores));
-    // U = 2 KiB chunks unless tuned to 4 (netc_gpu_tune's unroll; 1 and 8 map to 2 and 4)
-    if (cfg.unroll >= 4) return launch_enc_u<4>(a, wire_bound, nt, cfg.max_blocks, stream);
+    // U = 2 KiB chunks (124 VGPRs: 4 wavefronts per SIMD; measured faster than 4 KiB at
+    // configs 2 and 4) unless netc_gpu_tune's unroll is 8, which selects 4 KiB
+    if (cfg.unroll >= 8) return launch_enc_u<4>(a, wire_bound, nt, cfg.max_blocks, stream);
     return launch_enc_u<2>(a, wire_bound, nt, cfg.max_blocks, stream);
 }
 

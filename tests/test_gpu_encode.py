@@ -202,9 +202,9 @@ def test_errors(torch_cuda):
         nm.encode_frames(big, wo, src, off, None, masked=True)
 
 
-@pytest.mark.parametrize("unroll,max_blocks", [(4, 0), (2, 1), (4, 3)])
+@pytest.mark.parametrize("unroll,max_blocks", [(4, 0), (2, 1), (8, 3), (8, 0)])
 def test_launch_shapes(torch_cuda, unroll, max_blocks):
-    # both chunk sizes, and grids far smaller than the work (long grid-stride walks)
+    # both chunk sizes (unroll 8 selects 4 KiB), and grids far smaller than the work (long grid-stride walks)
     try:
         nm.tune(unroll, max_blocks)
         rng = np.random.default_rng(31 + unroll)

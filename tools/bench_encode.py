@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workloads", default="c2,c4")
-    ap.add_argument("--unroll", default="2,4", help="netc_gpu_tune unroll values to time (KiB per chunk)")
+    ap.add_argument("--unroll", default="4,8", help="netc_gpu_tune unroll values to time (4: 2 KiB chunks, the default; 8: 4 KiB)")
     args = ap.parse_args()
 
     import torch
