@@ -220,8 +220,29 @@ __device__ uint64_t walk_exit(const ScanArgs& a, uint64_t B, const uint32_t* wor
     return p >= Bend ? term(kExit, p) : 0;
 }
 
+// x into the chunk's LDS set of distinct exits (open addressing); *overflow when full
+__device__ __forceinline__ void set_insert(unsigned long long* set, uint64_t x, int* overflow) {
+    uint32_t h = (uint32_t)((x * 0x9E3779B97F4A7C15ull) >> 58);
+    for (int tries = 0; tries < kSet; ++tries, h = (h + 1) & (kSet - 1)) {
+        const unsigned long long cur = set[h];
+        if (cur == x) return;
+        if (cur == ~0ull) {
+            const unsigned long long prev = atomicCAS(&set[h], ~0ull, (unsigned long long)x);
+            if (prev == ~0ull || prev == x) return;
+        }
+    }
+    *overflow = 1;
+}
+
+static constexpr int kWalkHops = 32;   // K1: hop budget of a direct chain walk
+
 // K1: distinct exits of each chunk, appended to the candidate lists of the chunks
 // they land in; the stream start is the candidate (root) of its chunk.
+// Strict mode: each position passing the quick check on its 2 first bytes (~2 % of
+// payload positions, and every real header) walks its chain directly -- garbage
+// chains die within a hop or two, the true chain has chunk / frame-size hops.  A
+// chain longer than kWalkHops (frames of a few bytes), or non-strict mode (every
+// position a candidate), sends the block to pointer jumping over all positions.
 __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     __shared__ uint32_t words[kWords];
     __shared__ uint64_t lk[kChunk];
@@ -233,28 +254,46 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     if (tid < kSet) set[tid] = ~0ull;
     if (tid == 0) overflow = 0;
     load_chunk(a, B, words);
-    chunk_links(a, B, words, lk);
-    // dedup: a wave retires one distinct value per round (exits repeat a lot)
-    for (int k = 0; k < kPer; ++k) {
-        const uint64_t v = lk[k * kScanT + tid];
-        bool pending = (v & kTerm) && term_type(v) == kExit;
-        uint64_t x = term_pos(v);
-        while (__ballot(pending)) {
-            const int leader = __builtin_ctzll(__ballot(pending));
-            const uint64_t x0 = readlane64(x, leader);
-            if (pending && x == x0) pending = false;
-            if ((tid & (kWave - 1)) == leader) {
-                uint32_t h = (uint32_t)((x0 * 0x9E3779B97F4A7C15ull) >> 58);
-                int tries = 0;
-                for (; tries < kSet; ++tries, h = (h + 1) & (kSet - 1)) {
-                    const unsigned long long cur = set[h];
-                    if (cur == x0) break;
-                    if (cur == ~0ull) {
-                        const unsigned long long prev = atomicCAS(&set[h], ~0ull, (unsigned long long)x0);
-                        if (prev == ~0ull || prev == x0) break;
-                    }
-                }
-                if (tries == kSet) overflow = 1;
+    bool walk_failed = !a.strict;
+    if (a.strict) {
+        const int i0 = kPer * tid;
+        uint32_t w[kPer / 4 + 1];
+#pragma unroll
+        for (int k = 0; k < kPer / 4 + 1; ++k) w[k] = words[i0 / 4 + k];
+        auto byte_at = [&](int j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
+        uint32_t cand = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const uint32_t first = byte_at(j), second = byte_at(j + 1), opcode = first & 0x0F;
+            const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
+            const bool reject = !(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80));
+            if (!reject && B + i0 + j >= a.start) cand |= 1u << j;
+        }
+        while (cand) {
+            const int j = __builtin_ctz(cand);
+            cand &= cand - 1;
+            const uint64_t v = walk_exit(a, B, words, B + i0 + j, kWalkHops);
+            if (v == 0) {
+                walk_failed = true;
+                break;
+            }
+            if (term_type(v) == kExit) set_insert(set, term_pos(v), &overflow);
+        }
+    }
+    if (__syncthreads_or(walk_failed)) {
+        // every position pointer-jumped to its chain's end in LDS (the exits found
+        // by the walks above are exits of real chains too: they stay in the set)
+        chunk_links(a, B, words, lk);
+        // dedup: a wave retires one distinct value per round (exits repeat a lot)
+        for (int k = 0; k < kPer; ++k) {
+            const uint64_t v = lk[k * kScanT + tid];
+            bool pending = (v & kTerm) && term_type(v) == kExit;
+            uint64_t x = term_pos(v);
+            while (__ballot(pending)) {
+                const int leader = __builtin_ctzll(__ballot(pending));
+                const uint64_t x0 = readlane64(x, leader);
+                if (pending && x == x0) pending = false;
+                if ((tid & (kWave - 1)) == leader) set_insert(set, x0, &overflow);
             }
         }
     }
@@ -324,19 +363,28 @@ __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
     }
 }
 
-// K3, pass k: src = J_k (the 2^k-th successor; J_0 = link).  Builds J_{k+1} =
-// J_k o J_k into dst (unless last) and marks the J_k-successor of every marked
-// node: after pass k every node within 2^(k+1) - 1 steps of the start is marked,
-// so after log2(chunks) passes exactly the chain's nodes are (one per chunk it
-// enters).  Marks set during a pass may be followed in the same pass: they are
-// on the chain too.
+// K3, pass k: src = J (the 4^k-th successor; J = link in pass 0).  Builds J^4 into
+// dst (unless last) and marks the J, J^2 and J^3 successors of every marked node:
+// after pass k every node within 4^(k+1) - 1 steps of the start is marked (a node
+// d steps away is 0..3 J-steps past a node marked before the pass), so after
+// ceil(log4(chunks)) passes exactly the chain's nodes are (one per chunk it
+// enters).  Marks set during a pass may be followed in the same pass: they are on
+// the chain too.
 __global__ void scan_lift(const int32_t* src, int32_t* dst, uint8_t* mark, uint64_t nodes) {
     const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= nodes) return;
-    int32_t u = src[v];
-    if (u >= 0 && (uint64_t)u >= nodes) u = -1;   // (range check: defence in depth)
-    if (dst) dst[v] = u < 0 ? -1 : src[u];
-    if (u >= 0 && mark[v]) mark[u] = 1;
+    auto step = [&](int32_t u) -> int32_t {   // (range check: defence in depth)
+        return (u >= 0 && (uint64_t)u < nodes) ? src[u] : -1;
+    };
+    int32_t u1 = src[v];
+    if (u1 >= 0 && (uint64_t)u1 >= nodes) u1 = -1;
+    const int32_t u2 = step(u1), u3 = step(u2);
+    if (dst) dst[v] = step(u3);
+    if (mark[v]) {
+        if (u1 >= 0) mark[u1] = 1;
+        if (u2 >= 0 && (uint64_t)u2 < nodes) mark[u2] = 1;
+        if (u3 >= 0 && (uint64_t)u3 < nodes) mark[u3] = 1;
+    }
 }
 
 // Walk the true frames of a chunk from its entry e (in LDS bytes), calling emit
@@ -530,8 +578,8 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.strict = strict ? 1 : 0;
     a.nc = (len + kChunk - 1) / kChunk;   // real chunks 0 .. nc-1; chunk nc is virtual (positions >= len)
     const uint64_t chunks = a.nc + 1, nodes = chunks * kCand;
-    int levels = 1;   // doubling passes: 2^levels - 1 >= chunks steps along the chain
-    while ((1ull << levels) < chunks + 1) ++levels;
+    int levels = 1;   // lifting passes: 4^levels - 1 >= chunks steps along the chain
+    while ((1ull << (2 * levels)) < chunks + 1) ++levels;
     a.hdr = hdr;
     a.keys = keys;
     a.b0 = b0;
