@@ -62,7 +62,9 @@ struct ScanArgs {
     int32_t* link;         // (nc + 1) * kCand: node -> next node, -1 = chain ends
     uint64_t* nterm;       // (nc + 1) * kCand: the terminal where the chain ends (END / DEAD)
     uint8_t* mark;         // (nc + 1) * kCand: node is on the chain from the stream start
-    uint32_t* flags;       // [0] overflow, [1] root node
+    uint32_t* flags;       // [0] overflow, [1] root node, [2] / [3] entries of slow / slow2
+    uint32_t* slow;        // K1 chunks left to the LDS kernel (nc + 1)
+    uint32_t* slow2;       // K2 nodes left to the LDS kernel ((nc + 1) * kCand)
     uint64_t* status;      // chained-scan status words (nc + 1)
     uint32_t epoch;
     uint64_t* hdr;         // outputs
@@ -220,6 +222,46 @@ __device__ uint64_t walk_exit(const ScanArgs& a, uint64_t B, const uint32_t* wor
     return p >= Bend ? term(kExit, p) : 0;
 }
 
+// 16 stream bytes from p (zero past len) straight from global memory: the walks
+// of K1 (strict), K2 and K4 touch only the header bytes of the frames they visit,
+// so they read them where they lie instead of staging the chunk in LDS.
+__device__ __forceinline__ Win window_global(const ScanArgs& a, uint64_t p) {
+    typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+    Win w;
+    if (p + 16 <= a.len) {
+        const u32x4 x = *(const NETC_GLOBAL u32x4u*)(a.wire + p);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w.d[k] = x[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w.d[k] = 0;
+        for (int j = 0; j < 16; ++j)
+            if (p + j < a.len) w.d[j >> 2] |= (uint32_t)gptr(a.wire)[p + j] << (8 * (j & 3));
+    }
+    return w;
+}
+
+// Walk the frames from e until the chain leaves the chunk [B, B + kChunk) (its
+// terminal: EXIT, END or DEAD), calling emit(p, key, b0) for each complete frame;
+// 0 if `hops` frames did not get there.  Windows from LDS (words, the chunk) or
+// from global memory.
+template <bool LDS, typename F>
+__device__ uint64_t walk_frames(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t e, int hops, F&& emit) {
+    const uint64_t Bend = B + kChunk;
+    uint64_t p = e;
+    for (int h = 0;; ++h) {
+        if (p >= Bend) return term(kExit, p);
+        if (h == hops) return 0;
+        uint32_t key;
+        uint8_t b0;
+        const uint64_t v = LDS ? parse_at(a, p, window_at(words, (int)(p - B)), &key, &b0)
+                               : parse_at(a, p, window_global(a, p), &key, &b0);
+        if (v & kTerm) return v;
+        emit(p, key, b0);
+        p = v;
+    }
+}
+
 // x into the chunk's LDS set of distinct exits (open addressing); *overflow when full
 __device__ __forceinline__ void set_insert(unsigned long long* set, uint64_t x, int* overflow) {
     uint32_t h = (uint32_t)((x * 0x9E3779B97F4A7C15ull) >> 58);
@@ -234,18 +276,35 @@ __device__ __forceinline__ void set_insert(unsigned long long* set, uint64_t x, 
     *overflow = 1;
 }
 
-static constexpr int kWalkHops = 32;   // K1: hop budget of a direct chain walk
+static constexpr int kWalkHops = 32;   // K1 / K2: hop budget of a direct chain walk
 
-// K1: distinct exits of each chunk, appended to the candidate lists of the chunks
-// they land in; the stream start is the candidate (root) of its chunk.
-// Strict mode: each position passing the quick check on its 2 first bytes (~2 % of
-// payload positions, and every real header) walks its chain directly -- garbage
-// chains die within a hop or two, the true chain has chunk / frame-size hops.  A
-// chain longer than kWalkHops (frames of a few bytes), or non-strict mode (every
-// position a candidate), sends the block to pointer jumping over all positions.
+// publish a chunk's distinct exits as candidates of the chunks they land in, and the
+// stream start as the candidate (root) of its chunk.  Strict mode prunes exits that
+// cannot start a frame (2 header bytes fail the checks): payload bytes parsed as a
+// chain land on random positions, and a random position passes with ~2 % odds,
+// while the true chain always lands on a real header.  This keeps the candidate
+// lists at about one entry per chunk.
+__device__ __forceinline__ void publish_exits(const ScanArgs& a, uint64_t chunk, const unsigned long long* set,
+                                              int overflow, int tid) {
+    auto append = [&](uint64_t x) {
+        const uint64_t t = x / kChunk;   // x <= len: t <= nc
+        const uint32_t slot = atomicAdd(&a.ccount[t], 1u);
+        if (slot < (uint32_t)kCand) a.cand[t * kCand + slot] = x;
+        else atomicOr(&a.flags[0], 1u);
+    };
+    if (tid < kSet && set[tid] != ~0ull && !quick_reject(a, set[tid])) append(set[tid]);
+    if (tid == 0) {
+        if (overflow) atomicOr(&a.flags[0], 1u);
+        if (a.start / kChunk == chunk) append(a.start);
+    }
+}
+
+// K1: distinct exits of each chunk.  Strict mode: each position passing the quick
+// check on its 2 first bytes (~2 % of payload positions, and every real header)
+// walks its chain directly from global memory -- garbage chains die within a hop or
+// two, the true chain has chunk / frame-size hops.  A chain longer than kWalkHops
+// (frames of a few bytes) leaves the chunk to K1' (LDS pointer jumping).
 __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
-    __shared__ uint32_t words[kWords];
-    __shared__ uint64_t lk[kChunk];
     __shared__ unsigned long long set[kSet];
     __shared__ int overflow;
     const uint64_t chunk = blockIdx.x;
@@ -253,36 +312,57 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     const int tid = threadIdx.x;
     if (tid < kSet) set[tid] = ~0ull;
     if (tid == 0) overflow = 0;
-    load_chunk(a, B, words);
-    bool walk_failed = !a.strict;
-    if (a.strict) {
-        const int i0 = kPer * tid;
-        uint32_t w[kPer / 4 + 1];
+    __syncthreads();
+    // this thread's kPer positions and the 4 bytes after them
+    const uint64_t p0 = B + (uint64_t)kPer * tid;
+    uint32_t w[kPer / 4 + 1];
+    const Win x0 = window_global(a, p0);
+    const Win x1 = window_global(a, p0 + 16);
 #pragma unroll
-        for (int k = 0; k < kPer / 4 + 1; ++k) w[k] = words[i0 / 4 + k];
-        auto byte_at = [&](int j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
-        uint32_t cand = 0;
+    for (int k = 0; k < 4; ++k) w[k] = x0.d[k];
+    w[4] = x1.d[0];
+    auto byte_at = [&](int j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
+    uint32_t cand = 0;
 #pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const uint32_t first = byte_at(j), second = byte_at(j + 1), opcode = first & 0x0F;
-            const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
-            const bool reject = !(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80));
-            if (!reject && B + i0 + j >= a.start) cand |= 1u << j;
-        }
-        while (cand) {
-            const int j = __builtin_ctz(cand);
-            cand &= cand - 1;
-            const uint64_t v = walk_exit(a, B, words, B + i0 + j, kWalkHops);
-            if (v == 0) {
-                walk_failed = true;
-                break;
-            }
-            if (term_type(v) == kExit) set_insert(set, term_pos(v), &overflow);
-        }
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t first = byte_at(j), second = byte_at(j + 1), opcode = first & 0x0F;
+        const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
+        const bool reject = !(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80));
+        if (!reject && p0 + j >= a.start && p0 + j < a.len) cand |= 1u << j;
     }
-    if (__syncthreads_or(walk_failed)) {
-        // every position pointer-jumped to its chain's end in LDS (the exits found
-        // by the walks above are exits of real chains too: they stay in the set)
+    bool failed = false;
+    while (cand) {
+        const int j = __builtin_ctz(cand);
+        cand &= cand - 1;
+        const uint64_t v = walk_frames<false>(a, B, nullptr, p0 + j, kWalkHops, [](uint64_t, uint32_t, uint8_t) {});
+        if (v == 0) {
+            failed = true;
+            break;
+        }
+        if (term_type(v) == kExit) set_insert(set, term_pos(v), &overflow);
+    }
+    if (__syncthreads_or(failed)) {
+        if (tid == 0) a.slow[atomicAdd(&a.flags[2], 1u)] = (uint32_t)chunk;
+        return;
+    }
+    publish_exits(a, chunk, set, overflow, tid);
+}
+
+// K1': the chunks K1 left (tiny frames), or every chunk in non-strict mode (every
+// position a candidate): each position's chain pointer-jumped to its end in LDS.
+__global__ __launch_bounds__(kScanT) void scan_exits_lds(ScanArgs a, int all) {
+    __shared__ uint32_t words[kWords];
+    __shared__ uint64_t lk[kChunk];
+    __shared__ unsigned long long set[kSet];
+    __shared__ int overflow;
+    const int tid = threadIdx.x;
+    const uint64_t count = all ? a.nc + 1 : __hip_atomic_load(&a.flags[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint64_t q = blockIdx.x; q < count; q += gridDim.x) {
+        const uint64_t chunk = all ? q : a.slow[q];
+        const uint64_t B = chunk * kChunk;
+        if (tid < kSet) set[tid] = ~0ull;
+        if (tid == 0) overflow = 0;
+        load_chunk(a, B, words);
         chunk_links(a, B, words, lk);
         // dedup: a wave retires one distinct value per round (exits repeat a lot)
         for (int k = 0; k < kPer; ++k) {
@@ -296,70 +376,69 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
                 if ((tid & (kWave - 1)) == leader) set_insert(set, x0, &overflow);
             }
         }
-    }
-    __syncthreads();
-    auto append = [&](uint64_t x) {
-        const uint64_t t = x / kChunk;   // x <= len: t <= nc
-        const uint32_t slot = atomicAdd(&a.ccount[t], 1u);
-        if (slot < (uint32_t)kCand) a.cand[t * kCand + slot] = x;
-        else atomicOr(&a.flags[0], 1u);
-    };
-    // Strict mode prunes exits that cannot start a frame (2 header bytes fail the
-    // checks): payload bytes parsed as a chain land on random positions, and a
-    // random position passes with ~2 % odds, while the true chain always lands on
-    // a real header.  This keeps the candidate lists at about one entry per chunk.
-    if (tid < kSet && set[tid] != ~0ull && !quick_reject(a, set[tid])) append(set[tid]);
-    if (tid == 0) {
-        if (overflow) atomicOr(&a.flags[0], 1u);
-        if (a.start / kChunk == chunk) append(a.start);
+        __syncthreads();
+        publish_exits(a, chunk, set, overflow, tid);
+        __syncthreads();   // set / words reused by the next chunk
     }
 }
 
-// K2: for each candidate entry of the chunk, the candidate its chain exits to.
-__global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
+// node -> the candidate its chain exits to (or -1) and the terminal where it ends
+__device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint64_t x, uint64_t v) {
+    if (x == a.start) {
+        a.flags[1] = (uint32_t)node;
+        a.mark[node] = 1;
+    }
+    int32_t next = -1;
+    if (term_type(v) == kExit) {
+        const uint64_t y = term_pos(v), t = y / kChunk;
+        const uint32_t cnt = min(a.ccount[t], (uint32_t)kCand);
+        for (uint32_t i = 0; i < cnt; ++i)
+            if (a.cand[t * kCand + i] == y) next = (int32_t)(t * kCand + i);
+        // not a candidate: pruned by K1 (the chain dies at y), or its bucket overflowed
+        if (next < 0 && !quick_reject(a, y)) atomicOr(&a.flags[0], 1u);
+    }
+    a.link[node] = next;
+    a.nterm[node] = v;
+}
+
+// K2: one thread per node (candidate slot): the candidate entry's chain walked from
+// global memory to the candidate it exits to; a chain longer than kWalkHops goes
+// to K2' (LDS).  Unused slots hold stale values from earlier calls: dead ends.
+__global__ __launch_bounds__(256) void scan_links(ScanArgs a) {
+    const uint64_t node = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t chunk = node / kCand;
+    if (chunk > a.nc) return;
+    const uint32_t i = (uint32_t)(node % kCand);
+    if (i >= min(a.ccount[chunk], (uint32_t)kCand)) {
+        a.link[node] = -1;
+        return;
+    }
+    const uint64_t B = chunk * kChunk;
+    const uint64_t x = a.cand[node];
+    const uint64_t v = x - B < kChunk ? walk_frames<false>(a, B, nullptr, x, 2 * kWalkHops,
+                                                           [](uint64_t, uint32_t, uint8_t) {})
+                                      : term(kEnd, x);   // x == len on a chunk edge
+    if (v == 0) {
+        a.slow2[atomicAdd(&a.flags[3], 1u)] = (uint32_t)node;
+        return;
+    }
+    link_node(a, node, x, v);
+}
+
+// K2': the nodes K2 left: their chunk pointer-jumped in LDS.
+__global__ __launch_bounds__(kScanT) void scan_links_lds(ScanArgs a) {
     __shared__ uint32_t words[kWords];
     __shared__ uint64_t lk[kChunk];
-    __shared__ int long_chain;
-    const uint64_t chunk = blockIdx.x;
-    const uint64_t B = chunk * kChunk;
-    const uint32_t nc_here = min(a.ccount[chunk], (uint32_t)kCand);
-    const int tid = threadIdx.x;
-    // unused node slots hold stale values from earlier calls: make them dead ends
-    if (tid >= (int)nc_here && tid < kCand) a.link[chunk * kCand + tid] = -1;
-    if (nc_here == 0) return;   // uniform per block
-    if (tid == 0) long_chain = 0;
-    load_chunk(a, B, words);
-    // each candidate walks its chain directly (a few frames per chunk); only if a
-    // chain runs longer (tiny frames) does the block pointer-jump the whole chunk
-    uint64_t v = 0;
-    uint64_t x = 0;
-    if (tid < (int)nc_here) {
-        x = a.cand[chunk * kCand + tid];
-        v = x - B < kChunk ? walk_exit(a, B, words, x, 64) : term(kEnd, x);   // x == len on a chunk edge
-        if (v == 0) long_chain = 1;
-    }
-    __syncthreads();
-    if (long_chain) {
+    const uint64_t count = __hip_atomic_load(&a.flags[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint64_t q = blockIdx.x; q < count; q += gridDim.x) {
+        const uint64_t node = a.slow2[q], chunk = node / kCand, B = chunk * kChunk;
+        load_chunk(a, B, words);
         chunk_links(a, B, words, lk);
-        if (tid < (int)nc_here && v == 0) v = lk[x - B];
-    }
-    if (tid < (int)nc_here) {
-        const uint64_t node = chunk * kCand + tid;
-        if (x == a.start) {
-            a.flags[1] = (uint32_t)node;
-            a.mark[node] = 1;
+        if (threadIdx.x == 0) {
+            const uint64_t x = a.cand[node];
+            link_node(a, node, x, lk[x - B]);
         }
-        int32_t next = -1;
-        if (term_type(v) == kExit) {
-            const uint64_t y = term_pos(v), t = y / kChunk;
-            const uint32_t cnt = min(a.ccount[t], (uint32_t)kCand);
-            for (uint32_t i = 0; i < cnt; ++i)
-                if (a.cand[t * kCand + i] == y) next = (int32_t)(t * kCand + i);
-            // not a candidate: pruned by K1 (the chain dies at y), or its bucket overflowed
-            if (next < 0 && !quick_reject(a, y)) atomicOr(&a.flags[0], 1u);
-        }
-        a.link[node] = next;
-        a.nterm[node] = v;
+        __syncthreads();
     }
 }
 
@@ -387,24 +466,9 @@ __global__ void scan_lift(const int32_t* src, int32_t* dst, uint8_t* mark, uint6
     }
 }
 
-// Walk the true frames of a chunk from its entry e (in LDS bytes), calling emit
-// for each complete frame; returns the terminal where the walk left the chunk.
-template <typename F>
-__device__ uint64_t walk_chunk(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t e, F&& emit) {
-    uint64_t p = e;
-    const uint64_t Bend = B + kChunk;
-    while (p < Bend) {
-        uint32_t key;
-        uint8_t b0;
-        const uint64_t v = parse_at(a, p, window_at(words, (int)(p - B)), &key, &b0);
-        if (v & kTerm) return v;
-        emit(p, key, b0);
-        p = v;
-    }
-    return term(kExit, p);
-}
-
 __device__ __forceinline__ uint64_t cand_pos(const ScanArgs& a, int32_t node) { return a.cand[node]; }
+
+static constexpr int kEmitHops = 64;   // K4: frames walked from global memory before staging in LDS
 
 // K4: one wavefront per chunk.
 __global__ __launch_bounds__(64) void scan_emit(ScanArgs a) {
@@ -451,11 +515,21 @@ __global__ __launch_bounds__(64) void scan_emit(ScanArgs a) {
         for (uint32_t i = 0; i < cnt; ++i)
             if (a.mark[chunk * kCand + i]) entry = (int64_t)cand_pos(a, (int32_t)(chunk * kCand + i));
     }
+    // the chunk's frames walked from global memory (header bytes only); a chunk of
+    // very many frames is staged in LDS instead
     uint64_t count = 0;
     uint64_t stop = 0;
+    bool lds = false;
     if (entry >= 0) {
-        load_chunk(a, B, words);
-        if (lane == 0) stop = walk_chunk(a, B, words, (uint64_t)entry, [&](uint64_t, uint32_t, uint8_t) { ++count; });
+        if (lane == 0)
+            stop = walk_frames<false>(a, B, nullptr, (uint64_t)entry, kEmitHops, [&](uint64_t, uint32_t, uint8_t) { ++count; });
+        lds = __builtin_amdgcn_readfirstlane(stop == 0 ? 1 : 0) != 0;
+        if (lds) {
+            count = 0;
+            load_chunk(a, B, words);
+            if (lane == 0)
+                stop = walk_frames<true>(a, B, words, (uint64_t)entry, -1, [&](uint64_t, uint32_t, uint8_t) { ++count; });
+        }
     }
     // chained scan of the frame counts: lane 0 publishes, the wavefront looks back
     count = (uint64_t)__builtin_amdgcn_readfirstlane((int)count) |
@@ -471,14 +545,16 @@ __global__ __launch_bounds__(64) void scan_emit(ScanArgs a) {
         if (chunk == a.nc) a.result[0] = base + count;
         if (entry >= 0) {
             uint64_t k = base;
-            walk_chunk(a, B, words, (uint64_t)entry, [&](uint64_t p, uint32_t key, uint8_t b0) {
+            auto emit = [&](uint64_t p, uint32_t key, uint8_t b0) {
                 if (k < a.max_frames) {
                     a.hdr[k] = p;
                     a.keys[k] = key;
                     a.b0[k] = b0;
                 }
                 ++k;
-            });
+            };
+            if (lds) walk_frames<true>(a, B, words, (uint64_t)entry, -1, emit);
+            else walk_frames<false>(a, B, nullptr, (uint64_t)entry, -1, emit);
             // the chain ends in this chunk, or leaves it onto a header K1 pruned
             if (term_type(stop) == kExit && quick_reject(a, term_pos(stop))) stop = term(kDead, term_pos(stop));
             if (term_type(stop) != kExit) {
@@ -586,8 +662,8 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.max_frames = max_frames;
     a.result = result;
     // scratch layout, per (device, stream)
-    const uint64_t need = chunks * 4 + nodes * 8 + nodes * 4 + nodes * 8 + 2 * nodes * 4 + nodes + 16 +
-                          chunks * 8 + 64 * 9;   // + alignment padding of the 9 regions
+    const uint64_t need = chunks * 4 + 32 + nodes + nodes * 8 + nodes * 4 + nodes * 8 + 2 * nodes * 4 + chunks * 8 +
+                          chunks * 4 + nodes * 4 + 64 * 11;   // + alignment padding of the 11 regions
     static std::map<std::pair<int, hipStream_t>, ScanScratchSet> scratch;
     static std::mutex mu;
     int dev = 0;
@@ -595,6 +671,7 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     if (e != hipSuccess) return e;
     uint8_t* m;
     int32_t *jp, *jq;   // ping-pong doubling tables
+    uint64_t cleared = 0;
     {
         std::lock_guard<std::mutex> g(mu);
         ScanScratchSet& s = scratch[{dev, stream}];
@@ -612,15 +689,19 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         m = (uint8_t*)s.mem;
         auto align = [](uint64_t x) { return (x + 63) & ~63ull; };
         uint64_t o = 0;
+        // ccount, flags and mark first: one memset clears them per call
         a.ccount = (uint32_t*)(m + o); o = align(o + chunks * 4);
-        a.flags = (uint32_t*)(m + o); o = align(o + 16);
+        a.flags = (uint32_t*)(m + o); o = align(o + 32);
+        a.mark = m + o; o = align(o + nodes);
+        cleared = o;
         a.cand = (uint64_t*)(m + o); o = align(o + nodes * 8);
         a.link = (int32_t*)(m + o); o = align(o + nodes * 4);
         a.nterm = (uint64_t*)(m + o); o = align(o + nodes * 8);
         a.status = (uint64_t*)(m + o); o = align(o + chunks * 8);
         jp = (int32_t*)(m + o); o = align(o + nodes * 4);
         jq = (int32_t*)(m + o); o = align(o + nodes * 4);
-        a.mark = m + o;
+        a.slow = (uint32_t*)(m + o); o = align(o + chunks * 4);
+        a.slow2 = (uint32_t*)(m + o);
         if (s.epoch == 0) {   // epochs wrapped: clear the status words
             if ((e = hipMemsetAsync(a.status, 0, chunks * 8, stream)) != hipSuccess) return e;
             s.epoch = 1;
@@ -628,11 +709,16 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         a.epoch = s.epoch;
     }
     // counters + flags, and the default results (no frames, nothing consumed past start)
-    if ((e = hipMemsetAsync(a.ccount, 0, chunks * 4, stream)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(a.flags, 0, 16, stream)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(a.mark, 0, nodes, stream)) != hipSuccess) return e;
-    hipLaunchKernelGGL(scan_exits, dim3((unsigned)chunks), dim3(kScanT), 0, stream, a);
-    hipLaunchKernelGGL(scan_links, dim3((unsigned)chunks), dim3(kScanT), 0, stream, a);
+    if ((e = hipMemsetAsync(a.ccount, 0, cleared, stream)) != hipSuccess) return e;
+    const unsigned slow_grid = (unsigned)(chunks < 1024 ? chunks : 1024);
+    if (strict) {
+        hipLaunchKernelGGL(scan_exits, dim3((unsigned)chunks), dim3(kScanT), 0, stream, a);
+        hipLaunchKernelGGL(scan_exits_lds, dim3(slow_grid), dim3(kScanT), 0, stream, a, 0);
+    } else {
+        hipLaunchKernelGGL(scan_exits_lds, dim3(slow_grid), dim3(kScanT), 0, stream, a, 1);
+    }
+    hipLaunchKernelGGL(scan_links, dim3((unsigned)((nodes + 255) / 256)), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(scan_links_lds, dim3(slow_grid), dim3(kScanT), 0, stream, a);
     const unsigned lb = (unsigned)((nodes + 255) / 256);
     const int32_t* src = a.link;
     for (int k = 0; k < levels; ++k) {
