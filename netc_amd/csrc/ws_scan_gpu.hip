@@ -60,11 +60,14 @@ struct ScanArgs {
     uint32_t* ccount;      // nc + 1 candidate counters (zeroed per call)
     uint64_t* cand;        // (nc + 1) * kCand candidate positions
     int32_t* link;         // (nc + 1) * kCand: node -> next node, -1 = chain ends
-    uint64_t* nterm;       // (nc + 1) * kCand: the terminal where the chain ends (END / DEAD)
+    uint64_t* nterm;       // (nc + 1) * kCand: the terminal where the node's walk leaves its chunk
+    uint32_t* ncnt;        // (nc + 1) * kCand: frames on that walk (~0: not counted, K2')
     uint8_t* mark;         // (nc + 1) * kCand: node is on the chain from the stream start
-    uint32_t* flags;       // [0] overflow, [1] root node, [2] / [3] entries of slow / slow2
+    uint32_t* flags;       // [0] overflow, [1] root node, [2] / [3] / [4] entries of slow / slow2 / slow3
     uint32_t* slow;        // K1 chunks left to the LDS kernel (nc + 1)
     uint32_t* slow2;       // K2 nodes left to the LDS kernel ((nc + 1) * kCand)
+    uint32_t* slow3;       // K4 chunks of many frames left to the LDS emit kernel (nc + 1)
+    uint64_t* cbase;       // K4: index of each chunk's first frame (nc + 1)
     uint64_t* status;      // chained-scan status words (nc + 1)
     uint32_t epoch;
     uint64_t* hdr;         // outputs
@@ -208,6 +211,73 @@ __device__ void chunk_links(const ScanArgs& a, uint64_t B, const uint32_t* words
     }
 }
 
+// chunk_links plus, per position, the complete frames on its chain until the
+// terminal (hc).  Jumps are synchronous (read phase, barrier, write phase) so that
+// each link and its count stay a consistent pair.  Fallback kernels only.
+__device__ void chunk_links_counted(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t* lk,
+                                    uint16_t* hc) {
+    const int tid = threadIdx.x;
+    const uint64_t Bend = B + kChunk;
+    // a position that cannot start a header ends its chain right there (exact
+    // terminals: K4 reports where the chain ends): END past the stream, else DEAD
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint64_t pos = B + (uint64_t)(k * kScanT + tid);
+        lk[k * kScanT + tid] = pos + 2 > a.len ? term(kEnd, pos) : term(kDead, pos);
+        hc[k * kScanT + tid] = 0;
+    }
+    const int i0 = kPer * tid;
+    uint32_t w[kPer / 4 + 1];
+#pragma unroll
+    for (int k = 0; k < kPer / 4 + 1; ++k) w[k] = words[i0 / 4 + k];
+    auto byte_at = [&](int j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
+    uint32_t cand = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t first = byte_at(j), second = byte_at(j + 1), opcode = first & 0x0F;
+        const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
+        const bool reject = a.strict && (!(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80)));
+        if (!reject && B + i0 + j >= a.start) cand |= 1u << j;
+    }
+    __syncthreads();
+    while (cand) {
+        const int j = __builtin_ctz(cand);
+        cand &= cand - 1;
+        const int i = i0 + j;
+        uint64_t v = parse_at(a, B + i, window_at(words, i), nullptr, nullptr);
+        if (!(v & kTerm)) {
+            v = v < Bend ? v - B : term(kExit, v);
+            hc[i] = 1;
+        }
+        lk[i] = v;
+    }
+    __syncthreads();
+    for (;;) {
+        uint64_t nv[kPer];
+        uint16_t nh[kPer];
+        int changed = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int i = k * kScanT + tid;
+            const uint64_t v = lk[i];
+            nv[k] = v;
+            nh[k] = hc[i];
+            if (!(v & kTerm)) {
+                nv[k] = lk[v];
+                nh[k] = (uint16_t)(hc[i] + hc[v]);
+                changed |= !(nv[k] & kTerm);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            lk[k * kScanT + tid] = nv[k];
+            hc[k * kScanT + tid] = nh[k];
+        }
+        if (!__syncthreads_or(changed)) break;
+    }
+}
+
 // Walk one chain from x inside the chunk for at most `hops` frames: its terminal,
 // or 0 if the hop budget ran out.
 __device__ uint64_t walk_exit(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t x, int hops) {
@@ -305,6 +375,7 @@ __device__ __forceinline__ void publish_exits(const ScanArgs& a, uint64_t chunk,
 // two, the true chain has chunk / frame-size hops.  A chain longer than kWalkHops
 // (frames of a few bytes) leaves the chunk to K1' (LDS pointer jumping).
 __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
+    __shared__ uint32_t words[kWords];
     __shared__ unsigned long long set[kSet];
     __shared__ int overflow;
     const uint64_t chunk = blockIdx.x;
@@ -312,15 +383,12 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     const int tid = threadIdx.x;
     if (tid < kSet) set[tid] = ~0ull;
     if (tid == 0) overflow = 0;
-    __syncthreads();
+    load_chunk(a, B, words);   // 4 KiB in LDS: the walks' hops are LDS reads
     // this thread's kPer positions and the 4 bytes after them
     const uint64_t p0 = B + (uint64_t)kPer * tid;
     uint32_t w[kPer / 4 + 1];
-    const Win x0 = window_global(a, p0);
-    const Win x1 = window_global(a, p0 + 16);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) w[k] = x0.d[k];
-    w[4] = x1.d[0];
+    for (int k = 0; k < kPer / 4 + 1; ++k) w[k] = words[kPer / 4 * tid + k];
     auto byte_at = [&](int j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
     uint32_t cand = 0;
 #pragma unroll
@@ -334,7 +402,7 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     while (cand) {
         const int j = __builtin_ctz(cand);
         cand &= cand - 1;
-        const uint64_t v = walk_frames<false>(a, B, nullptr, p0 + j, kWalkHops, [](uint64_t, uint32_t, uint8_t) {});
+        const uint64_t v = walk_frames<true>(a, B, words, p0 + j, kWalkHops, [](uint64_t, uint32_t, uint8_t) {});
         if (v == 0) {
             failed = true;
             break;
@@ -383,7 +451,7 @@ __global__ __launch_bounds__(kScanT) void scan_exits_lds(ScanArgs a, int all) {
 }
 
 // node -> the candidate its chain exits to (or -1) and the terminal where it ends
-__device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint64_t x, uint64_t v) {
+__device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint64_t x, uint64_t v, uint32_t cnt) {
     if (x == a.start) {
         a.flags[1] = (uint32_t)node;
         a.mark[node] = 1;
@@ -399,6 +467,7 @@ __device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint
     }
     a.link[node] = next;
     a.nterm[node] = v;
+    a.ncnt[node] = cnt;
 }
 
 // K2: one thread per node (candidate slot): the candidate entry's chain walked from
@@ -415,28 +484,30 @@ __global__ __launch_bounds__(256) void scan_links(ScanArgs a) {
     }
     const uint64_t B = chunk * kChunk;
     const uint64_t x = a.cand[node];
+    uint32_t cnt = 0;   // K4 takes the frame count of the true entry's walk from here
     const uint64_t v = x - B < kChunk ? walk_frames<false>(a, B, nullptr, x, 2 * kWalkHops,
-                                                           [](uint64_t, uint32_t, uint8_t) {})
+                                                           [&](uint64_t, uint32_t, uint8_t) { ++cnt; })
                                       : term(kEnd, x);   // x == len on a chunk edge
     if (v == 0) {
         a.slow2[atomicAdd(&a.flags[3], 1u)] = (uint32_t)node;
         return;
     }
-    link_node(a, node, x, v);
+    link_node(a, node, x, v, cnt);
 }
 
 // K2': the nodes K2 left: their chunk pointer-jumped in LDS.
 __global__ __launch_bounds__(kScanT) void scan_links_lds(ScanArgs a) {
     __shared__ uint32_t words[kWords];
     __shared__ uint64_t lk[kChunk];
+    __shared__ uint16_t hc[kChunk];
     const uint64_t count = __hip_atomic_load(&a.flags[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (uint64_t q = blockIdx.x; q < count; q += gridDim.x) {
         const uint64_t node = a.slow2[q], chunk = node / kCand, B = chunk * kChunk;
         load_chunk(a, B, words);
-        chunk_links(a, B, words, lk);
+        chunk_links_counted(a, B, words, lk, hc);
         if (threadIdx.x == 0) {
             const uint64_t x = a.cand[node];
-            link_node(a, node, x, lk[x - B]);
+            link_node(a, node, x, lk[x - B], hc[x - B]);
         }
         __syncthreads();
     }
@@ -468,27 +539,56 @@ __global__ void scan_lift(const int32_t* src, int32_t* dst, uint8_t* mark, uint6
 
 __device__ __forceinline__ uint64_t cand_pos(const ScanArgs& a, int32_t node) { return a.cand[node]; }
 
-static constexpr int kEmitHops = 64;   // K4: frames walked from global memory before staging in LDS
+static constexpr int kEmitHops = 64;   // K4: a chunk of more frames is emitted from LDS
 
-// K4: one wavefront per chunk.
-__global__ __launch_bounds__(64) void scan_emit(ScanArgs a) {
-    __shared__ uint32_t words[kWords];
-    const uint64_t chunk = blockIdx.x;
-    const uint64_t B = chunk * kChunk;
-    const int lane = threadIdx.x;
-    const bool overflow = __hip_atomic_load(&a.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-    if (overflow) {
-        // serial fallback: wavefront 0 walks the whole stream from global memory
-        if (chunk != 0) return;
-        if (lane == 0) {
+// the marked (true) entry of a chunk: its node, or -1
+__device__ __forceinline__ int64_t chunk_entry(const ScanArgs& a, uint64_t chunk) {
+    int64_t enode = -1;
+    const uint32_t cnt = min(a.ccount[chunk], (uint32_t)kCand);
+    for (uint32_t i = 0; i < cnt; ++i)
+        if (a.mark[chunk * kCand + i]) enode = (int64_t)(chunk * kCand + i);
+    return enode;
+}
+
+// exclusive prefix sum over a 256-thread block; the block total in *total
+__device__ uint64_t block_scan256(uint64_t v, uint64_t* total) {
+    __shared__ uint64_t wsum[4];
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    uint64_t inc = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint64_t o = (uint64_t)__shfl_up((unsigned long long)inc, d, kWave);
+        if (lane >= d) inc += o;
+    }
+    if (lane == kWave - 1) wsum[w] = inc;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        before += i < w ? wsum[i] : 0;
+        all += wsum[i];
+    }
+    __syncthreads();
+    *total = all;
+    return before + inc - v;
+}
+
+// K4a: one thread per chunk.  The chain's frames in the chunk are the frames K2
+// counted on its marked entry's walk; a chained scan over tiles of 256 chunks
+// (decoupled look-back) gives each chunk's first frame index.  The chunk where
+// the chain ends sets the results.  On candidate overflow, one thread walks the
+// whole stream instead (serial fallback).
+__global__ __launch_bounds__(256) void scan_count(ScanArgs a) {
+    __shared__ uint64_t tile_prefix;
+    const uint64_t tile = blockIdx.x;
+    const uint64_t chunk = tile * 256 + threadIdx.x;
+    if (__hip_atomic_load(&a.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+        if (tile == 0 && threadIdx.x == 0) {
             uint64_t p = a.start, n = 0, err = ~0ull;
             for (;;) {
-                uint8_t hb[14];
-#pragma unroll
-                for (int j = 0; j < 14; ++j) hb[j] = p + j < a.len ? a.wire[p + j] : 0;
                 uint32_t key;
                 uint8_t b0;
-                const uint64_t v = parse_at(a, p, hb, &key, &b0);
+                const uint64_t v = parse_at(a, p, window_global(a, p), &key, &b0);
                 if (v & kTerm) {
                     if (term_type(v) == kDead) err = p;
                     break;
@@ -508,62 +608,84 @@ __global__ __launch_bounds__(64) void scan_emit(ScanArgs a) {
         }
         return;
     }
-    // the true entry of this chunk: its candidate node on the chain (at most one)
-    int64_t entry = -1;
-    {
-        const uint32_t cnt = min(a.ccount[chunk], (uint32_t)kCand);
-        for (uint32_t i = 0; i < cnt; ++i)
-            if (a.mark[chunk * kCand + i]) entry = (int64_t)cand_pos(a, (int32_t)(chunk * kCand + i));
-    }
-    // the chunk's frames walked from global memory (header bytes only); a chunk of
-    // very many frames is staged in LDS instead
-    uint64_t count = 0;
-    uint64_t stop = 0;
-    bool lds = false;
-    if (entry >= 0) {
+    const int64_t enode = chunk <= a.nc ? chunk_entry(a, chunk) : -1;
+    const uint64_t count = enode >= 0 ? a.ncnt[enode] : 0;
+    uint64_t agg;
+    const uint64_t ex = block_scan256(count, &agg);
+    if (threadIdx.x < kWave) {
+        const int lane = threadIdx.x;
         if (lane == 0)
-            stop = walk_frames<false>(a, B, nullptr, (uint64_t)entry, kEmitHops, [&](uint64_t, uint32_t, uint8_t) { ++count; });
-        lds = __builtin_amdgcn_readfirstlane(stop == 0 ? 1 : 0) != 0;
-        if (lds) {
-            count = 0;
-            load_chunk(a, B, words);
-            if (lane == 0)
-                stop = walk_frames<true>(a, B, words, (uint64_t)entry, -1, [&](uint64_t, uint32_t, uint8_t) { ++count; });
+            __hip_atomic_store(&a.status[tile], status_word(tile == 0 ? 2 : 1, a.epoch, agg), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t prefix = tile == 0 ? 0 : look_back(a.status, (int64_t)tile, a.epoch, lane);
+        if (lane == 0) {
+            if (tile)
+                __hip_atomic_store(&a.status[tile], status_word(2, a.epoch, prefix + agg), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            tile_prefix = prefix;
         }
     }
-    // chained scan of the frame counts: lane 0 publishes, the wavefront looks back
-    count = (uint64_t)__builtin_amdgcn_readfirstlane((int)count) |
-            ((uint64_t)__builtin_amdgcn_readfirstlane((int)(count >> 32)) << 32);
-    if (lane == 0)
-        __hip_atomic_store(&a.status[chunk], status_word(chunk == 0 ? 2 : 1, a.epoch, count), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t base = chunk == 0 ? 0 : look_back(a.status, (int64_t)chunk, a.epoch, lane);
-    if (lane == 0) {
-        if (chunk)
-            __hip_atomic_store(&a.status[chunk], status_word(2, a.epoch, base + count), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        if (chunk == a.nc) a.result[0] = base + count;
-        if (entry >= 0) {
-            uint64_t k = base;
-            auto emit = [&](uint64_t p, uint32_t key, uint8_t b0) {
-                if (k < a.max_frames) {
-                    a.hdr[k] = p;
-                    a.keys[k] = key;
-                    a.b0[k] = b0;
-                }
-                ++k;
-            };
-            if (lds) walk_frames<true>(a, B, words, (uint64_t)entry, -1, emit);
-            else walk_frames<false>(a, B, nullptr, (uint64_t)entry, -1, emit);
-            // the chain ends in this chunk, or leaves it onto a header K1 pruned
-            if (term_type(stop) == kExit && quick_reject(a, term_pos(stop))) stop = term(kDead, term_pos(stop));
-            if (term_type(stop) != kExit) {
-                const uint64_t end = term_pos(stop);
-                a.result[1] = end;
-                a.result[2] = term_type(stop) == kDead ? end : ~0ull;
-                if (k <= a.max_frames) a.hdr[k] = end;
-            }
+    __syncthreads();
+    if (chunk > a.nc) return;
+    const uint64_t base = tile_prefix + ex;
+    a.cbase[chunk] = base;
+    if (chunk == a.nc) a.result[0] = base + count;
+    if (enode < 0) return;
+    // the chain ends in this chunk, or leaves it onto a header K1 pruned
+    uint64_t stop = a.nterm[enode];
+    if (term_type(stop) == kExit && quick_reject(a, term_pos(stop))) stop = term(kDead, term_pos(stop));
+    if (term_type(stop) != kExit) {
+        const uint64_t end = term_pos(stop), k = base + count;
+        a.result[1] = end;
+        a.result[2] = term_type(stop) == kDead ? end : ~0ull;
+        if (k <= a.max_frames) a.hdr[k] = end;
+    }
+}
+
+// K4b: one thread per chunk walks the chunk's frames from global memory (header
+// bytes only) and writes their descriptors from the chunk's first index on; a
+// chunk of more than kEmitHops frames goes to K4b' (LDS).
+__global__ __launch_bounds__(256) void scan_emit(ScanArgs a) {
+    const uint64_t chunk = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (chunk > a.nc) return;
+    if (__hip_atomic_load(&a.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+    const int64_t enode = chunk_entry(a, chunk);
+    if (enode < 0) return;
+    if (a.ncnt[enode] > (uint32_t)kEmitHops) {
+        a.slow3[atomicAdd(&a.flags[4], 1u)] = (uint32_t)chunk;
+        return;
+    }
+    uint64_t k = a.cbase[chunk];
+    walk_frames<false>(a, chunk * kChunk, nullptr, a.cand[enode], -1, [&](uint64_t p, uint32_t key, uint8_t b0) {
+        if (k < a.max_frames) {
+            a.hdr[k] = p;
+            a.keys[k] = key;
+            a.b0[k] = b0;
         }
+        ++k;
+    });
+}
+
+// K4b': the chunks of many (tiny) frames, walked in LDS.
+__global__ __launch_bounds__(kScanT) void scan_emit_lds(ScanArgs a) {
+    __shared__ uint32_t words[kWords];
+    const uint64_t count = __hip_atomic_load(&a.flags[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint64_t q = blockIdx.x; q < count; q += gridDim.x) {
+        const uint64_t chunk = a.slow3[q], B = chunk * kChunk;
+        load_chunk(a, B, words);
+        if (threadIdx.x == 0) {
+            uint64_t k = a.cbase[chunk];
+            walk_frames<true>(a, B, words, a.cand[chunk_entry(a, chunk)], -1,
+                              [&](uint64_t p, uint32_t key, uint8_t b0) {
+                                  if (k < a.max_frames) {
+                                      a.hdr[k] = p;
+                                      a.keys[k] = key;
+                                      a.b0[k] = b0;
+                                  }
+                                  ++k;
+                              });
+        }
+        __syncthreads();
     }
 }
 
@@ -663,7 +785,8 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.result = result;
     // scratch layout, per (device, stream)
     const uint64_t need = chunks * 4 + 32 + nodes + nodes * 8 + nodes * 4 + nodes * 8 + 2 * nodes * 4 + chunks * 8 +
-                          chunks * 4 + nodes * 4 + 64 * 11;   // + alignment padding of the 11 regions
+                          chunks * 4 + nodes * 4 + nodes * 4 + chunks * 4 + chunks * 8 +
+                          64 * 14;   // + alignment padding of the 14 regions
     static std::map<std::pair<int, hipStream_t>, ScanScratchSet> scratch;
     static std::mutex mu;
     int dev = 0;
@@ -697,11 +820,14 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         a.cand = (uint64_t*)(m + o); o = align(o + nodes * 8);
         a.link = (int32_t*)(m + o); o = align(o + nodes * 4);
         a.nterm = (uint64_t*)(m + o); o = align(o + nodes * 8);
+        a.ncnt = (uint32_t*)(m + o); o = align(o + nodes * 4);
         a.status = (uint64_t*)(m + o); o = align(o + chunks * 8);
         jp = (int32_t*)(m + o); o = align(o + nodes * 4);
         jq = (int32_t*)(m + o); o = align(o + nodes * 4);
         a.slow = (uint32_t*)(m + o); o = align(o + chunks * 4);
-        a.slow2 = (uint32_t*)(m + o);
+        a.slow2 = (uint32_t*)(m + o); o = align(o + nodes * 4);
+        a.slow3 = (uint32_t*)(m + o); o = align(o + chunks * 4);
+        a.cbase = (uint64_t*)(m + o);
         if (s.epoch == 0) {   // epochs wrapped: clear the status words
             if ((e = hipMemsetAsync(a.status, 0, chunks * 8, stream)) != hipSuccess) return e;
             s.epoch = 1;
@@ -726,7 +852,10 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         hipLaunchKernelGGL(scan_lift, dim3(lb), dim3(256), 0, stream, src, dst, a.mark, nodes);
         src = dst;
     }
-    hipLaunchKernelGGL(scan_emit, dim3((unsigned)chunks), dim3(64), 0, stream, a);
+    const unsigned cb = (unsigned)((chunks + 255) / 256);
+    hipLaunchKernelGGL(scan_count, dim3(cb), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(scan_emit, dim3(cb), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(scan_emit_lds, dim3(slow_grid), dim3(kScanT), 0, stream, a);
     return hipGetLastError();
 }
 
