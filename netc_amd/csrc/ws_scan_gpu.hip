@@ -332,6 +332,18 @@ __device__ uint64_t walk_frames(const ScanArgs& a, uint64_t B, const uint32_t* w
     }
 }
 
+// The strict quick check for 4 positions at once: x = bytes 0 of positions 0..3,
+// y = their bytes 1.  Bit 7 of a byte of the result is set when that position can
+// start a client frame: MASK set, RSV clear, opcode 0/1/2/8/9/A, FIN on a control
+// frame (the checks of quick_reject, SWAR).
+__device__ __forceinline__ uint32_t quick_ok4(uint32_t x, uint32_t y) {
+    const uint32_t H = 0x80808080u;
+    const uint32_t rsv_ok = ~((x & 0x70707070u) + 0x70707070u) & H;   // bits 4-6 clear
+    const uint32_t op_ok = ~((x << 5) | ((x << 7) & (x << 6))) & H;    // opcode & 7 in {0, 1, 2}
+    const uint32_t ctl_bad = (x << 4) & ~x & H;                        // opcode >= 8 without FIN
+    return y & rsv_ok & op_ok & ~ctl_bad & H;
+}
+
 // x into the chunk's LDS set of distinct exits (open addressing); *overflow when full
 __device__ __forceinline__ void set_insert(unsigned long long* set, uint64_t x, int* overflow) {
     uint32_t h = (uint32_t)((x * 0x9E3779B97F4A7C15ull) >> 58);
@@ -389,15 +401,17 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     uint32_t w[kPer / 4 + 1];
 #pragma unroll
     for (int k = 0; k < kPer / 4 + 1; ++k) w[k] = words[kPer / 4 * tid + k];
-    auto byte_at = [&](int j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
+    // the quick check four positions at a time (bit 7 of each byte: position passes)
     uint32_t cand = 0;
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const uint32_t first = byte_at(j), second = byte_at(j + 1), opcode = first & 0x0F;
-        const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
-        const bool reject = !(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80));
-        if (!reject && p0 + j >= a.start && p0 + j < a.len) cand |= 1u << j;
+    for (int k = 0; k < kPer / 4; ++k) {
+        const uint32_t m = quick_ok4(w[k], __builtin_amdgcn_alignbyte(w[k + 1], w[k], 1));
+        const uint32_t b = (m >> 7) & 0x01010101u;
+        cand |= ((b | b >> 7 | b >> 14 | b >> 21) & 0xFu) << (4 * k);
     }
+    // positions before the stream start or past its end are not candidates
+    if (p0 < a.start) cand &= a.start - p0 >= (uint64_t)kPer ? 0u : ~0u << (a.start - p0);
+    if (p0 + kPer > a.len) cand &= p0 >= a.len ? 0u : (1u << (a.len - p0)) - 1;
     bool failed = false;
     while (cand) {
         const int j = __builtin_ctz(cand);
@@ -513,28 +527,27 @@ __global__ __launch_bounds__(kScanT) void scan_links_lds(ScanArgs a) {
     }
 }
 
-// K3, pass k: src = J (the 4^k-th successor; J = link in pass 0).  Builds J^4 into
-// dst (unless last) and marks the J, J^2 and J^3 successors of every marked node:
-// after pass k every node within 4^(k+1) - 1 steps of the start is marked (a node
-// d steps away is 0..3 J-steps past a node marked before the pass), so after
-// ceil(log4(chunks)) passes exactly the chain's nodes are (one per chunk it
-// enters).  Marks set during a pass may be followed in the same pass: they are on
-// the chain too.
+// K3, pass k: src = J (the 8^k-th successor; J = link in pass 0).  Builds J^8 into
+// dst (unless last) and marks the J .. J^7 successors of every marked node: after
+// pass k every node within 8^(k+1) - 1 steps of the start is marked (a node d
+// steps away is 0..7 J-steps past a node marked before the pass), so after
+// ceil(log8(chunks)) passes exactly the chain's nodes are (one per chunk it
+// enters).  The passes are launch-bound, hence 3 doubling levels each.  Marks set
+// during a pass may be followed in the same pass: they are on the chain too.
 __global__ void scan_lift(const int32_t* src, int32_t* dst, uint8_t* mark, uint64_t nodes) {
     const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= nodes) return;
     auto step = [&](int32_t u) -> int32_t {   // (range check: defence in depth)
         return (u >= 0 && (uint64_t)u < nodes) ? src[u] : -1;
     };
-    int32_t u1 = src[v];
-    if (u1 >= 0 && (uint64_t)u1 >= nodes) u1 = -1;
-    const int32_t u2 = step(u1), u3 = step(u2);
-    if (dst) dst[v] = step(u3);
-    if (mark[v]) {
-        if (u1 >= 0) mark[u1] = 1;
-        if (u2 >= 0 && (uint64_t)u2 < nodes) mark[u2] = 1;
-        if (u3 >= 0 && (uint64_t)u3 < nodes) mark[u3] = 1;
+    const bool marked = mark[v] != 0;
+    int32_t u = step((int32_t)v);
+#pragma unroll
+    for (int h = 1; h < 8; ++h) {   // u = J^h(v)
+        if (marked && u >= 0 && (uint64_t)u < nodes) mark[u] = 1;
+        u = step(u);
     }
+    if (dst) dst[v] = u;   // J^8(v)
 }
 
 __device__ __forceinline__ uint64_t cand_pos(const ScanArgs& a, int32_t node) { return a.cand[node]; }
@@ -776,8 +789,8 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.strict = strict ? 1 : 0;
     a.nc = (len + kChunk - 1) / kChunk;   // real chunks 0 .. nc-1; chunk nc is virtual (positions >= len)
     const uint64_t chunks = a.nc + 1, nodes = chunks * kCand;
-    int levels = 1;   // lifting passes: 4^levels - 1 >= chunks steps along the chain
-    while ((1ull << (2 * levels)) < chunks + 1) ++levels;
+    int levels = 1;   // lifting passes: 8^levels - 1 >= chunks steps along the chain
+    while ((1ull << (3 * levels)) < chunks + 1) ++levels;
     a.hdr = hdr;
     a.keys = keys;
     a.b0 = b0;
