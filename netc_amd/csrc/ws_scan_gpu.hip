@@ -141,6 +141,35 @@ __device__ __forceinline__ Win window_at(const uint32_t* words, int i) {
     return x;
 }
 
+// parse_at for a 16-byte window (every caller but the serial fallback): the same
+// checks in the same order, computed without branches -- lanes of a wavefront parse
+// different headers, and the branchy form cost about one scalar (exec-mask)
+// instruction per vector instruction.  Window bytes past len are zero.
+__device__ __forceinline__ uint64_t parse_at(const ScanArgs& a, uint64_t p, const Win& w, uint32_t* key_out,
+                                             uint8_t* b0_out) {
+    const uint32_t first = w.d[0] & 0xFF, second = (w.d[0] >> 8) & 0xFF;
+    const uint32_t code = second & 0x7F, mask = second >> 7, opcode = first & 0x0F;
+    const uint64_t ext = code == 126 ? 2 : (code == 127 ? 8 : 0);
+    const uint32_t b25 = __builtin_amdgcn_alignbyte(w.d[1], w.d[0], 2);   // bytes 2..5
+    const uint32_t b69 = __builtin_amdgcn_alignbyte(w.d[2], w.d[1], 2);   // bytes 6..9
+    const uint64_t len16 = __builtin_bswap32(b25) >> 16;
+    const uint64_t len64 = __builtin_bswap64((uint64_t)b69 << 32 | b25);
+    const uint64_t plen = ext == 0 ? code : (ext == 2 ? len16 : len64);
+    const uint64_t hl = 2 + ext + (mask ? 4 : 0);
+    const bool hdr_short = p + 2 + ext > a.len;
+    const bool reserved = (opcode >= 3) & ((opcode <= 7) | (opcode >= 11));
+    const bool control = opcode >= 8;
+    const bool dead = (a.strict != 0) & ((mask == 0) | ((first & 0x70) != 0) | reserved |
+                                         (control & (((first & 0x80) == 0) | (plen > 125))) | ((plen >> 63) != 0));
+    const bool pay_short = (p + hl > a.len) | (plen > a.len - (p + hl));
+    if (key_out) {
+        const uint32_t k = ext == 0 ? b25 : (ext == 2 ? w.d[1] : __builtin_amdgcn_alignbyte(w.d[3], w.d[2], 2));
+        *key_out = mask ? k : 0u;
+        *b0_out = (uint8_t)first;
+    }
+    return hdr_short ? term(kEnd, p) : (dead ? term(kDead, p) : (pay_short ? term(kEnd, p) : p + hl + plen));
+}
+
 // LDS copy of the chunk: stream bytes [B, B + kChunk + 32), zero past len.
 static constexpr int kWords = (int)((kChunk + 32) / 4);
 
@@ -412,16 +441,38 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     // positions before the stream start or past its end are not candidates
     if (p0 < a.start) cand &= a.start - p0 >= (uint64_t)kPer ? 0u : ~0u << (a.start - p0);
     if (p0 + kPer > a.len) cand &= p0 >= a.len ? 0u : (1u << (a.len - p0)) - 1;
-    bool failed = false;
-    while (cand) {
-        const int j = __builtin_ctz(cand);
-        cand &= cand - 1;
-        const uint64_t v = walk_frames<true>(a, B, words, p0 + j, kWalkHops, [](uint64_t, uint32_t, uint8_t) {});
-        if (v == 0) {
-            failed = true;
-            break;
+    // every candidate's chain walked to where it leaves the chunk, one hop per trip
+    // for every lane: a lane whose walk ends takes its next candidate, so a trip
+    // never waits on another lane's longer walk of an earlier candidate
+    bool failed = false, active = false;
+    uint64_t p = 0;
+    int hop = 0;
+    const uint64_t Bend = B + kChunk;
+    for (;;) {
+        if (!active && cand) {
+            p = p0 + __builtin_ctz(cand);
+            cand &= cand - 1;
+            hop = 0;
+            active = true;
         }
-        if (term_type(v) == kExit) set_insert(set, term_pos(v), &overflow);
+        if (!__ballot(active)) break;
+        if (active) {
+            if (p >= Bend) {   // leaves the chunk: an exit
+                set_insert(set, p, &overflow);
+                active = false;
+            } else if (hop == kWalkHops) {   // frames of a few bytes: K1'
+                failed = true;
+                active = false;
+                cand = 0;
+            } else {
+                const uint64_t v = parse_at(a, p, window_at(words, (int)(p - B)), nullptr, nullptr);
+                if (v & kTerm) active = false;   // END / DEAD inside the chunk
+                else {
+                    p = v;
+                    ++hop;
+                }
+            }
+        }
     }
     if (__syncthreads_or(failed)) {
         if (tid == 0) a.slow[atomicAdd(&a.flags[2], 1u)] = (uint32_t)chunk;
