@@ -376,20 +376,22 @@ __device__ u32x4 compose_vec(const EncArgs& a, EncTable& t, int l0, uint64_t A0,
 // [off[k], off[k+1])), so the wire is the source with the headers inserted.  For a
 // lane's wire vector at W, take the frame l holding W (header start S <= W < next
 // header start Sn): one unaligned 16-B load at s = W + (off[l] - pw_l) (pw = wire
-// payload start) gives byte i = the payload byte of frame l at wire W + i, and for
-// the next frame (whose header starts at cut c = Sn - W < 16) byte i - hl_n.  So a
-// vector is the load XOR frame l's key, with at most two header insertions (frame
-// l's, if W is inside it, and frame l+1's at the cut) and the tail after the cut
-// shifted up by the next header's length -- the last two only in the lane or two a
-// header touches.  A span takes this path when every frame ending inside it has at
-// least 16 wire bytes (one cut per vector) and every load stays inside the payload
-// buffer; any other span is queued for the compose kernel.
+// payload start) XOR frame l's key rotated to W gives every byte of the vector that
+// is payload of frame l.  The others -- frame l's header bytes when W is inside it,
+// and everything from the next header start on -- are at most a header plus 15
+// bytes per frame, and fix_frame (one thread per frame, in the queued launch)
+// rewrites exactly those.  So the vector path has no per-lane header work: the
+// previous form inserted the header and shifted the tail in the lane a header
+// touched, with a wave-wide branch costing about 200 vector instructions per span at
+// 1 KiB frames.  A span takes this path when the 64-entry table covers it and every
+// load stays inside the payload buffer; any other span is queued for the compose
+// kernel.
 
 // per-lane frame data from the table (ds_bpermute: every lane of the wave executes it)
 struct LaneFrames {
-    uint64_t S, Sn;         // wire header starts of frames l and l + 1 (W coordinates)
-    uint64_t P, Pn, Pnn;    // payload offsets of frames l, l + 1, l + 2
-    uint32_t K, Kn, B, Bn;  // keys and header bytes of frames l and l + 1
+    uint64_t S;       // wire header start of frame l (W coordinates)
+    uint64_t P, Pn;   // payload offsets of frames l, l + 1
+    uint32_t K;       // key of frame l
 };
 
 __device__ __forceinline__ uint32_t bperm32(uint32_t x, int src) {
@@ -399,37 +401,25 @@ __device__ __forceinline__ uint32_t bperm32(uint32_t x, int src) {
 __device__ __forceinline__ LaneFrames lane_frames(const EncTable& t, int l) {
     LaneFrames f;
     f.S = bperm64(t.start, l);
-    f.Sn = bperm64(t.start, l + 1);
     f.P = bperm64(t.poff, l);
     f.Pn = bperm64(t.poff, l + 1);
-    f.Pnn = bperm64(t.poff, l + 2);
     f.K = bperm32(t.key, l);
-    f.Kn = bperm32(t.key, l + 1);
-    f.B = bperm32(t.b0, l);
-    f.Bn = bperm32(t.b0, l + 1);
     return f;
 }
 
-// The same for a span holding at most one frame start (nb <= 1): entries l0 .. l0 + 3
+// The same for a span holding at most one frame start (nb <= 1): entries l0 .. l0 + 2
 // read once for the wave (readlane), each lane picks frame l0 or l0 + 1.
 __device__ __forceinline__ LaneFrames frames_near(const EncTable& t, int l0, int nb, uint64_t W, int l) {
     if (nb > 1) return lane_frames(t, l);
-    const uint64_t S0 = readlane64(t.start, l0), S1 = readlane64(t.start, l0 + 1), S2 = readlane64(t.start, l0 + 2);
+    const uint64_t S0 = readlane64(t.start, l0), S1 = readlane64(t.start, l0 + 1);
     const uint64_t P0 = readlane64(t.poff, l0), P1 = readlane64(t.poff, l0 + 1), P2 = readlane64(t.poff, l0 + 2);
-    const uint64_t P3 = readlane64(t.poff, l0 + 3 < kWave ? l0 + 3 : kWave - 1);
-    const uint32_t K0 = readlane32(t.key, l0), K1 = readlane32(t.key, l0 + 1), K2 = readlane32(t.key, l0 + 2);
-    const uint32_t B0 = readlane32(t.b0, l0), B1 = readlane32(t.b0, l0 + 1), B2 = readlane32(t.b0, l0 + 2);
+    const uint32_t K0 = readlane32(t.key, l0), K1 = readlane32(t.key, l0 + 1);
     const bool in1 = nb == 1 && W >= S1;
     LaneFrames f;
     f.S = in1 ? S1 : S0;
-    f.Sn = in1 ? S2 : S1;
     f.P = in1 ? P1 : P0;
     f.Pn = in1 ? P2 : P1;
-    f.Pnn = in1 ? P3 : P2;
     f.K = in1 ? K1 : K0;
-    f.Kn = in1 ? K2 : K1;
-    f.B = in1 ? B1 : B0;
-    f.Bn = in1 ? B2 : B1;
     return f;
 }
 
@@ -439,13 +429,11 @@ __device__ __forceinline__ uint64_t header_len(uint64_t len, bool masked) {
 
 enum : int { kSpanFast = 0, kSpanQueued = 2, kSpanNone = 3 };
 
-// What the store phase needs for one span: the load, the rotated key, and per lane
-// the table entry of its frame (bits 0-5) | W inside that frame's header (bit 6) |
-// the next frame's header starts inside the vector (bit 7).
+// What the store phase needs for one span: the load and the rotated key.
 struct SpanPlan {
     int kind, l0, nb;   // kind; the span's first table entry and frame starts inside it (uniform)
     u32x4 d;
-    uint32_t rk, info;
+    uint32_t rk;
 };
 template <int U>
 struct Plan {
@@ -477,7 +465,7 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
         // with full vmcnt drains)
         int kind = kSpanNone, l0 = 0, nb = 0;
         int64_t ad = 0;
-        uint32_t rk = 0, info = 0;
+        uint32_t rk = 0;
         do {
             if (A0 >= whi) break;
             kind = kSpanQueued;
@@ -495,15 +483,7 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
                 kind = kSpanFast;
                 ad = (int64_t)W + delta;
                 rk = rotr8(readlane32(t.key, l0), A0 - pw);
-                info = (uint32_t)l0 | (W < pw ? 64u : 0u);
                 break;
-            }
-            // every frame ending inside the span has >= 16 wire bytes: one cut per vector
-            if (nb == 1) {
-                if (readlane64(t.start, l0 + 1) - readlane64(t.start, l0) < 16) break;
-            } else {
-                const uint64_t nxt = bperm64(t.start, lane < kWave - 1 ? lane + 1 : lane);
-                if (__ballot(lane >= l0 && lane < l0 + nb && nxt - t.start < 16)) break;
             }
             // this lane's frame: the entries starting at or before W
             int l = l0;
@@ -515,13 +495,11 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
             kind = kSpanFast;
             ad = s0;
             rk = rotr8(f.K, W - pw);
-            info = (uint32_t)l | (W < pw ? 64u : 0u) | (f.Sn < W + 16 ? 128u : 0u);
         } while (false);
         sp.l0 = l0;
         sp.nb = nb;
         sp.kind = kind;
         sp.rk = rk;
-        sp.info = info;
         sp.d = u32x4{0, 0, 0, 0};
         // a payload buffer under 16 bytes (possibly NULL when empty) is never read
         // here: every span is queued then, and the compose kernel reads byte-wise
@@ -534,7 +512,6 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
 template <int U, bool NT>
 __device__ __forceinline__ void finish_chunk(const EncArgs& a, const EncTable& t, uint64_t A, uint64_t wlo,
                                              uint64_t whi, int lane, const Plan<U>& P) {
-    const bool masked = a.masked != 0;
     static_for<0, U>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
         const SpanPlan& sp = P.s[u];
@@ -549,32 +526,7 @@ __device__ __forceinline__ void finish_chunk(const EncArgs& a, const EncTable& t
             return;
         }
         const u32x4 kv = {sp.rk, sp.rk, sp.rk, sp.rk};
-        u32x4 v = sp.d ^ kv;
-        if (__ballot(sp.info >= 64)) {   // a header touches some lane's vector (wave-uniform)
-            const LaneFrames f = frames_near(t, sp.l0, sp.nb, W, (int)(sp.info & 63));
-            const uint64_t len = f.Pn - f.P, hl = header_len(len, masked);
-            if (sp.info & 64) {   // W inside frame l's header: its bytes from S - W to pw - W
-                const int64_t hs = (int64_t)(f.S - W), he = hs + (int64_t)hl;
-                uint64_t lo, hi;
-                build_header(f.B, len, masked, f.K, lo, hi);
-                const u32x4 m = select_range(hs, he);
-                v = (v & ~m) | (shift_bytes(lo, hi, (int)hs) & m);
-            }
-            if (sp.info & 128) {   // frame l + 1 starts at c: its header, then its payload shifted by hn
-                const int64_t c = (int64_t)(f.Sn - W);
-                const uint64_t lenn = f.Pnn - f.Pn, hn = header_len(lenn, masked);
-                const uint64_t pwn = f.Sn + hn;
-                uint64_t lo, hi;
-                build_header(f.Bn, lenn, masked, f.Kn, lo, hi);
-                const uint64_t dlo = (uint64_t)sp.d[0] | (uint64_t)sp.d[1] << 32;
-                const uint64_t dhi = (uint64_t)sp.d[2] | (uint64_t)sp.d[3] << 32;
-                const uint32_t rkn = rotr8(f.Kn, W - pwn);
-                const u32x4 kn = {rkn, rkn, rkn, rkn};
-                const u32x4 tail = shift_bytes(dlo, dhi, (int)hn) ^ kn;
-                const u32x4 mh = select_range(c, c + (int64_t)hn), mt = select_from(c + (int64_t)hn);
-                v = (v & ~(mh | mt)) | (shift_bytes(lo, hi, (int)c) & mh) | (tail & mt);
-            }
-        }
+        const u32x4 v = sp.d ^ kv;
         store_wire<NT>(a, W, v, wlo, whi);
     });
 }
@@ -635,7 +587,28 @@ __global__ __launch_bounds__(256) void encode_frames_kernel(EncArgs a) {
     }
 }
 
-// The queued spans: each wavefront takes queue entries in turn and composes them.
+// Frame k's header, and its payload bytes from the header's end to the end of the
+// 16-byte wire vector the header starts in (clipped to the frame): the bytes the
+// assembly kernel leaves wrong, since it maps a whole vector through the frame that
+// holds its first byte.  The compose kernel's vectors may cover some of the same
+// bytes, with the same values, so the two need no ordering.
+__device__ __forceinline__ void fix_frame(const EncArgs& a, uint64_t k) {
+    const bool masked = a.masked != 0;
+    const uint64_t w0 = gptr(a.wo)[k], p0 = gptr(a.off)[k];
+    const uint64_t len = gptr(a.off)[k + 1] - p0, hl = header_len(len, masked);
+    const uint32_t key = masked ? gptr(a.keys)[k] : 0u;
+    uint64_t lo, hi;
+    build_header(a.b0 ? (uint32_t)gptr(a.b0)[k] : 0x82u, len, masked, key, lo, hi);
+    NETC_GLOBAL uint8_t* w = gptr(a.wire_base) + a.wmis + w0;
+    if (!ENC_OK(4, w0 + hl + len, gptr(a.wo)[a.n])) return;
+    for (uint64_t i = 0; i < hl; ++i) w[i] = (uint8_t)(i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8)));
+    const uint64_t vend = (((w0 + a.wmis) | 15) + 1) - a.wmis;   // wire end of the header's vector
+    const uint64_t m = min(vend > w0 + hl ? vend - (w0 + hl) : 0ull, len);
+    for (uint64_t i = 0; i < m; ++i) w[hl + i] = gptr(a.src)[p0 + i] ^ (uint8_t)(key >> (8 * (i & 3)));
+}
+
+// The queued spans: each wavefront takes queue entries in turn and composes them;
+// then every frame's header bytes (fix_frame), one thread per frame.
 __global__ __launch_bounds__(256) void encode_queued_kernel(EncArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / kWave);
@@ -653,6 +626,8 @@ __global__ __launch_bounds__(256) void encode_queued_kernel(EncArgs a) {
         const u32x4 v = compose_vec(a, t, l0, A0, W, lane);
         if (W < whi) store_wire<false>(a, W, v, wlo, whi);
     }
+    const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.n; k += nth) fix_frame(a, k);
 }
 
 template <int U, bool NT>
@@ -749,7 +724,9 @@ static hipError_t launch_enc_u(EncArgs a, uint64_t wire_bound, bool nt, int max_
     else hipLaunchKernelGGL((encode_frames_kernel<U, false>), dim3(blocks), dim3(256), 0, stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(encode_queued_kernel, dim3(256), dim3(256), 0, stream, a);
+    const uint64_t fix_blocks = (a.n + 255) / 256;   // one thread per frame, up to 64 frames each
+    const unsigned qb = (unsigned)(fix_blocks < 256 ? 256 : (fix_blocks > 4096 ? 4096 : fix_blocks));
+    hipLaunchKernelGGL(encode_queued_kernel, dim3(qb), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
