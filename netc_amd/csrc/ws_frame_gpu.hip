@@ -17,14 +17,14 @@
 //   2. the assembly kernel, output-driven: the wire buffer is walked in 16-byte
 //      vectors aligned to the destination, chunk by chunk in grid-stride order as
 //      in ws_mask_gpu.hip.  A 64-entry frame table in VGPRs (wire start, payload
-//      offset, key, header byte of 64 consecutive frames) places each vector.  A
-//      vector inside one frame's payload is one unaligned 16-B load, one XOR with
-//      the key rotated to its phase, one aligned store; a vector holding a frame
-//      edge takes two loads and the header bytes (built once per frame,
-//      wave-uniform).  Software pipeline: while chunk c is stored, chunk c+W's
-//      loads and chunk c+2W's frame table are in flight.  Spans outside those two
-//      shapes (frames under 16 B, the buffer edges) are queued;
-//   3. the queued spans, composed byte-exactly from every frame they touch.
+//      offset, key, header byte of 64 consecutive frames) places each vector:
+//      one unaligned 16-B load, one XOR with the key of the frame holding the
+//      vector's first byte, rotated to its phase, one aligned store.  Spans the
+//      table does not cover (more than ~60 frames in 1 KiB) and the buffer edges
+//      are queued;
+//   3. the queued spans, composed byte-exactly from every frame they touch; then
+//      per frame (one thread each) the header and the payload bytes after it in
+//      the header's vector, which step 2 mapped through the previous frame.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -72,23 +72,39 @@ __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total) {
     return before + inc - v;
 }
 
+// One tile = kScanBlock frames.  The offsets go through LDS both ways so that every
+// global access is coalesced (thread t owns frames t*16 .. t*16+15 of the tile: read
+// straight from HBM, each load instruction would touch 64 cache lines, and with one
+// tile per CU that strided traffic, not the scan, set the kernel's time).
 __global__ __launch_bounds__(kScanThreads) void wire_offsets_chained(const uint64_t* off, uint64_t n, uint32_t fixed,
                                                                      uint64_t* wo, uint64_t* status, uint32_t epoch,
                                                                      uint32_t* defer_count) {
     __shared__ uint64_t tile_prefix;
-    const uint64_t tile = blockIdx.x;
-    const uint64_t first = tile * kScanBlock + (uint64_t)threadIdx.x * kScanPer;   // this thread's frames
+    __shared__ uint64_t v[kScanBlock + kScanBlock / kScanPer + 1];   // entry j at j + j / kScanPer
+    auto pos = [](uint32_t j) { return j + j / kScanPer; };
+    const uint64_t tile = blockIdx.x, base = tile * kScanBlock;
+    const uint32_t t0 = threadIdx.x * kScanPer;   // this thread's frames: base + t0 ..
     if (tile == 0 && threadIdx.x == 0) *defer_count = 0;   // the assembly kernel's queue (runs after)
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+        const uint32_t j = i * kScanThreads + threadIdx.x;
+        v[pos(j)] = gptr(off)[base + j < n ? base + j : n];
+    }
+    if (threadIdx.x == 0) v[pos(kScanBlock)] = gptr(off)[base + kScanBlock < n ? base + kScanBlock : n];
+    const uint64_t off0 = gptr(off)[0];
+    __syncthreads();
+    uint64_t o[kScanPer + 1];
+#pragma unroll
+    for (int i = 0; i <= kScanPer; ++i) o[i] = v[pos(t0 + i)];
     uint32_t e[kScanPer];
     uint64_t s = 0;
 #pragma unroll
     for (int i = 0; i < kScanPer; ++i) {
-        const uint64_t j = first + i;
-        e[i] = j < n ? ext_len(gptr(off)[j + 1] - gptr(off)[j]) : 0u;
+        e[i] = base + t0 + i < n ? ext_len(o[i + 1] - o[i]) : 0u;
         s += e[i];
     }
     uint64_t agg;
-    const uint64_t ex = block_exclusive_scan(s, &agg);
+    const uint64_t ex = block_exclusive_scan(s, &agg);   // its barriers also end the LDS reads above
     if (threadIdx.x < kWave) {
         const int lane = threadIdx.x;
         if (lane == 0)
@@ -103,12 +119,17 @@ __global__ __launch_bounds__(kScanThreads) void wire_offsets_chained(const uint6
     }
     __syncthreads();
     uint64_t run = tile_prefix + ex;
-    const uint64_t off0 = gptr(off)[0];
 #pragma unroll
     for (int i = 0; i < kScanPer; ++i) {
-        const uint64_t j = first + i;
-        if (j <= n) gptr(wo)[j] = (gptr(off)[j] - off0) + (uint64_t)fixed * j + run;
+        const uint64_t j = base + t0 + i;
+        v[pos(t0 + i)] = (o[i] - off0) + (uint64_t)fixed * j + run;
         run += e[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+        const uint32_t j = i * kScanThreads + threadIdx.x;
+        if (base + j <= n) gptr(wo)[base + j] = v[pos(j)];
     }
 }
 
@@ -601,10 +622,29 @@ __device__ __forceinline__ void fix_frame(const EncArgs& a, uint64_t k) {
     build_header(a.b0 ? (uint32_t)gptr(a.b0)[k] : 0x82u, len, masked, key, lo, hi);
     NETC_GLOBAL uint8_t* w = gptr(a.wire_base) + a.wmis + w0;
     if (!ENC_OK(4, w0 + hl + len, gptr(a.wo)[a.n])) return;
-    for (uint64_t i = 0; i < hl; ++i) w[i] = (uint8_t)(i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8)));
     const uint64_t vend = (((w0 + a.wmis) | 15) + 1) - a.wmis;   // wire end of the header's vector
-    const uint64_t m = min(vend > w0 + hl ? vend - (w0 + hl) : 0ull, len);
-    for (uint64_t i = 0; i < m; ++i) w[hl + i] = gptr(a.src)[p0 + i] ^ (uint8_t)(key >> (8 * (i & 3)));
+    const uint64_t m = min(vend > w0 + hl ? vend - (w0 + hl) : 0ull, len);   // <= 15
+    // the payload bytes read before any byte is written (a load-store byte loop
+    // waits out each load in turn): one 16-B load, bytewise only at the buffer end
+    uint64_t dlo = 0, dhi = 0;
+    if (m) {
+        if (p0 + 16 <= a.src_total) {
+            const u32x4 d = load_u<false>(a.src + p0);
+            dlo = (uint64_t)d[0] | (uint64_t)d[1] << 32;
+            dhi = (uint64_t)d[2] | (uint64_t)d[3] << 32;
+        } else {
+            for (uint64_t i = 0; i < m; ++i) {
+                const uint64_t b = gptr(a.src)[p0 + i];
+                if (i < 8) dlo |= b << (8 * i);
+                else dhi |= b << (8 * (i - 8));
+            }
+        }
+        const uint64_t k2 = (uint64_t)key | (uint64_t)key << 32;   // phase 0 at p0
+        dlo ^= k2;
+        dhi ^= k2;
+    }
+    for (uint64_t i = 0; i < hl; ++i) w[i] = (uint8_t)(i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8)));
+    for (uint64_t i = 0; i < m; ++i) w[hl + i] = (uint8_t)(i < 8 ? dlo >> (8 * i) : dhi >> (8 * (i - 8)));
 }
 
 // The queued spans: each wavefront takes queue entries in turn and composes them;
