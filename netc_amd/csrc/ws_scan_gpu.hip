@@ -419,6 +419,7 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     __shared__ uint32_t words[kWords];
     __shared__ unsigned long long set[kSet];
     __shared__ int overflow;
+    __shared__ uint16_t queue[kScanT / kWave][kChunk / (kScanT / kWave)];   // per wave: its candidates
     const uint64_t chunk = blockIdx.x;
     const uint64_t B = chunk * kChunk;
     const int tid = threadIdx.x;
@@ -441,19 +442,40 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     // positions before the stream start or past its end are not candidates
     if (p0 < a.start) cand &= a.start - p0 >= (uint64_t)kPer ? 0u : ~0u << (a.start - p0);
     if (p0 + kPer > a.len) cand &= p0 >= a.len ? 0u : (1u << (a.len - p0)) - 1;
+    // the wavefront's candidates into its LDS queue: ~2 % of positions pass, so a
+    // lane owns 0-3 of its 16 -- walked by their owners, a trip waited on the lane
+    // with the most; from the queue every idle lane takes the next one
+    const int lane = tid & (kWave - 1);
+    uint16_t* q = queue[tid / kWave];
+    const uint32_t mine = __popc(cand);
+    uint32_t incl = mine;   // inclusive prefix of the counts over the wave
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d, kWave);
+        if (lane >= d) incl += o;
+    }
+    const uint32_t total = __shfl(incl, kWave - 1, kWave);
+    uint32_t at = incl - mine;
+    for (uint32_t c = cand; c; c &= c - 1) q[at++] = (uint16_t)(kPer * tid + __builtin_ctz(c));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     // every candidate's chain walked to where it leaves the chunk, one hop per trip
-    // for every lane: a lane whose walk ends takes its next candidate, so a trip
-    // never waits on another lane's longer walk of an earlier candidate
+    // for every lane
     bool failed = false, active = false;
     uint64_t p = 0;
     int hop = 0;
+    uint32_t head = 0;
     const uint64_t Bend = B + kChunk;
     for (;;) {
-        if (!active && cand) {
-            p = p0 + __builtin_ctz(cand);
-            cand &= cand - 1;
-            hop = 0;
-            active = true;
+        const uint64_t idle = __ballot(!active);
+        if (head < total && idle) {   // wave-uniform
+            const uint32_t r =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+            if (!active && head + r < total) {
+                p = B + q[head + r];
+                hop = 0;
+                active = true;
+            }
+            head += (uint32_t)__popcll(idle);
         }
         if (!__ballot(active)) break;
         if (active) {
@@ -463,7 +485,6 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
             } else if (hop == kWalkHops) {   // frames of a few bytes: K1'
                 failed = true;
                 active = false;
-                cand = 0;
             } else {
                 const uint64_t v = parse_at(a, p, window_at(words, (int)(p - B)), nullptr, nullptr);
                 if (v & kTerm) active = false;   // END / DEAD inside the chunk
@@ -473,6 +494,7 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
                 }
             }
         }
+        if (__ballot(failed)) break;   // the chunk goes to K1' anyway
     }
     if (__syncthreads_or(failed)) {
         if (tid == 0) a.slow[atomicAdd(&a.flags[2], 1u)] = (uint32_t)chunk;
