@@ -6,17 +6,17 @@
 // the stream (header offset, key, byte 0) in parallel.
 //
 // Frame starts form a chain: the next header follows the current frame's payload.
-// Chunks of C bytes are processed independently, for EVERY byte position:
-//   K1 / K2  per chunk, in LDS: parse a header at each position p (invalid under
-//            the strict RFC checks -> DEAD; not complete inside the stream -> END),
-//            link p to the next header, and pointer-jump the links until each
-//            position knows where its chain leaves the chunk (EXIT at a position
-//            in a later chunk) or ends (END / DEAD).  K1 publishes each chunk's
-//            distinct exits as "candidate entries" of the chunk they land in (the
-//            true chain enters each chunk at one of them); K2 maps every candidate
-//            entry of its chunk to the candidate it exits to: a graph of a few
-//            nodes per chunk whose path from the stream start is the true chain,
-//            one node per chunk it enters.
+// The stream is cut into chunks of C bytes:
+//   K1       per chunk, in LDS: every position that can start a header (strict
+//            mode: passes the RFC checks on its first 2 bytes) is parsed once.  A
+//            chain inside the chunk only steps between such positions, so the
+//            distinct places where chains leave the chunk are the direct exits of
+//            those positions; K1 publishes them as "candidate entries" of the
+//            chunks they land in (the true chain enters each chunk at one of them).
+//   K2       per candidate entry: its chain walked (header bytes from global
+//            memory; K2' pointer-jumps the chunk in LDS when the walk is long) to
+//            the candidate it exits to: a graph of a few nodes per chunk whose path
+//            from the stream start is the true chain, one node per chunk it enters.
 //   K3       pointer doubling over that graph, marking the nodes reachable from
 //            the start node (log2(chunks) passes);
 //   K4       per chunk: the true entry (its marked node), a walk of
@@ -63,8 +63,7 @@ struct ScanArgs {
     uint64_t* nterm;       // (nc + 1) * kCand: the terminal where the node's walk leaves its chunk
     uint32_t* ncnt;        // (nc + 1) * kCand: frames on that walk (~0: not counted, K2')
     uint8_t* mark;         // (nc + 1) * kCand: node is on the chain from the stream start
-    uint32_t* flags;       // [0] overflow, [1] root node, [2] / [3] / [4] entries of slow / slow2 / slow3
-    uint32_t* slow;        // K1 chunks left to the LDS kernel (nc + 1)
+    uint32_t* flags;       // [0] overflow, [1] root node, [3] / [4] entries of slow2 / slow3
     uint32_t* slow2;       // K2 nodes left to the LDS kernel ((nc + 1) * kCand)
     uint32_t* slow3;       // K4 chunks of many frames left to the LDS emit kernel (nc + 1)
     uint64_t* cbase;       // K4: index of each chunk's first frame (nc + 1)
@@ -191,58 +190,9 @@ __device__ void load_chunk(const ScanArgs& a, uint64_t B, uint32_t* words) {
     __syncthreads();
 }
 
-// Link every position of the chunk (local index, or a terminal) and pointer-jump
-// until every link is terminal: EXIT(x) with x >= chunk end, END(p) or DEAD(p).
-__device__ void chunk_links(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t* lk) {
-    const int tid = threadIdx.x;
-    const uint64_t Bend = B + kChunk;
-    // every link starts DEAD (coalesced); only positions that can start a header are parsed
-    const uint64_t kDeadLink = term(kDead, 0);
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) lk[k * kScanT + tid] = kDeadLink;
-    // this thread's kPer consecutive positions: bytes [kPer tid, kPer tid + kPer + 14) in 8 dwords
-    const int i0 = kPer * tid;
-    uint32_t w[kPer / 4 + 4];
-#pragma unroll
-    for (int k = 0; k < kPer / 4 + 4; ++k) w[k] = words[i0 / 4 + k];
-    auto byte_at = [&](int j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
-    // strict quick check on bytes 0-1 of each position (~98 % of payload positions fail it)
-    uint32_t cand = 0;
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const uint32_t first = byte_at(j), second = byte_at(j + 1), opcode = first & 0x0F;
-        const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
-        const bool reject = a.strict && (!(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80)));
-        if (!reject && B + i0 + j >= a.start) cand |= 1u << j;
-    }
-    __syncthreads();   // DEAD fill done before the scattered writes
-    while (cand) {
-        const int j = __builtin_ctz(cand);
-        cand &= cand - 1;
-        const int i = i0 + j;
-        uint64_t v = parse_at(a, B + i, window_at(words, i), nullptr, nullptr);
-        if (!(v & kTerm)) v = v < Bend ? v - B : term(kExit, v);
-        lk[i] = v;
-    }
-    __syncthreads();
-    for (;;) {
-        int changed = 0;
-        for (int k = 0; k < kPer; ++k) {
-            const int i = k * kScanT + tid;
-            const uint64_t v = lk[i];
-            if (!(v & kTerm)) {
-                const uint64_t w = lk[v];
-                lk[i] = w;
-                changed |= !(w & kTerm);
-            }
-        }
-        if (!__syncthreads_or(changed)) break;
-    }
-}
-
-// chunk_links plus, per position, the complete frames on its chain until the
-// terminal (hc).  Jumps are synchronous (read phase, barrier, write phase) so that
-// each link and its count stay a consistent pair.  Fallback kernels only.
+// K2' / K4b': every position of the chunk linked (local index, or a terminal) and
+// pointer-jumped until every link is terminal -- EXIT(x) with x >= chunk end, END(p)
+// or DEAD(p) -- with hc = the frames (hops) on the way.
 __device__ void chunk_links_counted(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t* lk,
                                     uint16_t* hc) {
     const int tid = threadIdx.x;
@@ -307,22 +257,8 @@ __device__ void chunk_links_counted(const ScanArgs& a, uint64_t B, const uint32_
     }
 }
 
-// Walk one chain from x inside the chunk for at most `hops` frames: its terminal,
-// or 0 if the hop budget ran out.
-__device__ uint64_t walk_exit(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t x, int hops) {
-    const uint64_t Bend = B + kChunk;
-    uint64_t p = x;
-    for (int h = 0; h < hops; ++h) {
-        if (p >= Bend) return term(kExit, p);
-        const uint64_t v = parse_at(a, p, window_at(words, (int)(p - B)), nullptr, nullptr);
-        if (v & kTerm) return v;
-        p = v;
-    }
-    return p >= Bend ? term(kExit, p) : 0;
-}
-
 // 16 stream bytes from p (zero past len) straight from global memory: the walks
-// of K1 (strict), K2 and K4 touch only the header bytes of the frames they visit,
+// of K2 and K4 touch only the header bytes of the frames they visit,
 // so they read them where they lie instead of staging the chunk in LDS.
 __device__ __forceinline__ Win window_global(const ScanArgs& a, uint64_t p) {
     typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
@@ -410,11 +346,10 @@ __device__ __forceinline__ void publish_exits(const ScanArgs& a, uint64_t chunk,
     }
 }
 
-// K1: distinct exits of each chunk.  Strict mode: each position passing the quick
-// check on its 2 first bytes (~2 % of payload positions, and every real header)
-// walks its chain directly from global memory -- garbage chains die within a hop or
-// two, the true chain has chunk / frame-size hops.  A chain longer than kWalkHops
-// (frames of a few bytes) leaves the chunk to K1' (LDS pointer jumping).
+// K1: distinct exits of each chunk.  The chunk's candidates -- strict mode: the
+// positions passing the quick check on their 2 first bytes (~2 % of payload
+// positions, and every real header); otherwise every position -- are each parsed
+// once, from the chunk's LDS copy.
 __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     __shared__ uint32_t words[kWords];
     __shared__ unsigned long long set[kSet];
@@ -431,10 +366,12 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     uint32_t w[kPer / 4 + 1];
 #pragma unroll
     for (int k = 0; k < kPer / 4 + 1; ++k) w[k] = words[kPer / 4 * tid + k];
-    // the quick check four positions at a time (bit 7 of each byte: position passes)
-    uint32_t cand = 0;
+    // the quick check four positions at a time (bit 7 of each byte: position passes);
+    // without the strict checks every position is a candidate
+    uint32_t cand = a.strict ? 0u : (1u << kPer) - 1;
 #pragma unroll
     for (int k = 0; k < kPer / 4; ++k) {
+        if (!a.strict) break;
         const uint32_t m = quick_ok4(w[k], __builtin_amdgcn_alignbyte(w[k + 1], w[k], 1));
         const uint32_t b = (m >> 7) & 0x01010101u;
         cand |= ((b | b >> 7 | b >> 14 | b >> 21) & 0xFu) << (4 * k);
@@ -442,9 +379,8 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     // positions before the stream start or past its end are not candidates
     if (p0 < a.start) cand &= a.start - p0 >= (uint64_t)kPer ? 0u : ~0u << (a.start - p0);
     if (p0 + kPer > a.len) cand &= p0 >= a.len ? 0u : (1u << (a.len - p0)) - 1;
-    // the wavefront's candidates into its LDS queue: ~2 % of positions pass, so a
-    // lane owns 0-3 of its 16 -- walked by their owners, a trip waited on the lane
-    // with the most; from the queue every idle lane takes the next one
+    // the wavefront's candidates into its LDS queue (~2 % of positions pass, 0-3 per
+    // lane), then parsed round-robin by its lanes
     const int lane = tid & (kWave - 1);
     uint16_t* q = queue[tid / kWave];
     const uint32_t mine = __popc(cand);
@@ -458,83 +394,21 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     uint32_t at = incl - mine;
     for (uint32_t c = cand; c; c &= c - 1) q[at++] = (uint16_t)(kPer * tid + __builtin_ctz(c));
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // every candidate's chain walked to where it leaves the chunk, one hop per trip
-    // for every lane
-    bool failed = false, active = false;
-    uint64_t p = 0;
-    int hop = 0;
-    uint32_t head = 0;
+    // Each candidate is parsed once.  A chain inside the chunk moves from candidate
+    // to candidate (a position that fails the quick check would parse DEAD), so a
+    // chain leaves the chunk exactly where its last candidate's own frame does: the
+    // chunk's exits are the direct exits of its candidates, and no chain is walked.
+    // (An earlier form walked every candidate's chain to the chunk end, and handed
+    // chunks of tiny frames, whose chains outran the hop budget, to an LDS
+    // pointer-jumping kernel -- also the whole non-strict path.)
     const uint64_t Bend = B + kChunk;
-    for (;;) {
-        const uint64_t idle = __ballot(!active);
-        if (head < total && idle) {   // wave-uniform
-            const uint32_t r =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-            if (!active && head + r < total) {
-                p = B + q[head + r];
-                hop = 0;
-                active = true;
-            }
-            head += (uint32_t)__popcll(idle);
-        }
-        if (!__ballot(active)) break;
-        if (active) {
-            if (p >= Bend) {   // leaves the chunk: an exit
-                set_insert(set, p, &overflow);
-                active = false;
-            } else if (hop == kWalkHops) {   // frames of a few bytes: K1'
-                failed = true;
-                active = false;
-            } else {
-                const uint64_t v = parse_at(a, p, window_at(words, (int)(p - B)), nullptr, nullptr);
-                if (v & kTerm) active = false;   // END / DEAD inside the chunk
-                else {
-                    p = v;
-                    ++hop;
-                }
-            }
-        }
-        if (__ballot(failed)) break;   // the chunk goes to K1' anyway
+    for (uint32_t i = lane; i < total; i += kWave) {
+        const uint64_t p = B + q[i];
+        const uint64_t v = parse_at(a, p, window_at(words, (int)(p - B)), nullptr, nullptr);
+        if (!(v & kTerm) && v >= Bend) set_insert(set, v, &overflow);
     }
-    if (__syncthreads_or(failed)) {
-        if (tid == 0) a.slow[atomicAdd(&a.flags[2], 1u)] = (uint32_t)chunk;
-        return;
-    }
+    __syncthreads();
     publish_exits(a, chunk, set, overflow, tid);
-}
-
-// K1': the chunks K1 left (tiny frames), or every chunk in non-strict mode (every
-// position a candidate): each position's chain pointer-jumped to its end in LDS.
-__global__ __launch_bounds__(kScanT) void scan_exits_lds(ScanArgs a, int all) {
-    __shared__ uint32_t words[kWords];
-    __shared__ uint64_t lk[kChunk];
-    __shared__ unsigned long long set[kSet];
-    __shared__ int overflow;
-    const int tid = threadIdx.x;
-    const uint64_t count = all ? a.nc + 1 : __hip_atomic_load(&a.flags[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint64_t q = blockIdx.x; q < count; q += gridDim.x) {
-        const uint64_t chunk = all ? q : a.slow[q];
-        const uint64_t B = chunk * kChunk;
-        if (tid < kSet) set[tid] = ~0ull;
-        if (tid == 0) overflow = 0;
-        load_chunk(a, B, words);
-        chunk_links(a, B, words, lk);
-        // dedup: a wave retires one distinct value per round (exits repeat a lot)
-        for (int k = 0; k < kPer; ++k) {
-            const uint64_t v = lk[k * kScanT + tid];
-            bool pending = (v & kTerm) && term_type(v) == kExit;
-            uint64_t x = term_pos(v);
-            while (__ballot(pending)) {
-                const int leader = __builtin_ctzll(__ballot(pending));
-                const uint64_t x0 = readlane64(x, leader);
-                if (pending && x == x0) pending = false;
-                if ((tid & (kWave - 1)) == leader) set_insert(set, x0, &overflow);
-            }
-        }
-        __syncthreads();
-        publish_exits(a, chunk, set, overflow, tid);
-        __syncthreads();   // set / words reused by the next chunk
-    }
 }
 
 // node -> the candidate its chain exits to (or -1) and the terminal where it ends
@@ -871,8 +745,8 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.result = result;
     // scratch layout, per (device, stream)
     const uint64_t need = chunks * 4 + 32 + nodes + nodes * 8 + nodes * 4 + nodes * 8 + 2 * nodes * 4 + chunks * 8 +
-                          chunks * 4 + nodes * 4 + nodes * 4 + chunks * 4 + chunks * 8 +
-                          64 * 14;   // + alignment padding of the 14 regions
+                          nodes * 4 + nodes * 4 + chunks * 4 + chunks * 8 +
+                          64 * 13;   // + alignment padding of the 13 regions
     static std::map<std::pair<int, hipStream_t>, ScanScratchSet> scratch;
     static std::mutex mu;
     int dev = 0;
@@ -910,7 +784,6 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         a.status = (uint64_t*)(m + o); o = align(o + chunks * 8);
         jp = (int32_t*)(m + o); o = align(o + nodes * 4);
         jq = (int32_t*)(m + o); o = align(o + nodes * 4);
-        a.slow = (uint32_t*)(m + o); o = align(o + chunks * 4);
         a.slow2 = (uint32_t*)(m + o); o = align(o + nodes * 4);
         a.slow3 = (uint32_t*)(m + o); o = align(o + chunks * 4);
         a.cbase = (uint64_t*)(m + o);
@@ -923,12 +796,7 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     // counters + flags, and the default results (no frames, nothing consumed past start)
     if ((e = hipMemsetAsync(a.ccount, 0, cleared, stream)) != hipSuccess) return e;
     const unsigned slow_grid = (unsigned)(chunks < 1024 ? chunks : 1024);
-    if (strict) {
-        hipLaunchKernelGGL(scan_exits, dim3((unsigned)chunks), dim3(kScanT), 0, stream, a);
-        hipLaunchKernelGGL(scan_exits_lds, dim3(slow_grid), dim3(kScanT), 0, stream, a, 0);
-    } else {
-        hipLaunchKernelGGL(scan_exits_lds, dim3(slow_grid), dim3(kScanT), 0, stream, a, 1);
-    }
+    hipLaunchKernelGGL(scan_exits, dim3((unsigned)chunks), dim3(kScanT), 0, stream, a);
     hipLaunchKernelGGL(scan_links, dim3((unsigned)((nodes + 255) / 256)), dim3(256), 0, stream, a);
     hipLaunchKernelGGL(scan_links_lds, dim3(slow_grid), dim3(kScanT), 0, stream, a);
     const unsigned lb = (unsigned)((nodes + 255) / 256);

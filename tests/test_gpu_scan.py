@@ -106,6 +106,17 @@ def test_unmasked_and_non_strict(torch_cuda):
     assert run_scan(torch_cuda, wire, strict=True) == 0   # the first unmasked header is rejected
 
 
+@pytest.mark.parametrize("masked", [False, True])
+def test_non_strict_many_chunks(torch_cuda, masked):
+    # every position a K1 candidate: tiny, 7-bit, 16-bit and 64-bit lengths over ~1,000 chunks
+    rng = np.random.default_rng(18 + masked)
+    sizes = np.concatenate([rng.integers(0, 8, 3000), rng.integers(0, 126, 3000), rng.integers(126, 9000, 400),
+                            [70000, 131072]])
+    rng.shuffle(sizes)
+    wire, _ = _stream(rng, sizes, masked=masked)
+    assert run_scan(torch_cuda, wire, strict=False) == sizes.size
+
+
 def test_strict_errors_mid_stream(torch_cuda):
     rng = np.random.default_rng(9)
     good, _ = _stream(rng, rng.integers(0, 6000, 100))
