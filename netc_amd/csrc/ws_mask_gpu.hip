@@ -664,10 +664,34 @@ __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uin
                     h1 = b;
                 }
                 // the first 3 bytes of every chunk inside the frame, which phase A skips
-                // (in place, another wavefront's chunk held the bytes before them)
-                for (uint64_t c = (lo + 3 + mis + win - 1) / win * win; c < hi + mis && !bad; c += win) {
-                    for (uint64_t p = c - mis; p < c - mis + 3 && p < hi; ++p)
-                        if (p >= lo + 3) bad |= utf8_rule(dst[p - 3], dst[p - 2], dst[p - 1], dst[p]);
+                // (in place, another wavefront's chunk held the bytes before them).  The
+                // 4 bytes before and after each chunk start (aligned dwords: dst - mis is
+                // 16-aligned, chunk starts are multiples of win >= 4096) are read for 8
+                // chunks at a time -- one at a time, a 64 KiB frame's 16 seams were 16
+                // round trips to memory in a row.
+                for (uint64_t cb = (lo + 3 + mis + win - 1) / win * win; cb < hi + mis && !bad; cb += 8 * win) {
+                    uint32_t wb[8], wa[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const uint64_t c = cb + (uint64_t)i * win, q = c - mis;   // q: the chunk's first byte
+                        wb[i] = wa[i] = 0;
+                        if (c < hi + mis) {
+                            wb[i] = *(const NETC_GLOBAL uint32_t*)(dst + q - 4);
+                            if (q + 4 <= hi) wa[i] = *(const NETC_GLOBAL uint32_t*)(dst + q);
+                            else
+                                for (uint64_t t = q; t < hi; ++t) wa[i] |= (uint32_t)dst[t] << (8 * (t - q));
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const uint64_t c = cb + (uint64_t)i * win, q = c - mis;
+                        const uint64_t w = (uint64_t)wa[i] << 32 | wb[i];   // bytes q - 4 .. q + 3
+                        auto B = [&](int j) { return (uint32_t)(w >> (8 * j)) & 0xFFu; };
+#pragma unroll
+                        for (int d = 0; d < 3; ++d)
+                            if (c < hi + mis && q + d >= lo + 3 && q + d < hi)
+                                bad |= utf8_rule(B(1 + d), B(2 + d), B(3 + d), B(4 + d));
+                    }
                 }
                 if (hi - lo > 3) {   // the frame's own last 3 bytes become the history
                     h3 = dst[hi - 3];

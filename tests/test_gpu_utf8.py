@@ -159,6 +159,25 @@ def test_errors_at_every_boundary(torch_cuda):
     assert (exp[:-1] == 0).all() and exp[-1] == 1
 
 
+@pytest.mark.parametrize("shift", [0, 5])
+def test_errors_at_chunk_seams(torch_cuda, shift):
+    # long frames (many 4 KiB chunks each) with one broken byte among the first 3 bytes
+    # of a chunk -- the bytes only phase B checks -- or just before / after them
+    rng = np.random.default_rng(70 + shift)
+    flen, win, mis = 70000, 4096, shift & 15   # torch allocations are 256-B aligned
+    frames, o = [], 0
+    for i in range(30):
+        body = bytearray(text_bytes(rng, flen)[:flen]) if i % 3 else bytearray(rng.integers(0x20, 0x7F, flen, dtype=np.uint8).tobytes())
+        if i % 6 != 5:
+            c = ((o + mis + 3 + win - 1) // win + int(rng.integers(0, 12))) * win   # a chunk start inside the frame
+            p = c - mis - o + (-1, 0, 1, 2, 3)[i % 5]
+            if 3 <= p < flen:
+                body[p] = (0xFF, 0x80, 0xC0)[i % 3]
+        frames.append((0x81, bytes(body)))
+        o += flen
+    run_validate(torch_cuda, frames, shift=shift)
+
+
 def test_large_text_batch(torch_cuda):
     # ~64 MiB of 1 KiB TEXT frames (config 2 shape), 1 % corrupted
     rng = np.random.default_rng(70)
