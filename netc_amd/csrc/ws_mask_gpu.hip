@@ -170,9 +170,40 @@ __device__ __forceinline__ u32x4 span_mask(const Args& a, Table& t, uint64_t A0,
     u32x4 mask = {rk0, rk0, rk0, rk0};
     // frame boundaries strictly inside (A0, Aend)
     uint64_t b = __ballot(t.start > A0 && t.start < Aend);
-    if (b == 0 && (t.tail || t.last >= Aend)) return mask;   // common case: one frame
+    const bool covered = t.tail || t.last >= Aend;
+    if (b == 0 && covered) return mask;   // common case: one frame
 
     const uint64_t a_lane = A0 + 16ull * (uint64_t)lane;
+    if (covered && __popcll(b) > 2) {
+        // Dense span (frames under ~340 B): per lane instead of per boundary.  The
+        // frame holding the lane's first byte by a binary search of the table
+        // (ds_bpermute), then the frames starting inside the lane's 16 bytes in turn
+        // -- one for frames of 16 B or more; the loop runs as long as any lane has
+        // another.  Every lane takes part in each ds_bpermute (the loop is uniform).
+        int l = j0;   // entries 0 .. j0 start at or before A0 <= a_lane
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const int c = l + step < kWave ? l + step : kWave - 1;
+            if (bperm64(t.start, c) <= a_lane) l = c;
+        }
+        const uint64_t sl = bperm64(t.start, l);
+        const uint32_t rl = rotr8((uint32_t)__builtin_amdgcn_ds_bpermute(l << 2, (int)t.key), a_lane - sl);
+        u32x4 m = {rl, rl, rl, rl};
+        for (int j = l + 1;; ++j) {
+            const int c = j < kWave ? j : kWave - 1;
+            const uint64_t sj = bperm64(t.start, c);
+            const uint32_t kj = (uint32_t)__builtin_amdgcn_ds_bpermute(c << 2, (int)t.key);
+            const bool in = j < kWave && sj < a_lane + 16;
+            if (in) {
+                const uint32_t rj = rotr8(kj, a_lane - sj);
+                const u32x4 sel = select_from((int64_t)(sj - a_lane));
+                const u32x4 kv = {rj, rj, rj, rj};
+                m = (m & ~sel) | (kv & sel);
+            }
+            if (!__ballot(in)) break;
+        }
+        return m;
+    }
     for (;;) {
         while (b) {
             const int j = __builtin_ctzll(b);
