@@ -123,6 +123,19 @@ def test_dense_tiny_frames(torch_cuda):
     run_case(torch_cuda, payload, off, synth.random_keys(sizes.size, 8), 5, 5)
 
 
+@pytest.mark.parametrize("shift", [0, 7])
+def test_dense_spans_per_lane(torch_cuda, shift):
+    # 3..63 frame starts per 1 KiB span (the per-lane keying path): frames under 16 B
+    # (several starts inside one 16 B vector), empty frames, and some long ones between
+    g = synth.rng(31 + shift)
+    sizes = g.choice([0, 1, 2, 5, 9, 12, 15, 16, 17, 23, 31, 48, 64, 100, 200, 333], size=60000)
+    sizes[g.choice(sizes.size, 30, replace=False)] = g.integers(1000, 9000, 30)
+    off = frames_from_sizes(sizes)
+    payload = synth.host_payload(int(off[-1]), 31)
+    run_case(torch_cuda, payload, off, synth.random_keys(sizes.size, 31, 4), shift, shift)
+    run_case(torch_cuda, payload, off, synth.random_keys(sizes.size, 32), shift, (shift + 3) % 16)
+
+
 def test_unframed_bytes_pass_through(torch_cuda):
     off = frames_from_sizes([100, 5000, 7, 0, 33333], start=123)
     total = int(off[-1]) + 77
