@@ -130,13 +130,12 @@ struct Win {
 
 __device__ __forceinline__ Win window_at(const uint32_t* words, int i) {
     const int q = i >> 2;
-    const uint32_t r = (uint32_t)(i & 3) * 8;
     uint32_t w[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) w[k] = words[q + k];
     Win x;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) x.d[k] = (uint32_t)((((uint64_t)w[k + 1] << 32) | w[k]) >> r);
+    for (int k = 0; k < 4; ++k) x.d[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], (uint32_t)(i & 3));
     return x;
 }
 
@@ -366,19 +365,23 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     uint32_t w[kPer / 4 + 1];
 #pragma unroll
     for (int k = 0; k < kPer / 4 + 1; ++k) w[k] = words[kPer / 4 * tid + k];
-    // the quick check four positions at a time (bit 7 of each byte: position passes);
+    // the quick check four positions at a time (bit 7 of each byte: position passes),
+    // the four results interleaved into one word: bit 8 j + k <-> position 4 k + j;
     // without the strict checks every position is a candidate
-    uint32_t cand = a.strict ? 0u : (1u << kPer) - 1;
+    uint32_t cand = 0x0F0F0F0Fu;
+    if (a.strict) {
+        cand = 0;
 #pragma unroll
-    for (int k = 0; k < kPer / 4; ++k) {
-        if (!a.strict) break;
-        const uint32_t m = quick_ok4(w[k], __builtin_amdgcn_alignbyte(w[k + 1], w[k], 1));
-        const uint32_t b = (m >> 7) & 0x01010101u;
-        cand |= ((b | b >> 7 | b >> 14 | b >> 21) & 0xFu) << (4 * k);
+        for (int k = 0; k < kPer / 4; ++k)
+            cand |= quick_ok4(w[k], __builtin_amdgcn_alignbyte(w[k + 1], w[k], 1)) >> (7 - k);
     }
-    // positions before the stream start or past its end are not candidates
-    if (p0 < a.start) cand &= a.start - p0 >= (uint64_t)kPer ? 0u : ~0u << (a.start - p0);
-    if (p0 + kPer > a.len) cand &= p0 >= a.len ? 0u : (1u << (a.len - p0)) - 1;
+    // positions before the stream start or past its end are not candidates (only the
+    // chunks holding either end: a wave-uniform test)
+    if (B < a.start || B + kChunk > a.len) {
+#pragma unroll
+        for (int i = 0; i < kPer; ++i)
+            if (p0 + i < a.start || p0 + i >= a.len) cand &= ~(1u << (8 * (i & 3) + (i >> 2)));
+    }
     // the wavefront's candidates into its LDS queue (~2 % of positions pass, 0-3 per
     // lane), then parsed round-robin by its lanes
     const int lane = tid & (kWave - 1);
@@ -392,7 +395,10 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     }
     const uint32_t total = __shfl(incl, kWave - 1, kWave);
     uint32_t at = incl - mine;
-    for (uint32_t c = cand; c; c &= c - 1) q[at++] = (uint16_t)(kPer * tid + __builtin_ctz(c));
+    for (uint32_t c = cand; c; c &= c - 1) {
+        const int b = __builtin_ctz(c);
+        q[at++] = (uint16_t)(kPer * tid + 4 * (b & 7) + (b >> 3));
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     // Each candidate is parsed once.  A chain inside the chunk moves from candidate
     // to candidate (a position that fails the quick check would parse DEAD), so a
