@@ -606,22 +606,14 @@ __global__ __launch_bounds__(256) void scan_count(ScanArgs a) {
         a.result[2] = term_type(stop) == kDead ? end : ~0ull;
         if (k <= a.max_frames) a.hdr[k] = end;
     }
-}
-
-// K4b: one thread per chunk walks the chunk's frames from global memory (header
-// bytes only) and writes their descriptors from the chunk's first index on; a
-// chunk of more than kEmitHops frames goes to K4b' (LDS).
-__global__ __launch_bounds__(256) void scan_emit(ScanArgs a) {
-    const uint64_t chunk = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (chunk > a.nc) return;
-    if (__hip_atomic_load(&a.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-    const int64_t enode = chunk_entry(a, chunk);
-    if (enode < 0) return;
-    if (a.ncnt[enode] > (uint32_t)kEmitHops) {
+    // K4b, in the same thread now that the base is known: the chunk's frames walked
+    // from global memory (header bytes only), descriptors from the base on; a chunk
+    // of more than kEmitHops frames goes to K4b' (LDS)
+    if (count > (uint64_t)kEmitHops) {
         a.slow3[atomicAdd(&a.flags[4], 1u)] = (uint32_t)chunk;
         return;
     }
-    uint64_t k = a.cbase[chunk];
+    uint64_t k = base;
     walk_frames<false>(a, chunk * kChunk, nullptr, a.cand[enode], -1, [&](uint64_t p, uint32_t key, uint8_t b0) {
         if (k < a.max_frames) {
             a.hdr[k] = p;
@@ -814,7 +806,6 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     }
     const unsigned cb = (unsigned)((chunks + 255) / 256);
     hipLaunchKernelGGL(scan_count, dim3(cb), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL(scan_emit, dim3(cb), dim3(256), 0, stream, a);
     hipLaunchKernelGGL(scan_emit_lds, dim3(slow_grid), dim3(kScanT), 0, stream, a);
     return hipGetLastError();
 }
