@@ -276,9 +276,9 @@ def main():
         step(args.warmup + i, sh)
     ev1.record(stream)
     torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0            # this rank's K steps, sync to sync
     if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
+        torch.distributed.barrier()               # closing bracket; the max over ranks follows
     kern_ms = np.array([ev0.elapsed_time(ev1) / args.steps])
 
     # secondary figure: the same steps with two batches in flight on two HIP streams
@@ -295,9 +295,9 @@ def main():
         for i in range(args.steps):
             step(i, s2[i % 2].cuda_stream)
         torch.cuda.synchronize(device)
+        pipelined = time.perf_counter() - t1
         if world > 1:
             torch.distributed.barrier()
-        pipelined = time.perf_counter() - t1
 
     if world > 1:
         t = torch.tensor([elapsed, kern_ms.mean(), pipelined or 0.0], dtype=torch.float64, device=coll_dev)
