@@ -3,7 +3,8 @@
 overlapped H2D / kernel / D2H on separate HIP streams).  Reports the host-to-host rate
 (payload GiB/s, PCIe-inclusive) for DESIGN.md -- it is never bench.py's `value`.
 
-Default: 16 GiB of 4 KiB frames, in place in one pinned host buffer, 4 slots of 256 MiB.
+Default: 16 GiB of 4 KiB frames, in place in one pinned host buffer, 2 slots of 512 MiB
+(the fastest shape of a sweep over 32 MiB - 2 GiB slots and 2 - 16 slots).
 A sample of frames is checked against the oracle after the timed call.
 """
 
@@ -23,8 +24,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=16.0)
     ap.add_argument("--frame", type=int, default=4096)
-    ap.add_argument("--slot-mib", type=int, default=256)
-    ap.add_argument("--slots", type=int, default=4)
+    ap.add_argument("--slot-mib", type=int, default=512)
+    ap.add_argument("--slots", type=int, default=2)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--pageable", action="store_true", help="plain malloc'd host memory instead of pinned")
     args = ap.parse_args()
