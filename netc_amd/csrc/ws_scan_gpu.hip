@@ -359,6 +359,7 @@ __global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
     const int tid = threadIdx.x;
     if (tid < kSet) set[tid] = ~0ull;
     if (tid == 0) overflow = 0;
+    if (chunk == 0 && tid == 0) a.flags[4] = 0;   // K4b''s queue length, left set by the previous call
     load_chunk(a, B, words);   // 4 KiB in LDS: the walks' hops are LDS reads
     // this thread's kPer positions and the 4 bytes after them
     const uint64_t p0 = B + (uint64_t)kPer * tid;
@@ -544,11 +545,19 @@ __device__ uint64_t block_scan256(uint64_t v, uint64_t* total) {
 // (decoupled look-back) gives each chunk's first frame index.  The chunk where
 // the chain ends sets the results.  On candidate overflow, one thread walks the
 // whole stream instead (serial fallback).
+// The chunk's candidate counter and mark bytes are read here for the last time: the
+// thread zeroes them, so the next call on this scratch needs no clearing launch.
+__device__ __forceinline__ void clear_chunk(const ScanArgs& a, uint64_t chunk) {
+    a.ccount[chunk] = 0;
+    *(uint64_t*)(a.mark + chunk * kCand) = 0;   // kCand == 8 mark bytes, 8-aligned
+}
+
 __global__ __launch_bounds__(256) void scan_count(ScanArgs a) {
     __shared__ uint64_t tile_prefix;
     const uint64_t tile = blockIdx.x;
     const uint64_t chunk = tile * 256 + threadIdx.x;
     if (__hip_atomic_load(&a.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+        if (chunk <= a.nc) clear_chunk(a, chunk);
         if (tile == 0 && threadIdx.x == 0) {
             uint64_t p = a.start, n = 0, err = ~0ull;
             for (;;) {
@@ -575,6 +584,7 @@ __global__ __launch_bounds__(256) void scan_count(ScanArgs a) {
         return;
     }
     const int64_t enode = chunk <= a.nc ? chunk_entry(a, chunk) : -1;
+    if (chunk <= a.nc) clear_chunk(a, chunk);
     const uint64_t count = enode >= 0 ? a.ncnt[enode] : 0;
     uint64_t agg;
     const uint64_t ex = block_scan256(count, &agg);
@@ -610,7 +620,7 @@ __global__ __launch_bounds__(256) void scan_count(ScanArgs a) {
     // from global memory (header bytes only), descriptors from the base on; a chunk
     // of more than kEmitHops frames goes to K4b' (LDS)
     if (count > (uint64_t)kEmitHops) {
-        a.slow3[atomicAdd(&a.flags[4], 1u)] = (uint32_t)chunk;
+        a.slow3[atomicAdd(&a.flags[4], 1u)] = (uint32_t)enode;   // the node: its mark is gone
         return;
     }
     uint64_t k = base;
@@ -625,15 +635,21 @@ __global__ __launch_bounds__(256) void scan_count(ScanArgs a) {
 }
 
 // K4b': the chunks of many (tiny) frames, walked in LDS.
+// The last kernel of a scan: it also zeroes flags 0-3 for the next call (no longer
+// read here; flag 4, this kernel's own queue length, is zeroed by the next call's K1,
+// which runs before anything counts into it).  A last-block-done counter instead cost
+// 1,024 same-address atomics per call (~10 us).
 __global__ __launch_bounds__(kScanT) void scan_emit_lds(ScanArgs a) {
     __shared__ uint32_t words[kWords];
     const uint64_t count = __hip_atomic_load(&a.flags[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int i = 0; i < 4; ++i) a.flags[i] = 0;
     for (uint64_t q = blockIdx.x; q < count; q += gridDim.x) {
-        const uint64_t chunk = a.slow3[q], B = chunk * kChunk;
+        const uint64_t node = a.slow3[q], chunk = node / kCand, B = chunk * kChunk;
         load_chunk(a, B, words);
         if (threadIdx.x == 0) {
             uint64_t k = a.cbase[chunk];
-            walk_frames<true>(a, B, words, a.cand[chunk_entry(a, chunk)], -1,
+            walk_frames<true>(a, B, words, a.cand[node], -1,
                               [&](uint64_t p, uint32_t key, uint8_t b0) {
                                   if (k < a.max_frames) {
                                       a.hdr[k] = p;
@@ -721,7 +737,9 @@ hipError_t launch_unmask_scanned(uint8_t* wire, uint64_t len, const uint64_t* hd
 struct ScanScratchSet {
     void* mem = nullptr;
     uint64_t bytes = 0;
+    uint64_t cap = 0;      // chunks the layout is sized for
     uint32_t epoch = 0;
+    bool dirty = false;    // a call did not launch all its kernels: clear before the next
 };
 
 hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start, bool strict, uint64_t* hdr,
@@ -741,10 +759,16 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.b0 = b0;
     a.max_frames = max_frames;
     a.result = result;
-    // scratch layout, per (device, stream)
-    const uint64_t need = chunks * 4 + 32 + nodes + nodes * 8 + nodes * 4 + nodes * 8 + 2 * nodes * 4 + chunks * 8 +
-                          nodes * 4 + nodes * 4 + chunks * 4 + chunks * 8 +
-                          64 * 13;   // + alignment padding of the 13 regions
+    // scratch layout, per (device, stream), sized for `cap` chunks.  The flags, the
+    // candidate counters and the mark bytes must be zero when a call starts: a fresh
+    // allocation is cleared once, and every call leaves them zeroed behind it (K4a and
+    // K4b' clear them), so no clearing launch is needed per call.
+    auto need_for = [](uint64_t c) {
+        const uint64_t n = c * kCand;
+        // flags, ccount, mark, cand, link, nterm, ncnt, status, jp, jq, slow2, slow3, cbase
+        return 64 + c * 4 + n + n * 8 + n * 4 + n * 8 + n * 4 + c * 8 + n * 4 + n * 4 + n * 4 + c * 4 + c * 8 +
+               64 * 13;   // + alignment padding of the 13 regions
+    };
     static std::map<std::pair<int, hipStream_t>, ScanScratchSet> scratch;
     static std::mutex mu;
     int dev = 0;
@@ -753,46 +777,56 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     uint8_t* m;
     int32_t *jp, *jq;   // ping-pong doubling tables
     uint64_t cleared = 0;
+    bool* dirty_flag = nullptr;
     {
         std::lock_guard<std::mutex> g(mu);
         ScanScratchSet& s = scratch[{dev, stream}];
-        if (s.bytes < need) {
+        if (s.cap < chunks) {   // outgrown (earlier allocations are kept: queued work may use them)
+            uint64_t cap = s.cap ? 2 * s.cap : 256;
+            while (cap < chunks) cap *= 2;
+            const uint64_t want = need_for(cap);
             void* p = nullptr;
-            uint64_t want = s.bytes ? 2 * s.bytes : (1ull << 20);
-            while (want < need) want *= 2;
             if ((e = hipMalloc(&p, want)) != hipSuccess) return e;
-            if ((e = hipMemsetAsync(p, 0, want, stream)) != hipSuccess) return e;   // status words: epoch 0
+            if ((e = hipMemsetAsync(p, 0, want, stream)) != hipSuccess) return e;   // zero flags, epoch 0
             s.mem = p;
             s.bytes = want;
+            s.cap = cap;
             s.epoch = 0;
+            s.dirty = false;
         }
         s.epoch = (s.epoch + 1) & 0xFFFF;
         m = (uint8_t*)s.mem;
         auto align = [](uint64_t x) { return (x + 63) & ~63ull; };
+        const uint64_t cap_nodes = s.cap * kCand;
         uint64_t o = 0;
-        // ccount, flags and mark first: one memset clears them per call
-        a.ccount = (uint32_t*)(m + o); o = align(o + chunks * 4);
-        a.flags = (uint32_t*)(m + o); o = align(o + 32);
-        a.mark = m + o; o = align(o + nodes);
+        // flags, ccount and mark first, at capacity offsets: the region left zeroed
+        a.flags = (uint32_t*)(m + o); o = 64;
+        a.ccount = (uint32_t*)(m + o); o = align(o + s.cap * 4);
+        a.mark = m + o; o = align(o + cap_nodes);
         cleared = o;
-        a.cand = (uint64_t*)(m + o); o = align(o + nodes * 8);
-        a.link = (int32_t*)(m + o); o = align(o + nodes * 4);
-        a.nterm = (uint64_t*)(m + o); o = align(o + nodes * 8);
-        a.ncnt = (uint32_t*)(m + o); o = align(o + nodes * 4);
-        a.status = (uint64_t*)(m + o); o = align(o + chunks * 8);
-        jp = (int32_t*)(m + o); o = align(o + nodes * 4);
-        jq = (int32_t*)(m + o); o = align(o + nodes * 4);
-        a.slow2 = (uint32_t*)(m + o); o = align(o + nodes * 4);
-        a.slow3 = (uint32_t*)(m + o); o = align(o + chunks * 4);
+        if (s.dirty) {
+            if ((e = hipMemsetAsync(m, 0, cleared, stream)) != hipSuccess) return e;
+            s.dirty = false;
+        }
+        dirty_flag = &s.dirty;
+        a.cand = (uint64_t*)(m + o); o = align(o + cap_nodes * 8);
+        a.link = (int32_t*)(m + o); o = align(o + cap_nodes * 4);
+        a.nterm = (uint64_t*)(m + o); o = align(o + cap_nodes * 8);
+        a.ncnt = (uint32_t*)(m + o); o = align(o + cap_nodes * 4);
+        a.status = (uint64_t*)(m + o); o = align(o + s.cap * 8);
+        jp = (int32_t*)(m + o); o = align(o + cap_nodes * 4);
+        jq = (int32_t*)(m + o); o = align(o + cap_nodes * 4);
+        a.slow2 = (uint32_t*)(m + o); o = align(o + cap_nodes * 4);
+        a.slow3 = (uint32_t*)(m + o); o = align(o + s.cap * 4);
         a.cbase = (uint64_t*)(m + o);
+        if (o + s.cap * 8 > s.bytes) return hipErrorInvalidValue;   // layout and need_for disagree
         if (s.epoch == 0) {   // epochs wrapped: clear the status words
-            if ((e = hipMemsetAsync(a.status, 0, chunks * 8, stream)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(a.status, 0, s.cap * 8, stream)) != hipSuccess) return e;
             s.epoch = 1;
         }
         a.epoch = s.epoch;
     }
-    // counters + flags, and the default results (no frames, nothing consumed past start)
-    if ((e = hipMemsetAsync(a.ccount, 0, cleared, stream)) != hipSuccess) return e;
+    (void)cleared;
     const unsigned slow_grid = (unsigned)(chunks < 1024 ? chunks : 1024);
     hipLaunchKernelGGL(scan_exits, dim3((unsigned)chunks), dim3(kScanT), 0, stream, a);
     hipLaunchKernelGGL(scan_links, dim3((unsigned)((nodes + 255) / 256)), dim3(256), 0, stream, a);
@@ -807,7 +841,12 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     const unsigned cb = (unsigned)((chunks + 255) / 256);
     hipLaunchKernelGGL(scan_count, dim3(cb), dim3(256), 0, stream, a);
     hipLaunchKernelGGL(scan_emit_lds, dim3(slow_grid), dim3(kScanT), 0, stream, a);
-    return hipGetLastError();
+    e = hipGetLastError();
+    if (e != hipSuccess) {   // a launch failed: the flags may be left set
+        std::lock_guard<std::mutex> g(mu);
+        *dirty_flag = true;
+    }
+    return e;
 }
 
 }  // namespace netc_gpu

@@ -142,6 +142,26 @@ def test_max_frames_cap(torch_cuda):
     run_scan(torch_cuda, wire, max_frames=0)
 
 
+def test_scratch_left_clean_between_calls(torch_cuda):
+    # every call leaves its counters, marks and flags zeroed for the next one on the
+    # same stream (no clearing launch): alternate sizes, the serial fallback, the LDS
+    # fallbacks (tiny frames), an error stop and non-strict mode, each checked
+    rng = np.random.default_rng(21)
+    rec = b"".join(bytes.fromhex("82fe") + (5000 + i % 997).to_bytes(2, "big") + bytes(4) for i in range(997))
+    inner = np.tile(np.frombuffer(rec, dtype=np.uint8), 20)
+    adv, _ = orc.encode_batch(inner, np.array([0, inner.size], dtype=np.uint64), np.array([0], dtype=np.uint32),
+                              None, True)
+    big, _ = _stream(rng, np.full(6000, 1024))
+    small, _ = _stream(rng, rng.integers(0, 3000, 40))
+    tiny, _ = _stream(rng, rng.integers(0, 4, 3000))
+    bad = small.copy()
+    bad[int(np.flatnonzero(bad)[0])] ^= 0x70   # RSV bits on the first header
+    unmasked, _ = _stream(rng, rng.integers(0, 2000, 100), masked=False)
+    for wire, strict in [(big, True), (small, True), (adv, True), (small, True), (tiny, True), (big, True),
+                         (bad, True), (unmasked, False), (big, True), (tiny, True), (small, True)]:
+        run_scan(torch_cuda, wire, strict=strict)
+
+
 def test_adversarial_payload_falls_back(torch_cuda):
     # a big frame masked with the zero key whose payload is a run of valid-looking
     # 8-byte headers (16-bit lengths 5000..5996) that each jump to a different place:
