@@ -343,7 +343,7 @@ __device__ int64_t frame_of(const Args& a, uint64_t P) {
 // the message; utf8_messages() checks them), bytes in no frame, and, with seam set
 // (a chunk's first span), the chunk's first 3 bytes: the bytes before them belong to
 // another wavefront's chunk, which in place may already hold unmasked or still
-// masked bytes -- utf8_seams() checks them once the whole batch is unmasked.
+// masked bytes -- utf8_messages() checks them once the whole batch is unmasked.
 // Errors are rare: their frame lookup is a slow path.
 __device__ __forceinline__ void validate_span(const Args& a, const Table& t, uint64_t A0, u32x4 out, uint32_t prevd,
                                               bool seam, int lane) {
