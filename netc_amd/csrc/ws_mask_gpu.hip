@@ -174,33 +174,47 @@ __device__ __forceinline__ u32x4 span_mask(const Args& a, Table& t, uint64_t A0,
     if (b == 0 && covered) return mask;   // common case: one frame
 
     const uint64_t a_lane = A0 + 16ull * (uint64_t)lane;
-    if (covered && __popcll(b) > 2) {
+    if (__popcll(b) > 2) {
         // Dense span (frames under ~340 B): per lane instead of per boundary.  The
         // frame holding the lane's first byte by a binary search of the table
         // (ds_bpermute), then the frames starting inside the lane's 16 bytes in turn
         // -- one for frames of 16 B or more; the loop runs as long as any lane has
         // another.  Every lane takes part in each ds_bpermute (the loop is uniform).
-        int l = j0;   // entries 0 .. j0 start at or before A0 <= a_lane
+        // More than 63 frame starts in the span (frames under ~16 B): the table is
+        // walked in 63-entry windows, the next window's load in flight while this
+        // one is applied; a lane whose first byte lies before a window's entry 0
+        // keeps what the earlier windows gave it (re-applying the shared entry is
+        // idempotent), so the last window holding entries at or before the lane's
+        // bytes decides, as one table covering the whole span would.
+        u32x4 m = mask;   // the frame holding A0 (same rotation for every lane)
+        for (;;) {
+            const bool more = !(t.tail || t.last >= Aend);   // wave-uniform
+            Table tn;
+            if (more) table_issue(a, tn, t.kb + (kWave - 1), lane);
+            int l = 0;
 #pragma unroll
-        for (int step = 32; step > 0; step >>= 1) {
-            const int c = l + step < kWave ? l + step : kWave - 1;
-            if (bperm64(t.start, c) <= a_lane) l = c;
-        }
-        const uint64_t sl = bperm64(t.start, l);
-        const uint32_t rl = rotr8((uint32_t)__builtin_amdgcn_ds_bpermute(l << 2, (int)t.key), a_lane - sl);
-        u32x4 m = {rl, rl, rl, rl};
-        for (int j = l + 1;; ++j) {
-            const int c = j < kWave ? j : kWave - 1;
-            const uint64_t sj = bperm64(t.start, c);
-            const uint32_t kj = (uint32_t)__builtin_amdgcn_ds_bpermute(c << 2, (int)t.key);
-            const bool in = j < kWave && sj < a_lane + 16;
-            if (in) {
-                const uint32_t rj = rotr8(kj, a_lane - sj);
-                const u32x4 sel = select_from((int64_t)(sj - a_lane));
-                const u32x4 kv = {rj, rj, rj, rj};
-                m = (m & ~sel) | (kv & sel);
+            for (int step = 32; step > 0; step >>= 1)
+                if (bperm64(t.start, l + step) <= a_lane) l += step;
+            const uint64_t sl = bperm64(t.start, l);
+            const uint32_t rl = rotr8((uint32_t)__builtin_amdgcn_ds_bpermute(l << 2, (int)t.key), a_lane - sl);
+            const bool has = sl <= a_lane;   // false: entry 0 starts after the lane's first byte
+            if (has) m = u32x4{rl, rl, rl, rl};
+            for (int j = has ? l + 1 : 0;; ++j) {
+                const int c = j < kWave ? j : kWave - 1;
+                const uint64_t sj = bperm64(t.start, c);
+                const uint32_t kj = (uint32_t)__builtin_amdgcn_ds_bpermute(c << 2, (int)t.key);
+                const bool in = j < kWave && sj < a_lane + 16;
+                if (in) {
+                    const uint32_t rj = rotr8(kj, a_lane - sj);
+                    const u32x4 sel = select_from((int64_t)(sj - a_lane));
+                    const u32x4 kv = {rj, rj, rj, rj};
+                    m = (m & ~sel) | (kv & sel);
+                }
+                if (!__ballot(in)) break;
             }
-            if (!__ballot(in)) break;
+            if (!more) break;
+            t = tn;
+            table_finish(t);
         }
         return m;
     }

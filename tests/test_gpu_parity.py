@@ -136,6 +136,22 @@ def test_dense_spans_per_lane(torch_cuda, shift):
     run_case(torch_cuda, payload, off, synth.random_keys(sizes.size, 32), shift, (shift + 3) % 16)
 
 
+@pytest.mark.parametrize("shift,inplace", [(0, False), (9, False), (3, True)])
+def test_dense_span_windows(torch_cuda, shift, inplace):
+    # 64+ frame starts per 1 KiB span (frames of ~16 B and less): the per-lane path
+    # walks the table in 63-entry windows.  Runs of uniform 16 / 15 / 8 B frames, a
+    # mixed 0..24 B stretch, and a few long frames so spans switch between the
+    # sparse, per-lane and windowed cases.
+    g = synth.rng(57 + shift)
+    parts = [np.full(9000, 16), np.full(7000, 15), g.choice([0, 1, 4, 7, 8, 13, 16, 24], size=12000),
+             np.array([5000, 1, 3000]), np.full(6000, 8), g.integers(0, 3, size=3000), np.full(4000, 17)]
+    sizes = np.concatenate(parts).astype(np.int64)
+    off = frames_from_sizes(sizes, start=5)
+    payload = synth.host_payload(int(off[-1]) + 11, 57)
+    run_case(torch_cuda, payload, off, synth.random_keys(sizes.size, 57), shift, shift, inplace)
+    run_case(torch_cuda, payload, off, synth.random_keys(sizes.size, 58), shift, (shift + 5) % 16)
+
+
 def test_unframed_bytes_pass_through(torch_cuda):
     off = frames_from_sizes([100, 5000, 7, 0, 33333], start=123)
     total = int(off[-1]) + 77
