@@ -27,6 +27,7 @@
 //      the header's vector, which step 2 mapped through the previous frame.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <map>
 #include <mutex>
@@ -149,7 +150,11 @@ struct EncArgs {
     uint64_t* defer;           // queued span starts (W coordinates), capacity defer_cap
     uint32_t* defer_count;
     uint64_t defer_cap;
+    uint32_t all_spans;        // dense batch: the compose launch takes every span (no assembly launch)
 };
+
+// spans per wave trip of the dense compose launch
+static constexpr int kDenseGroup = 4;
 
 // Frame table: lane l holds virtual frame kb + l.  W coordinates = wire byte + wmis.
 struct EncTable {
@@ -355,39 +360,69 @@ __device__ __forceinline__ u32x4 put_header(const EncArgs& a, const FrameInfo& f
     return v;
 }
 
-// Wire vector of this lane for the span at A0, composed from every frame touching
-// it (header bytes and any number of frame edges), starting at table entry l0; the
-// table slides forward as needed.
-__device__ u32x4 compose_vec(const EncArgs& a, EncTable& t, int l0, uint64_t A0, uint64_t W, int lane) {
+// Frame in table entry c (needs entry c + 1), per lane: each lane reads the entry its
+// own walk is at (ds_bpermute; every lane of the wave executes it)
+__device__ __forceinline__ FrameInfo frame_info_lane(const EncArgs& a, const EncTable& t, int c) {
+    FrameInfo f;
+    f.Ws = bperm64(t.start, c);
+    f.We = bperm64(t.start, c + 1);
+    f.o = bperm64(t.poff, c);
+    f.len = bperm64(t.poff, c + 1) - f.o;
+    f.key = (uint32_t)__builtin_amdgcn_ds_bpermute(c << 2, (int)t.key);
+    f.b0 = (uint32_t)__builtin_amdgcn_ds_bpermute(c << 2, (int)t.b0);
+    f.pw = f.Ws + 2 + ext_len(f.len) + (a.masked ? 4 : 0);
+    return f;
+}
+
+// Wire vector of this lane for the span at A0, composed byte-exactly from every frame
+// touching it (header bytes, payload bytes, any number of frame edges).  Per lane: a
+// binary search of the table (entries 0 .. 62, each needs the next one) finds the
+// frame holding the lane's first byte, then the lane walks the frames starting inside
+// its 16 bytes -- at most three (a masked frame is 6 wire bytes or more), so the walk
+// is a few trips whatever the frame count of the span.  A span with more frames than
+// the table holds is walked in 62-entry windows, the next window's load in flight
+// while this one is composed; entry 62 is shared by two windows and its bytes are
+// ORed twice with the same values.  On entry entry 0 of t starts at or before A0.
+__device__ u32x4 compose_vec(const EncArgs& a, EncTable& t, uint64_t A0, uint64_t W, int lane) {
+    constexpr int kLast = kWave - 2;   // last usable entry
     const uint64_t Aend = A0 + kSpan;
     u32x4 out = {0, 0, 0, 0};
-    int l = l0;
     for (;;) {
-        if (l >= kWave - 1) {   // entry l needs entry l + 1: slide the table
-            enc_table_load(a, t, t.kb + l, lane);
-            l = 0;
+        const bool more = !t.tail && t.last < Aend;   // wave-uniform
+        EncTable tn;
+        if (more) enc_table_issue(a, tn, t.kb + kLast, lane);
+        int l = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const int c = l + step;
+            const uint64_t sc = bperm64(t.start, c <= kLast ? c : kLast);   // every lane takes part
+            if (c <= kLast && sc <= W) l = c;
         }
-        const int64_t j = t.kb + l;
-        if (j >= (int64_t)a.n) break;
-        if (j < 0) {
-            ++l;
-            continue;
+        if (readlane64(t.start, 0) > W) l = 0;   // no entry at or before W: walk from entry 0
+        for (int c = l;; ++c) {
+            const int cc = c <= kLast ? c : kLast;
+            const FrameInfo f = frame_info_lane(a, t, cc);
+            const int64_t j = t.kb + cc;
+            const bool active = c <= kLast && j < (int64_t)a.n && f.Ws < W + 16;
+            if (active && j >= 0) {
+                out = put_header(a, f, W, out);
+                // payload bytes [pw, We) of this vector
+                const int64_t plo = (int64_t)(f.pw - W), phi = (int64_t)(f.We - W);
+                if (phi > 0 && plo < 16 && phi > plo) {
+                    const int64_t s0 = (int64_t)f.o - plo;   // src offset of the vector's byte 0
+                    u32x4 v;
+                    if (s0 >= 0 && (uint64_t)s0 + 16 <= a.src_total) v = load_u<false>(a.src + s0);
+                    else v = load_guarded(a, s0, plo < 0 ? 0 : (int)plo, phi > 16 ? 16 : (int)phi);
+                    const uint32_t rk = rotr8(f.key, (uint64_t)(-plo));   // phase of byte 0: W - pw
+                    const u32x4 kv = {rk, rk, rk, rk};
+                    out |= (v ^ kv) & select_range(plo, phi);
+                }
+            }
+            if (!__ballot(active)) break;
         }
-        const FrameInfo f = frame_info(a, t, l);
-        if (f.Ws >= Aend) break;
-        out = put_header(a, f, W, out);
-        // payload bytes [pw, We) of this vector
-        const int64_t plo = (int64_t)(f.pw - W), phi = (int64_t)(f.We - W);
-        if (phi > 0 && plo < 16 && phi > plo) {
-            const int64_t s0 = (int64_t)f.o - plo;   // src offset of the vector's byte 0
-            u32x4 v;
-            if (s0 >= 0 && (uint64_t)s0 + 16 <= a.src_total) v = load_u<false>(a.src + s0);
-            else v = load_guarded(a, s0, plo < 0 ? 0 : (int)plo, phi > 16 ? 16 : (int)phi);
-            const uint32_t rk = rotr8(f.key, (uint64_t)(-plo));   // phase of byte 0: W - pw
-            const u32x4 kv = {rk, rk, rk, rk};
-            out |= (v ^ kv) & select_range(plo, phi);
-        }
-        ++l;
+        if (!more) break;
+        t = tn;
+        enc_table_finish(t);
     }
     return out;
 }
@@ -656,14 +691,34 @@ __global__ __launch_bounds__(256) void encode_queued_kernel(EncArgs a) {
     const uint64_t count = min((uint64_t)*a.defer_count, a.defer_cap);
     const uint64_t wire_total = gptr(a.wo)[a.n];
     const uint64_t wlo = a.wmis, whi = a.wmis + wire_total;
+    if (a.all_spans) {
+        // dense batch: no assembly launch before this one -- every span is composed
+        // here, so no header fixups either.  A wave takes kDenseGroup consecutive
+        // spans per trip: one search for the first, then each next span's table is
+        // re-based at the frame holding its start (one load, no search).
+        const uint64_t nspans = (whi + kSpan - 1) / kSpan;
+        const uint64_t ngroups = (nspans + kDenseGroup - 1) / kDenseGroup;
+        for (uint64_t g = wave; g < ngroups; g += nwaves) {
+            uint64_t A0 = g * kDenseGroup * kSpan;
+            EncTable t;
+            enc_table_load(a, t, enc_locate(a, A0, wire_total, lane), lane);
+            for (int s = 0; s < kDenseGroup && A0 < whi; ++s, A0 += kSpan) {
+                const int j = __popcll(__ballot(t.start <= A0)) - 1;   // >= 0: entry 0 is at or before A0
+                if (j > 0 && !t.tail) enc_table_load(a, t, t.kb + j, lane);
+                const uint64_t W = A0 + 16ull * (uint64_t)lane;
+                const u32x4 v = compose_vec(a, t, A0, W, lane);
+                if (W < whi) store_wire<false>(a, W, v, wlo, whi);
+            }
+        }
+        return;
+    }
     for (uint64_t q = wave; q < count; q += nwaves) {
         const uint64_t A0 = a.defer[q];
         if (!ENC_OK(3, A0, whi)) continue;
         EncTable t;
         enc_table_load(a, t, enc_locate(a, A0, wire_total, lane), lane);
-        const int l0 = __popcll(__ballot(t.start <= A0)) - 1;
         const uint64_t W = A0 + 16ull * (uint64_t)lane;
-        const u32x4 v = compose_vec(a, t, l0, A0, W, lane);
+        const u32x4 v = compose_vec(a, t, A0, W, lane);
         if (W < whi) store_wire<false>(a, W, v, wlo, whi);
     }
     const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
@@ -752,6 +807,14 @@ hipError_t launch_wire_offsets(const uint64_t* off, uint64_t n, bool masked, uin
     return launch_scan(off, n, masked, wo, stream, sc);
 }
 
+// mean payload bytes per frame under which a batch takes the dense compose path
+// (NETC_ENC_DENSE_BYTES overrides, read per call: measurement and the parity tests
+// run both paths over the same batches; 0 = never dense)
+static uint64_t dense_bytes() {
+    const char* e = getenv("NETC_ENC_DENSE_BYTES");
+    return e ? (uint64_t)strtoull(e, nullptr, 10) : (uint64_t)80;
+}
+
 template <int U>
 static hipError_t launch_enc_u(EncArgs a, uint64_t wire_bound, bool nt, int max_blocks, hipStream_t stream) {
     const uint64_t nwin = (a.wmis + wire_bound + kSpan * U - 1) / (kSpan * U);
@@ -760,6 +823,12 @@ static hipError_t launch_enc_u(EncArgs a, uint64_t wire_bound, bool nt, int max_
     const uint64_t want = (nwin + 3) / 4;
     const int blocks = (int)(want < cap ? want : cap);
     if (blocks <= 0) return hipSuccess;
+    if (a.all_spans) {
+        const uint64_t groups = (nwin * U + kDenseGroup - 1) / kDenseGroup;
+        const uint64_t gb = (groups + 3) / 4;   // one group per wavefront, 4 per block
+        hipLaunchKernelGGL(encode_queued_kernel, dim3((unsigned)(gb < 8192 ? gb : 8192)), dim3(256), 0, stream, a);
+        return hipGetLastError();
+    }
     if (nt) hipLaunchKernelGGL((encode_frames_kernel<U, true>), dim3(blocks), dim3(256), 0, stream, a);
     else hipLaunchKernelGGL((encode_frames_kernel<U, false>), dim3(blocks), dim3(256), 0, stream, a);
     hipError_t e = hipGetLastError();
@@ -796,6 +865,9 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     a.defer = sc.defer;
     a.defer_count = (uint32_t*)(sc.defer + sc.defer_cap);
     a.defer_cap = sc.defer_cap;
+    // frames averaging under dense_bytes() of payload: every span is composed per lane
+    // (the vector path would queue most spans and leave a header fixup per frame)
+    a.all_spans = src_total < dense_bytes() * n ? 1u : 0u;
     const bool nt = cfg.flags < 0 || (cfg.flags & (kNtLoads | kNtStores));
     // U = 2 KiB chunks (124 VGPRs: 4 wavefronts per SIMD; measured faster than 4 KiB at
     // configs 2 and 4) unless netc_gpu_tune's unroll is 8, which selects 4 KiB

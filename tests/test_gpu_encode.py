@@ -216,3 +216,22 @@ def test_launch_shapes(torch_cuda, unroll, max_blocks):
         run_encode(torch_cuda, payload, off, keys, masked=False)
     finally:
         nm.tune()
+
+
+@pytest.mark.parametrize("dense", ["0", "100000"])
+@pytest.mark.parametrize("masked", [True, False])
+def test_both_compose_paths(torch_cuda, monkeypatch, dense, masked):
+    # the same batches through the vector path + queued compose (NETC_ENC_DENSE_BYTES=0)
+    # and through the dense per-lane compose of every span (threshold above any mean):
+    # uniform 16 / 8 / 1 B frames, empty frames, 0..30 B mixes, and long frames between
+    monkeypatch.setenv("NETC_ENC_DENSE_BYTES", dense)
+    rng = np.random.default_rng(21)
+    parts = [np.full(3000, 16), np.full(2000, 8), rng.integers(0, 31, 4000), np.full(1500, 1),
+             np.array([126, 65536, 0, 0, 125, 3000]), np.zeros(700, dtype=np.int64), rng.integers(100, 300, 200)]
+    sizes = np.concatenate(parts)
+    off = frames_from_sizes(sizes, start=3)
+    payload = _payload(rng, int(off[-1]) + 9)
+    keys = rng.integers(0, 2**32, len(sizes), dtype=np.uint64).astype(np.uint32)
+    h0 = rng.choice(np.array([0x81, 0x82, 0x01, 0x00, 0x80, 0x89], dtype=np.uint8), len(sizes))
+    run_encode(torch_cuda, payload, off, keys, header0=h0, masked=masked, wire_shift=5, src_shift=11)
+    run_encode(torch_cuda, payload, off, keys, masked=masked)
