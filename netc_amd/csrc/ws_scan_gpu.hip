@@ -189,73 +189,6 @@ __device__ void load_chunk(const ScanArgs& a, uint64_t B, uint32_t* words) {
     __syncthreads();
 }
 
-// K2' / K4b': every position of the chunk linked (local index, or a terminal) and
-// pointer-jumped until every link is terminal -- EXIT(x) with x >= chunk end, END(p)
-// or DEAD(p) -- with hc = the frames (hops) on the way.
-__device__ void chunk_links_counted(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t* lk,
-                                    uint16_t* hc) {
-    const int tid = threadIdx.x;
-    const uint64_t Bend = B + kChunk;
-    // a position that cannot start a header ends its chain right there (exact
-    // terminals: K4 reports where the chain ends): END past the stream, else DEAD
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        const uint64_t pos = B + (uint64_t)(k * kScanT + tid);
-        lk[k * kScanT + tid] = pos + 2 > a.len ? term(kEnd, pos) : term(kDead, pos);
-        hc[k * kScanT + tid] = 0;
-    }
-    const int i0 = kPer * tid;
-    uint32_t w[kPer / 4 + 1];
-#pragma unroll
-    for (int k = 0; k < kPer / 4 + 1; ++k) w[k] = words[i0 / 4 + k];
-    auto byte_at = [&](int j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
-    uint32_t cand = 0;
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const uint32_t first = byte_at(j), second = byte_at(j + 1), opcode = first & 0x0F;
-        const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
-        const bool reject = a.strict && (!(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80)));
-        if (!reject && B + i0 + j >= a.start) cand |= 1u << j;
-    }
-    __syncthreads();
-    while (cand) {
-        const int j = __builtin_ctz(cand);
-        cand &= cand - 1;
-        const int i = i0 + j;
-        uint64_t v = parse_at(a, B + i, window_at(words, i), nullptr, nullptr);
-        if (!(v & kTerm)) {
-            v = v < Bend ? v - B : term(kExit, v);
-            hc[i] = 1;
-        }
-        lk[i] = v;
-    }
-    __syncthreads();
-    for (;;) {
-        uint64_t nv[kPer];
-        uint16_t nh[kPer];
-        int changed = 0;
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int i = k * kScanT + tid;
-            const uint64_t v = lk[i];
-            nv[k] = v;
-            nh[k] = hc[i];
-            if (!(v & kTerm)) {
-                nv[k] = lk[v];
-                nh[k] = (uint16_t)(hc[i] + hc[v]);
-                changed |= !(nv[k] & kTerm);
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            lk[k * kScanT + tid] = nv[k];
-            hc[k * kScanT + tid] = nh[k];
-        }
-        if (!__syncthreads_or(changed)) break;
-    }
-}
-
 // 16 stream bytes from p (zero past len) straight from global memory: the walks
 // of K2 and K4 touch only the header bytes of the frames they visit,
 // so they read them where they lie instead of staging the chunk in LDS.
@@ -438,6 +371,53 @@ __device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint
     a.ncnt[node] = cnt;
 }
 
+// K2' / K4b': every position of the chunk that can start a header (strict: passes
+// the quick check; else every position) parsed once into a 16-bit in-chunk link
+// (kNoLink: the chain ends or leaves the chunk there), then four doubling passes:
+// returns the 16-hop links (l1 keeps the 1-hop ones).  The caller has loaded words.
+static constexpr uint16_t kNoLink = 0xFFFF;
+static constexpr int kStride = 16;   // hops per 16-hop link
+
+__device__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const uint32_t* words, uint16_t* l1,
+                                         uint16_t* lj, uint16_t* lk16) {
+    const int tid = threadIdx.x;
+    const uint64_t Bend = B + kChunk;
+    const int i0 = kPer * tid;
+    uint32_t w[kPer / 4 + 1];
+#pragma unroll
+    for (int k = 0; k < kPer / 4 + 1; ++k) w[k] = words[i0 / 4 + k];
+    auto byte_at = [&](int j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t first = byte_at(j), second = byte_at(j + 1), opcode = first & 0x0F;
+        const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
+        const bool reject =
+            a.strict && (!(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80)));
+        uint16_t lnk = kNoLink;
+        if (!reject) {
+            const uint64_t v = parse_at(a, B + i0 + j, window_at(words, i0 + j), nullptr, nullptr);
+            if (!(v & kTerm) && v < Bend) lnk = (uint16_t)(v - B);
+        }
+        l1[i0 + j] = lnk;
+    }
+    __syncthreads();
+    const uint16_t* src = l1;
+    uint16_t* dst = lj;
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {   // 2, 4, 8, 16 hops
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int i = k * kScanT + tid;
+            const uint16_t x = src[i];
+            dst[i] = x == kNoLink ? kNoLink : src[x];
+        }
+        __syncthreads();
+        src = dst;
+        dst = dst == lj ? lk16 : lj;
+    }
+    return src;
+}
+
 // K2: one thread per node (candidate slot): the candidate entry's chain walked from
 // global memory to the candidate it exits to; a chain longer than kWalkHops goes
 // to K2' (LDS).  Unused slots hold stale values from earlier calls: dead ends.
@@ -463,19 +443,37 @@ __global__ __launch_bounds__(256) void scan_links(ScanArgs a) {
     link_node(a, node, x, v, cnt);
 }
 
-// K2': the nodes K2 left: their chunk pointer-jumped in LDS.
+// K2': the nodes K2 left (chains of more than 2 kWalkHops frames in the chunk): the
+// chunk's 16-hop links built in LDS, then one thread walks them from the entry --
+// count / 16 + at most 15 hops -- and re-parses the last header for the exact
+// terminal (EXIT to the next chunk, END or DEAD) and whether it adds a frame.
 __global__ __launch_bounds__(kScanT) void scan_links_lds(ScanArgs a) {
     __shared__ uint32_t words[kWords];
-    __shared__ uint64_t lk[kChunk];
-    __shared__ uint16_t hc[kChunk];
+    __shared__ uint16_t l1[kChunk];
+    __shared__ uint16_t lj[kChunk];
+    __shared__ uint16_t lk16[kChunk];
     const uint64_t count = __hip_atomic_load(&a.flags[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (uint64_t q = blockIdx.x; q < count; q += gridDim.x) {
         const uint64_t node = a.slow2[q], chunk = node / kCand, B = chunk * kChunk;
         load_chunk(a, B, words);
-        chunk_links_counted(a, B, words, lk, hc);
+        const uint16_t* l16 = chunk_links16(a, B, words, l1, lj, lk16);
         if (threadIdx.x == 0) {
-            const uint64_t x = a.cand[node];
-            link_node(a, node, x, lk[x - B], hc[x - B]);
+            const uint64_t x = a.cand[node];   // in [B, B + kChunk): K2's walk started there
+            uint32_t p = (uint32_t)(x - B), hops = 0;
+            while (l16[p] != kNoLink) {
+                p = l16[p];
+                hops += kStride;
+            }
+            while (l1[p] != kNoLink) {
+                p = l1[p];
+                ++hops;
+            }
+            uint64_t v = parse_at(a, B + p, window_at(words, (int)p), nullptr, nullptr);
+            if (!(v & kTerm)) {   // the last frame of the chunk: its successor is past the chunk
+                v = term(kExit, v);
+                ++hops;
+            }
+            link_node(a, node, x, v, hops);
         }
         __syncthreads();
     }
@@ -634,30 +632,64 @@ __global__ __launch_bounds__(256) void scan_count(ScanArgs a) {
     });
 }
 
-// K4b': the chunks of many (tiny) frames, walked in LDS.
+// K4b': the chunks of many (tiny) frames, emitted from LDS in parallel.  Every
+// position of the chunk that can start a header is parsed once into a 16-bit
+// in-chunk link (kNoLink: the chain ends or leaves the chunk there); four doubling
+// passes make the 16-hop links; one thread walks those from the entry, leaving an
+// anchor every 16 frames; then thread t walks 16 frames from anchor t and writes
+// their descriptors from index cbase + 16 t.  Serial depth count / 16 + 16 hops
+// instead of count (a 4 KiB chunk of 16-B frames holds ~186).
 // The last kernel of a scan: it also zeroes flags 0-3 for the next call (no longer
 // read here; flag 4, this kernel's own queue length, is zeroed by the next call's K1,
 // which runs before anything counts into it).  A last-block-done counter instead cost
 // 1,024 same-address atomics per call (~10 us).
 __global__ __launch_bounds__(kScanT) void scan_emit_lds(ScanArgs a) {
     __shared__ uint32_t words[kWords];
+    __shared__ uint16_t l1[kChunk];    // next header (local index) or kNoLink
+    __shared__ uint16_t lj[kChunk];    // 2^k hops (ping)
+    __shared__ uint16_t lk16[kChunk];  // 2^k hops (pong); 16 hops after the last pass
+    __shared__ uint16_t anchor[kChunk / kStride + 1];
+    __shared__ int nanchor;
+    const int tid = threadIdx.x;
     const uint64_t count = __hip_atomic_load(&a.flags[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (blockIdx.x == 0 && threadIdx.x == 0)
+    if (blockIdx.x == 0 && tid == 0)
         for (int i = 0; i < 4; ++i) a.flags[i] = 0;
     for (uint64_t q = blockIdx.x; q < count; q += gridDim.x) {
-        const uint64_t node = a.slow3[q], chunk = node / kCand, B = chunk * kChunk;
-        load_chunk(a, B, words);
-        if (threadIdx.x == 0) {
-            uint64_t k = a.cbase[chunk];
-            walk_frames<true>(a, B, words, a.cand[node], -1,
-                              [&](uint64_t p, uint32_t key, uint8_t b0) {
-                                  if (k < a.max_frames) {
-                                      a.hdr[k] = p;
-                                      a.keys[k] = key;
-                                      a.b0[k] = b0;
-                                  }
-                                  ++k;
-                              });
+        const uint64_t node = a.slow3[q], chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
+        load_chunk(a, B, words);   // ends with a barrier
+        const uint16_t* l16 = chunk_links16(a, B, words, l1, lj, lk16);
+        if (tid == 0) {
+            int na = 0;
+            const uint64_t e = a.cand[node];
+            if (e < Bend) {
+                uint16_t p = (uint16_t)(e - B);
+                anchor[na++] = p;
+                while (na <= (int)(kChunk / kStride) && l16[p] != kNoLink) {
+                    p = l16[p];
+                    anchor[na++] = p;
+                }
+            }
+            nanchor = na;
+        }
+        __syncthreads();
+        const int na = nanchor;
+        const uint64_t base = a.cbase[chunk];
+        for (int t = tid; t < na; t += kScanT) {
+            uint64_t k = base + (uint64_t)t * kStride;
+            uint64_t pos = B + anchor[t];
+            for (int h = 0; h < kStride && pos < Bend; ++h) {
+                uint32_t key;
+                uint8_t b0;
+                const uint64_t v = parse_at(a, pos, window_at(words, (int)(pos - B)), &key, &b0);
+                if (v & kTerm) break;
+                if (k < a.max_frames) {
+                    a.hdr[k] = pos;
+                    a.keys[k] = key;
+                    a.b0[k] = b0;
+                }
+                ++k;
+                pos = v;
+            }
         }
         __syncthreads();
     }

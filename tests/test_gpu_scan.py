@@ -220,3 +220,21 @@ def test_repeat_calls_same_stream(torch_cuda):
     for i in range(5):
         wire, _ = _stream(rng, rng.integers(0, 4000, 300 + 50 * i))
         run_scan(torch_cuda, wire)
+
+
+@pytest.mark.parametrize("masked,strict", [(True, True), (False, False)])
+def test_dense_chunks_parallel_walks(torch_cuda, masked, strict):
+    # chunks of 64+ frames (K2' and K4b': 16-hop links, anchored emit): uniform 16 / 8 B
+    # payloads, empty frames (2-byte unmasked / 6-byte masked wire frames: up to 2,048
+    # per chunk), mixes, and a long frame between; then truncations and start offsets
+    # inside the dense stretch and a frame cap that ends inside an anchor's run
+    rng = np.random.default_rng(41 + masked)
+    sizes = np.concatenate([np.full(3000, 16), np.full(2500, 8), np.zeros(3000, dtype=np.int64),
+                            rng.integers(0, 20, 3000), [70000], np.full(1000, 1)])
+    wire, wo = _stream(rng, sizes, masked=masked)
+    assert run_scan(torch_cuda, wire, strict=strict) == sizes.size
+    for cut in (int(wo[3100]) + 1, int(wo[6000]), int(wo[9001]) + 3):
+        run_scan(torch_cuda, wire[:cut], strict=strict)
+    for s in (int(wo[17]), int(wo[5600])):
+        run_scan(torch_cuda, wire, start=s, strict=strict)
+    run_scan(torch_cuda, wire, strict=strict, max_frames=4123)
