@@ -28,6 +28,7 @@
 // walk in K4 instead — same results, slower.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <map>
 #include <mutex>
@@ -774,6 +775,15 @@ struct ScanScratchSet {
     bool dirty = false;    // a call did not launch all its kernels: clear before the next
 };
 
+
+// workgroups of the LDS kernels K2' / K4b' (each loops over its queue); the queue
+// lengths are only known on the device.  NETC_SCAN_SLOW_BLOCKS overrides (measurement).
+static uint64_t slow_blocks() {
+    const char* e = getenv("NETC_SCAN_SLOW_BLOCKS");
+    const uint64_t v = e ? (uint64_t)strtoull(e, nullptr, 10) : 0;
+    return v ? v : 1024;
+}
+
 hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start, bool strict, uint64_t* hdr,
                               uint32_t* keys, uint8_t* b0, uint64_t max_frames, uint64_t* result,
                               hipStream_t stream) {
@@ -859,7 +869,8 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         a.epoch = s.epoch;
     }
     (void)cleared;
-    const unsigned slow_grid = (unsigned)(chunks < 1024 ? chunks : 1024);
+    const uint64_t slow_cap = slow_blocks();
+    const unsigned slow_grid = (unsigned)(chunks < slow_cap ? chunks : slow_cap);
     hipLaunchKernelGGL(scan_exits, dim3((unsigned)chunks), dim3(kScanT), 0, stream, a);
     hipLaunchKernelGGL(scan_links, dim3((unsigned)((nodes + 255) / 256)), dim3(256), 0, stream, a);
     hipLaunchKernelGGL(scan_links_lds, dim3(slow_grid), dim3(kScanT), 0, stream, a);
