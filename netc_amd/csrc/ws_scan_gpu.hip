@@ -68,6 +68,10 @@ struct ScanArgs {
     uint32_t* slow2;       // K2 nodes left to the LDS kernel ((nc + 1) * kCand)
     uint32_t* slow3;       // K4 chunks of many frames left to the LDS emit kernel (nc + 1)
     uint64_t* cbase;       // K4: index of each chunk's first frame (nc + 1)
+    uint16_t* anc;         // K2' -> K4b': 16-frame anchors of K2' slot q at anc[q * kAncSlot]
+    uint32_t* anc_n;       // anchors in slot q
+    uint32_t* anq;         // per node: its K2' slot (this call), or ~0 when none was left
+    uint64_t anc_cap;      // anchor slots
     uint64_t* status;      // chained-scan status words (nc + 1)
     uint32_t epoch;
     uint64_t* hdr;         // outputs
@@ -378,6 +382,8 @@ __device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint
 // returns the 16-hop links (l1 keeps the 1-hop ones).  The caller has loaded words.
 static constexpr uint16_t kNoLink = 0xFFFF;
 static constexpr int kStride = 16;   // hops per 16-hop link
+static constexpr int kAncMax = (int)(kChunk / kStride) + 1;   // anchors of one chain in a chunk
+static constexpr int kAncSlot = kAncMax + 1;                  // uint16 per slot (4-byte multiple)
 
 __device__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const uint32_t* words, uint16_t* l1,
                                          uint16_t* lj, uint16_t* lk16) {
@@ -461,10 +467,19 @@ __global__ __launch_bounds__(kScanT) void scan_links_lds(ScanArgs a) {
         if (threadIdx.x == 0) {
             const uint64_t x = a.cand[node];   // in [B, B + kChunk): K2's walk started there
             uint32_t p = (uint32_t)(x - B), hops = 0;
+            // the walk's positions every 16 frames are K4b's anchors if this node turns out
+            // to be its chunk's true entry: kept in slot q while slots last
+            const bool keep = q < a.anc_cap;
+            uint16_t* anc = a.anc + (keep ? q : 0) * kAncSlot;
+            int na = 0;
+            if (keep) anc[na++] = (uint16_t)p;
             while (l16[p] != kNoLink) {
                 p = l16[p];
                 hops += kStride;
+                if (keep && na < kAncMax) anc[na++] = (uint16_t)p;
             }
+            if (keep) a.anc_n[q] = (uint32_t)na;
+            a.anq[node] = keep ? (uint32_t)q : ~0u;
             while (l1[p] != kNoLink) {
                 p = l1[p];
                 ++hops;
@@ -657,6 +672,30 @@ __global__ __launch_bounds__(kScanT) void scan_emit_lds(ScanArgs a) {
         for (int i = 0; i < 4; ++i) a.flags[i] = 0;
     for (uint64_t q = blockIdx.x; q < count; q += gridDim.x) {
         const uint64_t node = a.slow3[q], chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
+        const uint32_t slot = a.anq[node];   // K2' left this node's anchors (block-uniform)
+        if (slot != ~0u) {
+            // thread t: the 16 frames from anchor t, header bytes from global memory
+            const int na = (int)a.anc_n[slot];
+            const uint64_t base = a.cbase[chunk];
+            for (int t = tid; t < na; t += kScanT) {
+                uint64_t k = base + (uint64_t)t * kStride;
+                uint64_t pos = B + a.anc[(uint64_t)slot * kAncSlot + t];
+                for (int h = 0; h < kStride && pos < Bend; ++h) {
+                    uint32_t key;
+                    uint8_t b0;
+                    const uint64_t v = parse_at(a, pos, window_global(a, pos), &key, &b0);
+                    if (v & kTerm) break;
+                    if (k < a.max_frames) {
+                        a.hdr[k] = pos;
+                        a.keys[k] = key;
+                        a.b0[k] = b0;
+                    }
+                    ++k;
+                    pos = v;
+                }
+            }
+            continue;
+        }
         load_chunk(a, B, words);   // ends with a barrier
         const uint16_t* l16 = chunk_links16(a, B, words, l1, lj, lk16);
         if (tid == 0) {
@@ -807,9 +846,10 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     // K4b' clear them), so no clearing launch is needed per call.
     auto need_for = [](uint64_t c) {
         const uint64_t n = c * kCand;
-        // flags, ccount, mark, cand, link, nterm, ncnt, status, jp, jq, slow2, slow3, cbase
+        // flags, ccount, mark, cand, link, nterm, ncnt, status, jp, jq, slow2, slow3, cbase,
+        // anc (one anchor slot per chunk), anc_n, anq
         return 64 + c * 4 + n + n * 8 + n * 4 + n * 8 + n * 4 + c * 8 + n * 4 + n * 4 + n * 4 + c * 4 + c * 8 +
-               64 * 13;   // + alignment padding of the 13 regions
+               c * kAncSlot * 2 + c * 4 + n * 4 + 64 * 16;   // + alignment padding of the 16 regions
     };
     static std::map<std::pair<int, hipStream_t>, ScanScratchSet> scratch;
     static std::mutex mu;
@@ -860,8 +900,12 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         jq = (int32_t*)(m + o); o = align(o + cap_nodes * 4);
         a.slow2 = (uint32_t*)(m + o); o = align(o + cap_nodes * 4);
         a.slow3 = (uint32_t*)(m + o); o = align(o + s.cap * 4);
-        a.cbase = (uint64_t*)(m + o);
-        if (o + s.cap * 8 > s.bytes) return hipErrorInvalidValue;   // layout and need_for disagree
+        a.cbase = (uint64_t*)(m + o); o = align(o + s.cap * 8);
+        a.anc = (uint16_t*)(m + o); o = align(o + s.cap * kAncSlot * 2);
+        a.anc_n = (uint32_t*)(m + o); o = align(o + s.cap * 4);
+        a.anq = (uint32_t*)(m + o);
+        a.anc_cap = s.cap;
+        if (o + cap_nodes * 4 > s.bytes) return hipErrorInvalidValue;   // layout and need_for disagree
         if (s.epoch == 0) {   // epochs wrapped: clear the status words
             if ((e = hipMemsetAsync(a.status, 0, s.cap * 8, stream)) != hipSuccess) return e;
             s.epoch = 1;
