@@ -379,11 +379,13 @@ __device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint
 // K2' / K4b': every position of the chunk that can start a header (strict: passes
 // the quick check; else every position) parsed once into a 16-bit in-chunk link
 // (kNoLink: the chain ends or leaves the chunk there), then four doubling passes:
-// returns the 16-hop links (l1 keeps the 1-hop ones).  The caller has loaded words.
+// returns the 16-hop links (l1 keeps the 1-hop ones, lj the 8-hop ones).  The caller
+// has loaded words.
 static constexpr uint16_t kNoLink = 0xFFFF;
 static constexpr int kStride = 16;   // hops per 16-hop link
-static constexpr int kAncMax = (int)(kChunk / kStride) + 1;   // anchors of one chain in a chunk
-static constexpr int kAncSlot = kAncMax + 1;                  // uint16 per slot (4-byte multiple)
+static constexpr int kAncStride = 8;                              // frames per K2' anchor
+static constexpr int kAncMax = (int)(kChunk / 2 / kAncStride) + 1;   // a frame is 2 bytes or more
+static constexpr int kAncSlot = kAncMax + 1;                         // uint16 per slot (4-byte multiple)
 
 __device__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const uint32_t* words, uint16_t* l1,
                                          uint16_t* lj, uint16_t* lk16) {
@@ -463,19 +465,20 @@ __global__ __launch_bounds__(kScanT) void scan_links_lds(ScanArgs a) {
     for (uint64_t q = blockIdx.x; q < count; q += gridDim.x) {
         const uint64_t node = a.slow2[q], chunk = node / kCand, B = chunk * kChunk;
         load_chunk(a, B, words);
-        const uint16_t* l16 = chunk_links16(a, B, words, l1, lj, lk16);
+        chunk_links16(a, B, words, l1, lj, lk16);
+        const uint16_t* l8 = lj;   // the 8-hop links (the pass before the last)
         if (threadIdx.x == 0) {
             const uint64_t x = a.cand[node];   // in [B, B + kChunk): K2's walk started there
             uint32_t p = (uint32_t)(x - B), hops = 0;
-            // the walk's positions every 16 frames are K4b's anchors if this node turns out
+            // the walk's positions every 8 frames are K4b's anchors if this node turns out
             // to be its chunk's true entry: kept in slot q while slots last
             const bool keep = q < a.anc_cap;
             uint16_t* anc = a.anc + (keep ? q : 0) * kAncSlot;
             int na = 0;
             if (keep) anc[na++] = (uint16_t)p;
-            while (l16[p] != kNoLink) {
-                p = l16[p];
-                hops += kStride;
+            while (l8[p] != kNoLink) {
+                p = l8[p];
+                hops += kAncStride;
                 if (keep && na < kAncMax) anc[na++] = (uint16_t)p;
             }
             if (keep) a.anc_n[q] = (uint32_t)na;
@@ -648,6 +651,42 @@ __global__ __launch_bounds__(256) void scan_count(ScanArgs a) {
     });
 }
 
+// K4b' for the chunks whose entry K2' left anchors for (all of them unless the anchor
+// slots ran out): one wavefront per chunk, lane t parses the kAncStride frames from
+// anchor t, header bytes straight from global memory, and writes their descriptors
+// from index cbase + kAncStride t.  No LDS: the chunk is never reloaded.  Runs at the
+// start of scan_emit_lds (one launch fewer: at C2 shape nothing is queued at all).
+__device__ void emit_anchored(const ScanArgs& a, uint64_t count) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / kWave);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    for (uint64_t q = wave; q < count; q += nwaves) {
+        const uint64_t node = a.slow3[q];
+        const uint32_t slot = a.anq[node];
+        if (slot == ~0u) continue;   // scan_emit_lds takes it
+        const uint64_t chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
+        const int na = (int)a.anc_n[slot];
+        const uint64_t base = a.cbase[chunk];
+        for (int t = lane; t < na; t += kWave) {
+            uint64_t k = base + (uint64_t)t * kAncStride;
+            uint64_t pos = B + a.anc[(uint64_t)slot * kAncSlot + t];
+            for (int h = 0; h < kAncStride && pos < Bend; ++h) {
+                uint32_t key;
+                uint8_t b0;
+                const uint64_t v = parse_at(a, pos, window_global(a, pos), &key, &b0);
+                if (v & kTerm) break;
+                if (k < a.max_frames) {
+                    a.hdr[k] = pos;
+                    a.keys[k] = key;
+                    a.b0[k] = b0;
+                }
+                ++k;
+                pos = v;
+            }
+        }
+    }
+}
+
 // K4b': the chunks of many (tiny) frames, emitted from LDS in parallel.  Every
 // position of the chunk that can start a header is parsed once into a 16-bit
 // in-chunk link (kNoLink: the chain ends or leaves the chunk there); four doubling
@@ -670,32 +709,10 @@ __global__ __launch_bounds__(kScanT) void scan_emit_lds(ScanArgs a) {
     const uint64_t count = __hip_atomic_load(&a.flags[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (blockIdx.x == 0 && tid == 0)
         for (int i = 0; i < 4; ++i) a.flags[i] = 0;
+    emit_anchored(a, count);
     for (uint64_t q = blockIdx.x; q < count; q += gridDim.x) {
         const uint64_t node = a.slow3[q], chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
-        const uint32_t slot = a.anq[node];   // K2' left this node's anchors (block-uniform)
-        if (slot != ~0u) {
-            // thread t: the 16 frames from anchor t, header bytes from global memory
-            const int na = (int)a.anc_n[slot];
-            const uint64_t base = a.cbase[chunk];
-            for (int t = tid; t < na; t += kScanT) {
-                uint64_t k = base + (uint64_t)t * kStride;
-                uint64_t pos = B + a.anc[(uint64_t)slot * kAncSlot + t];
-                for (int h = 0; h < kStride && pos < Bend; ++h) {
-                    uint32_t key;
-                    uint8_t b0;
-                    const uint64_t v = parse_at(a, pos, window_global(a, pos), &key, &b0);
-                    if (v & kTerm) break;
-                    if (k < a.max_frames) {
-                        a.hdr[k] = pos;
-                        a.keys[k] = key;
-                        a.b0[k] = b0;
-                    }
-                    ++k;
-                    pos = v;
-                }
-            }
-            continue;
-        }
+        if (a.anq[node] != ~0u) continue;   // anchored: emit_anchored wrote it
         load_chunk(a, B, words);   // ends with a barrier
         const uint16_t* l16 = chunk_links16(a, B, words, l1, lj, lk16);
         if (tid == 0) {
@@ -905,6 +922,10 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         a.anc_n = (uint32_t*)(m + o); o = align(o + s.cap * 4);
         a.anq = (uint32_t*)(m + o);
         a.anc_cap = s.cap;
+        if (const char* env = getenv("NETC_SCAN_ANCHOR_SLOTS")) {   // tests: fewer slots (0: none)
+            const uint64_t v = (uint64_t)strtoull(env, nullptr, 10);
+            a.anc_cap = v < a.anc_cap ? v : a.anc_cap;
+        }
         if (o + cap_nodes * 4 > s.bytes) return hipErrorInvalidValue;   // layout and need_for disagree
         if (s.epoch == 0) {   // epochs wrapped: clear the status words
             if ((e = hipMemsetAsync(a.status, 0, s.cap * 8, stream)) != hipSuccess) return e;

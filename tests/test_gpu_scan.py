@@ -222,12 +222,17 @@ def test_repeat_calls_same_stream(torch_cuda):
         run_scan(torch_cuda, wire)
 
 
+@pytest.mark.parametrize("slots", [None, "0", "3"])
 @pytest.mark.parametrize("masked,strict", [(True, True), (False, False)])
-def test_dense_chunks_parallel_walks(torch_cuda, masked, strict):
+def test_dense_chunks_parallel_walks(torch_cuda, monkeypatch, masked, strict, slots):
     # chunks of 64+ frames (K2' and K4b': 16-hop links, anchored emit): uniform 16 / 8 B
     # payloads, empty frames (2-byte unmasked / 6-byte masked wire frames: up to 2,048
     # per chunk), mixes, and a long frame between; then truncations and start offsets
-    # inside the dense stretch and a frame cap that ends inside an anchor's run
+    # inside the dense stretch and a frame cap that ends inside an anchor's run.  slots:
+    # K2' anchor slots (None: one per chunk, K4b' emits from them; "0": none, every
+    # dense chunk goes through the LDS emit; "3": both paths in one call)
+    if slots is not None:
+        monkeypatch.setenv("NETC_SCAN_ANCHOR_SLOTS", slots)
     rng = np.random.default_rng(41 + masked)
     sizes = np.concatenate([np.full(3000, 16), np.full(2500, 8), np.zeros(3000, dtype=np.int64),
                             rng.integers(0, 20, 3000), [70000], np.full(1000, 1)])
