@@ -4,8 +4,8 @@
 # Run through gpurun from the repo root; every GPU step is time-limited.
 set -o pipefail
 mkdir -p gpurun_out/${TAG:-r01v}
-for g in 1024 2048 4096 16384; do
-  NETC_SCAN_SLOW_BLOCKS=$g timeout -k 10 120 python3 tools/bench_sizes.py --sizes 16,64 > gpurun_out/${TAG:-r01v}/g$g.json 2>> gpurun_out/${TAG:-r01v}/err.txt || exit $?
-  echo "grid $g"; cat gpurun_out/${TAG:-r01v}/g$g.json | cut -c1-60,200-300
+for g in ${GRIDS:-1024 2048 4096 16384}; do
+  NETC_SCAN_SLOW_BLOCKS=$g timeout -k 10 120 python3 tools/bench_sizes.py --sizes 16,64,1024 > gpurun_out/${TAG:-r01v}/g$g.json 2>> gpurun_out/${TAG:-r01v}/err.txt || exit $?
+  echo "grid $g"; cat gpurun_out/${TAG:-r01v}/g$g.json | python3 -c "import sys,json; [print(json.loads(l)[\"frame_bytes\"], json.loads(l)[\"scan_us\"]) for l in sys.stdin]"
 done
 cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/${TAG:-r01v}/trace -o run -- python3 $GRAFT_REPO_ROOT/tools/bench_sizes.py --sizes 16 > $GRAFT_REPO_ROOT/gpurun_out/${TAG:-r01v}/trace.log 2>&1
