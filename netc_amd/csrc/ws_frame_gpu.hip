@@ -22,9 +22,11 @@
 //      vector's first byte, rotated to its phase, one aligned store.  Spans the
 //      table does not cover (more than ~60 frames in 1 KiB) and the buffer edges
 //      are queued;
-//   3. the queued spans, composed byte-exactly from every frame they touch; then
-//      per frame (one thread each) the header and the payload bytes after it in
-//      the header's vector, which step 2 mapped through the previous frame.
+//   3. the queued spans, composed byte-exactly per lane from every frame they
+//      touch; then per frame (one thread each) the header and the payload bytes
+//      after it in the header's vector, which step 2 mapped through the previous
+//      frame.  A batch averaging under 80 B of payload per frame skips step 2 and
+//      the per-frame fixups: step 3 composes every span.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>

@@ -14,14 +14,17 @@
 //            those positions; K1 publishes them as "candidate entries" of the
 //            chunks they land in (the true chain enters each chunk at one of them).
 //   K2       per candidate entry: its chain walked (header bytes from global
-//            memory; K2' pointer-jumps the chunk in LDS when the walk is long) to
-//            the candidate it exits to: a graph of a few nodes per chunk whose path
-//            from the stream start is the true chain, one node per chunk it enters.
+//            memory; past 64 frames K2' builds the chunk's 16-bit links in LDS,
+//            doubles them to 8 / 16 hops and walks those, leaving an anchor every
+//            8 frames for K4b') to the candidate it exits to: a graph of a few nodes
+//            per chunk whose path from the stream start is the true chain, one node
+//            per chunk it enters.
 //   K3       pointer doubling over that graph, marking the nodes reachable from
 //            the start node (log2(chunks) passes);
-//   K4       per chunk: the true entry (its marked node), a walk of
-//            the chunk's frames in LDS to count them, a chained scan of the counts
-//            (decoupled look-back), and a second walk that writes the descriptors.
+//   K4       per chunk: the true entry (its marked node) and its frame count from
+//            K2, a chained scan of the counts (decoupled look-back), and a walk that
+//            writes the descriptors (K4b'; past 64 frames one wavefront per chunk,
+//            a lane per K2' anchor).
 // Garbage chains (payload bytes parsed as headers) die within a hop or two under
 // the strict checks, so chunks have few distinct exits; a stream whose exits
 // overflow the fixed capacities (adversarial payloads) is finished by a serial
