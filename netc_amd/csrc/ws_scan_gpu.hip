@@ -399,18 +399,26 @@ __device__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const ui
 #pragma unroll
     for (int k = 0; k < kPer / 4 + 1; ++k) w[k] = words[i0 / 4 + k];
     auto byte_at = [&](int j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
+    uint32_t cand = 0;   // this thread's positions that can start a header
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
         const uint32_t first = byte_at(j), second = byte_at(j + 1), opcode = first & 0x0F;
         const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
         const bool reject =
             a.strict && (!(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80)));
-        uint16_t lnk = kNoLink;
-        if (!reject) {
-            const uint64_t v = parse_at(a, B + i0 + j, window_at(words, i0 + j), nullptr, nullptr);
-            if (!(v & kTerm) && v < Bend) lnk = (uint16_t)(v - B);
-        }
-        l1[i0 + j] = lnk;
+        if (!reject) cand |= 1u << j;
+    }
+    // no link anywhere first (bank-conflict-free order), then the candidates parsed:
+    // the wave takes as many trips as its busiest lane has candidates (a few in
+    // strict mode), not one full parse per position
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) l1[k * kScanT + tid] = kNoLink;
+    __syncthreads();
+    while (cand) {
+        const int j = __builtin_ctz(cand);
+        cand &= cand - 1;
+        const uint64_t v = parse_at(a, B + i0 + j, window_at(words, i0 + j), nullptr, nullptr);
+        if (!(v & kTerm) && v < Bend) l1[i0 + j] = (uint16_t)(v - B);
     }
     __syncthreads();
     const uint16_t* src = l1;
