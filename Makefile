@@ -2,7 +2,8 @@
 # test-only oracle (oracle/Makefile).  Outputs stay in-tree so they travel to
 # the GPU box with the repository snapshot.
 #
-#   make            libnetc.so + libnetc_ws_gpu.so + oracle
+#   make            libnetc.so + libnetc_ws_gpu.so (+ libnetc_ceiling.so) + oracle
+#   make diag       instrumented builds + probes under tools/ (diagnostics only)
 #   make host       libnetc.so only (no hipcc needed)
 #   make clean
 
@@ -20,22 +21,33 @@ GPU_SRCS   := netc_amd/csrc/ws_mask_gpu.hip netc_amd/csrc/ws_frame_gpu.hip netc_
 GPU_HDRS   := netc_amd/csrc/ws_mask_gpu.h netc_amd/csrc/gpu_util.h include/ws/mask.h include/ws/frame.h include/ws/ingest.h
 
 .PHONY: all host gpu oracle diag clean
-all: host gpu oracle diag
+all: host gpu oracle
 host: $(LIBDIR)/libnetc.so
-gpu: $(LIBDIR)/libnetc_ws_gpu.so
+gpu: $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc_ceiling.so
 
 $(LIBDIR)/libnetc.so: $(HOST_SRCS) $(HOST_HDRS)
 	@mkdir -p $(LIBDIR)
 	$(CC) $(CFLAGS) -shared -o $@ $(HOST_SRCS) -lpthread
 
-$(LIBDIR)/libnetc_ws_gpu.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN'
+# one object per source (make -j compiles them in parallel), linked into one library
+GPU_OBJS   := $(patsubst netc_amd/csrc/%.hip,build/%.o,$(GPU_SRCS))
+build/%.o: netc_amd/csrc/%.hip $(GPU_HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIBDIR)/libnetc_ws_gpu.so: $(GPU_OBJS) $(LIBDIR)/libnetc.so
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(GPU_OBJS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN'
+
+# measurement-only HBM stream kernels bench.py times beside the mask kernel (roofline ceilings)
+$(LIBDIR)/libnetc_ceiling.so: netc_amd/csrc/ceiling.hip
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(LIBDIR)/*.so
+	rm -f $(LIBDIR)/*.so build/*.o
 	$(MAKE) -C oracle clean
 
 # diagnostics (tools/, not part of the product)

@@ -12,12 +12,16 @@ Cache cannot serve a batch from the previous touch.
 
 Multi-GPU: one process per GPU (torchrun); every rank masks its own shard of
 frames -- no data-path collective (frames are independent); the
-only collectives are the timing barrier and the max-over-ranks of the elapsed time.
+only collectives are the timing barrier and the gather of every rank's elapsed
+time (the max is the job's; each rank's own rate is reported as per_gpu).
 
 Prints ONE JSON line on rank 0.  Roofline: 2 x payload bytes per launch (read +
-write) / mean kernel duration (HIP events on the launch stream) vs 8.0 TB/s.
-cpu_baseline: the oracle's restatement of the reference loop on this host, rank 0,
-N = 1 only, bounded sample (see --cpu-seconds).
+write) / mean kernel duration (HIP events on the launch stream) vs 8.0 TB/s, next
+to in-bench frame-free stream ceilings (hand-written kernels, same rotation).
+After the timed region: the timed entry is checked (involution + every frame's
+keystream), BASELINE config 5's host-to-host rate is measured (rank 0, N = 1), and
+cpu_baseline times the oracle's restatement of the reference loop on this host,
+rank 0, N = 1 only, bounded sample (see --cpu-seconds).
 """
 
 from __future__ import annotations
@@ -56,7 +60,10 @@ def parse_args():
     p.add_argument("--unroll", type=int, default=None)
     p.add_argument("--max-blocks", type=int, default=None)
     p.add_argument("--nt-flags", type=int, default=None)
-    p.add_argument("--no-copy-ceiling", action="store_true")
+    p.add_argument("--no-copy-ceiling", action="store_true", help="skip the in-bench HBM stream ceilings")
+    p.add_argument("--c5-gib", type=float, default=16.0,
+                   help="BASELINE config 5 leg: GiB of 4 KiB frames streamed host->device->host from a pinned "
+                        "ring (rank 0, N = 1; 0 disables)")
     p.add_argument("--no-pipelined-probe", dest="pipelined_probe", action="store_false")
     return p.parse_args()
 
@@ -66,6 +73,12 @@ def dist_env():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     return world, rank, local
+
+
+def synth_config(workload: str, rank: int):
+    from netc_amd import synth
+
+    return synth.config(workload, shard=rank)
 
 
 def make_batches(torch, workload: str, rank: int, rotation_bytes: int, device):
@@ -96,22 +109,101 @@ def traffic_per_launch(workload: str):
         return None
 
 
-def copy_ceiling(torch, device, nbytes=64 << 20, reps=64):
-    """Practical roofline: device-to-device copy of rotating 64 MiB buffers (read + write bytes / time)."""
-    nb = 16
-    bufs = [torch.empty(nbytes, dtype=torch.uint8, device=device) for _ in range(nb + 1)]
-    for i in range(8):
-        bufs[(i + 1) % (nb + 1)].copy_(bufs[i % (nb + 1)])
+def stream_ceilings(torch, batches, total, stream, steps):
+    """Practical rooflines measured here, on the same rotation of batches and the same stream:
+    hand-written gfx950 stream kernels with no frame logic (netc_amd/csrc/ceiling.hip), each
+    walking the batch as the mask kernel does (one window of 2 x 1 KiB per wavefront, NT).
+      xor_inplace_GBps : buf[i] ^= key, in place          -- the mask kernel minus its frames
+      copy_GBps        : dst[i] = src[i], out of place    -- the guide's "float4 copy"
+    (read + write bytes) / HIP-event time per launch, averaged over `steps` launches."""
+    import ctypes
+
+    lib = ctypes.CDLL(os.path.join(ROOT, "netc_amd", "lib", "libnetc_ceiling.so"))
+    lib.netc_ceiling_walk.argtypes = [ctypes.c_int] * 8 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    nb = len(batches)
+    sink = torch.zeros(1024, dtype=torch.int32, device=batches[0][0].device)
+    out = {}
+    for name, mode in (("xor_inplace_GBps", 1), ("copy_GBps", 0)):
+        def launch(i):
+            src = batches[i % nb][0]
+            dst = batches[(i + nb // 2) % nb][0] if mode == 0 else src   # a batch no recent step wrote
+            rc = lib.netc_ceiling_walk(mode, 1, 1, 0, 2, 256, -1, 4, dst.data_ptr(), src.data_ptr(), total,
+                                       0x5A5A5A5A, sink.data_ptr(), stream.cuda_stream)
+            if rc != 0:
+                raise RuntimeError(f"netc_ceiling_walk failed ({rc})")
+        for i in range(4):
+            launch(i)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for i in range(steps):
+            launch(4 + i)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        out[name] = round(2.0 * (total // 1024 * 1024) / (e0.elapsed_time(e1) / steps * 1e-3) / 1e9, 1)
+    out["kernel"] = "netc_amd/csrc/ceiling.hip netc_ceiling_walk (NT, 2 x 1 KiB per wavefront, 256-thread workgroups)"
+    return out
+
+
+def verify_step(torch, nm, batch, total, nframes, off_h, keys_h, stream):
+    """Checks what the timed loop ran, after the timed region, with the same C-ABI entry:
+      * involution: masking a timed batch twice gives its bytes back, and once changes them;
+      * keystream: masking a zero buffer yields, for EVERY frame, its 4 key bytes repeated
+        from phase 0 (RFC 6455 §5.3; src/ws/common.c:321) -- checked with numpy here."""
+    p, o, k = batch
+    before = p.clone()
+    nm.mask_batch(p, p, o, k, stream=stream)
     torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for i in range(reps):
-        bufs[(i + 1) % (nb + 1)].copy_(bufs[i % (nb + 1)])
-    e.record()
+    once_differs = not torch.equal(p, before)
+    nm.mask_batch(p, p, o, k, stream=stream)
     torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / reps
-    del bufs
-    return 2 * nbytes / (ms * 1e-3) / 1e9
+    involution = torch.equal(p, before)
+    zero = torch.zeros(total, dtype=torch.uint8, device=p.device)
+    nm.mask_batch(zero, zero, o, k, stream=stream)
+    torch.cuda.synchronize()
+    ks = zero.cpu().numpy()
+    del zero
+    keys_b = np.ascontiguousarray(keys_h, dtype=np.uint32).view(np.uint8).reshape(-1, 4)
+    off64 = off_h.astype(np.int64)
+    keystream = bool((ks[:off64[0]] == 0).all() and (ks[off64[-1]:] == 0).all())
+    a = 0
+    while keystream and a < nframes:   # frames in groups of ~32 MiB (bounded host memory)
+        b = int(np.searchsorted(off64, off64[a] + (32 << 20), side="right"))
+        b = min(max(b - 1, a + 1), nframes)
+        sizes = np.diff(off64[a:b + 1])
+        frame_of = np.repeat(np.arange(a, b), sizes)
+        phase = np.arange(off64[a], off64[b], dtype=np.int64) - np.repeat(off64[a:b], sizes)
+        keystream = bool(np.array_equal(ks[off64[a]:off64[b]], keys_b[frame_of, phase & 3]))
+        a = b
+    return {"involution": bool(involution and once_differs), "keystream_all_frames": keystream}
+
+
+def c5_host_to_host(nm, gib: float):
+    """BASELINE config 5: `gib` GiB of 4 KiB frames in a pinned host ring, streamed through the
+    default persistent handle (2 x 512 MiB device slots, H2D / kernel / D2H overlapped), in place.
+    Host to host GiB/s, best of 2 passes (the first also touches the slots); never `value`."""
+    from netc_amd import synth
+
+    total = int(gib * (1 << 30)) // 4096 * 4096
+    nframes = total // 4096
+    off = synth.uniform_offsets(nframes, 4096)
+    keys = synth.random_keys(nframes, stream=900)
+    ring = nm.PinnedArray(total)
+    try:
+        synth.fill_payload(ring.array)
+        best = None
+        with nm.HostStream(0) as hs:
+            for _ in range(2):
+                t0 = time.perf_counter()
+                hs.mask(ring.array, ring.array, off, keys)
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+    finally:
+        ring.close()
+    return {"value": round(total / best / GIB, 2), "unit": "GiB/s host to host", "bytes": total,
+            "frames": nframes, "slots": "2 x 512 MiB (defaults)", "passes": 2,
+            "note": "BASELINE config 5: pinned ring -> H2D -> mask -> D2H -> same ring, in place; PCIe-bound"}
 
 
 def cpu_baseline(workload: str, budget_s: float):
@@ -299,22 +391,39 @@ def main():
         if world > 1:
             torch.distributed.barrier()
 
+    per_rank_elapsed = [elapsed]
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms.mean(), pipelined or 0.0], dtype=torch.float64, device=coll_dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed, kern_mean, pipelined = float(t[0]), float(t[1]), (float(t[2]) or None)
+        mine = torch.tensor([elapsed, kern_ms.mean(), pipelined or 0.0], dtype=torch.float64, device=coll_dev)
+        gathered = [torch.zeros_like(mine) for _ in range(world)]
+        torch.distributed.all_gather(gathered, mine)
+        per_rank_elapsed = [float(g[0]) for g in gathered]
+        elapsed = max(per_rank_elapsed)
+        kern_mean = max(float(g[1]) for g in gathered)
+        pipelined = max(float(g[2]) for g in gathered) or None
     else:
         kern_mean = float(kern_ms.mean())
 
-    ceiling = None
+    ceilings = None
     if rank == 0 and not args.no_copy_ceiling:
-        ceiling = copy_ceiling(torch, device)
+        ceilings = stream_ceilings(torch, batches, total, stream, max(20, args.steps))
+
+    off_h, keys_h, _ = synth_config(args.workload, rank)
+    check = verify_step(torch, nm, batches[(args.warmup + args.steps - 1) % nb], total, nframes, off_h, keys_h,
+                        stream)
+    if world > 1:
+        ok = torch.tensor([int(check["involution"] and check["keystream_all_frames"])], device=coll_dev)
+        torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
+        check["all_ranks_ok"] = bool(ok.item())
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        del batches
+    c5 = None
+    if rank == 0 and world == 1:
+        del batches, prepared
         torch.cuda.empty_cache()
-        cpu = cpu_baseline(args.workload, args.cpu_seconds)
+        if args.c5_gib > 0:
+            c5 = c5_host_to_host(nm, args.c5_gib)
+        if args.cpu_seconds > 0:
+            cpu = cpu_baseline(args.workload, args.cpu_seconds)
 
     if rank == 0:
         payload_all = float(total) * world * args.steps
@@ -351,8 +460,12 @@ def main():
                 "kernel_ms_mean": round(kern_mean, 5),
                 "kernel_timing": "HIP events on the launch stream around the K timed launches, / K",
                 "algorithmic_bytes_per_launch": 2 * total,
-                "copy_ceiling_GBps": round(ceiling, 1) if ceiling else None,
+                "ceilings": ceilings,
+                "frac_of_xor_stream": round(achieved / ceilings["xor_inplace_GBps"], 4) if ceilings else None,
             },
+            "per_gpu": [round(float(total) * args.steps / e / GIB, 3) for e in per_rank_elapsed],
+            "verified": check,
+            "c5_host_to_host": c5,
             "cpu_baseline": cpu,
             "pipelined_2stream": None if not pipelined else {
                 "value": round(float(total) * world * args.steps / pipelined / GIB, 3),

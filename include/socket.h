@@ -3,7 +3,11 @@
 
 /*
  * Socket helpers — same declarations as the reference's include/socket.h:1-28
- * (POSIX build; the reference's WinSock branch is out of scope here).
+ * (POSIX build; the reference's WinSock branch is out of scope here).  The header is
+ * part of the kept C API (BASELINE.json north_star); the implementations are NOT in
+ * this repo's libraries: they stay netc's own src/socket.c ("header API
+ * kept verbatim; implementation out of scope"), linked next to libnetc.so
+ * (tests/test_dropin.py).
  */
 
 #include "./utils/vector.h"

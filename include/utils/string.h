@@ -3,7 +3,8 @@
 
 /*
  * Small-string-optimised string used by the socket helpers; same layout and
- * functions as the reference's include/utils/string.h:6-49.
+ * functions as the reference's include/utils/string.h:6-49.  Declarations only:
+ * the implementation stays netc's own src/utils/string.c (out of scope).
  */
 
 #include <stddef.h>

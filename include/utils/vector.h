@@ -28,11 +28,11 @@ int vector_resize(struct vector *vec, size_t new_capacity);
 
 /** Appends one element, doubling capacity when full. */
 void vector_push(struct vector *vec, void *element);
-/** Overwrites the element at `index`. */
+/** Overwrites the element at `index`; size grows by one when index >= size (as the reference). */
 void vector_set_index(struct vector *vec, void *element, size_t index);
-/** Pointer to the element at `index` (NULL when out of range). */
+/** Pointer to the element at `index` (no range check, as the reference). */
 void *vector_get(struct vector *vec, size_t index);
-/** Pointer to the storage. */
+/** Pointer to the end of the data (elements + size * element_size): where the next element goes. */
 void *vector_get_buffer(struct vector *vec);
 /** Removes the element at `index`, shifting the tail down. */
 void vector_delete(struct vector *vec, size_t index);
@@ -42,7 +42,7 @@ void vector_clear(struct vector *vec);
 /** Zeroes every element in use, keeping size. */
 void vector_reset(struct vector *vec);
 
-/** Releases storage. */
+/** Releases storage; size = 0, elements = NULL (capacity is left as it was, as the reference). */
 void vector_free(struct vector *vec);
 
 #endif // VECTOR_H

@@ -93,19 +93,24 @@ int netc_gpu_device_count(void);
 int netc_gpu_init(int device);
 
 /**
- * Process-wide launch shape of the batch kernel (defaults: 4, 0, AUTO).
- * unroll: KiB per chunk, the unit a wavefront masks per loop trip (1, 2, 4 or
- * 8); max_blocks: cap on 256-thread workgroups, 0 = exactly the workgroups the
- * device holds at once; flags: NETC_GPU_TUNE_AUTO (non-temporal payload stream)
- * or 0 (plain loads / stores) or NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES
- * (either bit selects the non-temporal stream).  The frame assembly of
+ * Process-wide launch shape of the batch kernel (defaults: 1, 0, AUTO).
+ * unroll: KiB of payload a wavefront loads at once (1, 2, 4 or 8); flags:
+ * NETC_GPU_TUNE_AUTO (non-temporal payload stream; a grid covering the batch, one
+ * window of two steps of `unroll` KiB per wavefront) or a mix of the bits below
+ * (0 = plain loads / stores, one step per window).  NETC_GPU_TUNE_PERSISTENT
+ * selects round 1's walk — one resident round of workgroups striding over the
+ * chunks — where max_blocks caps the workgroups (0 = exactly the workgroups the
+ * device holds at once); max_blocks is ignored otherwise.  The frame assembly of
  * include/ws/frame.h reads the same knob: unroll 8 selects 4 KiB chunks there,
- * anything else 2 KiB.  Diagnostic knob: call before launching work; it is not
- * synchronised with concurrent launches.
+ * anything else 2 KiB, and it always walks persistently.  Diagnostic knob: call
+ * before launching work; it is not synchronised with concurrent launches.
  */
-#define NETC_GPU_TUNE_AUTO     -1
-#define NETC_GPU_TUNE_NT_LOADS  1   /* non-temporal payload loads  */
-#define NETC_GPU_TUNE_NT_STORES 2   /* non-temporal payload stores */
+#define NETC_GPU_TUNE_AUTO       -1
+#define NETC_GPU_TUNE_NT_LOADS    1   /* non-temporal payload loads                        */
+#define NETC_GPU_TUNE_NT_STORES   2   /* non-temporal payload stores                       */
+#define NETC_GPU_TUNE_PERSISTENT  4   /* round 1's persistent grid-stride walk             */
+#define NETC_GPU_TUNE_TWO_STEPS   8   /* a wavefront's window is two steps of unroll KiB   */
+#define NETC_GPU_TUNE_XCD_ORDER  16   /* each XCD takes a contiguous share of the windows  */
 int netc_gpu_tune(int unroll, int max_blocks, int flags);
 
 /** Message for the last failing netc_gpu_* call on this thread ("" if none). */
@@ -159,20 +164,39 @@ int netc_gpu_mask_batch_multi(int nshards, const int *devices, void *const *d_ds
 
 /**
  * Host-resident batch: h_src → device → mask → h_dst, through `nslots`
- * device/pinned staging slots of `slot_bytes` payload bytes each, cut at frame
- * boundaries, with H2D copy, kernel and D2H copy of consecutive slots
- * overlapped on separate HIP streams.  h_offsets / h_keys are host arrays laid
- * out as for netc_gpu_mask_batch.  h_dst == h_src is allowed.  A frame longer
- * than slot_bytes is split across slots (its phase is carried).  Synchronous:
- * returns when h_dst is complete.  Pinned (hipHostMalloc / hipHostRegister)
- * h_src / h_dst run at the PCIe rate; pageable memory works but is slower.
- * Two slots of 256-512 MiB are the fastest shape measured on MI355X (one copy
- * in each direction in flight: 40.6 GiB/s host to host with 2 x 512 MiB, 29
- * with 4 x 256 MiB).
+ * device slots of `slot_bytes` payload bytes each, cut at frame boundaries, with
+ * H2D copy, kernel and D2H copy of consecutive slots overlapped on separate HIP
+ * streams (BASELINE config 5).  h_offsets / h_keys are host arrays laid out as for
+ * netc_gpu_mask_batch.  h_dst == h_src is allowed.  A frame longer than
+ * slot_bytes is split across slots (its phase is carried).  Synchronous: returns
+ * when h_dst is complete.  Page-locked h_src / h_dst (netc_gpu_host_alloc, or
+ * hipHostMalloc / hipHostRegister) run at the PCIe rate; pageable memory works
+ * but is slower (the runtime stages it).  Two slots of 512 MiB are the fastest
+ * shape measured on MI355X (one copy in each direction in flight).
+ *
+ * netc_gpu_stream_create / _mask / _destroy: the same pipeline with the slots,
+ * streams, events and descriptor staging kept in a handle across calls (a call
+ * allocates only when one of its slots holds more frames than any earlier call's
+ * did).  slot_bytes 0 = 512 MiB, nslots 0 = 2.  A handle serves one thread at a
+ * time.  netc_gpu_mask_stream_host is create + mask + destroy.
  */
 int netc_gpu_mask_stream_host(int device, void *h_dst, const void *h_src, size_t total_bytes,
                               const uint64_t *h_frame_offsets, const uint32_t *h_keys, size_t nframes,
                               size_t slot_bytes, int nslots);
+
+struct netc_gpu_stream;
+int netc_gpu_stream_create(struct netc_gpu_stream **out, int device, size_t slot_bytes, int nslots);
+int netc_gpu_stream_mask(struct netc_gpu_stream *stream, void *h_dst, const void *h_src, size_t total_bytes,
+                         const uint64_t *h_frame_offsets, const uint32_t *h_keys, size_t nframes);
+void netc_gpu_stream_destroy(struct netc_gpu_stream *stream);
+
+/**
+ * Page-locked host memory for the host side of the pipeline (the pinned receive
+ * ring of a netc server): NULL on failure (error set as above).  Free with
+ * netc_gpu_host_free.
+ */
+void *netc_gpu_host_alloc(size_t bytes);
+void netc_gpu_host_free(void *ptr);
 
 #ifdef __cplusplus
 }

@@ -90,6 +90,16 @@ def gpu() -> ctypes.CDLL:
             lib.netc_gpu_mask_stream_host.argtypes = [ctypes.c_int, vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t,
                                                       ctypes.c_size_t, ctypes.c_int]
             lib.netc_gpu_mask_stream_host.restype = ctypes.c_int
+            lib.netc_gpu_stream_create.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_int]
+            lib.netc_gpu_stream_create.restype = ctypes.c_int
+            lib.netc_gpu_stream_mask.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t]
+            lib.netc_gpu_stream_mask.restype = ctypes.c_int
+            lib.netc_gpu_stream_destroy.argtypes = [vp]
+            lib.netc_gpu_stream_destroy.restype = None
+            lib.netc_gpu_host_alloc.argtypes = [ctypes.c_size_t]
+            lib.netc_gpu_host_alloc.restype = vp
+            lib.netc_gpu_host_free.argtypes = [vp]
+            lib.netc_gpu_host_free.restype = None
             lib.netc_gpu_encode_frames.argtypes = [ctypes.c_int, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp, vp,
                                                    vp, ctypes.c_size_t, ctypes.c_int, vp]
             lib.netc_gpu_encode_frames.restype = ctypes.c_int

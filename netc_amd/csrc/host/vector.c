@@ -1,4 +1,16 @@
-/* struct vector (include/utils/vector.h); behaviour as the reference's src/utils/vector.c:8-90. */
+/*
+ * struct vector (include/utils/vector.h) with the reference's semantics,
+ * src/utils/vector.c:8-90 — libnetc.so exports these under netc's own names, and a
+ * netc program that links its own src/utils/vector.c interposes them (the drop-in
+ * check, tests/test_dropin.py, shows libnetc.so binding the program's copies), so
+ * the two must behave alike: vector_set_index grows size when it writes at or past
+ * it (:38-44), vector_get does no range check (:46-49), vector_get_buffer is the
+ * end of the data — where the next element goes (:51-54), vector_free leaves the
+ * capacity field as it was (:84-89).  Departures only where the reference has
+ * undefined behaviour: a push into capacity 0 grows to 1 (the reference asks for
+ * 0 * 2 and writes past the allocation, :31-33), and deleting at or past size is a
+ * no-op (the reference's memmove length underflows, :60).
+ */
 #include "../../../include/utils/vector.h"
 
 #include <stdlib.h>
@@ -33,17 +45,17 @@ void vector_push(struct vector *vec, void *element)
 void vector_set_index(struct vector *vec, void *element, size_t index)
 {
     memcpy((char *)vec->elements + vec->element_size * index, element, vec->element_size);
+    if (index >= vec->size) ++vec->size;
 }
 
 void *vector_get(struct vector *vec, size_t index)
 {
-    if (index >= vec->size) return NULL;
     return (char *)vec->elements + vec->element_size * index;
 }
 
 void *vector_get_buffer(struct vector *vec)
 {
-    return vec->elements;
+    return (char *)vec->elements + vec->element_size * vec->size;
 }
 
 void vector_delete(struct vector *vec, size_t index)
@@ -67,8 +79,7 @@ void vector_reset(struct vector *vec)
 
 void vector_free(struct vector *vec)
 {
+    vec->size = 0;
     free(vec->elements);
     vec->elements = NULL;
-    vec->size = 0;
-    vec->capacity = 0;
 }

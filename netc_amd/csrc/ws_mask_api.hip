@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <new>
 #include <utility>
 #include <vector>
 
@@ -39,20 +40,21 @@ int fail_hip(int code, const char* what, hipError_t e) {
     return fail(code, "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
 }
 
-// Selects `device` for the calling thread for the lifetime of the guard.
+// Selects `device` for the calling thread for the lifetime of the guard.  The hot
+// path (the device is already current) costs one hipGetDevice (a thread-local read
+// in the runtime) and nothing on exit.
 struct DeviceGuard {
     int prev = -1;
+    bool switched = false;
     hipError_t err = hipSuccess;
     explicit DeviceGuard(int device) {
         err = hipGetDevice(&prev);
-        if (err != hipSuccess) return;
-        if (prev != device) err = hipSetDevice(device);
+        if (err != hipSuccess || prev == device) return;
+        err = hipSetDevice(device);
+        switched = err == hipSuccess;
     }
     ~DeviceGuard() {
-        if (prev >= 0) {
-            int cur = -1;
-            if (hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-        }
+        if (switched) (void)hipSetDevice(prev);
     }
 };
 
@@ -134,7 +136,8 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags) {
         return fail(NETC_GPU_EINVAL, "unroll must be 1, 2, 4 or 8 (got %d)", unroll);
     if (max_blocks < 0 || max_blocks > (1 << 24)) return fail(NETC_GPU_EINVAL, "max_blocks out of range");
     if (flags != NETC_GPU_TUNE_AUTO &&
-        (flags & ~(NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES)))
+        (flags & ~(NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES | NETC_GPU_TUNE_PERSISTENT |
+                   NETC_GPU_TUNE_TWO_STEPS | NETC_GPU_TUNE_XCD_ORDER)))
         return fail(NETC_GPU_EINVAL, "unknown tune flags");
     g_cfg.unroll = unroll;
     g_cfg.max_blocks = max_blocks;
@@ -306,11 +309,16 @@ int netc_gpu_unmask_frames(int device, void* d_wire, size_t len, const uint64_t*
     return 0;
 }
 
+}  // extern "C"
+
 // ---------------------------------------------------------------------------
 // Host → device → host pipeline (BASELINE config 5).  Slots are fixed byte
 // ranges of the payload; a frame cut by a slot edge continues in the next slot
 // with its key pre-rotated by the bytes already consumed (the phase carry of
-// the reference's received_length, src/ws/common.c:301,321).
+// the reference's received_length, src/ws/common.c:301,321).  A persistent
+// handle (netc_gpu_stream_*) owns the device slots, the pinned descriptor
+// staging, the streams and the events, so a run allocates nothing unless a slot
+// holds more frames than any earlier run's did.
 // ---------------------------------------------------------------------------
 
 namespace {
@@ -330,63 +338,126 @@ size_t upper_frame(const uint64_t* off, size_t n, uint64_t pos) {
     return (size_t)(std::upper_bound(off, off + n, pos) - off);
 }
 
+void free_desc(Slot& s) {
+    if (s.d_off) (void)hipFree(s.d_off);
+    if (s.d_key) (void)hipFree(s.d_key);
+    if (s.h_off) (void)hipHostFree(s.h_off);
+    if (s.h_key) (void)hipHostFree(s.h_key);
+    s.d_off = nullptr;
+    s.d_key = nullptr;
+    s.h_off = nullptr;
+    s.h_key = nullptr;
+}
+
 }  // namespace
 
-int netc_gpu_mask_stream_host(int device, void* h_dst, const void* h_src, size_t total, const uint64_t* h_off,
-                              const uint32_t* h_keys, size_t nframes, size_t slot_bytes, int nslots) {
+struct netc_gpu_stream {
+    int device = 0;
+    size_t slot_bytes = 0;
+    size_t cap = 0;   // descriptor entries each slot holds
+    std::vector<Slot> slots;
+};
+
+namespace {
+
+void stream_release(netc_gpu_stream* h) {
+    for (Slot& s : h->slots) {
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        if (s.d_buf) (void)hipFree(s.d_buf);
+        free_desc(s);
+        if (s.desc_free) (void)hipEventDestroy(s.desc_free);
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+    }
+    delete h;
+}
+
+// every slot's descriptor staging holds >= want entries (grown only when a run needs more)
+int ensure_desc(netc_gpu_stream* h, size_t want) {
+    if (want <= h->cap) return 0;
+    size_t cap = h->cap ? h->cap : 4096;
+    while (cap < want) cap *= 2;
+    hipError_t e;
+    for (Slot& s : h->slots) {
+        if ((e = hipStreamSynchronize(s.stream)) != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "stream sync", e);
+        free_desc(s);
+        if ((e = hipMalloc(&s.d_off, (cap + 1) * sizeof(uint64_t))) != hipSuccess ||
+            (e = hipMalloc(&s.d_key, cap * sizeof(uint32_t))) != hipSuccess ||
+            (e = hipHostMalloc(&s.h_off, (cap + 1) * sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess ||
+            (e = hipHostMalloc(&s.h_key, cap * sizeof(uint32_t), hipHostMallocDefault)) != hipSuccess) {
+            free_desc(s);
+            h->cap = 0;
+            return fail_hip(NETC_GPU_ENOMEM, "slot descriptor allocation", e);
+        }
+    }
+    h->cap = cap;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int netc_gpu_stream_create(struct netc_gpu_stream** out, int device, size_t slot_bytes, int nslots) {
+    if (!out) return fail(NETC_GPU_EINVAL, "null output pointer");
+    *out = nullptr;
     if (int r = check_device(device)) return r;
+    if (!slot_bytes) slot_bytes = (size_t)512 << 20;
+    if (!nslots) nslots = 2;
+    if (slot_bytes < 4096 || nslots < 2 || nslots > 16)
+        return fail(NETC_GPU_EINVAL, "need slot_bytes >= 4096 and 2 <= nslots <= 16");
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+    netc_gpu_stream* h = new (std::nothrow) netc_gpu_stream();
+    if (!h) return fail(NETC_GPU_ENOMEM, "host allocation");
+    h->device = device;
+    h->slot_bytes = slot_bytes & ~(size_t)15;
+    h->slots.resize((size_t)nslots);
+    hipError_t e;
+    for (Slot& s : h->slots) {
+        if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&s.desc_free, hipEventDisableTiming)) != hipSuccess) {
+            stream_release(h);
+            return fail_hip(NETC_GPU_ERUNTIME, "stream/event create", e);
+        }
+        if ((e = hipMalloc(&s.d_buf, h->slot_bytes)) != hipSuccess) {
+            stream_release(h);
+            return fail_hip(NETC_GPU_ENOMEM, "slot allocation", e);
+        }
+    }
+    *out = h;
+    return 0;
+}
+
+void netc_gpu_stream_destroy(struct netc_gpu_stream* h) {
+    if (!h) return;
+    DeviceGuard g(h->device);
+    stream_release(h);
+}
+
+int netc_gpu_stream_mask(struct netc_gpu_stream* h, void* h_dst, const void* h_src, size_t total,
+                         const uint64_t* h_off, const uint32_t* h_keys, size_t nframes) {
+    if (!h) return fail(NETC_GPU_EINVAL, "null stream handle");
     if (total == 0) return 0;
     if (!h_dst || !h_src || !h_off || (nframes && !h_keys)) return fail(NETC_GPU_EINVAL, "null host buffer");
     if (partial_overlap(h_dst, h_src, total)) return fail(NETC_GPU_EINVAL, "dst and src partially overlap");
-    if (slot_bytes < 4096 || nslots < 2 || nslots > 16)
-        return fail(NETC_GPU_EINVAL, "need slot_bytes >= 4096 and 2 <= nslots <= 16");
     if (h_off[nframes] > total) return fail(NETC_GPU_EINVAL, "offsets[nframes] > total_bytes");
-    slot_bytes &= ~(size_t)15;
-    DeviceGuard g(device);
+    DeviceGuard g(h->device);
     if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
-
+    const size_t slot_bytes = h->slot_bytes, nslots = h->slots.size();
     const size_t nchunks = (total + slot_bytes - 1) / slot_bytes;
     // descriptor capacity: frames overlapping any one slot
-    size_t cap = 1;
+    size_t need = 1;
     for (size_t c = 0; c < nchunks; ++c) {
         const uint64_t lo = c * slot_bytes, hi = std::min<uint64_t>(total, lo + slot_bytes);
         const size_t k0 = upper_frame(h_off, nframes, lo), k1 = upper_frame(h_off, nframes, hi - 1);
         const size_t first = k0 ? k0 - 1 : 0;
-        cap = std::max(cap, k1 - first + 1);
+        need = std::max(need, k1 - first + 1);
     }
-
-    std::vector<Slot> slots((size_t)nslots);
+    if (int r = ensure_desc(h, need)) return r;
     int rc = 0;
     hipError_t e = hipSuccess;
-    auto cleanup = [&]() {
-        for (Slot& s : slots) {
-            if (s.stream) (void)hipStreamSynchronize(s.stream);
-            if (s.d_buf) (void)hipFree(s.d_buf);
-            if (s.d_off) (void)hipFree(s.d_off);
-            if (s.d_key) (void)hipFree(s.d_key);
-            if (s.h_off) (void)hipHostFree(s.h_off);
-            if (s.h_key) (void)hipHostFree(s.h_key);
-            if (s.desc_free) (void)hipEventDestroy(s.desc_free);
-            if (s.stream) (void)hipStreamDestroy(s.stream);
-        }
-    };
-    for (Slot& s : slots) {
-        if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&s.desc_free, hipEventDisableTiming)) != hipSuccess) {
-            rc = fail_hip(NETC_GPU_ERUNTIME, "stream/event create", e);
-            break;
-        }
-        if ((e = hipMalloc(&s.d_buf, slot_bytes)) != hipSuccess ||
-            (e = hipMalloc(&s.d_off, (cap + 1) * sizeof(uint64_t))) != hipSuccess ||
-            (e = hipMalloc(&s.d_key, cap * sizeof(uint32_t))) != hipSuccess ||
-            (e = hipHostMalloc(&s.h_off, (cap + 1) * sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess ||
-            (e = hipHostMalloc(&s.h_key, cap * sizeof(uint32_t), hipHostMallocDefault)) != hipSuccess) {
-            rc = fail_hip(NETC_GPU_ENOMEM, "slot allocation", e);
-            break;
-        }
-    }
     for (size_t c = 0; rc == 0 && c < nchunks; ++c) {
-        Slot& s = slots[c % (size_t)nslots];
+        Slot& s = h->slots[c % nslots];
         const uint64_t lo = c * slot_bytes, hi = std::min<uint64_t>(total, lo + slot_bytes);
         const size_t len = (size_t)(hi - lo);
         // the previous chunk of this slot must have consumed its descriptors
@@ -398,6 +469,7 @@ int netc_gpu_mask_stream_host(int device, void* h_dst, const void* h_src, size_t
         size_t m = 0;
         const size_t k0 = upper_frame(h_off, nframes, lo);
         size_t k = k0 ? k0 - 1 : 0;
+        s.h_off[0] = 0;
         for (; k < nframes && h_off[k] < hi; ++k) {
             const uint64_t fs = h_off[k], fe = h_off[k + 1];
             if (fe <= lo) continue;
@@ -409,7 +481,6 @@ int netc_gpu_mask_stream_host(int device, void* h_dst, const void* h_src, size_t
             ++m;
             s.h_off[m] = std::min<uint64_t>(fe, hi) - lo;
         }
-        if (m == 0) s.h_off[0] = 0;
         const uint8_t* src = (const uint8_t*)h_src + lo;
         uint8_t* dst = (uint8_t*)h_dst + lo;
         if ((e = hipMemcpyAsync(s.d_buf, src, len, hipMemcpyHostToDevice, s.stream)) != hipSuccess ||
@@ -427,12 +498,40 @@ int netc_gpu_mask_stream_host(int device, void* h_dst, const void* h_src, size_t
             break;
         }
     }
-    for (Slot& s : slots) {
-        if (rc == 0 && s.stream && (e = hipStreamSynchronize(s.stream)) != hipSuccess)
-            rc = fail_hip(NETC_GPU_ERUNTIME, "hipStreamSynchronize", e);
+    for (Slot& s : h->slots) {
+        const hipError_t w = hipStreamSynchronize(s.stream);
+        if (rc == 0 && w != hipSuccess) rc = fail_hip(NETC_GPU_ERUNTIME, "hipStreamSynchronize", w);
     }
-    cleanup();
     return rc;
+}
+
+int netc_gpu_mask_stream_host(int device, void* h_dst, const void* h_src, size_t total, const uint64_t* h_off,
+                              const uint32_t* h_keys, size_t nframes, size_t slot_bytes, int nslots) {
+    if (int r = check_device(device)) return r;
+    if (total == 0) return 0;
+    if (!h_dst || !h_src || !h_off || (nframes && !h_keys)) return fail(NETC_GPU_EINVAL, "null host buffer");
+    if (slot_bytes < 4096 || nslots < 2 || nslots > 16)
+        return fail(NETC_GPU_EINVAL, "need slot_bytes >= 4096 and 2 <= nslots <= 16");
+    netc_gpu_stream* h = nullptr;
+    if (int r = netc_gpu_stream_create(&h, device, slot_bytes, nslots)) return r;
+    const int rc = netc_gpu_stream_mask(h, h_dst, h_src, total, h_off, h_keys, nframes);
+    netc_gpu_stream_destroy(h);
+    return rc;
+}
+
+void* netc_gpu_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (bytes == 0) bytes = 1;
+    const hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        fail_hip(NETC_GPU_ENOMEM, "hipHostMalloc", e);
+        return nullptr;
+    }
+    return p;
+}
+
+void netc_gpu_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 }  // extern "C"

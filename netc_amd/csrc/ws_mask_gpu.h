@@ -22,14 +22,18 @@ struct Args {
     const uint64_t* n_dev;     // if set: the frame count is read from device memory at kernel start
     uint8_t* verr;             // TEXT validation (VAL kernels): per-frame "local UTF-8 rule broken" flags
     uint8_t vtag;              // ... written as this call's tag (verr[f] == vtag: flagged by this call)
+    uint8_t xcd_remap;         // one-window-per-wave walk: give each XCD a contiguous share of the windows
 };
 
-enum : int { kNtLoads = 1, kNtStores = 2 };   // LaunchCfg::flags (NETC_GPU_TUNE_NT_*)
+// LaunchCfg::flags (NETC_GPU_TUNE_*): bits 0-1 non-temporal payload stream, 2 the
+// persistent grid-stride walk (round-1 kernel), 3 two steps per wavefront window,
+// 4 XCD-contiguous window order
+enum : int { kNtLoads = 1, kNtStores = 2, kPersistent = 4, kTwoSteps = 8, kXcdRemap = 16 };
 
 struct LaunchCfg {
-    int unroll = 4;            // U: 1 KiB spans per window (1, 2, 4, 8)
-    int max_blocks = 0;        // cap on 256-thread workgroups; 0 = one resident round (occupancy x CUs)
-    int flags = -1;            // -1 (auto) or kNtLoads | kNtStores: non-temporal payload stream; 0 = plain
+    int unroll = 1;            // KiB loaded per wavefront at once (1, 2, 4, 8)
+    int max_blocks = 0;        // persistent walk only: cap on 256-thread workgroups; 0 = one resident round
+    int flags = -1;            // -1 (auto: non-temporal, one window of two steps per wavefront) or a kNt* | k* mix
 };
 
 hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,

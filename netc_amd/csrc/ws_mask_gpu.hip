@@ -28,6 +28,7 @@
 //     16-B vector, and the same for every lane of a span.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "gpu_util.h"
 #include "ws_mask_gpu.h"
@@ -244,13 +245,12 @@ __device__ __forceinline__ u32x4 load_vec(const Args& a, uint64_t P) {
         if constexpr (NT) return __builtin_nontemporal_load(p);
         return *p;
     } else {
-        const NETC_GLOBAL uint8_t* p = gptr(a.src_base + P);
-        u32x4 v;
-#pragma unroll
-        for (int w = 0; w < 4; ++w)
-            v[w] = (uint32_t)p[4 * w] | ((uint32_t)p[4 * w + 1] << 8) | ((uint32_t)p[4 * w + 2] << 16) |
-                   ((uint32_t)p[4 * w + 3] << 24);
-        return v;
+        // src and dst differ mod 16: one unaligned 16-B load (global_load_dwordx4 takes
+        // any byte address on gfx950; it was 16 global_load_ubyte per lane in round 1)
+        typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+        const NETC_GLOBAL u32x4u* p = (const NETC_GLOBAL u32x4u*)gptr(a.src_base + P);
+        if constexpr (NT) return __builtin_nontemporal_load(p);
+        return *p;
     }
 }
 
@@ -585,6 +585,109 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
     process(d, t, A);
 }
 
+// ---------------------------------------------------------------------------
+// The default walk: one window of U x K KiB per wavefront, a grid covering the
+// batch (no persistent loop).  The dispatcher hands the next workgroup to a CU as
+// soon as one retires, and that sustains more of the HBM rate than any persistent
+// grid-stride walk measured on MI355X: a frame-free XOR stream over 1 GiB ran at
+// 6.45-6.58 TB/s this way and at <= 5.95 TB/s as one resident round striding over
+// the chunks (tools/ceiling_sweep.py).
+//
+// Per wavefront: the window's payload loads are issued first (U vectors per lane);
+// the frame-table lookup runs while they are in flight.  Its loads hit L2 / MALL
+// almost always (neighbouring wavefronts read the same descriptor lines), so the
+// lookup hides under the payload's HBM latency:
+//   1. a 64-entry table at the base the batch's mean density predicts (exact for
+//      evenly sized frames: configs 2, 3, 5);
+//   2. on a miss, at most two interpolation steps from the window's own edge
+//      entries (the distance left, times the density: for independent random
+//      sizes the error shrinks from ~sqrt(frames before) to ~sqrt(frames skipped));
+//   3. then locate() (comb + 64-ary narrowing), which always converges.
+// K > 1: the window's K steps of U KiB run one after another (load, mask, store),
+// the table carried across them.
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ int64_t clamp_base(const Args& a, int64_t g) {
+    g = g < -1 ? -1 : g;
+    return g > (int64_t)a.n ? (int64_t)a.n : g;
+}
+
+// make t (issued at a guessed base) hold the frame containing A
+__device__ __forceinline__ void np_resolve(const Args& a, Table& t, uint64_t A, int lane) {
+    table_finish(t);
+#pragma unroll 1
+    for (int step = 0; step < 2; ++step) {
+        const uint64_t m = __ballot(t.start <= A);
+        if (m != 0 && (t.tail || m != ~0ull)) return;   // brackets A
+        int64_t g;
+        if (m == 0) {   // every entry starts after A: step back by the distance from entry 0
+            const uint64_t s0 = readlane64(t.start, 0);
+            g = t.kb - (int64_t)((double)(s0 - A) * a.density) - 40;
+        } else {        // every entry starts at or before A: step on from entry 63
+            g = t.kb + (kWave - 1) + (int64_t)((double)(A - t.last) * a.density) - 24;
+        }
+        table_load(a, t, clamp_base(a, g), lane);
+    }
+    if (!table_brackets(t, A)) table_load(a, t, locate(a, A, lane), lane);
+}
+
+template <int U, int K, bool SRC_ALIGNED, bool NT, bool VAL = false>
+__global__ __launch_bounds__(256) void mask_np_kernel(Args a) {
+    constexpr uint64_t kStep = kSpan * U;
+    constexpr uint64_t kWin = kStep * K;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t wpb = blockDim.x / kWave;
+    uint64_t block = blockIdx.x;
+    if (a.xcd_remap) {
+        // blocks b and b + 8 share an XCD (round-robin dispatch): give each XCD one
+        // contiguous share of the batch, so its L2 fetches only that share's descriptors
+        const uint64_t nb = gridDim.x, per = nb / 8;
+        if (block < per * 8) block = (block % 8) * per + block / 8;
+    }
+    const uint64_t wave = block * wpb + (threadIdx.x / kWave);
+    if (wave >= a.nwin) return;
+    extern __shared__ uint32_t lds_occupancy_pad[];   // dynamic LDS only limits workgroups per CU
+    (void)lds_occupancy_pad;
+    if (a.n_dev) {   // frame count produced on the device by an earlier kernel (scan -> unmask)
+        a.n = *gptr(a.n_dev);
+        a.density = a.total ? (double)a.n / (double)a.total : 0.0;
+    }
+    const uint64_t A = wave * kWin;
+    const uint64_t full_lo = a.mis ? 16 : 0;
+    const uint64_t full_hi = (a.mis + a.total) & ~15ull;
+    if (A < full_lo || A + kWin > full_hi) {   // a window holding a partial vector (<= 2 per batch)
+#pragma unroll 1
+        for (int k = 0; k < K; ++k) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, A + (uint64_t)k * kStep, lane);
+        return;
+    }
+    u32x4 d[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) d[u] = load_vec<SRC_ALIGNED, NT>(a, A + (uint64_t)u * kSpan + 16ull * lane);
+    Table t;
+    table_issue(a, t, guess_base(a, 0, a.mis, A), lane);
+    np_resolve(a, t, A, lane);
+    uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t base = A + (uint64_t)k * kStep;
+        if (k > 0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) d[u] = load_vec<SRC_ALIGNED, NT>(a, base + (uint64_t)u * kSpan + 16ull * lane);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t A0 = base + (uint64_t)u * kSpan;
+            const u32x4 m = span_mask(a, t, A0, lane);
+            const u32x4 out = d[u] ^ m;
+            store_vec<NT>(a, A0 + 16ull * lane, out);
+            if constexpr (VAL) {
+                const uint32_t up = (uint32_t)__shfl_up((int)out[3], 1, kWave);
+                validate_span(a, t, A0, out, lane ? up : carry, k == 0 && u == 0, lane);
+                carry = (uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1);
+            }
+        }
+    }
+}
 
 }  // namespace netc_gpu
 
@@ -624,13 +727,53 @@ static hipError_t launch_nt(const Args& a, bool nt, int max_blocks, hipStream_t 
     return nt ? launch_u<U, true, true>(a, max_blocks, s) : launch_u<U, true, false>(a, max_blocks, s);
 }
 
-hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,
-                              const uint32_t* keys, uint64_t n, hipStream_t stream, const LaunchCfg& cfg,
-                              const uint64_t* n_dev) {
-    // n_dev: n is only an upper bound here (keys must then always be readable)
+// dynamic LDS per workgroup of the one-window-per-wave walk (0 = none); only limits
+// workgroups per CU.  NETC_MASK_LDS overrides (measurement sweeps, tools/).
+static int np_lds_bytes() {
+    static const int v = [] {
+        const char* e = getenv("NETC_MASK_LDS");
+        const long x = e ? strtol(e, nullptr, 10) : 0;
+        return (int)(x < 0 ? 0 : (x > 65536 ? 65536 : x));
+    }();
+    return v;
+}
+
+template <int U, int K, bool AL, bool NT, bool VAL = false>
+static hipError_t launch_np(const Args& a, hipStream_t s) {
+    const uint64_t blocks = (a.nwin + 3) / 4;   // 4 wavefronts per 256-thread workgroup
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((mask_np_kernel<U, K, AL, NT, VAL>), dim3((unsigned)blocks), dim3(256), np_lds_bytes(), s, a);
+    return hipGetLastError();
+}
+
+template <int U, bool AL, bool NT>
+static hipError_t launch_np_k(const Args& a, bool two, hipStream_t s) {
+    return two ? launch_np<U, 2, AL, NT>(a, s) : launch_np<U, 1, AL, NT>(a, s);
+}
+
+template <int U, bool AL>
+static hipError_t launch_np_nt(const Args& a, bool nt, bool two, hipStream_t s) {
+    return nt ? launch_np_k<U, AL, true>(a, two, s) : launch_np_k<U, AL, false>(a, two, s);
+}
+
+template <bool AL>
+static hipError_t launch_np_u(const Args& a, int U, bool nt, bool two, hipStream_t s) {
+    switch (U) {
+        case 1: return launch_np_nt<1, AL>(a, nt, two, s);
+        case 4: return launch_np_nt<4, AL>(a, nt, two, s);
+        case 8: return launch_np_nt<8, AL>(a, nt, two, s);
+        default: return launch_np_nt<2, AL>(a, nt, two, s);
+    }
+}
+
+static Args make_args(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off, const uint32_t* keys,
+                      uint64_t n, const uint64_t* n_dev) {
     Args a;
     a.n_dev = n_dev;
     a.verr = nullptr;
+    a.vtag = 0;
+    a.xcd_remap = 0;
     a.mis = (uint64_t)(uintptr_t)dst & 15u;
     a.dst_base = dst - a.mis;
     a.src_base = src - a.mis;
@@ -638,25 +781,43 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
     a.off = off;
     a.keys = (n || n_dev) ? keys : reinterpret_cast<const uint32_t*>(off);   // frame_entry always reads keys[0]
     a.n = n;
-    const bool aligned = (((uintptr_t)src ^ (uintptr_t)dst) & 15u) == 0;
-    const int U = aligned ? cfg.unroll : 4;
-    const uint64_t nvec = (a.mis + total + 15) / 16;
-    const uint64_t win_vec = 64ull * (uint64_t)U;
-    a.nwin = (nvec + win_vec - 1) / win_vec;
-    if (a.nwin == 0) return hipSuccess;
     a.density = total ? (double)n / (double)total : 0.0;
-    const int mb = cfg.max_blocks;
+    a.nwin = 0;
+    return a;
+}
+
+hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,
+                              const uint32_t* keys, uint64_t n, hipStream_t stream, const LaunchCfg& cfg,
+                              const uint64_t* n_dev) {
+    // n_dev: n is only an upper bound here (keys must then always be readable)
+    Args a = make_args(dst, src, total, off, keys, n, n_dev);
+    const bool aligned = (((uintptr_t)src ^ (uintptr_t)dst) & 15u) == 0;
+    const uint64_t nvec = (a.mis + total + 15) / 16;
+    if (nvec == 0) return hipSuccess;
+    const int flags = cfg.flags;
     // payload loads / stores non-temporal unless asked otherwise: every byte is touched once
-    const bool nt = cfg.flags < 0 || (cfg.flags & (kNtLoads | kNtStores));
-    if (!aligned) {   // src and dst differ mod 16: byte-assembled loads, one shape
-        return nt ? launch_u<4, false, true>(a, mb, stream) : launch_u<4, false, false>(a, mb, stream);
+    const bool nt = flags < 0 || (flags & (kNtLoads | kNtStores));
+    if (flags >= 0 && (flags & kPersistent)) {   // round 1's walk: one resident round striding over the chunks
+        const int U = aligned ? cfg.unroll : 4;
+        const uint64_t win_vec = 64ull * (uint64_t)U;
+        a.nwin = (nvec + win_vec - 1) / win_vec;
+        const int mb = cfg.max_blocks;
+        if (!aligned) return nt ? launch_u<4, false, true>(a, mb, stream) : launch_u<4, false, false>(a, mb, stream);
+        switch (U) {
+            case 1: return launch_nt<1>(a, nt, mb, stream);
+            case 2: return launch_nt<2>(a, nt, mb, stream);
+            case 8: return launch_nt<8>(a, nt, mb, stream);
+            default: return launch_nt<4>(a, nt, mb, stream);
+        }
     }
-    switch (U) {
-        case 1: return launch_nt<1>(a, nt, mb, stream);
-        case 2: return launch_nt<2>(a, nt, mb, stream);
-        case 8: return launch_nt<8>(a, nt, mb, stream);
-        default: return launch_nt<4>(a, nt, mb, stream);
-    }
+    // auto: two steps of `unroll` KiB per wavefront (1 KiB x 2: the fastest walk measured,
+    // frame-free and with frames, at 64 MiB and at 1 GiB)
+    const bool two = flags < 0 || (flags & kTwoSteps);
+    a.xcd_remap = (flags >= 0 && (flags & kXcdRemap)) ? 1 : 0;
+    const uint64_t win_vec = 64ull * (uint64_t)cfg.unroll * (two ? 2 : 1);
+    a.nwin = (nvec + win_vec - 1) / win_vec;
+    return aligned ? launch_np_u<true>(a, cfg.unroll, nt, two, stream)
+                   : launch_np_u<false>(a, cfg.unroll, nt, two, stream);
 }
 
 
@@ -751,8 +912,10 @@ __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uin
     valid[k] = verdict;
 }
 
+// the VAL kernels: 4 KiB windows (the seams utf8_messages re-checks are at multiples of it)
 template <bool AL>
-static hipError_t launch_val(const Args& a, hipStream_t s) {
+static hipError_t launch_val(const Args& a, bool persistent, hipStream_t s) {
+    if (!persistent) return launch_np<4, 1, AL, true, true>(a, s);
     const uint64_t cap = (uint64_t)resident_blocks<4, AL, true>();
     const uint64_t want = (a.nwin + 3) / 4;
     const int blocks = (int)(want < cap ? want : cap);
@@ -763,26 +926,17 @@ static hipError_t launch_val(const Args& a, hipStream_t s) {
 hipError_t launch_mask_validate(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,
                                 const uint32_t* keys, const uint8_t* header0, uint64_t n, uint8_t* verr, uint8_t tag,
                                 uint8_t* valid, hipStream_t stream, const LaunchCfg& cfg) {
-    (void)cfg;
     if (n == 0) return hipSuccess;
-    Args a;
-    a.n_dev = nullptr;
+    Args a = make_args(dst, src, total, off, keys, n, nullptr);
     a.verr = verr;
     a.vtag = tag;
-    a.mis = (uint64_t)(uintptr_t)dst & 15u;
-    a.dst_base = dst - a.mis;
-    a.src_base = src - a.mis;
-    a.total = total;
-    a.off = off;
-    a.keys = keys;
-    a.n = n;
-    a.density = total ? (double)n / (double)total : 0.0;
     const uint64_t nvec = (a.mis + total + 15) / 16;
-    a.nwin = (nvec + 255) / 256;   // U = 4 chunks of 64 vectors x 4
+    a.nwin = (nvec + 255) / 256;   // windows of 4 KiB (64 vectors x 4)
+    const bool persistent = cfg.flags >= 0 && (cfg.flags & kPersistent);
     hipError_t e;
     if (a.nwin) {
         const bool aligned = (((uintptr_t)src ^ (uintptr_t)dst) & 15u) == 0;
-        e = aligned ? launch_val<true>(a, stream) : launch_val<false>(a, stream);
+        e = aligned ? launch_val<true>(a, persistent, stream) : launch_val<false>(a, persistent, stream);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(utf8_messages, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dst, off, header0, n,

@@ -92,13 +92,17 @@ def gpu_init(device: int = 0) -> None:
 
 NETC_GPU_TUNE_NT_LOADS = 1
 NETC_GPU_TUNE_NT_STORES = 2
+NETC_GPU_TUNE_PERSISTENT = 4
+NETC_GPU_TUNE_TWO_STEPS = 8
+NETC_GPU_TUNE_XCD_ORDER = 16
 
 
 NETC_GPU_TUNE_AUTO = -1
 
 
-def tune(unroll: int = 4, max_blocks: int = 0, flags: int = NETC_GPU_TUNE_AUTO) -> None:
-    """netc_gpu_tune: process-wide launch shape (KiB per wave per trip, workgroup cap, cache/pipeline flags)."""
+def tune(unroll: int = 1, max_blocks: int = 0, flags: int = NETC_GPU_TUNE_AUTO) -> None:
+    """netc_gpu_tune: process-wide launch shape (KiB a wavefront loads at once, workgroup cap of the
+    persistent walk, cache / walk flags); the defaults are the C library's."""
     _check(_lib.gpu().netc_gpu_tune(unroll, max_blocks, flags))
 
 
@@ -255,13 +259,75 @@ def unmask_frames(wire, hdr, keys, result, length: Optional[int] = None, stream=
 
 
 def mask_stream_host(dst: np.ndarray, src: np.ndarray, offsets: np.ndarray, keys: np.ndarray,
-                     slot_bytes: int = 256 << 20, nslots: int = 4, device: int = 0) -> None:
-    """netc_gpu_mask_stream_host: host buffers through pinned slots on overlapped streams."""
+                     slot_bytes: int = 512 << 20, nslots: int = 2, device: int = 0) -> None:
+    """netc_gpu_mask_stream_host: host buffers through device slots on overlapped streams."""
+    off, kk = _host_frames(dst, src, offsets, keys)
+    _check(_lib.gpu().netc_gpu_mask_stream_host(device, _ptr(dst), _ptr(src), src.size, _ptr(off), _ptr(kk),
+                                                kk.size, slot_bytes, nslots))
+
+
+def _host_frames(dst, src, offsets, keys):
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
     kk = np.ascontiguousarray(keys, dtype=np.uint32)
     if src.dtype != np.uint8 or dst.dtype != np.uint8 or dst.size != src.size:
         raise ValueError("dst/src must be uint8 arrays of equal size")
     if off.size != kk.size + 1:
         raise ValueError("offsets must have nframes + 1 entries")
-    _check(_lib.gpu().netc_gpu_mask_stream_host(device, _ptr(dst), _ptr(src), src.size, _ptr(off), _ptr(kk),
-                                                kk.size, slot_bytes, nslots))
+    return off, kk
+
+
+class HostStream:
+    """netc_gpu_stream_*: the config-5 pipeline with its slots kept across calls (include/ws/mask.h)."""
+
+    def __init__(self, device: int = 0, slot_bytes: int = 0, nslots: int = 0):
+        h = ctypes.c_void_p()
+        _check(_lib.gpu().netc_gpu_stream_create(ctypes.byref(h), device, slot_bytes, nslots))
+        self._h = h
+
+    def mask(self, dst: np.ndarray, src: np.ndarray, offsets: np.ndarray, keys: np.ndarray) -> None:
+        if self._h is None:
+            raise ValueError("stream handle destroyed")
+        off, kk = _host_frames(dst, src, offsets, keys)
+        _check(_lib.gpu().netc_gpu_stream_mask(self._h, _ptr(dst), _ptr(src), src.size, _ptr(off), _ptr(kk),
+                                               kk.size))
+
+    def close(self) -> None:
+        if self._h is not None:
+            _lib.gpu().netc_gpu_stream_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PinnedArray:
+    """A uint8 numpy view of netc_gpu_host_alloc memory (page-locked); freed by close()."""
+
+    def __init__(self, nbytes: int):
+        p = _lib.gpu().netc_gpu_host_alloc(nbytes)
+        if not p:
+            raise NetcGpuError(NETC_GPU_ENOMEM, _lib.gpu().netc_gpu_strerror().decode())
+        self._p = p
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p)) if nbytes else \
+            np.zeros(0, dtype=np.uint8)
+
+    def close(self) -> None:
+        if self._p:
+            self.array = None
+            _lib.gpu().netc_gpu_host_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

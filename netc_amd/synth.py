@@ -66,3 +66,12 @@ def config(name: str, shard: int = 0):
         raise ValueError(name)
     keys = random_keys(off.size - 1, stream=200 + shard)
     return off, keys, int(off[-1])
+
+
+def fill_payload(out: np.ndarray, seed: int = SEED, stream: int = 3, block: int = 64 << 20) -> None:
+    """Fill a large uint8 array (GiBs, e.g. a pinned host ring) with seeded bytes, fast: one
+    random block, XORed with the block index for every block it is copied to."""
+    base = rng(seed, stream).integers(0, 256, size=min(block, max(out.size, 1)), dtype=np.uint8)
+    for i, lo in enumerate(range(0, out.size, base.size)):
+        hi = min(out.size, lo + base.size)
+        np.bitwise_xor(base[: hi - lo], np.uint8(i & 0xFF), out=out[lo:hi])

@@ -186,10 +186,11 @@ def test_one_huge_frame(torch_cuda):
     run_case(torch_cuda, payload, frames_from_sizes([total]), np.array([0xDEADBEEF], dtype=np.uint32), 6, 6)
 
 
-@pytest.mark.parametrize("unroll,max_blocks", [(1, 2048), (2, 64), (8, 0), (4, 1), (4, 100000), (4, 0)])
-@pytest.mark.parametrize("flags", [-1, 0, 3])
+@pytest.mark.parametrize("unroll,max_blocks", [(1, 2048), (2, 64), (8, 0), (4, 1), (4, 100000), (2, 0)])
+@pytest.mark.parametrize("flags", [-1, 0, 3, 7, 4, 11, 27])
 def test_launch_shapes(torch_cuda, unroll, max_blocks, flags):
-    """Every kernel instantiation (U x cache-hint flags x grid cap) is bit-exact."""
+    """Every kernel instantiation is bit-exact: U x cache-hint flags x walk (one window per
+    wavefront, one or two steps, XCD order; or the persistent walk, flags & 4, with its grid cap)."""
     try:
         nm.tune(unroll, max_blocks, flags)
         off = synth.mixed_offsets(5 << 20, 1, 9000, seed=13)
@@ -200,7 +201,7 @@ def test_launch_shapes(torch_cuda, unroll, max_blocks, flags):
         nm.tune()
 
 
-@pytest.mark.parametrize("flags", [-1, 0])
+@pytest.mark.parametrize("flags", [-1, 0, 7, 11])
 def test_near_uniform_frames(torch_cuda, flags):
     """Evenly sized frames with sparse irregular ones: the table-base guesses are exact
     until an irregular frame shifts every later frame start, then must recover
