@@ -24,6 +24,8 @@
  *                              automatically when a slot fills)
  *   netc_ws_ingest_next()      the oldest finished batch
  *   netc_ws_ingest_release()   hand a batch's slot back to the ring
+ *   netc_ws_ingest_next_message()  the next reassembled message, in ws_parse_frame's
+ *                              form (struct ws_message, 0 / 1 / WS_FRAME_PARSE_ERROR_*)
  *   netc_ws_ingest_destroy()
  *   netc_ws_batch_payload()    where frame k's payload lies in a batch
  *
@@ -43,7 +45,8 @@ extern "C" {
 
 struct netc_ws_ingest;
 
-/** netc_ws_ingest_create flag: reject what RFC 6455 forbids from a client (as NETC_WS_SCAN_STRICT). */
+/** netc_ws_ingest_create flag: reject what RFC 6455 forbids from a client (as NETC_WS_SCAN_STRICT).
+ *  Without it (the default, 0) every header is accepted, as the reference's parser does. */
 #define NETC_WS_INGEST_STRICT 1
 
 /* return codes of the ingest entries, besides 0 and the NETC_GPU_E* codes of mask.h */
@@ -102,6 +105,36 @@ int netc_ws_ingest_next(struct netc_ws_ingest *ing, struct netc_ws_batch *out, i
 
 /** Returns a batch's slot to the ring.  0 or NETC_GPU_EINVAL. */
 int netc_ws_ingest_release(struct netc_ws_ingest *ing, const struct netc_ws_batch *batch);
+
+struct ws_message;   /* include/ws/common.h */
+
+/**
+ * The next complete message of the stream, with the reference's receive contract
+ * (ws_parse_frame, include/ws/common.h; src/ws/common.c:146-347), read from the
+ * delivered batches (payloads already unmasked on the GPU):
+ *   0   *message is filled: opcode = the last non-continuation frame's opcode (:163-164),
+ *       buffer = every frame's payload up to and including the one with FIN, back to
+ *       back, in one malloc'd buffer the caller now owns and frees with free(); a TEXT
+ *       message gets a NUL appended, counted in payload_length (:340-344)
+ *   1   no complete message yet: receive more (netc_ws_ingest_recv / _write) and call
+ *       again; with wait != 0 the call waits for batches already on the GPU
+ *   WS_FRAME_PARSE_ERROR_PAYLOAD_TOO_BIG (-3)  the message's accumulated payload would
+ *       exceed max_payload_length (:210-211, :261-262), or a frame exceeded the ring's
+ *       max_frame_bytes
+ *   WS_FRAME_PARSE_ERROR_INVALID_FRAME_LENGTH (-2)  strict mode rejected a header
+ *   WS_FRAME_PARSE_ERROR_RECV (-1)  the peer closed (or recv failed) and every complete
+ *       message before that point has been returned
+ *   NETC_GPU_E*  a device / runtime failure
+ * Errors are sticky: the connection is over, as with the reference (its caller closes
+ * with 1002, src/web/server.c:88-95).  As in the reference, a control frame that arrives
+ * between the fragments of a message is appended to that message and sets its opcode
+ * (the reference's reassembly does not set control frames aside); a control frame
+ * between messages is its own message.  A message the call has started stays in the
+ * ring object (freed by netc_ws_ingest_destroy if never completed).  Batches are taken
+ * and released by this call: do not mix it with netc_ws_ingest_next on one object.
+ */
+int netc_ws_ingest_next_message(struct netc_ws_ingest *ing, struct ws_message *message, size_t max_payload_length,
+                                int wait);
 
 /** Frame k's payload inside batch->wire: *offset, *length.  0 or NETC_GPU_EINVAL.  Host only. */
 int netc_ws_batch_payload(const struct netc_ws_batch *batch, uint64_t k, uint64_t *offset, uint64_t *length);

@@ -26,6 +26,7 @@
 
 #include <errno.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/socket.h>
 
@@ -37,6 +38,7 @@ extern "C" {
 #include "../../include/ws/mask.h"
 #include "../../include/ws/frame.h"
 #include "../../include/ws/ingest.h"
+#include "../../include/ws/common.h"
 extern __thread int netc_errno_reason;   // include/utils/error.h
 }
 
@@ -62,6 +64,7 @@ struct IngestSlot {
     uint64_t* h_res = nullptr;   // pinned: frames, consumed, error
     hipStream_t stream = nullptr;
     hipEvent_t scanned = nullptr, done = nullptr;
+    netc_gpu::ScanScratch* scratch = nullptr;   // the frame scan's device scratch, sized for the slot
     int state = kFree;
     uint64_t fill = 0;           // received bytes, at h_buf + carry_cap
     uint64_t carry = 0;          // carried bytes in front of them, at h_buf + carry_cap - carry
@@ -74,15 +77,29 @@ struct IngestSlot {
 
 struct DeviceGuard {
     int prev = -1;
+    bool switched = false;
     hipError_t err = hipSuccess;
     explicit DeviceGuard(int device) {
         err = hipGetDevice(&prev);
-        if (err == hipSuccess && prev != device) err = hipSetDevice(device);
+        if (err != hipSuccess || prev == device) return;
+        err = hipSetDevice(device);
+        switched = err == hipSuccess;
     }
     ~DeviceGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+        if (switched) (void)hipSetDevice(prev);
     }
+};
+
+// the message-level reader (netc_ws_ingest_next_message): the reference's reassembly
+// state, src/ws/common.c:163-164,210-216,303-309,333-347
+struct MessageState {
+    bool have = false;           // a batch is taken and being read
+    netc_ws_batch batch{};
+    uint64_t k = 0;              // next frame of the batch
+    uint8_t* buf = nullptr;      // the message so far (malloc; the caller's once delivered)
+    size_t size = 0, cap = 0;
+    uint8_t opcode = 0;          // the last non-continuation frame's opcode, as the reference
+    int err = 0;                 // sticky message-level error (WS_FRAME_PARSE_ERROR_*)
 };
 
 }  // namespace
@@ -100,12 +117,16 @@ struct netc_ws_ingest {
     int head = 0, count = 0;
     int sticky = 0;        // a stream error (TOO_BIG / PROTOCOL): reported from then on
     int sticky_after = -1; // ... once the batch of this slot has been handed out (-1: now)
+    uint64_t max_frame = 0;   // max_frame_bytes (payload bytes per frame)
+    bool closed = false;   // recv saw the peer close
+    MessageState msg;
 };
 
 namespace {
 
 void free_slot(IngestSlot& s) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
+    netc_gpu::scan_scratch_free(s.scratch);
     if (s.h_buf) (void)hipHostFree(s.h_buf);
     if (s.h_hdr) (void)hipHostFree(s.h_hdr);
     if (s.h_keys) (void)hipHostFree(s.h_keys);
@@ -141,6 +162,10 @@ int alloc_slot(const netc_ws_ingest* g, IngestSlot& s) {
         (e = hipMalloc((void**)&s.d_b0, mf)) != hipSuccess ||
         (e = hipMalloc((void**)&s.d_res, 3 * sizeof(uint64_t))) != hipSuccess)
         return api_fail_hip(NETC_GPU_ENOMEM, "ingest: device allocation", e);
+    // the scan's scratch belongs to the slot (freed with it), sized for a full slot now
+    if (!(s.scratch = netc_gpu::scan_scratch_new())) return api_fail(NETC_GPU_ENOMEM, "ingest: host allocation");
+    if ((e = netc_gpu::scan_scratch_reserve(s.scratch, g->cap, s.stream)) != hipSuccess)
+        return api_fail_hip(NETC_GPU_ENOMEM, "ingest: frame scan scratch", e);
     return 0;
 }
 
@@ -221,7 +246,7 @@ int submit_cur(netc_ws_ingest* g) {
     if ((e = hipMemcpyAsync(s.d_buf, h, len, hipMemcpyHostToDevice, s.stream)) != hipSuccess)
         return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: H2D copy", e);
     if ((e = netc_gpu::launch_scan_frames(s.d_buf, len, 0, g->strict != 0, s.d_hdr, s.d_keys, s.d_b0, g->max_frames,
-                                          s.d_res, s.stream)) != hipSuccess)
+                                          s.d_res, s.stream, s.scratch)) != hipSuccess)
         return api_fail_hip(e == hipErrorOutOfMemory ? NETC_GPU_ENOMEM : NETC_GPU_ELAUNCH, "ingest: frame scan", e);
     if ((e = hipMemcpyAsync(s.h_res, s.d_res, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
         (e = hipEventRecord(s.scanned, s.stream)) != hipSuccess)
@@ -276,6 +301,7 @@ int netc_ws_ingest_create(struct netc_ws_ingest** out, int device, size_t slot_b
     g->strict = (flags & NETC_WS_INGEST_STRICT) ? 1 : 0;
     g->nslots = nslots;
     g->slot_bytes = slot_bytes;
+    g->max_frame = max_frame_bytes;
     g->carry_cap = max_frame_bytes + 14;   // one whole frame: payload + the longest masked header
     g->cap = g->carry_cap + slot_bytes;
     // every frame is >= 6 bytes under the strict checks (masked), >= 2 otherwise
@@ -299,6 +325,7 @@ int netc_ws_ingest_create(struct netc_ws_ingest** out, int device, size_t slot_b
 
 void netc_ws_ingest_destroy(struct netc_ws_ingest* g) {
     if (!g) return;
+    free(g->msg.buf);   // a message not completed yet (delivered ones are the caller's)
     DeviceGuard dg(g->device);
     for (int i = 0; i < g->nslots; ++i) free_slot(g->slots[i]);
     delete[] g->slots;
@@ -311,6 +338,12 @@ long netc_ws_ingest_recv(struct netc_ws_ingest* g, int fd) {
     DeviceGuard dg(g->device);
     if (dg.err != hipSuccess) return api_fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", dg.err);
     if (int r = acquire(g)) return r;
+    if (g->slots[g->cur].fill == g->slot_bytes) {
+        // a full slot whose submission failed earlier: submit it (or report why not) rather
+        // than recv() into no room, which would read as the peer closing
+        if (int e = submit_cur(g)) return e;
+        if (int r = acquire(g)) return r;
+    }
     IngestSlot& s = g->slots[g->cur];
     uint8_t* dst = s.h_buf + g->carry_cap + s.fill;
     const size_t room = (size_t)(g->slot_bytes - s.fill);
@@ -326,6 +359,7 @@ long netc_ws_ingest_recv(struct netc_ws_ingest* g, int fd) {
         return NETC_WS_INGEST_ERECV;
     }
     if (r == 0) {   // the peer closed: what it sent goes to the GPU
+        g->closed = true;
         if (int e = submit_cur(g)) return e;
         return api_fail(NETC_WS_INGEST_CLOSED, "ingest: the peer closed the connection");
     }
@@ -368,10 +402,8 @@ int netc_ws_ingest_submit(struct netc_ws_ingest* g) {
 
 int netc_ws_ingest_next(struct netc_ws_ingest* g, struct netc_ws_batch* out, int wait) {
     if (!g || !out) return api_fail(NETC_GPU_EINVAL, "ingest: null argument");
-    if (g->count == 0) {
-        const int st = sticky_now(g);
-        return st ? api_fail(st, "ingest: the stream has ended (error)") : 0;
-    }
+    if (const int st = sticky_now(g)) return api_fail(st, "ingest: the stream has ended (error)");
+    if (g->count == 0) return 0;
     DeviceGuard dg(g->device);
     if (dg.err != hipSuccess) return api_fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", dg.err);
     const int i = g->fifo[g->head];
@@ -395,6 +427,21 @@ int netc_ws_ingest_next(struct netc_ws_ingest* g, struct netc_ws_batch* out, int
     s.state = kTaken;
     g->head = (g->head + 1) % 16;
     --g->count;
+    // the payload limit (the reference's PAYLOAD_TOO_BIG per frame, src/ws/common.c:210,261):
+    // a longer frame ends the batch before it, and the stream with NETC_WS_INGEST_TOO_BIG
+    // (frames that do not fit a slot's carry room never get here: submit_cur stops them)
+    if (g->max_frame < s.carry + s.fill) {
+        for (uint64_t k = 0; k < out->nframes; ++k) {
+            uint64_t off = 0, len = 0;
+            (void)netc_ws_batch_payload(out, k, &off, &len);
+            if (len > g->max_frame) {
+                out->nframes = k;
+                out->len = out->hdr[k];
+                set_sticky(g, NETC_WS_INGEST_TOO_BIG, i);   // reported from the next call on
+                return 1;
+            }
+        }
+    }
     if (s.err != ~0ull) set_sticky(g, NETC_WS_INGEST_PROTOCOL, i);   // reported from the next call on
     return 1;
 }
@@ -404,6 +451,83 @@ int netc_ws_ingest_release(struct netc_ws_ingest* g, const struct netc_ws_batch*
         return api_fail(NETC_GPU_EINVAL, "ingest: not a batch handed out by this ingest");
     g->slots[b->slot].state = kFree;
     return 0;
+}
+
+// the reference's error code for an ingest stream error (ws_parse_frame's contract)
+static int message_code(int r) {
+    switch (r) {
+        case NETC_WS_INGEST_TOO_BIG: return WS_FRAME_PARSE_ERROR_PAYLOAD_TOO_BIG;
+        case NETC_WS_INGEST_PROTOCOL: return WS_FRAME_PARSE_ERROR_INVALID_FRAME_LENGTH;
+        case NETC_WS_INGEST_CLOSED:
+        case NETC_WS_INGEST_ERECV: return WS_FRAME_PARSE_ERROR_RECV;
+        default: return r;   // NETC_GPU_E* (a device / runtime failure)
+    }
+}
+
+static bool msg_append(MessageState& m, const uint8_t* p, size_t n) {
+    if (m.size + n > m.cap || !m.buf) {
+        size_t cap = m.cap ? m.cap : 64;
+        while (cap < m.size + n) cap *= 2;
+        uint8_t* nb = (uint8_t*)realloc(m.buf, cap);
+        if (!nb) return false;
+        m.buf = nb;
+        m.cap = cap;
+    }
+    if (n) memcpy(m.buf + m.size, p, n);
+    m.size += n;
+    return true;
+}
+
+int netc_ws_ingest_next_message(struct netc_ws_ingest* g, struct ws_message* message, size_t max_payload_length,
+                                int wait) {
+    if (!g || !message) return api_fail(NETC_GPU_EINVAL, "ingest: null argument");
+    MessageState& m = g->msg;
+    if (m.err) return m.err;
+    for (;;) {
+        if (!m.have) {
+            int r = netc_ws_ingest_next(g, &m.batch, wait);
+            if (r == 0 && g->count == 0 && g->cur >= 0 && g->slots[g->cur].fill) {
+                // nothing in flight but received bytes waiting: send them to the GPU now
+                if (int e = netc_ws_ingest_submit(g)) return m.err = message_code(e);
+                r = netc_ws_ingest_next(g, &m.batch, wait);
+            }
+            if (r < 0) return m.err = message_code(r);
+            if (r == 0) {
+                if (g->closed && g->count == 0 && (g->cur < 0 || g->slots[g->cur].fill == 0))
+                    return m.err = WS_FRAME_PARSE_ERROR_RECV;   // the peer closed (recv() == 0, :151-154)
+                return 1;                                      // need more data (:153)
+            }
+            m.have = true;
+            m.k = 0;
+        }
+        const netc_ws_batch& b = m.batch;
+        while (m.k < b.nframes) {
+            const uint64_t k = m.k++;
+            const uint8_t b0 = b.b0[k];
+            const uint8_t op = b0 & 0x0F;
+            uint64_t off = 0, len = 0;
+            (void)netc_ws_batch_payload(&b, k, &off, &len);
+            if (op != WS_OPCODE_CONTINUE) m.opcode = op;                        // :163-164
+            if (len + m.size > max_payload_length)                             // :210-211, :261-262
+                return m.err = WS_FRAME_PARSE_ERROR_PAYLOAD_TOO_BIG;
+            if (!msg_append(m, b.wire + off, (size_t)len))
+                return m.err = api_fail(NETC_GPU_ENOMEM, "ingest: message buffer");
+            if (b0 & 0x80) {                                                    // FIN: the message (:340-346)
+                if (m.opcode == WS_OPCODE_TEXT && !msg_append(m, (const uint8_t*)"", 1))
+                    return m.err = api_fail(NETC_GPU_ENOMEM, "ingest: message buffer");
+                if (!m.buf && !(m.buf = (uint8_t*)malloc(1)))   // an empty message still gets a buffer
+                    return m.err = api_fail(NETC_GPU_ENOMEM, "ingest: message buffer");
+                message->opcode = m.opcode;
+                message->buffer = m.buf;
+                message->payload_length = m.size;
+                m.buf = nullptr;
+                m.size = m.cap = 0;
+                return 0;
+            }
+        }
+        (void)netc_ws_ingest_release(g, &b);
+        m.have = false;
+    }
 }
 
 int netc_ws_batch_payload(const struct netc_ws_batch* b, uint64_t k, uint64_t* offset, uint64_t* length) {

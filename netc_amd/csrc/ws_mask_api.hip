@@ -294,6 +294,17 @@ int netc_gpu_scan_frames(int device, const void* d_wire, size_t len, uint64_t st
     return 0;
 }
 
+int netc_gpu_scan_release(int device, void* stream) {
+    if (int r = check_device(device)) return r;
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+    // queued scans on that stream may still use the scratch
+    hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    if (e != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipStreamSynchronize", e);
+    (void)netc_gpu::release_stream_scratch(device, (hipStream_t)stream);
+    return 0;
+}
+
 int netc_gpu_unmask_frames(int device, void* d_wire, size_t len, const uint64_t* d_hdr, const uint32_t* d_keys,
                            size_t max_frames, const uint64_t* d_result, void* stream) {
     if (int r = check_device(device)) return r;
@@ -304,7 +315,6 @@ int netc_gpu_unmask_frames(int device, void* d_wire, size_t len, const uint64_t*
     if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
     hipError_t e = netc_gpu::launch_unmask_scanned((uint8_t*)d_wire, len, d_hdr, d_keys, max_frames, d_result,
                                                    (hipStream_t)stream, g_cfg);
-    if (e == hipErrorOutOfMemory) return fail_hip(NETC_GPU_ENOMEM, "unmask view scratch", e);
     if (e != hipSuccess) return fail_hip(NETC_GPU_ELAUNCH, "unmask launch", e);
     return 0;
 }

@@ -50,13 +50,23 @@ hipError_t launch_mask_validate(uint8_t* dst, const uint8_t* src, uint64_t total
 // ws_frame_gpu.hip: wire offsets (n + 1 entries into wo), then the wire bytes of
 // every frame (header, key, masked payload) into wire.  wire_bound >= wo[n].
 hipError_t launch_wire_offsets(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream);
-// ws_scan_gpu.hip: frame boundaries of a received stream (include/ws/frame.h)
+// ws_scan_gpu.hip: frame boundaries of a received stream (include/ws/frame.h).  Scratch:
+// caller-owned (`own`, e.g. one per ingest slot, freed with it) or, with own == nullptr,
+// cached per (device, stream) until release_stream_scratch (netc_gpu_scan_release).
+struct ScanScratch;
+ScanScratch* scan_scratch_new();
+void scan_scratch_free(ScanScratch* s);   // no work using it may be queued
+hipError_t scan_scratch_reserve(ScanScratch* s, uint64_t len, hipStream_t stream);   // sized for a len-byte stream
+int release_stream_scratch(int device, hipStream_t stream);   // 1 if there was a cached entry
 hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start, bool strict, uint64_t* hdr,
                               uint32_t* keys, uint8_t* b0, uint64_t max_frames, uint64_t* result,
-                              hipStream_t stream);
+                              hipStream_t stream, ScanScratch* own = nullptr);
 hipError_t launch_unmask_scanned(uint8_t* wire, uint64_t len, const uint64_t* hdr, const uint32_t* keys,
                                  uint64_t max_frames, const uint64_t* result, hipStream_t stream,
                                  const LaunchCfg& cfg);
+// ws_mask_gpu.hip: the batch kernel over the frames a scan found (no view array)
+hipError_t launch_mask_scanned(uint8_t* wire, uint64_t len, const uint64_t* hdr, const uint32_t* keys,
+                               uint64_t max_frames, const uint64_t* result, hipStream_t stream);
 
 // ws_mask_api.hip: the C-ABI's error side channel and process-wide launch shape
 int api_fail(int code, const char* fmt, ...);                 // sets the message + netc_errno_reason, returns code

@@ -55,24 +55,70 @@ struct Table {
     bool tail;        // frame n (the open-ended pass-through frame) is in the table
 };
 
+// Frame k's offset / key.  Args: the caller's arrays.  ArgsScan (frames a
+// netc_gpu_scan_frames call found, unmasked in place): virtual frame 2k is frame k's
+// header (key 0: passed through), 2k + 1 its payload, read from the scan's header
+// offsets, keys and the header bytes in the buffer itself -- no view array is built.
+__device__ __forceinline__ uint64_t off_at(const Args& a, int64_t i) { return gptr(a.off)[i]; }
+__device__ __forceinline__ uint32_t key_at(const Args& a, int64_t i) { return gptr(a.keys)[i]; }
+
+struct ArgsScan : Args {
+    const uint64_t* hdr;       // scan output: header offset of frame k
+    const uint32_t* fkeys;     // scan output: packed key of frame k
+    const uint64_t* result;    // scan result (frames found: result[0])
+    uint64_t max_frames;       // frames the scan recorded at most
+};
+
+// header length of the frame whose header starts at p (the wire bytes are in the buffer)
+__device__ __forceinline__ uint64_t header_len(const ArgsScan& a, uint64_t p) {
+    const uint32_t second = gptr(a.src_base + a.mis)[p + 1];
+    const uint32_t code = second & 0x7F;
+    return 2 + (code == 126 ? 2 : (code == 127 ? 8 : 0)) + ((second & 0x80) ? 4 : 0);
+}
+
+__device__ __forceinline__ uint64_t off_at(const ArgsScan& a, int64_t i) {
+    const int64_t nf = (int64_t)(a.n >> 1), k = i >> 1;
+    if (k < nf) {
+        const uint64_t p = gptr(a.hdr)[k];
+        return (i & 1) ? p + header_len(a, p) : p;
+    }
+    if (nf == 0) return 0;
+    // i == 2 nf: the end of the last frame's payload (its extended length read from the header)
+    const uint64_t p = gptr(a.hdr)[nf - 1];
+    const NETC_GLOBAL uint8_t* w = gptr(a.src_base + a.mis) + p;
+    const uint32_t code = w[1] & 0x7F;
+    uint64_t len = code;
+    if (code >= 126) {
+        len = 0;
+        for (int j = 0; j < (code == 126 ? 2 : 8); ++j) len = len << 8 | w[2 + j];
+    }
+    return p + header_len(a, p) + len;
+}
+
+__device__ __forceinline__ uint32_t key_at(const ArgsScan& a, int64_t i) {
+    return (i & 1) ? gptr(a.fkeys)[i >> 1] : 0u;
+}
+
 // start / key of virtual frame v in P coordinates.  Branch-free: both loads are
 // always issued at clamped (valid) indices and the virtual-frame values are
 // selected afterwards, so the loads stay straight-line code and the compiler can
 // count them in vmcnt instead of draining every outstanding load (a load under a
 // per-lane branch forces s_waitcnt vmcnt(0) at the next use).  With n == 0 the
 // host points keys at the offsets array, so keys[0] is always readable.
-__device__ __forceinline__ void frame_entry(const Args& a, int64_t v, uint64_t& s, uint32_t& k) {
+template <class A>
+__device__ __forceinline__ void frame_entry(const A& a, int64_t v, uint64_t& s, uint32_t& k) {
     const int64_t n = (int64_t)a.n;
     const int64_t vo = v < 0 ? 0 : (v > n ? n : v);
     const int64_t vk = v < 0 ? 0 : (v >= n ? (n > 0 ? n - 1 : 0) : v);
-    const uint64_t off = gptr(a.off)[vo];
-    const uint32_t key = gptr(a.keys)[vk];
+    const uint64_t off = off_at(a, vo);
+    const uint32_t key = key_at(a, vk);
     s = v < 0 ? 0 : (v <= n ? off + a.mis : kInf);
     k = (v >= 0 && v < n) ? key : 0u;
 }
 
 // issue the table loads (frames kb .. kb+63, one per lane) without waiting for them
-__device__ __forceinline__ void table_issue(const Args& a, Table& t, int64_t kb, int lane) {
+template <class A>
+__device__ __forceinline__ void table_issue(const A& a, Table& t, int64_t kb, int lane) {
     t.kb = kb;
     frame_entry(a, kb + lane, t.start, t.key);
     t.tail = kb + (kWave - 1) >= (int64_t)a.n;
@@ -80,7 +126,8 @@ __device__ __forceinline__ void table_issue(const Args& a, Table& t, int64_t kb,
 
 __device__ __forceinline__ void table_finish(Table& t) { t.last = readlane64(t.start, kWave - 1); }
 
-__device__ __forceinline__ void table_load(const Args& a, Table& t, int64_t kb, int lane) {
+template <class A>
+__device__ __forceinline__ void table_load(const A& a, Table& t, int64_t kb, int lane) {
     table_issue(a, t, kb, lane);
     table_finish(t);
 }
@@ -97,7 +144,8 @@ __device__ __forceinline__ bool table_brackets(const Table& t, uint64_t P) {
 // (index f_known) and the batch's mean frame density: frames are independent
 // draws, so the guess error grows only with the square root of the frames in
 // between; the window is biased forward so the chunk's later frames fit too.
-__device__ __forceinline__ int64_t guess_base(const Args& a, int64_t f_known, uint64_t s_known, uint64_t P) {
+template <class A>
+__device__ __forceinline__ int64_t guess_base(const A& a, int64_t f_known, uint64_t s_known, uint64_t P) {
     if (P < a.mis) return -1;
     const double ahead = (double)(P - s_known) * a.density;
     int64_t g = f_known + (int64_t)ahead - 24;
@@ -114,7 +162,8 @@ __device__ __forceinline__ int64_t guess_base(const Args& a, int64_t f_known, ui
 //      it brackets q (always, for uniform frames) H - L <= 16 after ONE load;
 //   2. otherwise 64-ary narrowing, one coalesced probe + one ballot per step.
 // The caller's table load is the final (second) dependent load.
-__device__ int64_t locate(const Args& a, uint64_t P, int lane) {
+template <class A>
+__device__ int64_t locate(const A& a, uint64_t P, int lane) {
     if (P < a.mis) return -1;
     const uint64_t q = P - a.mis;
     int64_t L = -1, H = (int64_t)a.n + 1;
@@ -126,7 +175,7 @@ __device__ int64_t locate(const Args& a, uint64_t P, int lane) {
         const int64_t base = g - 31 * kStride;
         const int64_t idx = base + (int64_t)lane * kStride;
         const bool valid = idx >= 0 && idx <= (int64_t)a.n;
-        const uint64_t val = valid ? gptr(a.off)[idx] : 0;
+        const uint64_t val = valid ? off_at(a, idx) : 0;
         const uint64_t le = __ballot(valid && val <= q);   // probes at or before q
         const uint64_t gt = __ballot(valid && val > q);    // probes after q
         if (le) {
@@ -145,7 +194,7 @@ __device__ int64_t locate(const Args& a, uint64_t P, int lane) {
         const int64_t step = (H - lo + kWave - 1) / kWave;   // probes lo, lo + step, ... cover [lo, H)
         const int64_t idx = lo + (int64_t)lane * step;
         const bool valid = idx < H;
-        const uint64_t val = valid ? gptr(a.off)[idx] : kInf;
+        const uint64_t val = valid ? off_at(a, idx) : kInf;
         const uint64_t le = __ballot(valid && val <= q);
         const uint64_t gt = __ballot(valid && val > q);
         if (le) L = lo + (int64_t)(63 - __builtin_clzll(le)) * step;
@@ -156,7 +205,8 @@ __device__ int64_t locate(const Args& a, uint64_t P, int lane) {
 
 // Mask for this lane's vector in the span starting at A0 (P coords, 16-aligned,
 // lane's vector = A0 + 16 * lane).  Slides the table forward when needed.
-__device__ __forceinline__ u32x4 span_mask(const Args& a, Table& t, uint64_t A0, int lane) {
+template <class A>
+__device__ __forceinline__ u32x4 span_mask(const A& a, Table& t, uint64_t A0, int lane) {
     const uint64_t Aend = A0 + kSpan;
     // invariant: entry 0 starts at or before A0.  Make the table cover the span.
     if (!t.tail && t.last < Aend) {
@@ -238,8 +288,8 @@ __device__ __forceinline__ u32x4 span_mask(const Args& a, Table& t, uint64_t A0,
     return mask;
 }
 
-template <bool SRC_ALIGNED, bool NT>
-__device__ __forceinline__ u32x4 load_vec(const Args& a, uint64_t P) {
+template <bool SRC_ALIGNED, bool NT, class A>
+__device__ __forceinline__ u32x4 load_vec(const A& a, uint64_t P) {
     if constexpr (SRC_ALIGNED) {
         const NETC_GLOBAL u32x4* p = gptr(reinterpret_cast<const u32x4*>(a.src_base + P));
         if constexpr (NT) return __builtin_nontemporal_load(p);
@@ -254,8 +304,8 @@ __device__ __forceinline__ u32x4 load_vec(const Args& a, uint64_t P) {
     }
 }
 
-template <bool NT>
-__device__ __forceinline__ void store_vec(const Args& a, uint64_t P, u32x4 v) {
+template <bool NT, class A>
+__device__ __forceinline__ void store_vec(const A& a, uint64_t P, u32x4 v) {
     NETC_GLOBAL u32x4* p = gptr(reinterpret_cast<u32x4*>(a.dst_base + P));
     if constexpr (NT) __builtin_nontemporal_store(v, p);
     else *p = v;
@@ -263,7 +313,8 @@ __device__ __forceinline__ void store_vec(const Args& a, uint64_t P, u32x4 v) {
 
 // Partial vector at either end of the buffer: byte-granular, only bytes in
 // P in [mis, mis + total) are read or written.
-__device__ __forceinline__ void edge_vec(const Args& a, uint64_t P, u32x4 mask) {
+template <class A>
+__device__ __forceinline__ void edge_vec(const A& a, uint64_t P, u32x4 mask) {
     const uint64_t lo = a.mis, hi = a.mis + a.total;
 #pragma unroll
     for (int bi = 0; bi < 16; ++bi) {
@@ -433,8 +484,8 @@ __device__ __forceinline__ void validate_span(const Args& a, const Table& t, uin
     }
 }
 
-template <int U, bool SRC_ALIGNED, bool NT, bool VAL>
-__device__ __forceinline__ void edge_chunk(const Args& a, uint64_t A, int lane) {
+template <int U, bool SRC_ALIGNED, bool NT, bool VAL, class AT>
+__device__ __forceinline__ void edge_chunk(const AT& a, uint64_t A, int lane) {
     const uint64_t full_lo = a.mis ? 16 : 0;
     const uint64_t full_hi = (a.mis + a.total) & ~15ull;
     const uint64_t vec_end = (a.mis + a.total + 15) & ~15ull;
@@ -607,13 +658,15 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
 // the table carried across them.
 // ---------------------------------------------------------------------------
 
-__device__ __forceinline__ int64_t clamp_base(const Args& a, int64_t g) {
+template <class A>
+__device__ __forceinline__ int64_t clamp_base(const A& a, int64_t g) {
     g = g < -1 ? -1 : g;
     return g > (int64_t)a.n ? (int64_t)a.n : g;
 }
 
 // make t (issued at a guessed base) hold the frame containing A
-__device__ __forceinline__ void np_resolve(const Args& a, Table& t, uint64_t A, int lane) {
+template <class AT>
+__device__ __forceinline__ void np_resolve(const AT& a, Table& t, uint64_t A, int lane) {
     table_finish(t);
 #pragma unroll 1
     for (int step = 0; step < 2; ++step) {
@@ -631,8 +684,21 @@ __device__ __forceinline__ void np_resolve(const Args& a, Table& t, uint64_t A, 
     if (!table_brackets(t, A)) table_load(a, t, locate(a, A, lane), lane);
 }
 
-template <int U, int K, bool SRC_ALIGNED, bool NT, bool VAL = false>
-__global__ __launch_bounds__(256) void mask_np_kernel(Args a) {
+// the frame count when it is produced on the device by an earlier kernel (scan -> unmask)
+__device__ __forceinline__ void init_frames(Args& a) {
+    if (a.n_dev) {
+        a.n = *gptr(a.n_dev);
+        a.density = a.total ? (double)a.n / (double)a.total : 0.0;
+    }
+}
+__device__ __forceinline__ void init_frames(ArgsScan& a) {
+    const uint64_t f = *gptr(a.result);
+    a.n = 2 * (f < a.max_frames ? f : a.max_frames);   // header + payload per frame
+    a.density = a.total ? (double)a.n / (double)a.total : 0.0;
+}
+
+template <int U, int K, bool SRC_ALIGNED, bool NT, bool VAL = false, class AT = Args>
+__global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
     constexpr uint64_t kStep = kSpan * U;
     constexpr uint64_t kWin = kStep * K;
     const int lane = threadIdx.x & (kWave - 1);
@@ -648,10 +714,7 @@ __global__ __launch_bounds__(256) void mask_np_kernel(Args a) {
     if (wave >= a.nwin) return;
     extern __shared__ uint32_t lds_occupancy_pad[];   // dynamic LDS only limits workgroups per CU
     (void)lds_occupancy_pad;
-    if (a.n_dev) {   // frame count produced on the device by an earlier kernel (scan -> unmask)
-        a.n = *gptr(a.n_dev);
-        a.density = a.total ? (double)a.n / (double)a.total : 0.0;
-    }
+    init_frames(a);
     const uint64_t A = wave * kWin;
     const uint64_t full_lo = a.mis ? 16 : 0;
     const uint64_t full_hi = (a.mis + a.total) & ~15ull;
@@ -784,6 +847,26 @@ static Args make_args(uint8_t* dst, const uint8_t* src, uint64_t total, const ui
     a.density = total ? (double)n / (double)total : 0.0;
     a.nwin = 0;
     return a;
+}
+
+// In-place unmask of the frames a scan found (ws_scan_gpu.hip): the default walk,
+// frames read from the scan's outputs on the device (ArgsScan; nothing is allocated).
+hipError_t launch_mask_scanned(uint8_t* wire, uint64_t len, const uint64_t* hdr, const uint32_t* keys,
+                               uint64_t max_frames, const uint64_t* result, hipStream_t stream) {
+    ArgsScan a;
+    static_cast<Args&>(a) = make_args(wire, wire, len, hdr, keys, 0, result);
+    a.hdr = hdr;
+    a.fkeys = keys;
+    a.result = result;
+    a.max_frames = max_frames;
+    const uint64_t nvec = (a.mis + len + 15) / 16;
+    a.nwin = (nvec + 127) / 128;   // windows of 2 x 1 KiB
+    const uint64_t blocks = (a.nwin + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((mask_np_kernel<1, 2, true, true, false, ArgsScan>), dim3((unsigned)blocks), dim3(256), 0,
+                       stream, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, const uint64_t* off,

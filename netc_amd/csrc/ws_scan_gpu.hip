@@ -35,6 +35,8 @@
 
 #include <map>
 #include <mutex>
+#include <new>
+#include <vector>
 #include <utility>
 
 #include "gpu_util.h"
@@ -763,84 +765,96 @@ __global__ __launch_bounds__(kScanT) void scan_emit_lds(ScanArgs a) {
     }
 }
 
-// In-place unmask of scanned frames: the "mask view" of the stream as the batch
-// kernel takes it -- 2 n frames alternating header (key 0, passed through) and
-// payload (the frame's key), closed at the last payload's end.  n is read from the
-// scan's result on the device, so scan -> view -> mask needs no host round trip.
-__global__ void scan_view(const uint8_t* wire, const uint64_t* hdr, const uint32_t* keys, uint64_t max_frames,
-                          const uint64_t* result, uint64_t* voff, uint32_t* vkey, uint64_t* vn) {
-    const uint64_t n = min(result[0], max_frames);
-    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k == 0) {
-        *vn = 2 * n;
-        if (n == 0) voff[0] = 0;
-    }
-    if (k >= n) return;
-    const uint64_t p = hdr[k];
-    const uint32_t second = wire[p + 1];
-    const uint32_t code = second & 0x7F, mask = second >> 7;
-    const uint64_t ext = code == 126 ? 2 : (code == 127 ? 8 : 0);
-    uint64_t plen = code;
-    if (ext) {
-        plen = 0;
-        for (uint64_t i = 0; i < ext; ++i) plen = plen << 8 | wire[p + 2 + i];
-    }
-    const uint64_t ps = p + 2 + ext + (mask ? 4 : 0);
-    voff[2 * k] = p;
-    voff[2 * k + 1] = ps;
-    vkey[2 * k] = 0;
-    vkey[2 * k + 1] = keys[k];
-    if (k == n - 1) voff[2 * n] = ps + plen;
-}
-
-struct ViewScratch {
-    uint64_t* voff = nullptr;
-    uint32_t* vkey = nullptr;
-    uint64_t* vn = nullptr;
-    uint64_t frames = 0;
-};
-
+// In-place unmask of scanned frames: the batch kernel reads each frame's header
+// offset and key from the scan's outputs and its header length from the header bytes
+// in the buffer (ArgsScan in ws_mask_gpu.hip); the frame count comes from the scan's
+// result on the device, so scan -> unmask needs no host round trip and no view array.
 hipError_t launch_unmask_scanned(uint8_t* wire, uint64_t len, const uint64_t* hdr, const uint32_t* keys,
                                  uint64_t max_frames, const uint64_t* result, hipStream_t stream,
                                  const LaunchCfg& cfg) {
-    static std::map<std::pair<int, hipStream_t>, ViewScratch> scratch;
-    static std::mutex mu;
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    ViewScratch v;
-    {
-        std::lock_guard<std::mutex> g(mu);
-        ViewScratch& s = scratch[{dev, stream}];
-        if (s.frames < max_frames || !s.voff) {
-            uint64_t want = s.frames ? 2 * s.frames : 4096;
-            while (want < max_frames) want *= 2;
-            void *a = nullptr, *b = nullptr;
-            if ((e = hipMalloc(&a, (2 * want + 2) * sizeof(uint64_t))) != hipSuccess) return e;
-            if ((e = hipMalloc(&b, (2 * want + 1) * sizeof(uint32_t))) != hipSuccess) return e;
-            s.voff = (uint64_t*)a;
-            s.vn = s.voff + 2 * want + 1;
-            s.vkey = (uint32_t*)b;
-            s.frames = want;
-        }
-        v = s;
-    }
-    const uint64_t threads = max_frames ? max_frames : 1;
-    hipLaunchKernelGGL(scan_view, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, wire, hdr, keys,
-                       max_frames, result, v.voff, v.vkey, v.vn);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    return launch_mask_frames(wire, wire, len, v.voff, v.vkey, 2 * max_frames, stream, cfg, v.vn);
+    (void)cfg;
+    return launch_mask_scanned(wire, len, hdr, keys, max_frames, result, stream);
 }
 
 // ------------------------------------------------------------------ launch --
 
-struct ScanScratchSet {
+struct ScanScratch {
     void* mem = nullptr;
     uint64_t bytes = 0;
     uint64_t cap = 0;      // chunks the layout is sized for
     uint32_t epoch = 0;
     bool dirty = false;    // a call did not launch all its kernels: clear before the next
+    std::vector<void*> retired;   // outgrown allocations (queued work may still use them)
 };
+
+ScanScratch* scan_scratch_new() { return new (std::nothrow) ScanScratch(); }
+
+void scan_scratch_free(ScanScratch* s) {
+    if (!s) return;
+    if (s->mem) (void)hipFree(s->mem);
+    for (void* p : s->retired) (void)hipFree(p);
+    delete s;
+}
+
+namespace {
+// the per-(device, stream) scratch of the public netc_gpu_scan_frames entry
+std::map<std::pair<int, hipStream_t>, ScanScratch*>& stream_scratch() {
+    static std::map<std::pair<int, hipStream_t>, ScanScratch*> m;
+    return m;
+}
+std::mutex& stream_scratch_mu() {
+    static std::mutex mu;
+    return mu;
+}
+}  // namespace
+
+// bytes of scratch for `c` chunks: flags, ccount, mark, cand, link, nterm, ncnt, status, jp, jq,
+// slow2, slow3, cbase, anc (one anchor slot per chunk), anc_n, anq
+static uint64_t scratch_need(uint64_t c) {
+    const uint64_t n = c * kCand;
+    return 64 + c * 4 + n + n * 8 + n * 4 + n * 8 + n * 4 + c * 8 + n * 4 + n * 4 + n * 4 + c * 4 + c * 8 +
+           c * kAncSlot * 2 + c * 4 + n * 4 + 64 * 16;   // + alignment padding of the 16 regions
+}
+
+// grow to hold `chunks` (+1 virtual) chunks; outgrown allocations are kept until the
+// scratch is freed (queued work may still use them)
+static hipError_t scratch_grow(ScanScratch& s, uint64_t chunks, hipStream_t stream) {
+    if (s.cap >= chunks) return hipSuccess;
+    uint64_t cap = s.cap ? 2 * s.cap : 256;
+    while (cap < chunks) cap *= 2;
+    const uint64_t want = scratch_need(cap);
+    void* p = nullptr;
+    hipError_t e;
+    if ((e = hipMalloc(&p, want)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(p, 0, want, stream)) != hipSuccess) {   // zero flags, epoch 0
+        (void)hipFree(p);
+        return e;
+    }
+    if (s.mem) s.retired.push_back(s.mem);
+    s.mem = p;
+    s.bytes = want;
+    s.cap = cap;
+    s.epoch = 0;
+    s.dirty = false;
+    return hipSuccess;
+}
+
+hipError_t scan_scratch_reserve(ScanScratch* s, uint64_t len, hipStream_t stream) {
+    return scratch_grow(*s, (len + kChunk - 1) / kChunk + 1, stream);
+}
+
+int release_stream_scratch(int device, hipStream_t stream) {
+    ScanScratch* s = nullptr;
+    {
+        std::lock_guard<std::mutex> g(stream_scratch_mu());
+        auto it = stream_scratch().find({device, stream});
+        if (it == stream_scratch().end()) return 0;
+        s = it->second;
+        stream_scratch().erase(it);
+    }
+    scan_scratch_free(s);
+    return 1;
+}
 
 
 // workgroups of the LDS kernels K2' / K4b' (each loops over its queue); the queue
@@ -853,7 +867,7 @@ static uint64_t slow_blocks() {
 
 hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start, bool strict, uint64_t* hdr,
                               uint32_t* keys, uint8_t* b0, uint64_t max_frames, uint64_t* result,
-                              hipStream_t stream) {
+                              hipStream_t stream, ScanScratch* own) {
     ScanArgs a;
     a.wire = wire;
     a.len = len;
@@ -868,42 +882,28 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.b0 = b0;
     a.max_frames = max_frames;
     a.result = result;
-    // scratch layout, per (device, stream), sized for `cap` chunks.  The flags, the
-    // candidate counters and the mark bytes must be zero when a call starts: a fresh
-    // allocation is cleared once, and every call leaves them zeroed behind it (K4a and
-    // K4b' clear them), so no clearing launch is needed per call.
-    auto need_for = [](uint64_t c) {
-        const uint64_t n = c * kCand;
-        // flags, ccount, mark, cand, link, nterm, ncnt, status, jp, jq, slow2, slow3, cbase,
-        // anc (one anchor slot per chunk), anc_n, anq
-        return 64 + c * 4 + n + n * 8 + n * 4 + n * 8 + n * 4 + c * 8 + n * 4 + n * 4 + n * 4 + c * 4 + c * 8 +
-               c * kAncSlot * 2 + c * 4 + n * 4 + 64 * 16;   // + alignment padding of the 16 regions
-    };
-    static std::map<std::pair<int, hipStream_t>, ScanScratchSet> scratch;
-    static std::mutex mu;
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
+    // scratch: sized for `cap` chunks (scratch_grow); the flags, the candidate counters
+    // and the mark bytes must be zero when a call starts: a fresh allocation is cleared
+    // once, and every call leaves them zeroed behind it (K4a and K4b' clear them), so
+    // no clearing launch is needed per call.
+    hipError_t e = hipSuccess;
+    ScanScratch* sp = own;
+    std::unique_lock<std::mutex> lk;
+    if (!sp) {   // the public entry: scratch cached per (device, stream) until released
+        int dev = 0;
+        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+        lk = std::unique_lock<std::mutex>(stream_scratch_mu());
+        ScanScratch*& slot = stream_scratch()[{dev, stream}];
+        if (!slot && !(slot = scan_scratch_new())) return hipErrorOutOfMemory;
+        sp = slot;
+    }
     uint8_t* m;
     int32_t *jp, *jq;   // ping-pong doubling tables
     uint64_t cleared = 0;
     bool* dirty_flag = nullptr;
     {
-        std::lock_guard<std::mutex> g(mu);
-        ScanScratchSet& s = scratch[{dev, stream}];
-        if (s.cap < chunks) {   // outgrown (earlier allocations are kept: queued work may use them)
-            uint64_t cap = s.cap ? 2 * s.cap : 256;
-            while (cap < chunks) cap *= 2;
-            const uint64_t want = need_for(cap);
-            void* p = nullptr;
-            if ((e = hipMalloc(&p, want)) != hipSuccess) return e;
-            if ((e = hipMemsetAsync(p, 0, want, stream)) != hipSuccess) return e;   // zero flags, epoch 0
-            s.mem = p;
-            s.bytes = want;
-            s.cap = cap;
-            s.epoch = 0;
-            s.dirty = false;
-        }
+        ScanScratch& s = *sp;
+        if ((e = scratch_grow(s, chunks, stream)) != hipSuccess) return e;
         s.epoch = (s.epoch + 1) & 0xFFFF;
         m = (uint8_t*)s.mem;
         auto align = [](uint64_t x) { return (x + 63) & ~63ull; };
@@ -961,10 +961,7 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     hipLaunchKernelGGL(scan_count, dim3(cb), dim3(256), 0, stream, a);
     hipLaunchKernelGGL(scan_emit_lds, dim3(slow_grid), dim3(kScanT), 0, stream, a);
     e = hipGetLastError();
-    if (e != hipSuccess) {   // a launch failed: the flags may be left set
-        std::lock_guard<std::mutex> g(mu);
-        *dirty_flag = true;
-    }
+    if (e != hipSuccess) *dirty_flag = true;   // a launch failed: the flags may be left set (lock still held)
     return e;
 }
 

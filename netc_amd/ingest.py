@@ -26,6 +26,19 @@ NETC_WS_INGEST_PROTOCOL = -23
 NETC_WS_INGEST_ERECV = -24
 
 
+class WsMessage(ctypes.Structure):
+    """struct ws_message (include/ws/common.h): opcode, buffer (malloc'd, caller frees), payload_length."""
+    _fields_ = [("opcode", ctypes.c_uint8), ("buffer", ctypes.c_void_p), ("payload_length", ctypes.c_size_t)]
+
+
+WS_FRAME_PARSE_ERROR_RECV = -1
+WS_FRAME_PARSE_ERROR_INVALID_FRAME_LENGTH = -2
+WS_FRAME_PARSE_ERROR_PAYLOAD_TOO_BIG = -3
+_libc = ctypes.CDLL(None)
+_libc.free.argtypes = [ctypes.c_void_p]
+_libc.free.restype = None
+
+
 class _RawBatch(ctypes.Structure):
     _fields_ = [("wire", ctypes.c_void_p), ("len", ctypes.c_uint64), ("hdr", ctypes.c_void_p),
                 ("keys", ctypes.c_void_p), ("b0", ctypes.c_void_p), ("nframes", ctypes.c_uint64),
@@ -53,6 +66,8 @@ def _bind(lib):
     lib.netc_ws_batch_payload.argtypes = [ctypes.POINTER(_RawBatch), ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.POINTER(ctypes.c_uint64)]
     lib.netc_ws_batch_payload.restype = ctypes.c_int
+    lib.netc_ws_ingest_next_message.argtypes = [vp, ctypes.POINTER(WsMessage), sz, ctypes.c_int]
+    lib.netc_ws_ingest_next_message.restype = ctypes.c_int
     lib._ingest_bound = True
     return lib
 
@@ -102,7 +117,7 @@ class Ingest:
     """netc_ws_ingest_*: one connection's byte stream -> pinned slots -> GPU scan + unmask -> batches."""
 
     def __init__(self, device: int = 0, slot_bytes: int = 16 << 20, nslots: int = 4, max_frame_bytes: int = 65536,
-                 strict: bool = True):
+                 strict: bool = False):
         lib = _bind(_lib.gpu())
         h = ctypes.c_void_p(0)
         rc = lib.netc_ws_ingest_create(ctypes.byref(h), device, slot_bytes, nslots, max_frame_bytes,
@@ -139,6 +154,23 @@ class Ingest:
         if rc < 0:
             _raise(rc)
         return Batch(self, raw) if rc == 1 else None
+
+    def next_message(self, max_payload_length: int = (1 << 64) - 1, wait: bool = True):
+        """netc_ws_ingest_next_message: (0, opcode, payload bytes) for a complete message (the C
+        buffer is copied and freed here; a TEXT payload ends with the NUL the contract appends),
+        (1, None, None) when more data is needed, or (code, None, None) for a
+        WS_FRAME_PARSE_ERROR_* code -- the same 0 / 1 / < 0 contract as ws_parse_frame.
+        Device / runtime failures (NETC_GPU_E*) raise."""
+        m = WsMessage()
+        rc = self._lib.netc_ws_ingest_next_message(self._h, ctypes.byref(m), max_payload_length, 1 if wait else 0)
+        if rc == 0:
+            data = ctypes.string_at(m.buffer, m.payload_length) if m.payload_length else b""
+            _libc.free(m.buffer)
+            return 0, int(m.opcode), data
+        if rc in (1, WS_FRAME_PARSE_ERROR_RECV, WS_FRAME_PARSE_ERROR_INVALID_FRAME_LENGTH,
+                  WS_FRAME_PARSE_ERROR_PAYLOAD_TOO_BIG):
+            return rc, None, None
+        _raise(rc)
 
     def close(self) -> None:
         if self._h:

@@ -7,8 +7,15 @@ receiver in tests/test_scan_oracle.py) plus the reference's unmask expression
 concatenated in order, hold exactly the oracle's frames -- header offsets (stream
 coordinates), keys, header bytes, unmasked payload bytes, untouched header bytes --
 and nothing else, whatever the slot size and however the bytes arrive.
+
+The message-level reader (netc_ws_ingest_next_message) is checked against
+libnetc's own ws_parse_frame on the same bytes (tests/wsutil.parse_stream) and against the
+reference's golden fixtures (tests/golden/ws_golden.json, generated from the compiled
+reference: fragmented, text_nul, rfc6455_kat).
 """
 
+import json
+import os
 import socket
 import threading
 
@@ -18,6 +25,7 @@ import pytest
 from netc_amd import ingest as ni
 from netc_amd.mask import NetcGpuError
 from oracle import oracle as orc
+from tests.wsutil import parse_stream
 
 pytestmark = pytest.mark.gpu
 
@@ -198,7 +206,7 @@ def test_strict_error_mid_stream(torch_cuda):
     good, *_ = make_stream(rng, rng.integers(0, 2000, 40))
     bad = np.frombuffer(bytes.fromhex("8105") + b"Hello", dtype=np.uint8)   # MASK clear: forbidden from a client
     wire = np.concatenate([good, bad, good])
-    with ni.Ingest(0, slot_bytes=1 << 20, nslots=2) as ing:
+    with ni.Ingest(0, slot_bytes=1 << 20, nslots=2, strict=True) as ing:
         col = Collector()
         ing.write(wire)
         ing.submit()
@@ -258,3 +266,190 @@ def test_socketpair_with_writer_thread(torch_cuda):
     finally:
         t.join()
         b.close()
+
+
+# ------------------------------------------------------- message contract ---
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ws_golden.json")))
+TEXT, BINARY, CONT = 1, 2, 0
+
+
+def gen(seed, n):
+    return np.random.Generator(np.random.PCG64(seed)).integers(0, 256, n, dtype=np.uint8).tobytes()
+
+
+def gpu_messages(wire: bytes, chunks=(), max_payload=(1 << 62), slot=4096, nslots=3, max_frame=65536):
+    """Feed `wire` to an ingest ring in `chunks`, reading netc_ws_ingest_next_message after each
+    piece (as an event loop would); returns (messages, last code) like wsutil.parse_stream."""
+    w = np.frombuffer(wire, dtype=np.uint8)
+    msgs, rc = [], 1
+    with ni.Ingest(0, slot_bytes=slot, nslots=nslots, max_frame_bytes=max_frame) as ing:
+        def drain(wait):
+            nonlocal rc
+            while True:
+                rc, op, data = ing.next_message(max_payload, wait=wait)
+                if rc != 0:
+                    return rc
+                msgs.append((op, data))
+        sizes = [int(n) for n in chunks]
+        if sum(sizes) < len(wire):
+            sizes.append(len(wire) - sum(sizes))
+        pos = 0
+        for n in sizes:
+            piece = w[pos:pos + n]
+            pos += piece.size
+            while piece.size:
+                r = ing.write(piece)
+                if r == ni.NETC_WS_INGEST_FULL:
+                    if drain(True) < 0:
+                        return msgs, rc
+                    continue
+                piece = piece[r:]
+            if drain(False) < 0:
+                return msgs, rc
+        drain(True)   # submits what is left, waits for the GPU
+        return msgs, rc
+
+
+def test_message_fragmented_golden(torch_cuda):
+    f = GOLDEN["fragmented"]
+    wire = bytes.fromhex(f["wire"])
+    for slot in (4096, 1 << 16):
+        msgs, rc = gpu_messages(wire, f["chunks"], slot=slot)
+        assert rc == 1 and msgs == [(f["opcode"], bytes.fromhex(f["message"]))]
+    assert msgs == parse_stream(wire, f["chunks"])[0]
+
+
+def test_message_text_nul_golden(torch_cuda):
+    t = GOLDEN["text_nul"]
+    msgs, rc = gpu_messages(bytes.fromhex(t["wire"]))
+    assert msgs == [(TEXT, bytes.fromhex(t["delivered"]))] and len(msgs[0][1]) == t["payload_length"]
+
+
+def test_message_rfc6455_kat_golden(torch_cuda):
+    msgs, rc = gpu_messages(bytes.fromhex(GOLDEN["rfc6455_kat"]["wire"]))
+    assert [[op, m.hex()] for op, m in msgs] == GOLDEN["rfc6455_kat"]["messages"]
+
+
+def many_messages_stream():
+    # the stream of tests/test_host_framing.py::test_many_messages_in_one_stream
+    g = np.random.Generator(np.random.PCG64(9))
+    wire, expect = b"", []
+    for i in range(50):
+        nfr = int(g.integers(1, 4))
+        parts = [gen(100 * i + j, int(g.integers(0, 3000))) for j in range(nfr)]
+        op = TEXT if i % 2 else BINARY
+        for j, part in enumerate(parts):
+            key = gen(7 * i + j, 4) if (i + j) % 3 else None
+            if key is not None and not part:
+                key = None
+            wire += orc.encode_frame(part, op if j == 0 else CONT, key, fin=(j == nfr - 1))
+        expect.append((op, b"".join(parts) + (b"\x00" if op == TEXT else b"")))
+    cuts = np.sort(g.choice(np.arange(1, len(wire)), 200, replace=False))
+    chunks = np.diff(np.concatenate([[0], cuts, [len(wire)]])).tolist()
+    return wire, expect, chunks
+
+
+@pytest.mark.parametrize("slot,nslots", [(4096, 2), (16384, 3), (1 << 20, 4)])
+def test_message_many_in_one_stream(torch_cuda, slot, nslots):
+    wire, expect, chunks = many_messages_stream()
+    msgs, rc = gpu_messages(wire, chunks, slot=slot, nslots=nslots)
+    assert msgs == expect
+    assert msgs == parse_stream(wire, chunks)[0]   # the same sequence libnetc's ws_parse_frame gives
+
+
+def test_message_control_frames_between_messages(torch_cuda):
+    wire = (orc.encode_frame(b"ab", TEXT, b"1234", fin=False) + orc.encode_frame(b"cd", CONT, b"5678") +
+            orc.encode_frame(b"hi", 0x9, b"abcd") + orc.encode_frame(b"", 0xA, None) +
+            orc.encode_frame(gen(3, 900), BINARY, b"\x00\x00\x00\x00"))
+    msgs, rc = gpu_messages(wire, [5, 9, 1, 30])
+    assert msgs == parse_stream(wire, [5, 9, 1, 30])[0]
+    assert [op for op, _ in msgs] == [TEXT, 0x9, 0xA, BINARY] and msgs[0][1] == b"abcd\x00"
+
+
+def test_message_payload_too_big_accumulated(torch_cuda):
+    # three 400-byte fragments: the third takes the message past 1000 bytes (src/ws/common.c:210,261)
+    wire = orc.encode_frame(b"x" * 10, BINARY, b"kkkk")
+    wire += b"".join(orc.encode_frame(gen(j, 400), BINARY if j == 0 else CONT, b"abcd", fin=(j == 2))
+                     for j in range(3))
+    msgs, rc = gpu_messages(wire, max_payload=1000)
+    ref_msgs, ref_rc = parse_stream(wire, max_payload=1000)
+    assert rc == ref_rc == -3 and msgs == ref_msgs == [(BINARY, b"x" * 10)]
+
+
+def test_frame_over_the_limit_inside_one_slot(torch_cuda):
+    # ADVICE r1: a frame longer than max_frame_bytes that fits in one slot is refused too
+    rng = np.random.default_rng(14)
+    wire, wo, *_ = make_stream(rng, [100, 5000, 300])
+    with ni.Ingest(0, slot_bytes=1 << 20, nslots=2, max_frame_bytes=1000) as ing:
+        ing.write(wire)
+        ing.submit()
+        b = ing.next(wait=True)
+        assert b.nframes == 1 and int(b.hdr[1]) == int(wo[1])
+        b.release()
+        with pytest.raises(NetcGpuError) as e:
+            ing.next(wait=True)
+        assert e.value.code == ni.NETC_WS_INGEST_TOO_BIG
+    msgs, rc = gpu_messages(wire.tobytes(), slot=1 << 20, max_frame=1000)
+    assert rc == -3 and len(msgs) == 1
+
+
+def test_message_socket_until_close(torch_cuda):
+    wire, expect, chunks = many_messages_stream()
+    a, b = socket.socketpair()
+
+    def writer():
+        v = memoryview(wire)
+        i = 0
+        for c in chunks:
+            a.sendall(v[i:i + c])
+            i += c
+        a.close()
+
+    t = threading.Thread(target=writer)
+    t.start()
+    msgs = []
+    try:
+        with ni.Ingest(0, slot_bytes=8192, nslots=3) as ing:
+            while True:
+                r = ing.recv(b.fileno())
+                while True:
+                    rc, op, data = ing.next_message(wait=r == ni.NETC_WS_INGEST_FULL)
+                    if rc != 0:
+                        break
+                    msgs.append((op, data))
+                if r == ni.NETC_WS_INGEST_CLOSED:
+                    break
+            while True:
+                rc, op, data = ing.next_message(wait=True)
+                if rc != 0:
+                    break
+                msgs.append((op, data))
+            assert rc == -1   # the peer closed after the last complete message (recv() == 0)
+    finally:
+        t.join()
+        b.close()
+    assert msgs == expect
+
+
+def test_create_destroy_does_not_leak_device_memory(torch_cuda):
+    # ADVICE r1: the scan scratch is owned by each slot and freed with it (it was cached per
+    # stream and leaked when an ingest destroyed its streams)
+    torch = torch_cuda
+    rng = np.random.default_rng(15)
+    wire, *_ = make_stream(rng, rng.integers(0, 3000, 200))
+
+    def one():
+        with ni.Ingest(0, slot_bytes=1 << 20, nslots=4) as ing:
+            ing.write(wire)
+            ing.submit()
+            while ing.next(wait=True) is not None:
+                pass
+    one()
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    for _ in range(12):
+        one()
+    torch.cuda.synchronize()
+    free1 = torch.cuda.mem_get_info()[0]
+    assert free0 - free1 < (16 << 20), f"{(free0 - free1) >> 20} MiB lost over 12 create/destroy cycles"
