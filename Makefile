@@ -5,6 +5,8 @@
 #   make            libnetc.so + libnetc_ws_gpu.so (+ libnetc_ceiling.so) + oracle
 #   make diag       instrumented builds + probes under tools/ (diagnostics only)
 #   make host       libnetc.so only (no hipcc needed)
+#   make asan       libnetc.so + the oracle built with ASan + UBSan, then the CPU suites
+#                   that drive them (host framing, CPU mask, oracle checks) run against those
 #   make clean
 
 HIPCC      ?= /opt/rocm/bin/hipcc
@@ -20,7 +22,7 @@ GPU_SRCS   := netc_amd/csrc/ws_mask_gpu.hip netc_amd/csrc/ws_frame_gpu.hip netc_
               netc_amd/csrc/ws_mask_api.hip
 GPU_HDRS   := netc_amd/csrc/ws_mask_gpu.h netc_amd/csrc/gpu_util.h include/ws/mask.h include/ws/frame.h include/ws/ingest.h
 
-.PHONY: all host gpu oracle diag clean
+.PHONY: all host gpu oracle diag clean asan
 all: host gpu oracle
 host: $(LIBDIR)/libnetc.so
 gpu: $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc_ceiling.so
@@ -63,3 +65,22 @@ tools/libdiag_order.so: tools/diag_order.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 tools/libdiag_policy.so: tools/diag_policy.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+
+# ASan + UBSan over the host C (the reference had two heap overflows on this
+# path, B1 src/ws/common.c:100 and B6 :306-315; this proves the rebuilt parser has none).
+# The instrumented libraries go to build/asan/; Python itself is not instrumented, so the
+# sanitizer runtimes are preloaded and leak checking is off (the interpreter's own).
+ASAN_FLAGS := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined
+ASAN_TESTS := tests/test_host_framing.py tests/test_mask_cpu.py tests/test_oracle.py tests/test_scan_oracle.py \
+              tests/test_utf8_oracle.py
+build/asan/libnetc.so: $(HOST_SRCS) $(HOST_HDRS)
+	@mkdir -p build/asan
+	$(CC) $(ASAN_FLAGS) -Wall -fPIC -std=gnu11 -shared -o $@ $(HOST_SRCS) -lpthread
+build/asan/liboracle.so: oracle/ws_oracle.c
+	@mkdir -p build/asan
+	$(CC) $(ASAN_FLAGS) -Wall -fPIC -shared -o $@ $<
+asan: build/asan/libnetc.so build/asan/liboracle.so oracle
+	NETC_HOST_LIB=build/asan/libnetc.so NETC_ORACLE_LIB=build/asan/liboracle.so \
+	LD_PRELOAD="$$($(CC) -print-file-name=libasan.so) $$($(CC) -print-file-name=libubsan.so)" \
+	ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 \
+	python3 -m pytest -q -m "not gpu" -p no:cacheprovider $(ASAN_TESTS)

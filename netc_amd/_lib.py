@@ -14,7 +14,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIBDIR = os.path.join(_HERE, "lib")
 HOST_LIB = os.path.join(LIBDIR, "libnetc.so")
 GPU_LIB = os.path.join(LIBDIR, "libnetc_ws_gpu.so")
-# diagnostics only (tools/): an instrumented build of the same library
+# instrumented builds of the same libraries: NETC_HOST_LIB (`make asan`: ASan + UBSan),
+# NETC_GPU_LIB (tools/: stamps, checks)
+if os.environ.get("NETC_HOST_LIB"):
+    HOST_LIB = os.path.abspath(os.environ["NETC_HOST_LIB"])
 if os.environ.get("NETC_GPU_LIB"):
     GPU_LIB = os.path.abspath(os.environ["NETC_GPU_LIB"])
 

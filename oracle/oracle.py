@@ -29,6 +29,8 @@ sz = ctypes.c_size_t
 def _load(name: str) -> ctypes.CDLL:
     if name not in _libs:
         path = os.path.join(_HERE, name)
+        if name == "liboracle.so" and os.environ.get("NETC_ORACLE_LIB"):   # `make asan`: instrumented build
+            path = os.path.abspath(os.environ["NETC_ORACLE_LIB"])
         if not os.path.exists(path):
             raise RuntimeError(f"oracle: {path} not built (run `make -C oracle`)")
         lib = ctypes.CDLL(path)

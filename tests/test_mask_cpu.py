@@ -67,3 +67,24 @@ def test_synth_shapes():
     sizes = np.diff(off4.astype(np.int64))
     assert total4 == 1 << 30 and sizes[:-1].min() >= 256 and sizes.max() <= 65536
     assert keys4[0] == 0 and keys4[1] == 0xFFFFFFFF
+
+
+def test_sanitized_build_is_the_one_loaded():
+    """Under `make asan` the suites run against the ASan + UBSan builds (NETC_HOST_LIB /
+    NETC_ORACLE_LIB); this checks that the instrumented libraries are the ones in use."""
+    import os
+    import subprocess
+
+    from netc_amd import _lib
+    from oracle import oracle as orc
+
+    host = os.environ.get("NETC_HOST_LIB")
+    if not host:
+        pytest.skip("not a `make asan` run")
+    _lib.host()
+    orc.lib()
+    for path in (os.path.abspath(host), os.path.abspath(os.environ["NETC_ORACLE_LIB"])):
+        syms = subprocess.run(["nm", "-D", path], capture_output=True, text=True, check=True).stdout
+        assert "__asan_report" in syms and "__ubsan_handle" in syms, path
+        maps = open("/proc/self/maps").read()
+        assert path in maps, f"{path} is not mapped in this process"
