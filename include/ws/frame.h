@@ -109,6 +109,16 @@ int netc_gpu_scan_frames(int device, const void *d_wire, size_t len, uint64_t st
 int netc_gpu_scan_release(int device, void *stream);
 
 /**
+ * Diagnostics: waits for `stream`, then returns why the last netc_gpu_scan_frames
+ * call on it finished with the serial walk instead of the parallel scan (0: it
+ * did not; bits 0-7: a capacity overflowed — a chunk's candidate bucket, a
+ * chunk's exit set, an exit onto no candidate, a tile's external list; 256+: the
+ * tile resolution), -1 when no scan ran on that stream, or a negative code.
+ * The results are the same either way; only the speed differs.
+ */
+int64_t netc_gpu_scan_diag(int device, void *stream);
+
+/**
  * Unmask, in place, the payloads of the frames a netc_gpu_scan_frames call found
  * in d_wire (the reference's unmask loop, src/ws/common.c:317-323, for every
  * frame of the stream at once); header bytes and bytes past the last recorded

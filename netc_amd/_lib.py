@@ -111,6 +111,8 @@ def gpu() -> ctypes.CDLL:
             lib.netc_gpu_scan_frames.restype = ctypes.c_int
             lib.netc_gpu_scan_release.argtypes = [ctypes.c_int, vp]
             lib.netc_gpu_scan_release.restype = ctypes.c_int
+            lib.netc_gpu_scan_diag.argtypes = [ctypes.c_int, vp]
+            lib.netc_gpu_scan_diag.restype = ctypes.c_int64
             lib.netc_gpu_unmask_frames.argtypes = [ctypes.c_int, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp, vp]
             lib.netc_gpu_unmask_frames.restype = ctypes.c_int
             lib.netc_gpu_unmask_validate.argtypes = [ctypes.c_int, vp, vp, ctypes.c_size_t, vp, vp, vp,

@@ -305,6 +305,15 @@ int netc_gpu_scan_release(int device, void* stream) {
     return 0;
 }
 
+int64_t netc_gpu_scan_diag(int device, void* stream) {
+    if (int r = check_device(device)) return r;
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+    hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    if (e != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipStreamSynchronize", e);
+    return netc_gpu::scan_diag(device, (hipStream_t)stream);
+}
+
 int netc_gpu_unmask_frames(int device, void* d_wire, size_t len, const uint64_t* d_hdr, const uint32_t* d_keys,
                            size_t max_frames, const uint64_t* d_result, void* stream) {
     if (int r = check_device(device)) return r;

@@ -58,6 +58,7 @@ ScanScratch* scan_scratch_new();
 void scan_scratch_free(ScanScratch* s);   // no work using it may be queued
 hipError_t scan_scratch_reserve(ScanScratch* s, uint64_t len, hipStream_t stream);   // sized for a len-byte stream
 int release_stream_scratch(int device, hipStream_t stream);   // 1 if there was a cached entry
+int64_t scan_diag(int device, hipStream_t stream);            // why the last scan walked serially (0: it did not)
 hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start, bool strict, uint64_t* hdr,
                               uint32_t* keys, uint8_t* b0, uint64_t max_frames, uint64_t* result,
                               hipStream_t stream, ScanScratch* own = nullptr);

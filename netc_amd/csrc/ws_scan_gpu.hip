@@ -6,29 +6,40 @@
 // the stream (header offset, key, byte 0) in parallel.
 //
 // Frame starts form a chain: the next header follows the current frame's payload.
-// The stream is cut into chunks of C bytes:
-//   K1       per chunk, in LDS: every position that can start a header (strict
-//            mode: passes the RFC checks on its first 2 bytes) is parsed once.  A
-//            chain inside the chunk only steps between such positions, so the
-//            distinct places where chains leave the chunk are the direct exits of
-//            those positions; K1 publishes them as "candidate entries" of the
-//            chunks they land in (the true chain enters each chunk at one of them).
-//   K2       per candidate entry: its chain walked (header bytes from global
-//            memory; past 64 frames K2' builds the chunk's 16-bit links in LDS,
-//            doubles them to 8 / 16 hops and walks those, leaving an anchor every
-//            8 frames for K4b') to the candidate it exits to: a graph of a few nodes
-//            per chunk whose path from the stream start is the true chain, one node
-//            per chunk it enters.
-//   K3       pointer doubling over that graph, marking the nodes reachable from
-//            the start node (log2(chunks) passes);
-//   K4       per chunk: the true entry (its marked node) and its frame count from
-//            K2, a chained scan of the counts (decoupled look-back), and a walk that
-//            writes the descriptors (K4b'; past 64 frames one wavefront per chunk,
-//            a lane per K2' anchor).
+// The stream is cut into chunks of C = 4 KiB, chunks into tiles of 256 (1 MiB).
+// Five launches:
+//   K1  scan_exits    one wavefront per chunk, straight from HBM (16-B loads, no
+//                     LDS staging): the strict quick check on bytes 0-1 of every
+//                     position, 4 positions per 5 VALU operations (SWAR).  A chain
+//                     inside the chunk only steps between positions that pass it, so
+//                     the places where chains LEAVE the chunk are direct exits of
+//                     passing positions -- and only two kinds can exit: a 16/64-bit
+//                     length (byte 1 & 0x7E == 0x7E) or a position in the chunk's last
+//                     132 bytes.  Those few are parsed; their distinct exits become
+//                     "candidate entries" (nodes) of the chunks they land in (the true
+//                     chain enters each chunk at one of them).
+//   K2  scan_links    per node: its chain walked inside its chunk (header bytes from
+//                     global memory) to the node it exits to, counting frames; chains
+//                     of more than 64 frames are finished by the workgroup in LDS
+//                     (16-bit in-chunk links doubled to 8 / 16 hops), leaving an anchor
+//                     every 8 frames for K4.
+//   K3a scan_tiles    per tile, in LDS: list ranking over the tile's nodes (Wyllie
+//                     pointer jumping): for every node the frames to the tile's exit
+//                     (W) and the last node before it, and, for each of the tile's
+//                     "external" nodes (entered from another tile: at most 32), a bit
+//                     pushed along its path.
+//   K3b scan_resolve  one workgroup: the same list ranking over the external nodes of
+//                     all tiles (a few per tile), from the stream start: which external
+//                     is each tile's true entry, the frames before it, and where the
+//                     chain ends (the results).
+//   K4  scan_emit     per chunk: its true entry (the node carrying its tile entry's
+//                     bit), its first frame index (tile base + W(entry) - W(node)), and
+//                     a walk writing the descriptors; past 64 frames one wavefront per
+//                     chunk from K2's anchors, or the workgroup from LDS.
 // Garbage chains (payload bytes parsed as headers) die within a hop or two under
 // the strict checks, so chunks have few distinct exits; a stream whose exits
-// overflow the fixed capacities (adversarial payloads) is finished by a serial
-// walk in K4 instead — same results, slower.
+// overflow the fixed capacities (adversarial payloads, non-strict mode) is finished
+// by a serial walk in K4 instead — same results, slower.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -44,41 +55,73 @@
 
 namespace netc_gpu {
 
-static constexpr uint64_t kChunk = 4096;        // bytes per chunk (LDS: bytes + 8 B link per byte)
-static constexpr int kScanT = 256;              // threads per K1 / K2 block
+static constexpr uint64_t kChunk = 4096;        // bytes per chunk
+static constexpr int kScanT = 256;              // threads per K2 / K3a / K4 block
 static constexpr int kPer = (int)(kChunk / kScanT);
-static constexpr int kCand = 8;                 // candidate entries per chunk
+static constexpr int kCand = 8;                 // candidate entries (node slots) per chunk
 static constexpr int kSet = 64;                 // distinct exits per chunk
 static constexpr uint64_t kTerm = 1ull << 63;   // link is terminal
 static constexpr uint64_t kPosMask = (1ull << 61) - 1;
 enum : uint64_t { kExit = 0, kEnd = 1, kDead = 2 };
+static constexpr uint64_t kTileChunks = 256;                  // K3a: chunks per tile (1 MiB of stream)
+static constexpr uint64_t kTileSlots = kTileChunks * kCand;   // node slots per tile
+static constexpr int kExt = 32;                               // external nodes per tile (bits)
+static constexpr int kResolveT = 1024;                        // K3b threads
+static constexpr int kExtCap = 4096;                          // K3b: external nodes of the whole stream
+static constexpr int kMaxTiles = 8192;                        // K3b: tiles (8 GiB of stream)
+static constexpr int kBlkChunks = 16;                         // K2 / K4: chunks per block
+static constexpr int32_t kDupLink = -2;                       // K2: slot repeats an earlier slot's position
+static constexpr int kWalkHops = 64;                          // K2 / K4: frames walked one by one
+static constexpr uint32_t kH = 0x80808080u;
+// why a scan fell back to the serial walk (flags[9], read by netc_gpu_scan_diag): bits
+// 0-7 flags[0] (K1 bucket full, K1 exit set full, K2 exit onto no candidate, K3a tile
+// external list full, K1 candidate queue full), 8+ K3b's own reason
+enum : uint32_t { kOvfBucket = 1, kOvfSet = 2, kOvfLink = 4, kOvfExt = 8, kOvfQueue = 16 };
+enum : uint32_t { kWhyRoot = 1u << 8, kWhyTiles = 2u << 8, kWhyExtCap = 3u << 8, kWhySucc = 4u << 8 };
 
 __device__ __forceinline__ uint64_t term(uint64_t type, uint64_t pos) { return kTerm | type << 61 | pos; }
 __device__ __forceinline__ uint64_t term_type(uint64_t v) { return (v >> 61) & 3; }
 __device__ __forceinline__ uint64_t term_pos(uint64_t v) { return v & kPosMask; }
 
+// K3a -> K3b: an external node of a tile
+struct TileExt {
+    uint32_t slot;   // its global node slot
+    uint32_t w;      // frames from it to the tile's exit
+    int32_t xl;      // the node its path exits to (another tile), or -1: the chain ends in the tile
+    uint32_t pad;
+    uint64_t term;   // K2's terminal of the path's last node in the tile
+};
+// K3b -> K4: a tile's true entry
+struct TileInfo {
+    int32_t j;       // its bit (index in the tile's external list), or -1: the chain does not enter the tile
+    uint32_t we;     // its W
+    uint64_t base;   // index of its first frame
+};
+
 struct ScanArgs {
     const uint8_t* wire;
+    const uint8_t* pf_base;   // K1's clamped loads: wire, or a scratch word for a stream under 16 bytes
+    uint64_t pf_lim;          // ... highest 16-byte load offset
     uint64_t len;          // stream bytes
     uint64_t start;        // offset of the first header
     uint64_t nc;           // chunks (the last one, index nc, is virtual: positions >= len)
     int strict;
-    uint32_t* ccount;      // nc + 1 candidate counters (zeroed per call)
+    uint32_t* flags;       // [0] overflow bits, [1] root slot + 1, [8] K3b -> K4: serial fallback, [9] why
+    uint32_t* ccount;      // nc + 1 candidate counters (zero when a call starts; K4 re-zeroes)
+    uint8_t* ext;          // (nc + 1) * kCand: slot entered from another tile (or the root); K4 re-zeroes
     uint64_t* cand;        // (nc + 1) * kCand candidate positions
-    int32_t* link;         // (nc + 1) * kCand: node -> next node, -1 = chain ends
-    uint64_t* nterm;       // (nc + 1) * kCand: the terminal where the node's walk leaves its chunk
-    uint32_t* ncnt;        // (nc + 1) * kCand: frames on that walk (~0: not counted, K2')
-    uint8_t* mark;         // (nc + 1) * kCand: node is on the chain from the stream start
-    uint32_t* flags;       // [0] overflow, [1] root node, [3] / [4] entries of slow2 / slow3
-    uint32_t* slow2;       // K2 nodes left to the LDS kernel ((nc + 1) * kCand)
-    uint32_t* slow3;       // K4 chunks of many frames left to the LDS emit kernel (nc + 1)
-    uint64_t* cbase;       // K4: index of each chunk's first frame (nc + 1)
-    uint16_t* anc;         // K2' -> K4b': 16-frame anchors of K2' slot q at anc[q * kAncSlot]
+    int32_t* link;         // node -> next node, -1 = chain ends, kDupLink
+    uint64_t* nterm;       // the terminal where the node's walk leaves its chunk
+    uint32_t* ncnt;        // frames on that walk
+    uint32_t* wsum;        // K3a: frames from the node to its tile's exit
+    uint32_t* pbits;       // K3a: external nodes of the tile whose path holds the node
+    TileExt* text;         // tiles * kExt
+    uint32_t* tcount;      // tiles
+    TileInfo* tinfo;       // tiles
+    uint16_t* anc;         // K2' -> K4: 8-frame anchors of anchor slot q at anc[q * kAncSlot]
     uint32_t* anc_n;       // anchors in slot q
-    uint32_t* anq;         // per node: its K2' slot (this call), or ~0 when none was left
+    uint32_t* anq;         // per node: its anchor slot, or ~0 when none was left
     uint64_t anc_cap;      // anchor slots
-    uint64_t* status;      // chained-scan status words (nc + 1)
-    uint32_t epoch;
     uint64_t* hdr;         // outputs
     uint32_t* keys;
     uint8_t* b0;
@@ -87,7 +130,7 @@ struct ScanArgs {
 };
 
 // One header at stream position p (bytes b[0..13] from p; bytes past len unused).
-// Returns the link: the next header position, or a terminal.
+// Returns the link: the next header position, or a terminal.  (The serial fallback.)
 template <typename Bytes>
 __device__ __forceinline__ uint64_t parse_at(const ScanArgs& a, uint64_t p, const Bytes& b, uint32_t* key_out,
                                              uint8_t* b0_out) {
@@ -200,8 +243,8 @@ __device__ void load_chunk(const ScanArgs& a, uint64_t B, uint32_t* words) {
 }
 
 // 16 stream bytes from p (zero past len) straight from global memory: the walks
-// of K2 and K4 touch only the header bytes of the frames they visit,
-// so they read them where they lie instead of staging the chunk in LDS.
+// touch only the header bytes of the frames they visit, so they read them where
+// they lie instead of staging the chunk in LDS.
 __device__ __forceinline__ Win window_global(const ScanArgs& a, uint64_t p) {
     typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
     Win w;
@@ -242,150 +285,231 @@ __device__ uint64_t walk_frames(const ScanArgs& a, uint64_t B, const uint32_t* w
 // The strict quick check for 4 positions at once: x = bytes 0 of positions 0..3,
 // y = their bytes 1.  Bit 7 of a byte of the result is set when that position can
 // start a client frame: MASK set, RSV clear, opcode 0/1/2/8/9/A, FIN on a control
-// frame (the checks of quick_reject, SWAR).
+// frame.  (first & 0x77) + 0x7D carries into bit 7 exactly when an RSV bit is set or
+// (opcode & 7) >= 3 (the reserved opcodes 3-7, B-F); (x << 4) & ~x has bit 7 set for
+// a control opcode (bit 3) without FIN (bit 7).  No carry crosses a byte; checked
+// against quick_reject over all 65,536 byte pairs.  5 VALU operations.
 __device__ __forceinline__ uint32_t quick_ok4(uint32_t x, uint32_t y) {
-    const uint32_t H = 0x80808080u;
-    const uint32_t rsv_ok = ~((x & 0x70707070u) + 0x70707070u) & H;   // bits 4-6 clear
-    const uint32_t op_ok = ~((x << 5) | ((x << 7) & (x << 6))) & H;    // opcode & 7 in {0, 1, 2}
-    const uint32_t ctl_bad = (x << 4) & ~x & H;                        // opcode >= 8 without FIN
-    return y & rsv_ok & op_ok & ~ctl_bad & H;
+    return y & ~((x & 0x77777777u) + 0x7D7D7D7Du) & ~((x << 4) & ~x) & kH;
 }
 
-// x into the chunk's LDS set of distinct exits (open addressing); *overflow when full
-__device__ __forceinline__ void set_insert(unsigned long long* set, uint64_t x, int* overflow) {
+// x into the wavefront's LDS set of distinct exits (open addressing): true if it is
+// new; *overflow when the set is full
+__device__ __forceinline__ bool set_insert(unsigned long long* set, uint64_t x, bool* overflow) {
     uint32_t h = (uint32_t)((x * 0x9E3779B97F4A7C15ull) >> 58);
     for (int tries = 0; tries < kSet; ++tries, h = (h + 1) & (kSet - 1)) {
         const unsigned long long cur = set[h];
-        if (cur == x) return;
+        if (cur == x) return false;
         if (cur == ~0ull) {
             const unsigned long long prev = atomicCAS(&set[h], ~0ull, (unsigned long long)x);
-            if (prev == ~0ull || prev == x) return;
+            if (prev == ~0ull) return true;
+            if (prev == x) return false;
         }
     }
-    *overflow = 1;
+    *overflow = true;
+    return false;
 }
 
-static constexpr int kWalkHops = 32;   // K1 / K2: hop budget of a direct chain walk
-
-// publish a chunk's distinct exits as candidates of the chunks they land in, and the
-// stream start as the candidate (root) of its chunk.  Strict mode prunes exits that
-// cannot start a frame (2 header bytes fail the checks): payload bytes parsed as a
-// chain land on random positions, and a random position passes with ~2 % odds,
-// while the true chain always lands on a real header.  This keeps the candidate
-// lists at about one entry per chunk.
-__device__ __forceinline__ void publish_exits(const ScanArgs& a, uint64_t chunk, const unsigned long long* set,
-                                              int overflow, int tid) {
-    auto append = [&](uint64_t x) {
-        const uint64_t t = x / kChunk;   // x <= len: t <= nc
-        const uint32_t slot = atomicAdd(&a.ccount[t], 1u);
-        if (slot < (uint32_t)kCand) a.cand[t * kCand + slot] = x;
-        else atomicOr(&a.flags[0], 1u);
-    };
-    if (tid < kSet && set[tid] != ~0ull && !quick_reject(a, set[tid])) append(set[tid]);
-    if (tid == 0) {
-        if (overflow) atomicOr(&a.flags[0], 1u);
-        if (a.start / kChunk == chunk) append(a.start);
+// x as a candidate entry (node slot) of the chunk it lies in; ext: appended from a
+// chunk of another tile, or the stream start (K3a's external nodes)
+__device__ __forceinline__ void append_cand(const ScanArgs& a, uint64_t x, bool ext) {
+    const uint64_t t = x / kChunk;   // x <= len: t <= nc
+    const uint32_t slot = atomicAdd(&a.ccount[t], 1u);
+    if (slot < (uint32_t)kCand) {
+        a.cand[t * kCand + slot] = x;
+        if (ext) a.ext[t * kCand + slot] = 1;
+    } else {
+        atomicOr(&a.flags[0], kOvfBucket);
     }
 }
 
-// K1: distinct exits of each chunk.  The chunk's candidates -- strict mode: the
-// positions passing the quick check on their 2 first bytes (~2 % of payload
-// positions, and every real header); otherwise every position -- are each parsed
-// once, from the chunk's LDS copy.
-__global__ __launch_bounds__(kScanT) void scan_exits(ScanArgs a) {
-    __shared__ uint32_t words[kWords];
-    __shared__ unsigned long long set[kSet];
-    __shared__ int overflow;
-    __shared__ uint16_t queue[kScanT / kWave][kChunk / (kScanT / kWave)];   // per wave: its candidates
-    const uint64_t chunk = blockIdx.x;
-    const uint64_t B = chunk * kChunk;
-    const int tid = threadIdx.x;
-    if (tid < kSet) set[tid] = ~0ull;
-    if (tid == 0) overflow = 0;
-    if (chunk == 0 && tid == 0) a.flags[4] = 0;   // K4b''s queue length, left set by the previous call
-    load_chunk(a, B, words);   // 4 KiB in LDS: the walks' hops are LDS reads
-    // this thread's kPer positions and the 4 bytes after them
-    const uint64_t p0 = B + (uint64_t)kPer * tid;
-    uint32_t w[kPer / 4 + 1];
+// a lane of the last vector of a chunk whose 16 positions can exit the chunk with a
+// 7-bit length: p + 2 + 4 + 125 >= chunk end  <=>  offset >= 3965 (lane 55 holds 3952-3967)
+static constexpr int kNearLane = 55;
+static constexpr int kQCap = 256;   // K1: exit-capable candidates queued per chunk (more: serial walk)
+
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+
+// The 4 stream bytes at p for the chunk at the end (clamped load; bytes at or past len
+// undefined)
+__device__ __forceinline__ uint32_t dword_clamped(const ScanArgs& a, uint64_t p) {
+    typedef uint32_t u32u __attribute__((aligned(1)));
+    const uint64_t lim = a.pf_lim + 12;   // len - 4 (a stream under 16 bytes: the scratch word)
+    const uint64_t pc = p < lim ? p : lim;
+    const uint32_t raw = *(const NETC_GLOBAL u32u*)(a.pf_base + pc);
+    const uint64_t sh = p - pc;
+    return sh >= 4 ? 0u : raw >> (8 * sh);
+}
+
+// K1: one wavefront per chunk (the mask kernel's lesson: one-shot waves over a covering
+// grid stream HBM best).  Lane l holds bytes 1024 i + 16 l .. + 15 of the chunk (i = 0..3:
+// four coalesced 16-B loads, addresses clamped into the buffer; the chunk at the end
+// re-reads what the clamp moved), also written to the wave's LDS copy of the chunk.
+// The quick check runs on the registers (the byte after a lane's 16 is the next lane's
+// first; lane 63: the next vector's lane 0, or the next chunk).  The exit-capable
+// candidates of the whole chunk are queued once and parsed round-robin by the lanes
+// from the LDS copy -- one pass, a few lanes busy -- and their distinct exits become
+// candidate entries of the chunks they land in.  (Parsing them vector by vector, a
+// window cut from registers each time, cost 13 us of K1's 27 at config 2.)
+__global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
+    __shared__ uint32_t stage[4][kWords];      // per wave: its chunk's bytes (+ 32 after)
+    __shared__ unsigned long long set[4][kSet];
+    __shared__ uint16_t queue[4][kQCap];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
+    if (c > a.nc) return;
+    const uint64_t B = c * kChunk, Bend = B + kChunk;
+    if (lane == 0 && a.start / kChunk == c) append_cand(a, a.start, true);   // the root node
+    if (B >= a.len) return;   // the virtual chunk: no bytes
+    uint32_t d[4][4], nx[4];
 #pragma unroll
-    for (int k = 0; k < kPer / 4 + 1; ++k) w[k] = words[kPer / 4 * tid + k];
-    // the quick check four positions at a time (bit 7 of each byte: position passes),
-    // the four results interleaved into one word: bit 8 j + k <-> position 4 k + j;
-    // without the strict checks every position is a candidate
-    uint32_t cand = 0x0F0F0F0Fu;
-    if (a.strict) {
-        cand = 0;
+    for (int i = 0; i < 4; ++i) {
+        uint64_t p = B + 1024 * i + 16 * (uint64_t)lane;
+        p = p < a.pf_lim ? p : a.pf_lim;
+        const u32x4 v = __builtin_nontemporal_load((const NETC_GLOBAL u32x4u*)(a.pf_base + p));
 #pragma unroll
-        for (int k = 0; k < kPer / 4; ++k)
-            cand |= quick_ok4(w[k], __builtin_amdgcn_alignbyte(w[k + 1], w[k], 1)) >> (7 - k);
+        for (int k = 0; k < 4; ++k) d[i][k] = v[k];
     }
-    // positions before the stream start or past its end are not candidates (only the
-    // chunks holding either end: a wave-uniform test)
-    if (B < a.start || B + kChunk > a.len) {
+    {
+        uint64_t q = Bend < a.pf_lim ? Bend : a.pf_lim;
+        const u32x4 v = *(const NETC_GLOBAL u32x4u*)(a.pf_base + q);
 #pragma unroll
-        for (int i = 0; i < kPer; ++i)
-            if (p0 + i < a.start || p0 + i >= a.len) cand &= ~(1u << (8 * (i & 3) + (i >> 2)));
+        for (int k = 0; k < 4; ++k) nx[k] = v[k];
     }
-    // the wavefront's candidates into its LDS queue (~2 % of positions pass, 0-3 per
-    // lane), then parsed round-robin by its lanes
-    const int lane = tid & (kWave - 1);
-    uint16_t* q = queue[tid / kWave];
-    const uint32_t mine = __popc(cand);
-    uint32_t incl = mine;   // inclusive prefix of the counts over the wave
+    const bool fast = B >= a.start && Bend + 16 <= a.len;
+    if (Bend + 16 > a.len) {
+        // a vector the clamped 16-B load did not read in place is re-read by dwords,
+        // clamped and shifted so a dword straddling len keeps its bytes below len.
+        // Bytes at or past len may hold anything: no position there is a candidate, and
+        // every parse checks its header and payload against len.
 #pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const uint32_t o = __shfl_up(incl, d, kWave);
-        if (lane >= d) incl += o;
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t p = B + 1024 * i + 16 * (uint64_t)lane;
+            if (p > a.pf_lim)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) d[i][k] = dword_clamped(a, p + 4 * k);
+        }
+        if (Bend > a.pf_lim)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) nx[k] = dword_clamped(a, Bend + 4 * k);
     }
-    const uint32_t total = __shfl(incl, kWave - 1, kWave);
+    uint32_t* st = stage[wv];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        *(u32x4*)&st[(1024 * i + 16 * lane) / 4] = u32x4{d[i][0], d[i][1], d[i][2], d[i][3]};
+    if (lane < 4) st[kChunk / 4 + lane] = nx[lane];
+    set[wv][lane] = ~0ull;   // the wave's exit set
+    // the dword after each lane's 16 bytes (readfirstlane outside the lane-63 branch:
+    // inside it lane 63 is the first active lane)
+    const uint32_t f1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d[1][0]);
+    const uint32_t f2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d[2][0]);
+    const uint32_t f3 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d[3][0]);
+    uint32_t nb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) nb[i] = (uint32_t)__shfl_down((int)d[i][0], 1, kWave);
+    if (lane == kWave - 1) {
+        nb[0] = f1;
+        nb[1] = f2;
+        nb[2] = f3;
+        nb[3] = nx[0];
+    }
+    // edge chunks: the lane's valid positions [start, len) per vector, bit b <-> byte b
+    uint32_t valid[4] = {0xFFFFu, 0xFFFFu, 0xFFFFu, 0xFFFFu};
+    if (!fast) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t q0 = B + 1024 * i + 16 * (uint64_t)lane;
+            const uint64_t lo = a.start <= q0 ? 0 : (a.start - q0 < 16 ? a.start - q0 : 16);
+            const uint64_t hi = a.len <= q0 ? 0 : (a.len - q0 < 16 ? a.len - q0 : 16);
+            valid[i] = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+        }
+    }
+    // exit-capable candidates: bit 32 h + 8 j + 4 (i & 1) + k <-> vector i = 2 h + (i & 1),
+    // dword k, byte j
+    uint32_t half[2] = {0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t ci = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t x = d[i][k];
+            const uint32_t y = __builtin_amdgcn_alignbyte(k < 3 ? d[i][k + 1] : nb[i], x, 1);
+            uint32_t ok = a.strict ? quick_ok4(x, y) : kH;
+            if (!fast) {   // positions before the start or at / past the end are not candidates
+                const uint32_t m4 = (valid[i] >> (4 * k)) & 0xFu;   // byte j valid <-> bit j
+                ok &= ((m4 * 0x00204081u) & 0x01010101u) << 7;
+            }
+            // a 7-bit length cannot leave the chunk unless the position is near its end
+            const uint32_t ext_len = (y & 0x7E7E7E7Eu) + 0x02020202u;   // bit 7: byte 1 & 0x7F >= 126
+            ci |= (ok & ((i == 3 && lane >= kNearLane) ? kH : ext_len) & kH) >> (7 - k);
+        }
+        half[i >> 1] |= ci << (4 * (i & 1));
+    }
+    uint64_t rel = (uint64_t)half[1] << 32 | half[0];
+    // queue them (chunk offsets), then parse round-robin
+    const uint32_t mine = (uint32_t)__popcll(rel);
+    uint32_t incl = mine;
+#pragma unroll
+    for (int dd = 1; dd < kWave; dd <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)incl, dd, kWave);
+        if (lane >= dd) incl += o;
+    }
+    const uint32_t total = (uint32_t)__shfl((int)incl, kWave - 1, kWave);
+    if (total > (uint32_t)kQCap) {   // wave-uniform (adversarial payloads, non-strict mode)
+        if (lane == 0) atomicOr(&a.flags[0], kOvfQueue);
+        return;
+    }
     uint32_t at = incl - mine;
-    for (uint32_t c = cand; c; c &= c - 1) {
-        const int b = __builtin_ctz(c);
-        q[at++] = (uint16_t)(kPer * tid + 4 * (b & 7) + (b >> 3));
+    for (; rel; rel &= rel - 1) {
+        const int b = __builtin_ctzll(rel);
+        const int q = b & 31, r = q & 7;
+        const int i = 2 * (b >> 5) + (r >> 2), k = r & 3, j = q >> 3;
+        queue[wv][at++] = (uint16_t)(1024 * i + 16 * lane + 4 * k + j);
     }
+    __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // Each candidate is parsed once.  A chain inside the chunk moves from candidate
-    // to candidate (a position that fails the quick check would parse DEAD), so a
-    // chain leaves the chunk exactly where its last candidate's own frame does: the
-    // chunk's exits are the direct exits of its candidates, and no chain is walked.
-    // (An earlier form walked every candidate's chain to the chunk end, and handed
-    // chunks of tiny frames, whose chains outran the hop budget, to an LDS
-    // pointer-jumping kernel -- also the whole non-strict path.)
-    const uint64_t Bend = B + kChunk;
-    for (uint32_t i = lane; i < total; i += kWave) {
-        const uint64_t p = B + q[i];
-        const uint64_t v = parse_at(a, p, window_at(words, (int)(p - B)), nullptr, nullptr);
-        if (!(v & kTerm) && v >= Bend) set_insert(set, v, &overflow);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    bool ovf = false;
+    for (uint32_t e = lane; e < total; e += kWave) {
+        const uint32_t off = queue[wv][e];
+        const uint64_t v = parse_at(a, B + off, window_at(st, (int)off), nullptr, nullptr);
+        // strict mode prunes exits that cannot start a frame: payload bytes parsed as a
+        // chain land on random positions, which pass with ~2 % odds, while the true chain
+        // always lands on a real header
+        if (!(v & kTerm) && v >= Bend && set_insert(set[wv], v, &ovf) && !quick_reject(a, v))
+            append_cand(a, v, v / kChunk / kTileChunks != c / kTileChunks);
     }
-    __syncthreads();
-    publish_exits(a, chunk, set, overflow, tid);
+    if (ovf) atomicOr(&a.flags[0], kOvfSet);
 }
 
-// node -> the candidate its chain exits to (or -1) and the terminal where it ends
+// node -> the candidate its chain exits to (the first slot holding that position, or
+// -1) and the terminal where it ends
 __device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint64_t x, uint64_t v, uint32_t cnt) {
-    if (x == a.start) {
-        a.flags[1] = (uint32_t)node;
-        a.mark[node] = 1;
-    }
+    if (x == a.start) a.flags[1] = (uint32_t)node + 1;
     int32_t next = -1;
     if (term_type(v) == kExit) {
         const uint64_t y = term_pos(v), t = y / kChunk;
-        const uint32_t cnt = min(a.ccount[t], (uint32_t)kCand);
-        for (uint32_t i = 0; i < cnt; ++i)
-            if (a.cand[t * kCand + i] == y) next = (int32_t)(t * kCand + i);
+        // the counter and the bucket's 8 positions (one line) in one trip
+        const uint32_t n = min(a.ccount[t], (uint32_t)kCand);
+        uint64_t ts[kCand];
+#pragma unroll
+        for (int j = 0; j < kCand; ++j) ts[j] = a.cand[t * kCand + j];
+#pragma unroll
+        for (int j = kCand - 1; j >= 0; --j)
+            if ((uint32_t)j < n && ts[j] == y) next = (int32_t)(t * kCand + j);   // the first match
         // not a candidate: pruned by K1 (the chain dies at y), or its bucket overflowed
-        if (next < 0 && !quick_reject(a, y)) atomicOr(&a.flags[0], 1u);
+        if (next < 0 && !quick_reject(a, y)) atomicOr(&a.flags[0], kOvfLink);
     }
     a.link[node] = next;
     a.nterm[node] = v;
     a.ncnt[node] = cnt;
 }
 
-// K2' / K4b': every position of the chunk that can start a header (strict: passes
-// the quick check; else every position) parsed once into a 16-bit in-chunk link
-// (kNoLink: the chain ends or leaves the chunk there), then four doubling passes:
-// returns the 16-hop links (l1 keeps the 1-hop ones, lj the 8-hop ones).  The caller
-// has loaded words.
+// Every position of the chunk that can start a header (strict: passes the quick
+// check; else every position) parsed once into a 16-bit in-chunk link (kNoLink: the
+// chain ends or leaves the chunk there), then four doubling passes: returns the
+// 16-hop links (l1 keeps the 1-hop ones, lj the 8-hop ones).  The caller has loaded
+// words.
 static constexpr uint16_t kNoLink = 0xFFFF;
 static constexpr int kStride = 16;   // hops per 16-hop link
 static constexpr int kAncStride = 8;                              // frames per K2' anchor
@@ -400,15 +524,12 @@ __device__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const ui
     uint32_t w[kPer / 4 + 1];
 #pragma unroll
     for (int k = 0; k < kPer / 4 + 1; ++k) w[k] = words[i0 / 4 + k];
-    auto byte_at = [&](int j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
     uint32_t cand = 0;   // this thread's positions that can start a header
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const uint32_t first = byte_at(j), second = byte_at(j + 1), opcode = first & 0x0F;
-        const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
-        const bool reject =
-            a.strict && (!(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80)));
-        if (!reject) cand |= 1u << j;
+    for (int k = 0; k < kPer / 4; ++k) {
+        const uint32_t ok = a.strict ? quick_ok4(w[k], __builtin_amdgcn_alignbyte(w[k + 1], w[k], 1)) : kH;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cand |= ((ok >> (8 * j + 7)) & 1u) << (4 * k + j);
     }
     // no link anywhere first (bank-conflict-free order), then the candidates parsed:
     // the wave takes as many trips as its busiest lane has candidates (a few in
@@ -440,52 +561,70 @@ __device__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const ui
     return src;
 }
 
-// K2: one thread per node (candidate slot): the candidate entry's chain walked from
-// global memory to the candidate it exits to; a chain longer than kWalkHops goes
-// to K2' (LDS).  Unused slots hold stale values from earlier calls: dead ends.
-__global__ __launch_bounds__(256) void scan_links(ScanArgs a) {
-    const uint64_t node = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t chunk = node / kCand;
-    if (chunk > a.nc) return;
-    const uint32_t i = (uint32_t)(node % kCand);
-    if (i >= min(a.ccount[chunk], (uint32_t)kCand)) {
-        a.link[node] = -1;
-        return;
-    }
-    const uint64_t B = chunk * kChunk;
-    const uint64_t x = a.cand[node];
-    uint32_t cnt = 0;   // K4 takes the frame count of the true entry's walk from here
-    const uint64_t v = x - B < kChunk ? walk_frames<false>(a, B, nullptr, x, 2 * kWalkHops,
-                                                           [&](uint64_t, uint32_t, uint8_t) { ++cnt; })
-                                      : term(kEnd, x);   // x == len on a chunk edge
-    if (v == 0) {
-        a.slow2[atomicAdd(&a.flags[3], 1u)] = (uint32_t)node;
-        return;
-    }
-    link_node(a, node, x, v, cnt);
-}
-
-// K2': the nodes K2 left (chains of more than 2 kWalkHops frames in the chunk): the
-// chunk's 16-hop links built in LDS, then one thread walks them from the entry --
-// count / 16 + at most 15 hops -- and re-parses the last header for the exact
-// terminal (EXIT to the next chunk, END or DEAD) and whether it adds a frame.
-__global__ __launch_bounds__(kScanT) void scan_links_lds(ScanArgs a) {
+// K2: nodes of kBlkChunks chunks per block, one thread per slot: a repeated position
+// defers to its first slot (passing on its external flag); a node's chain is walked
+// from global memory to the candidate it exits to.  Chains of more than kWalkHops
+// frames in the chunk are finished by the whole block afterwards: the chunk's 16-hop
+// links built in LDS, one thread walks them from the entry -- count / 8 + at most 7
+// hops, leaving an anchor every 8 frames -- and re-parses the last header for the exact
+// terminal.
+__global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
     __shared__ uint32_t words[kWords];
     __shared__ uint16_t l1[kChunk];
     __shared__ uint16_t lj[kChunk];
     __shared__ uint16_t lk16[kChunk];
-    const uint64_t count = __hip_atomic_load(&a.flags[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint64_t q = blockIdx.x; q < count; q += gridDim.x) {
-        const uint64_t node = a.slow2[q], chunk = node / kCand, B = chunk * kChunk;
+    __shared__ uint32_t queue[kBlkChunks * kCand];
+    __shared__ int nq;
+    const int tid = threadIdx.x;
+    if (tid == 0) nq = 0;
+    __syncthreads();
+    if (tid < kBlkChunks * kCand) {
+        const uint64_t s = (uint64_t)blockIdx.x * (kBlkChunks * kCand) + tid, c = s / kCand;
+        const uint32_t i = (uint32_t)(s % kCand);
+        // the counter, the bucket (one line) and the external flags in one trip
+        const uint32_t cc = c <= a.nc ? a.ccount[c] : 0;
+        uint64_t cs[kCand];
+#pragma unroll
+        for (int j = 0; j < kCand; ++j) cs[j] = c <= a.nc ? a.cand[c * kCand + j] : 0;
+        const uint64_t x = c <= a.nc ? a.cand[s] : 0;
+        if (c <= a.nc && i < min(cc, (uint32_t)kCand)) {
+            int dup = -1;
+#pragma unroll
+            for (int j = kCand - 1; j >= 0; --j)
+                if ((uint32_t)j < i && cs[j] == x) dup = j;   // the first earlier slot with x
+            if (dup >= 0) {
+                a.link[s] = kDupLink;
+                a.ncnt[s] = 0;
+                if (a.ext[s]) a.ext[c * kCand + dup] = 1;
+            } else {
+                const uint64_t B = c * kChunk;
+                uint32_t cnt = 0;
+                const uint64_t v = x - B < kChunk ? walk_frames<false>(a, B, nullptr, x, kWalkHops,
+                                                                       [&](uint64_t, uint32_t, uint8_t) { ++cnt; })
+                                                  : term(kEnd, x);   // x == len on a chunk edge
+                if (v == 0) {
+                    queue[atomicAdd(&nq, 1)] = (uint32_t)s;
+                } else {
+                    a.anq[s] = ~0u;
+                    link_node(a, s, x, v, cnt);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const int n = nq;
+    for (int qi = 0; qi < n; ++qi) {
+        const uint64_t node = queue[qi], chunk = node / kCand, B = chunk * kChunk;
         load_chunk(a, B, words);
         chunk_links16(a, B, words, l1, lj, lk16);
         const uint16_t* l8 = lj;   // the 8-hop links (the pass before the last)
-        if (threadIdx.x == 0) {
-            const uint64_t x = a.cand[node];   // in [B, B + kChunk): K2's walk started there
+        if (tid == 0) {
+            const uint64_t x = a.cand[node];   // in [B, B + kChunk): the walk above started there
             uint32_t p = (uint32_t)(x - B), hops = 0;
-            // the walk's positions every 8 frames are K4b's anchors if this node turns out
-            // to be its chunk's true entry: kept in slot q while slots last
-            const bool keep = q < a.anc_cap;
+            // the walk's positions every 8 frames are K4's anchors if this node turns out
+            // to be its chunk's true entry: kept in the block's slots while they last
+            const uint64_t q = (uint64_t)blockIdx.x * kBlkChunks + qi;
+            const bool keep = qi < kBlkChunks && q < a.anc_cap;
             uint16_t* anc = a.anc + (keep ? q : 0) * kAncSlot;
             int na = 0;
             if (keep) anc[na++] = (uint16_t)p;
@@ -511,45 +650,10 @@ __global__ __launch_bounds__(kScanT) void scan_links_lds(ScanArgs a) {
     }
 }
 
-// K3, pass k: src = J (the 8^k-th successor; J = link in pass 0).  Builds J^8 into
-// dst (unless last) and marks the J .. J^7 successors of every marked node: after
-// pass k every node within 8^(k+1) - 1 steps of the start is marked (a node d
-// steps away is 0..7 J-steps past a node marked before the pass), so after
-// ceil(log8(chunks)) passes exactly the chain's nodes are (one per chunk it
-// enters).  The passes are launch-bound, hence 3 doubling levels each.  Marks set
-// during a pass may be followed in the same pass: they are on the chain too.
-__global__ void scan_lift(const int32_t* src, int32_t* dst, uint8_t* mark, uint64_t nodes) {
-    const uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= nodes) return;
-    auto step = [&](int32_t u) -> int32_t {   // (range check: defence in depth)
-        return (u >= 0 && (uint64_t)u < nodes) ? src[u] : -1;
-    };
-    const bool marked = mark[v] != 0;
-    int32_t u = step((int32_t)v);
-#pragma unroll
-    for (int h = 1; h < 8; ++h) {   // u = J^h(v)
-        if (marked && u >= 0 && (uint64_t)u < nodes) mark[u] = 1;
-        u = step(u);
-    }
-    if (dst) dst[v] = u;   // J^8(v)
-}
-
-__device__ __forceinline__ uint64_t cand_pos(const ScanArgs& a, int32_t node) { return a.cand[node]; }
-
-static constexpr int kEmitHops = 64;   // K4: a chunk of more frames is emitted from LDS
-
-// the marked (true) entry of a chunk: its node, or -1
-__device__ __forceinline__ int64_t chunk_entry(const ScanArgs& a, uint64_t chunk) {
-    int64_t enode = -1;
-    const uint32_t cnt = min(a.ccount[chunk], (uint32_t)kCand);
-    for (uint32_t i = 0; i < cnt; ++i)
-        if (a.mark[chunk * kCand + i]) enode = (int64_t)(chunk * kCand + i);
-    return enode;
-}
-
-// exclusive prefix sum over a 256-thread block; the block total in *total
-__device__ uint64_t block_scan256(uint64_t v, uint64_t* total) {
-    __shared__ uint64_t wsum[4];
+// exclusive prefix sum over a block of NT threads; the block total in *total
+template <int NT>
+__device__ uint64_t block_scan(uint64_t v, uint64_t* total) {
+    __shared__ uint64_t wsum[NT / kWave];
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
     uint64_t inc = v;
 #pragma unroll
@@ -561,7 +665,7 @@ __device__ uint64_t block_scan256(uint64_t v, uint64_t* total) {
     __syncthreads();
     uint64_t before = 0, all = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NT / kWave; ++i) {
         before += i < w ? wsum[i] : 0;
         all += wsum[i];
     }
@@ -570,162 +674,471 @@ __device__ uint64_t block_scan256(uint64_t v, uint64_t* total) {
     return before + inc - v;
 }
 
-// K4a: one thread per chunk.  The chain's frames in the chunk are the frames K2
-// counted on its marked entry's walk; a chained scan over tiles of 256 chunks
-// (decoupled look-back) gives each chunk's first frame index.  The chunk where
-// the chain ends sets the results.  On candidate overflow, one thread walks the
-// whole stream instead (serial fallback).
-// The chunk's candidate counter and mark bytes are read here for the last time: the
-// thread zeroes them, so the next call on this scratch needs no clearing launch.
-__device__ __forceinline__ void clear_chunk(const ScanArgs& a, uint64_t chunk) {
-    a.ccount[chunk] = 0;
-    *(uint64_t*)(a.mark + chunk * kCand) = 0;   // kCand == 8 mark bytes, 8-aligned
-}
+// K3a: one block per tile of kTileChunks chunks (thread t: chunk t).  The tile's
+// nodes compacted into LDS; local links (to a node of the same tile) are followed by
+// Wyllie pointer jumping: W = frames to the tile's exit, L = the last node before it,
+// and each external node's bit pushed along its path (a node pushes its bits along
+// its current jump; after round r every node holds the bits of the nodes up to 2^(r+1)
+// - 1 links before it).  ~log2(path) rounds of a few LDS operations per node.
+static constexpr uint16_t kNone = 0xFFFF;
 
-__global__ __launch_bounds__(256) void scan_count(ScanArgs a) {
-    __shared__ uint64_t tile_prefix;
-    const uint64_t tile = blockIdx.x;
-    const uint64_t chunk = tile * 256 + threadIdx.x;
-    if (__hip_atomic_load(&a.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-        if (chunk <= a.nc) clear_chunk(a, chunk);
-        if (tile == 0 && threadIdx.x == 0) {
-            uint64_t p = a.start, n = 0, err = ~0ull;
-            for (;;) {
-                uint32_t key;
-                uint8_t b0;
-                const uint64_t v = parse_at(a, p, window_global(a, p), &key, &b0);
-                if (v & kTerm) {
-                    if (term_type(v) == kDead) err = p;
-                    break;
-                }
-                if (n < a.max_frames) {
-                    a.hdr[n] = p;
-                    a.keys[n] = key;
-                    a.b0[n] = b0;
-                }
-                ++n;
-                p = v;
-            }
-            if (n <= a.max_frames) a.hdr[n] = p;
-            a.result[0] = n;
-            a.result[1] = p;
-            a.result[2] = err;
-        }
+__global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
+    __shared__ uint16_t cid[kTileSlots];   // tile slot -> compact node
+    __shared__ uint16_t gsl[kTileSlots];   // compact node -> tile slot
+    __shared__ uint16_t P[kTileSlots];     // current jump (compact), kNone: at the last node
+    __shared__ uint16_t L[kTileSlots];     // last node reached
+    __shared__ uint32_t W[kTileSlots];     // frames from the node to L's exit
+    __shared__ uint32_t bits[kTileSlots];
+    __shared__ uint16_t elist[kExt];
+    __shared__ int skip;
+    const int t = threadIdx.x;
+    // overflow: K4 walks serially.  Read once for the block (another tile may set it meanwhile)
+    if (t == 0) skip = __hip_atomic_load(&a.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    __syncthreads();
+    if (skip) return;
+    const uint64_t tile = blockIdx.x, c = tile * kTileChunks + t, s0 = tile * kTileSlots;
+    // the chunk's counter, external flags, links and counts in one trip
+    const bool live = c <= a.nc;
+    const uint32_t cnt = live ? min(a.ccount[c], (uint32_t)kCand) : 0;
+    const uint64_t exf = live ? *(const uint64_t*)(a.ext + c * kCand) : 0;   // kCand == 8 flag bytes
+    int32_t lks[kCand];
+    uint32_t nws[kCand];
+#pragma unroll
+    for (int j = 0; j < kCand; ++j) {
+        lks[j] = live ? a.link[c * kCand + j] : kDupLink;
+        nws[j] = live ? a.ncnt[c * kCand + j] : 0;
+    }
+    uint32_t extm = 0;
+#pragma unroll
+    for (int j = 0; j < kCand; ++j)
+        if ((uint32_t)j < cnt && ((exf >> (8 * j)) & 0xFF) && lks[j] != kDupLink) extm |= 1u << j;
+    uint64_t V64, E64;
+    const uint32_t base = (uint32_t)block_scan<kScanT>(cnt, &V64);
+    uint32_t eidx = (uint32_t)block_scan<kScanT>((uint64_t)__popc(extm), &E64);
+    if (E64 > (uint64_t)kExt) {   // block-uniform
+        if (t == 0) atomicOr(&a.flags[0], kOvfExt);
         return;
     }
-    const int64_t enode = chunk <= a.nc ? chunk_entry(a, chunk) : -1;
-    if (chunk <= a.nc) clear_chunk(a, chunk);
-    const uint64_t count = enode >= 0 ? a.ncnt[enode] : 0;
-    uint64_t agg;
-    const uint64_t ex = block_scan256(count, &agg);
-    if (threadIdx.x < kWave) {
-        const int lane = threadIdx.x;
-        if (lane == 0)
-            __hip_atomic_store(&a.status[tile], status_word(tile == 0 ? 2 : 1, a.epoch, agg), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t prefix = tile == 0 ? 0 : look_back(a.status, (int64_t)tile, a.epoch, lane);
-        if (lane == 0) {
-            if (tile)
-                __hip_atomic_store(&a.status[tile], status_word(2, a.epoch, prefix + agg), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            tile_prefix = prefix;
+    const int V = (int)V64, E = (int)E64;
+    for (uint32_t i = 0; i < cnt; ++i) {
+        cid[t * kCand + i] = (uint16_t)(base + i);
+        gsl[base + i] = (uint16_t)(t * kCand + i);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kCand; ++i) {
+        if ((uint32_t)i >= cnt) break;
+        const uint32_t k = base + i;
+        const int32_t lk = lks[i];
+        P[k] = (lk >= 0 && (uint64_t)lk - s0 < kTileSlots) ? cid[(uint64_t)lk - s0] : kNone;
+        W[k] = lk == kDupLink ? 0u : nws[i];
+        L[k] = (uint16_t)k;
+        if ((extm >> i) & 1) {
+            bits[k] = 1u << eidx;
+            elist[eidx] = (uint16_t)k;
+            ++eidx;
+        } else {
+            bits[k] = 0;
         }
     }
     __syncthreads();
-    if (chunk > a.nc) return;
-    const uint64_t base = tile_prefix + ex;
-    a.cbase[chunk] = base;
-    if (chunk == a.nc) a.result[0] = base + count;
-    if (enode < 0) return;
-    // the chain ends in this chunk, or leaves it onto a header K1 pruned
-    uint64_t stop = a.nterm[enode];
-    if (term_type(stop) == kExit && quick_reject(a, term_pos(stop))) stop = term(kDead, term_pos(stop));
-    if (term_type(stop) != kExit) {
-        const uint64_t end = term_pos(stop), k = base + count;
-        a.result[1] = end;
-        a.result[2] = term_type(stop) == kDead ? end : ~0ull;
-        if (k <= a.max_frames) a.hdr[k] = end;
-    }
-    // K4b, in the same thread now that the base is known: the chunk's frames walked
-    // from global memory (header bytes only), descriptors from the base on; a chunk
-    // of more than kEmitHops frames goes to K4b' (LDS)
-    if (count > (uint64_t)kEmitHops) {
-        a.slow3[atomicAdd(&a.flags[4], 1u)] = (uint32_t)enode;   // the node: its mark is gone
-        return;
-    }
-    uint64_t k = base;
-    walk_frames<false>(a, chunk * kChunk, nullptr, a.cand[enode], -1, [&](uint64_t p, uint32_t key, uint8_t b0) {
-        if (k < a.max_frames) {
-            a.hdr[k] = p;
-            a.keys[k] = key;
-            a.b0[k] = b0;
-        }
-        ++k;
-    });
-}
-
-// K4b' for the chunks whose entry K2' left anchors for (all of them unless the anchor
-// slots ran out): one wavefront per chunk, lane t parses the kAncStride frames from
-// anchor t, header bytes straight from global memory, and writes their descriptors
-// from index cbase + kAncStride t.  No LDS: the chunk is never reloaded.  Runs at the
-// start of scan_emit_lds (one launch fewer: at C2 shape nothing is queued at all).
-__device__ void emit_anchored(const ScanArgs& a, uint64_t count) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / kWave);
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
-    for (uint64_t q = wave; q < count; q += nwaves) {
-        const uint64_t node = a.slow3[q];
-        const uint32_t slot = a.anq[node];
-        if (slot == ~0u) continue;   // scan_emit_lds takes it
-        const uint64_t chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
-        const int na = (int)a.anc_n[slot];
-        const uint64_t base = a.cbase[chunk];
-        for (int t = lane; t < na; t += kWave) {
-            uint64_t k = base + (uint64_t)t * kAncStride;
-            uint64_t pos = B + a.anc[(uint64_t)slot * kAncSlot + t];
-            for (int h = 0; h < kAncStride && pos < Bend; ++h) {
-                uint32_t key;
-                uint8_t b0;
-                const uint64_t v = parse_at(a, pos, window_global(a, pos), &key, &b0);
-                if (v & kTerm) break;
-                if (k < a.max_frames) {
-                    a.hdr[k] = pos;
-                    a.keys[k] = key;
-                    a.b0[k] = b0;
+    constexpr int kR = (int)(kTileSlots / kScanT);
+    for (;;) {
+        uint16_t np[kR], nl[kR];
+        uint32_t nw[kR];
+        int any = 0;
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            const int k = t + kScanT * r;
+            np[r] = kNone;
+            if (k < V) {
+                const uint16_t p = P[k];
+                if (p != kNone) {
+                    np[r] = P[p];
+                    nw[r] = W[k] + W[p];
+                    nl[r] = L[p];
+                    atomicOr(&bits[p], bits[k]);
+                    any |= np[r] != kNone;
                 }
-                ++k;
-                pos = v;
             }
         }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            const int k = t + kScanT * r;
+            if (k < V && P[k] != kNone) {
+                P[k] = np[r];
+                W[k] = nw[r];
+                L[k] = nl[r];
+            }
+        }
+        if (!__syncthreads_or(any)) break;
+    }
+    for (uint32_t i = 0; i < cnt; ++i) {
+        const uint64_t gs = c * kCand + i;
+        const uint32_t k = base + i;
+        a.wsum[gs] = W[k];
+        a.pbits[gs] = bits[k];
+    }
+    if (t < E) {
+        const uint32_t k = elist[t];
+        const uint64_t last = s0 + gsl[L[k]];
+        TileExt e;
+        e.slot = (uint32_t)(s0 + gsl[k]);
+        e.w = W[k];
+        e.xl = a.link[last];
+        e.pad = 0;
+        e.term = a.nterm[last];
+        a.text[tile * kExt + t] = e;
+    }
+    if (t == 0) a.tcount[tile] = (uint32_t)E;
+}
+
+// K3b: one block.  The external nodes of all tiles into LDS (tile by tile, in bit
+// order); each one's successor is the external node its path exits to; Wyllie
+// pointer jumping gives R = frames from the node to the end of its chain and marks
+// the nodes reachable from the root.  A marked node is its tile's true entry: frames
+// before it = R(root) - R(node).  The one whose path ends inside its tile holds the
+// terminal: the results.  Beyond the capacities (kMaxTiles, kExtCap) -> serial walk.
+// The tile counts and each tile's first two records are read in one trip (a tile
+// rarely has more: the true entry, now and then a garbage one); the rest in a second.
+static constexpr int kExtFirst = 2;
+
+__device__ __forceinline__ void put_ext(uint32_t* eslot, uint32_t* ew, int32_t* exl, uint64_t* R, uint32_t idx,
+                                        const TileExt& e) {
+    eslot[idx] = e.slot;
+    ew[idx] = e.w;
+    exl[idx] = e.xl;
+    R[idx] = e.w;
+}
+
+__global__ __launch_bounds__(kResolveT) void scan_resolve(ScanArgs a, uint64_t tiles) {
+    __shared__ uint32_t toff[kMaxTiles + 1];
+    __shared__ uint32_t eslot[kExtCap];
+    __shared__ uint32_t ew[kExtCap];
+    __shared__ int32_t exl[kExtCap];
+    __shared__ uint16_t succ[kExtCap];
+    __shared__ uint64_t R[kExtCap];
+    __shared__ uint8_t mark[kExtCap];
+    __shared__ int bad, root_idx;
+    __shared__ uint32_t root_slot, M;
+    const int t = threadIdx.x;
+    uint32_t ovf = 0, rs = 0;
+    if (t == 0) {
+        ovf = __hip_atomic_load(&a.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        rs = __hip_atomic_load(&a.flags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tiles > (uint64_t)kMaxTiles) {   // kernel-uniform
+        if (t == 0) {
+            a.flags[8] = 1u;
+            a.flags[9] = kWhyTiles | ovf;
+            a.flags[0] = 0;
+            a.flags[1] = 0;
+        }
+        return;
+    }
+    constexpr int kTR = kMaxTiles / kResolveT;
+    // trip 1: every tile's count, and the first records of the first kResolveT tiles
+    // (1 GiB of stream; issued together, used after the scan)
+    uint32_t tc[kTR];
+    TileExt e0, e1;
+#pragma unroll
+    for (int r = 0; r < kTR; ++r) {
+        const uint64_t tl = (uint64_t)t + (uint64_t)kResolveT * r;
+        tc[r] = tl < tiles ? a.tcount[tl] : 0;
+    }
+    if ((uint64_t)t < tiles) {
+        e0 = a.text[(uint64_t)t * kExt];
+        e1 = a.text[(uint64_t)t * kExt + 1];
+    }
+    __shared__ uint32_t why;
+    if (t == 0) {
+        bad = ovf != 0 || rs == 0;
+        why = ovf | (rs == 0 ? kWhyRoot : 0u);
+        root_slot = rs - 1;
+        root_idx = -1;
+    }
+    uint64_t run = 0;
+#pragma unroll
+    for (int r = 0; r < kTR; ++r) {
+        if ((uint64_t)kResolveT * r >= tiles) break;   // block-uniform
+        const uint64_t tl = (uint64_t)t + (uint64_t)kResolveT * r;
+        uint64_t tot;
+        const uint64_t ex = block_scan<kResolveT>(tc[r], &tot);
+        if (tl < tiles) toff[tl] = (uint32_t)(run + ex);
+        run += tot;
+    }
+    if (t == 0) {
+        toff[tiles] = (uint32_t)run;
+        M = (uint32_t)run;
+        if (run > (uint64_t)kExtCap) {
+            bad = 1;
+            why |= kWhyExtCap;
+        }
+    }
+    __syncthreads();
+    if (bad) {   // block-uniform
+        if (t == 0) {
+            a.flags[8] = 1u;
+            a.flags[9] = why;
+            a.flags[0] = 0;
+            a.flags[1] = 0;
+        }
+        return;
+    }
+    int more = 0;
+#pragma unroll
+    for (int r = 0; r < kTR; ++r) {
+        const uint64_t tl = (uint64_t)t + (uint64_t)kResolveT * r;
+        if (tl >= tiles) break;
+        const uint32_t o = toff[tl];
+        if (r == 0) {
+            if (tc[r] > 0) put_ext(eslot, ew, exl, R, o, e0);
+            if (tc[r] > 1) put_ext(eslot, ew, exl, R, o + 1, e1);
+        } else {
+            for (uint32_t j = 0; j < tc[r] && j < (uint32_t)kExtFirst; ++j)
+                put_ext(eslot, ew, exl, R, o + j, a.text[tl * kExt + j]);
+        }
+        more |= tc[r] > (uint32_t)kExtFirst;
+    }
+    if (__syncthreads_or(more)) {   // trip 2 (rare): tiles with more than two external nodes
+#pragma unroll
+        for (int r = 0; r < kTR; ++r) {
+            const uint64_t tl = (uint64_t)t + (uint64_t)kResolveT * r;
+            if (tl >= tiles) break;
+            for (uint32_t j = kExtFirst; j < tc[r]; ++j) put_ext(eslot, ew, exl, R, toff[tl] + j, a.text[tl * kExt + j]);
+        }
+        __syncthreads();
+    }
+    const int m = (int)M;
+    // successors: the external node (of a later tile) each path exits to, found in LDS
+    for (int i = t; i < m; i += kResolveT) {
+        const int32_t xl = exl[i];
+        uint16_t sx = kNone;
+        if (xl >= 0) {
+            const uint64_t t2 = (uint64_t)xl / kTileSlots;
+            for (uint32_t u = toff[t2]; u < toff[t2 + 1]; ++u)
+                if (eslot[u] == (uint32_t)xl) sx = (uint16_t)u;
+            if (sx == kNone) {   // an exit onto a node no tile listed (defence in depth)
+                bad = 1;
+                why = kWhySucc;
+            }
+        }
+        succ[i] = sx;
+        mark[i] = eslot[i] == root_slot;
+        if (eslot[i] == root_slot) root_idx = i;
+    }
+    __syncthreads();
+    if (bad || root_idx < 0) {   // block-uniform
+        if (t == 0) {
+            a.flags[8] = 1u;
+            a.flags[9] = bad ? why : kWhyRoot;
+            a.flags[0] = 0;
+            a.flags[1] = 0;
+        }
+        return;
+    }
+    constexpr int kR = kExtCap / kResolveT;
+    for (;;) {
+        uint16_t ns[kR];
+        uint64_t nr[kR];
+        int any = 0;
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            const int i = t + kResolveT * r;
+            ns[r] = kNone;
+            if (i < m) {
+                const uint16_t sx = succ[i];
+                if (sx != kNone) {
+                    ns[r] = succ[sx];
+                    nr[r] = R[i] + R[sx];
+                    if (mark[i]) mark[sx] = 1;
+                    any |= ns[r] != kNone;
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            const int i = t + kResolveT * r;
+            if (i < m && succ[i] != kNone) {
+                succ[i] = ns[r];
+                R[i] = nr[r];
+            }
+        }
+        if (!__syncthreads_or(any)) break;
+    }
+    // per tile: its marked external node (at most one: the chain enters a tile once)
+    const uint64_t total = R[root_idx];
+#pragma unroll
+    for (int r = 0; r < kTR; ++r) {
+        const uint64_t tl = (uint64_t)t + (uint64_t)kResolveT * r;
+        if (tl >= tiles) break;
+        TileInfo ti;
+        ti.j = -1;
+        ti.we = 0;
+        ti.base = 0;
+        for (uint32_t i = toff[tl]; i < toff[tl + 1]; ++i)
+            if (mark[i]) {
+                ti.j = (int32_t)(i - toff[tl]);
+                ti.we = ew[i];
+                ti.base = total - R[i];
+                if (exl[i] < 0) {   // the chain ends in this tile
+                    const uint64_t term_v = a.text[tl * kExt + ti.j].term;
+                    const uint64_t ty = term_type(term_v), pos = term_pos(term_v);
+                    // an exit onto a position K1 pruned: the chain dies there
+                    const bool dead = ty == kDead || ty == kExit;
+                    a.result[0] = total;
+                    a.result[1] = pos;
+                    a.result[2] = dead ? pos : ~0ull;
+                    if (total <= a.max_frames) a.hdr[total] = pos;
+                }
+            }
+        a.tinfo[tl] = ti;
+    }
+    if (t == 0) {
+        a.flags[8] = 0;
+        a.flags[9] = 0;
+        a.flags[0] = 0;
+        a.flags[1] = 0;
     }
 }
 
-// K4b': the chunks of many (tiny) frames, emitted from LDS in parallel.  Every
-// position of the chunk that can start a header is parsed once into a 16-bit
-// in-chunk link (kNoLink: the chain ends or leaves the chunk there); four doubling
-// passes make the 16-hop links; one thread walks those from the entry, leaving an
-// anchor every 16 frames; then thread t walks 16 frames from anchor t and writes
-// their descriptors from index cbase + 16 t.  Serial depth count / 16 + 16 hops
-// instead of count (a 4 KiB chunk of 16-B frames holds ~186).
-// The last kernel of a scan: it also zeroes flags 0-3 for the next call (no longer
-// read here; flag 4, this kernel's own queue length, is zeroed by the next call's K1,
-// which runs before anything counts into it).  A last-block-done counter instead cost
-// 1,024 same-address atomics per call (~10 us).
-__global__ __launch_bounds__(kScanT) void scan_emit_lds(ScanArgs a) {
+// K4, serial fallback (capacities overflowed): one thread walks the whole stream.
+__device__ void serial_walk(const ScanArgs& a) {
+    uint64_t p = a.start, n = 0, err = ~0ull;
+    for (;;) {
+        uint32_t key;
+        uint8_t b0;
+        const uint64_t v = parse_at(a, p, window_global(a, p), &key, &b0);
+        if (v & kTerm) {
+            if (term_type(v) == kDead) err = p;
+            break;
+        }
+        if (n < a.max_frames) {
+            a.hdr[n] = p;
+            a.keys[n] = key;
+            a.b0[n] = b0;
+        }
+        ++n;
+        p = v;
+    }
+    if (n <= a.max_frames) a.hdr[n] = p;
+    a.result[0] = n;
+    a.result[1] = p;
+    a.result[2] = err;
+}
+
+// Write frame k's descriptors (if recorded)
+__device__ __forceinline__ void put_frame(const ScanArgs& a, uint64_t k, uint64_t p, uint32_t key, uint8_t b0) {
+    if (k < a.max_frames) {
+        a.hdr[k] = p;
+        a.keys[k] = key;
+        a.b0[k] = b0;
+    }
+}
+
+// K4: the chunks' descriptors, kBlkChunks chunks per block.  Thread t < kBlkChunks
+// takes chunk t: its true entry is the node whose path bits hold the tile entry's bit;
+// a chunk of at most kWalkHops frames is walked by that thread (header bytes from
+// global memory).  Longer ones: with K2' anchors one wavefront per chunk, lane u
+// parsing the 8 frames from anchor u; without, the whole block from LDS (16-hop links,
+// an anchor every 16 frames, thread u the 16 frames from anchor u).  Every chunk's
+// candidate counter and external flags are zeroed here, after their last reader:
+// the next call needs no clearing launch.
+__global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a) {
     __shared__ uint32_t words[kWords];
     __shared__ uint16_t l1[kChunk];    // next header (local index) or kNoLink
     __shared__ uint16_t lj[kChunk];    // 2^k hops (ping)
     __shared__ uint16_t lk16[kChunk];  // 2^k hops (pong); 16 hops after the last pass
     __shared__ uint16_t anchor[kChunk / kStride + 1];
-    __shared__ int nanchor;
+    __shared__ int nanchor, nqa, nqb;
+    __shared__ uint32_t qa_node[kBlkChunks], qb_node[kBlkChunks];
+    __shared__ uint64_t qa_base[kBlkChunks], qb_base[kBlkChunks];
     const int tid = threadIdx.x;
-    const uint64_t count = __hip_atomic_load(&a.flags[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (blockIdx.x == 0 && tid == 0)
-        for (int i = 0; i < 4; ++i) a.flags[i] = 0;
-    emit_anchored(a, count);
-    for (uint64_t q = blockIdx.x; q < count; q += gridDim.x) {
-        const uint64_t node = a.slow3[q], chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
-        if (a.anq[node] != ~0u) continue;   // anchored: emit_anchored wrote it
+    if (tid == 0) {
+        nqa = 0;
+        nqb = 0;
+    }
+    const bool fb = __hip_atomic_load(&a.flags[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    __syncthreads();
+    if (tid < kBlkChunks) {
+        const uint64_t c = (uint64_t)blockIdx.x * kBlkChunks + tid;
+        if (c <= a.nc) {
+            // the chunk's counter, path bits, W, counts and positions, and its tile's entry, in one trip
+            const uint32_t cnt = min(a.ccount[c], (uint32_t)kCand);
+            const TileInfo ti = a.tinfo[c / kTileChunks];
+            uint32_t pb[kCand], ws[kCand], nct[kCand];
+            uint64_t cd[kCand];
+#pragma unroll
+            for (int j = 0; j < kCand; ++j) {
+                pb[j] = a.pbits[c * kCand + j];
+                ws[j] = a.wsum[c * kCand + j];
+                nct[j] = a.ncnt[c * kCand + j];
+                cd[j] = a.cand[c * kCand + j];
+            }
+            // the true entry: the first slot whose path bits hold the tile entry's bit
+            int ie = -1;
+            uint32_t we = 0, count = 0;
+            uint64_t x = 0;
+#pragma unroll
+            for (int j = kCand - 1; j >= 0; --j)
+                if (!fb && ti.j >= 0 && (uint32_t)j < cnt && ((pb[j] >> ti.j) & 1u)) {
+                    ie = j;
+                    we = ws[j];
+                    count = nct[j];
+                    x = cd[j];
+                }
+            if (ie >= 0) {
+                const uint64_t e = c * kCand + ie;
+                const uint64_t base = ti.base + ti.we - we;
+                if (count > (uint32_t)kWalkHops) {
+                    if (a.anq[e] != ~0u) {
+                        const int q = atomicAdd(&nqa, 1);
+                        qa_node[q] = (uint32_t)e;
+                        qa_base[q] = base;
+                    } else {
+                        const int q = atomicAdd(&nqb, 1);
+                        qb_node[q] = (uint32_t)e;
+                        qb_base[q] = base;
+                    }
+                } else {
+                    uint64_t k = base;
+                    walk_frames<false>(a, c * kChunk, nullptr, x, -1,
+                                       [&](uint64_t p, uint32_t key, uint8_t b0) { put_frame(a, k++, p, key, b0); });
+                }
+            }
+            a.ccount[c] = 0;
+            *(uint64_t*)(a.ext + c * kCand) = 0;   // kCand == 8 flag bytes, 8-aligned
+        }
+    }
+    if (fb) {   // block-uniform
+        if (blockIdx.x == 0 && tid == 0) serial_walk(a);
+        return;
+    }
+    __syncthreads();
+    // anchored chunks: one wavefront each
+    const int lane = tid & (kWave - 1), wv = tid / kWave;
+    for (int q = wv; q < nqa; q += kScanT / kWave) {
+        const uint64_t node = qa_node[q], chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
+        const uint32_t slot = a.anq[node];
+        const int na = (int)a.anc_n[slot];
+        for (int u = lane; u < na; u += kWave) {
+            uint64_t k = qa_base[q] + (uint64_t)u * kAncStride;
+            uint64_t pos = B + a.anc[(uint64_t)slot * kAncSlot + u];
+            for (int h = 0; h < kAncStride && pos < Bend; ++h) {
+                uint32_t key;
+                uint8_t b0;
+                const uint64_t v = parse_at(a, pos, window_global(a, pos), &key, &b0);
+                if (v & kTerm) break;
+                put_frame(a, k++, pos, key, b0);
+                pos = v;
+            }
+        }
+    }
+    // the rest: the block from LDS
+    for (int q = 0; q < nqb; ++q) {
+        const uint64_t node = qb_node[q], chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
         load_chunk(a, B, words);   // ends with a barrier
         const uint16_t* l16 = chunk_links16(a, B, words, l1, lj, lk16);
         if (tid == 0) {
@@ -743,21 +1156,15 @@ __global__ __launch_bounds__(kScanT) void scan_emit_lds(ScanArgs a) {
         }
         __syncthreads();
         const int na = nanchor;
-        const uint64_t base = a.cbase[chunk];
-        for (int t = tid; t < na; t += kScanT) {
-            uint64_t k = base + (uint64_t)t * kStride;
-            uint64_t pos = B + anchor[t];
+        for (int u = tid; u < na; u += kScanT) {
+            uint64_t k = qb_base[q] + (uint64_t)u * kStride;
+            uint64_t pos = B + anchor[u];
             for (int h = 0; h < kStride && pos < Bend; ++h) {
                 uint32_t key;
                 uint8_t b0;
                 const uint64_t v = parse_at(a, pos, window_at(words, (int)(pos - B)), &key, &b0);
                 if (v & kTerm) break;
-                if (k < a.max_frames) {
-                    a.hdr[k] = pos;
-                    a.keys[k] = key;
-                    a.b0[k] = b0;
-                }
-                ++k;
+                put_frame(a, k++, pos, key, b0);
                 pos = v;
             }
         }
@@ -782,7 +1189,6 @@ struct ScanScratch {
     void* mem = nullptr;
     uint64_t bytes = 0;
     uint64_t cap = 0;      // chunks the layout is sized for
-    uint32_t epoch = 0;
     bool dirty = false;    // a call did not launch all its kernels: clear before the next
     std::vector<void*> retired;   // outgrown allocations (queued work may still use them)
 };
@@ -806,27 +1212,50 @@ std::mutex& stream_scratch_mu() {
     static std::mutex mu;
     return mu;
 }
-}  // namespace
 
-// bytes of scratch for `c` chunks: flags, ccount, mark, cand, link, nterm, ncnt, status, jp, jq,
-// slow2, slow3, cbase, anc (one anchor slot per chunk), anc_n, anq
-static uint64_t scratch_need(uint64_t c) {
-    const uint64_t n = c * kCand;
-    return 64 + c * 4 + n + n * 8 + n * 4 + n * 8 + n * 4 + c * 8 + n * 4 + n * 4 + n * 4 + c * 4 + c * 8 +
-           c * kAncSlot * 2 + c * 4 + n * 4 + 64 * 16;   // + alignment padding of the 16 regions
+// The scratch layout for `cap` chunks (cap a multiple of kTileChunks): offsets of the
+// regions; flags, ccount and ext first -- the region every call leaves zeroed.
+struct Layout {
+    uint64_t flags, ccount, ext, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, text, tcount, tinfo,
+        total;
+};
+Layout layout_for(uint64_t cap) {
+    auto align = [](uint64_t x) { return (x + 63) & ~63ull; };
+    const uint64_t slots = cap * kCand, tiles = cap / kTileChunks;
+    Layout l;
+    uint64_t o = 0;
+    l.flags = o;   o = 64;
+    l.ccount = o;  o = align(o + cap * 4);
+    l.ext = o;     o = align(o + slots);
+    l.cleared = o;
+    l.cand = o;    o = align(o + slots * 8);
+    l.link = o;    o = align(o + slots * 4);
+    l.nterm = o;   o = align(o + slots * 8);
+    l.ncnt = o;    o = align(o + slots * 4);
+    l.wsum = o;    o = align(o + slots * 4);
+    l.pbits = o;   o = align(o + slots * 4);
+    l.anq = o;     o = align(o + slots * 4);
+    l.anc = o;     o = align(o + cap * kAncSlot * 2);
+    l.anc_n = o;   o = align(o + cap * 4);
+    l.text = o;    o = align(o + tiles * kExt * sizeof(TileExt));
+    l.tcount = o;  o = align(o + tiles * 4);
+    l.tinfo = o;   o = align(o + tiles * sizeof(TileInfo));
+    l.total = o;
+    return l;
 }
+}  // namespace
 
 // grow to hold `chunks` (+1 virtual) chunks; outgrown allocations are kept until the
 // scratch is freed (queued work may still use them)
 static hipError_t scratch_grow(ScanScratch& s, uint64_t chunks, hipStream_t stream) {
     if (s.cap >= chunks) return hipSuccess;
-    uint64_t cap = s.cap ? 2 * s.cap : 256;
+    uint64_t cap = s.cap ? 2 * s.cap : kTileChunks;
     while (cap < chunks) cap *= 2;
-    const uint64_t want = scratch_need(cap);
+    const uint64_t want = layout_for(cap).total;
     void* p = nullptr;
     hipError_t e;
     if ((e = hipMalloc(&p, want)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(p, 0, want, stream)) != hipSuccess) {   // zero flags, epoch 0
+    if ((e = hipMemsetAsync(p, 0, want, stream)) != hipSuccess) {   // zero flags, counters, ext flags
         (void)hipFree(p);
         return e;
     }
@@ -834,13 +1263,29 @@ static hipError_t scratch_grow(ScanScratch& s, uint64_t chunks, hipStream_t stre
     s.mem = p;
     s.bytes = want;
     s.cap = cap;
-    s.epoch = 0;
     s.dirty = false;
     return hipSuccess;
 }
 
 hipError_t scan_scratch_reserve(ScanScratch* s, uint64_t len, hipStream_t stream) {
     return scratch_grow(*s, (len + kChunk - 1) / kChunk + 1, stream);
+}
+
+// Why the last scan on (device, stream) took the serial walk (0: it did not); the
+// caller has synchronised the stream.  -1: no scratch for that stream.
+int64_t scan_diag(int device, hipStream_t stream) {
+    ScanScratch* s = nullptr;
+    {
+        std::lock_guard<std::mutex> g(stream_scratch_mu());
+        auto it = stream_scratch().find({device, stream});
+        if (it == stream_scratch().end()) return -1;
+        s = it->second;
+    }
+    uint32_t why = 0;
+    if (!s->mem || hipMemcpy(&why, (uint8_t*)s->mem + 9 * sizeof(uint32_t), sizeof(why), hipMemcpyDeviceToHost) !=
+                       hipSuccess)
+        return -1;
+    return why;
 }
 
 int release_stream_scratch(int device, hipStream_t stream) {
@@ -856,15 +1301,6 @@ int release_stream_scratch(int device, hipStream_t stream) {
     return 1;
 }
 
-
-// workgroups of the LDS kernels K2' / K4b' (each loops over its queue); the queue
-// lengths are only known on the device.  NETC_SCAN_SLOW_BLOCKS overrides (measurement).
-static uint64_t slow_blocks() {
-    const char* e = getenv("NETC_SCAN_SLOW_BLOCKS");
-    const uint64_t v = e ? (uint64_t)strtoull(e, nullptr, 10) : 0;
-    return v ? v : 1024;
-}
-
 hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start, bool strict, uint64_t* hdr,
                               uint32_t* keys, uint8_t* b0, uint64_t max_frames, uint64_t* result,
                               hipStream_t stream, ScanScratch* own) {
@@ -874,18 +1310,16 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.start = start;
     a.strict = strict ? 1 : 0;
     a.nc = (len + kChunk - 1) / kChunk;   // real chunks 0 .. nc-1; chunk nc is virtual (positions >= len)
-    const uint64_t chunks = a.nc + 1, nodes = chunks * kCand;
-    int levels = 1;   // lifting passes: 8^levels - 1 >= chunks steps along the chain
-    while ((1ull << (3 * levels)) < chunks + 1) ++levels;
+    const uint64_t chunks = a.nc + 1, tiles = (chunks + kTileChunks - 1) / kTileChunks;
     a.hdr = hdr;
     a.keys = keys;
     a.b0 = b0;
     a.max_frames = max_frames;
     a.result = result;
     // scratch: sized for `cap` chunks (scratch_grow); the flags, the candidate counters
-    // and the mark bytes must be zero when a call starts: a fresh allocation is cleared
-    // once, and every call leaves them zeroed behind it (K4a and K4b' clear them), so
-    // no clearing launch is needed per call.
+    // and the external flags must be zero when a call starts: a fresh allocation is
+    // cleared once, and every call leaves them zeroed behind it (K3b the flags, K4 the
+    // rest), so no clearing launch is needed per call.
     hipError_t e = hipSuccess;
     ScanScratch* sp = own;
     std::unique_lock<std::mutex> lk;
@@ -897,71 +1331,44 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         if (!slot && !(slot = scan_scratch_new())) return hipErrorOutOfMemory;
         sp = slot;
     }
-    uint8_t* m;
-    int32_t *jp, *jq;   // ping-pong doubling tables
-    uint64_t cleared = 0;
-    bool* dirty_flag = nullptr;
-    {
-        ScanScratch& s = *sp;
-        if ((e = scratch_grow(s, chunks, stream)) != hipSuccess) return e;
-        s.epoch = (s.epoch + 1) & 0xFFFF;
-        m = (uint8_t*)s.mem;
-        auto align = [](uint64_t x) { return (x + 63) & ~63ull; };
-        const uint64_t cap_nodes = s.cap * kCand;
-        uint64_t o = 0;
-        // flags, ccount and mark first, at capacity offsets: the region left zeroed
-        a.flags = (uint32_t*)(m + o); o = 64;
-        a.ccount = (uint32_t*)(m + o); o = align(o + s.cap * 4);
-        a.mark = m + o; o = align(o + cap_nodes);
-        cleared = o;
-        if (s.dirty) {
-            if ((e = hipMemsetAsync(m, 0, cleared, stream)) != hipSuccess) return e;
-            s.dirty = false;
-        }
-        dirty_flag = &s.dirty;
-        a.cand = (uint64_t*)(m + o); o = align(o + cap_nodes * 8);
-        a.link = (int32_t*)(m + o); o = align(o + cap_nodes * 4);
-        a.nterm = (uint64_t*)(m + o); o = align(o + cap_nodes * 8);
-        a.ncnt = (uint32_t*)(m + o); o = align(o + cap_nodes * 4);
-        a.status = (uint64_t*)(m + o); o = align(o + s.cap * 8);
-        jp = (int32_t*)(m + o); o = align(o + cap_nodes * 4);
-        jq = (int32_t*)(m + o); o = align(o + cap_nodes * 4);
-        a.slow2 = (uint32_t*)(m + o); o = align(o + cap_nodes * 4);
-        a.slow3 = (uint32_t*)(m + o); o = align(o + s.cap * 4);
-        a.cbase = (uint64_t*)(m + o); o = align(o + s.cap * 8);
-        a.anc = (uint16_t*)(m + o); o = align(o + s.cap * kAncSlot * 2);
-        a.anc_n = (uint32_t*)(m + o); o = align(o + s.cap * 4);
-        a.anq = (uint32_t*)(m + o);
-        a.anc_cap = s.cap;
-        if (const char* env = getenv("NETC_SCAN_ANCHOR_SLOTS")) {   // tests: fewer slots (0: none)
-            const uint64_t v = (uint64_t)strtoull(env, nullptr, 10);
-            a.anc_cap = v < a.anc_cap ? v : a.anc_cap;
-        }
-        if (o + cap_nodes * 4 > s.bytes) return hipErrorInvalidValue;   // layout and need_for disagree
-        if (s.epoch == 0) {   // epochs wrapped: clear the status words
-            if ((e = hipMemsetAsync(a.status, 0, s.cap * 8, stream)) != hipSuccess) return e;
-            s.epoch = 1;
-        }
-        a.epoch = s.epoch;
+    ScanScratch& s = *sp;
+    if ((e = scratch_grow(s, chunks, stream)) != hipSuccess) return e;
+    const Layout l = layout_for(s.cap);
+    uint8_t* m = (uint8_t*)s.mem;
+    if (s.dirty) {
+        if ((e = hipMemsetAsync(m, 0, l.cleared, stream)) != hipSuccess) return e;
+        s.dirty = false;
     }
-    (void)cleared;
-    const uint64_t slow_cap = slow_blocks();
-    const unsigned slow_grid = (unsigned)(chunks < slow_cap ? chunks : slow_cap);
-    hipLaunchKernelGGL(scan_exits, dim3((unsigned)chunks), dim3(kScanT), 0, stream, a);
-    hipLaunchKernelGGL(scan_links, dim3((unsigned)((nodes + 255) / 256)), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL(scan_links_lds, dim3(slow_grid), dim3(kScanT), 0, stream, a);
-    const unsigned lb = (unsigned)((nodes + 255) / 256);
-    const int32_t* src = a.link;
-    for (int k = 0; k < levels; ++k) {
-        int32_t* dst = k + 1 < levels ? ((k & 1) ? jq : jp) : nullptr;
-        hipLaunchKernelGGL(scan_lift, dim3(lb), dim3(256), 0, stream, src, dst, a.mark, nodes);
-        src = dst;
+    a.flags = (uint32_t*)(m + l.flags);
+    a.ccount = (uint32_t*)(m + l.ccount);
+    a.ext = m + l.ext;
+    a.cand = (uint64_t*)(m + l.cand);
+    a.link = (int32_t*)(m + l.link);
+    a.nterm = (uint64_t*)(m + l.nterm);
+    a.ncnt = (uint32_t*)(m + l.ncnt);
+    a.wsum = (uint32_t*)(m + l.wsum);
+    a.pbits = (uint32_t*)(m + l.pbits);
+    a.anq = (uint32_t*)(m + l.anq);
+    a.anc = (uint16_t*)(m + l.anc);
+    a.anc_n = (uint32_t*)(m + l.anc_n);
+    a.text = (TileExt*)(m + l.text);
+    a.tcount = (uint32_t*)(m + l.tcount);
+    a.tinfo = (TileInfo*)(m + l.tinfo);
+    a.anc_cap = s.cap;
+    if (const char* env = getenv("NETC_SCAN_ANCHOR_SLOTS")) {   // tests: fewer slots (0: none)
+        const uint64_t v = (uint64_t)strtoull(env, nullptr, 10);
+        a.anc_cap = v < a.anc_cap ? v : a.anc_cap;
     }
-    const unsigned cb = (unsigned)((chunks + 255) / 256);
-    hipLaunchKernelGGL(scan_count, dim3(cb), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL(scan_emit_lds, dim3(slow_grid), dim3(kScanT), 0, stream, a);
+    a.pf_base = len >= 16 ? wire : m + l.flags;
+    a.pf_lim = len >= 16 ? len - 16 : 0;
+    const unsigned blk = (unsigned)((chunks + kBlkChunks - 1) / kBlkChunks);
+    hipLaunchKernelGGL(scan_exits, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(scan_links, dim3(blk), dim3(kScanT), 0, stream, a);
+    hipLaunchKernelGGL(scan_tiles, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a);
+    hipLaunchKernelGGL(scan_resolve, dim3(1), dim3(kResolveT), 0, stream, a, tiles);
+    hipLaunchKernelGGL(scan_emit, dim3(blk), dim3(kScanT), 0, stream, a);
     e = hipGetLastError();
-    if (e != hipSuccess) *dirty_flag = true;   // a launch failed: the flags may be left set (lock still held)
+    if (e != hipSuccess) s.dirty = true;   // a launch failed: the flags may be left set (lock still held)
     return e;
 }
 

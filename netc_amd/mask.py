@@ -249,6 +249,14 @@ def scan_frames(wire, hdr, keys, b0, result, start: int = 0, strict: bool = True
                                            result.data_ptr(), _stream_handle(stream)))
 
 
+def scan_diag(stream=None, device: int = 0) -> int:
+    """netc_gpu_scan_diag: why the last scan on `stream` took the serial walk (0: it did not; -1: no scan)."""
+    r = int(_lib.gpu().netc_gpu_scan_diag(device, _stream_handle(stream)))
+    if r < -1:
+        _check(r)
+    return r
+
+
 def unmask_frames(wire, hdr, keys, result, length: Optional[int] = None, stream=None,
                   device: Optional[int] = None) -> None:
     """netc_gpu_unmask_frames: unmask in place the payloads scan_frames found (outputs read on the device)."""

@@ -18,14 +18,15 @@ GUARD = 64
 SENTINEL = 0xA5
 
 
-def _dev(torch, a: np.ndarray, _unused=None):
-    """uint64 offsets / uint32 keys -> device int64 / int32 tensors with the same bits."""
+def _dev(torch, a: np.ndarray, device=None):
+    """uint64 offsets / uint32 keys -> device int64 / int32 tensors with the same bits (on `device`, or cuda:0)."""
     a = np.ascontiguousarray(a)
     if a.dtype == np.uint64:
         a = a.view(np.int64)
     elif a.dtype == np.uint32:
         a = a.view(np.int32)
-    return torch.from_numpy(a).cuda()
+    t = torch.from_numpy(a)
+    return t.to(device) if device is not None else t.cuda()
 
 
 def run_case(torch, payload: np.ndarray, off: np.ndarray, keys: np.ndarray, dst_shift=0, src_shift=0, inplace=False):
@@ -284,6 +285,35 @@ def test_multi_shard_entry(torch_cuda):
         expect.append(orc.mask_batch(payload, off, keys))
     nm.mask_batch_multi(shards, synchronize=True)
     for (dst, _, _, _), e in zip(shards, expect):
+        assert np.array_equal(dst.cpu().numpy(), e)
+
+
+def test_multi_shard_distinct_devices(torch_cuda):
+    # BASELINE config 4's single-process form: a byte-balanced batch cut into shards
+    # (netc_shard_frames, offsets rebased per shard), one shard per device, launched
+    # on all devices before any is waited on; every shard == the oracle
+    torch = torch_cuda
+    ndev = torch.cuda.device_count()
+    if ndev < 2:
+        pytest.skip("one device: the distinct-device path needs a multi-GPU box")
+    off = synth.mixed_offsets(8 << 20, 256, 65536, seed=77)
+    keys = synth.random_keys(off.size - 1, 77)
+    payload = synth.host_payload(int(off[-1]), 77)
+    cuts = nm.shard_frames(off, ndev)
+    shards, expect, devs = [], [], []
+    for d in range(ndev):
+        f0, f1 = int(cuts[d]), int(cuts[d + 1])
+        lo, hi = int(off[f0]), int(off[f1])
+        o = (off[f0:f1 + 1] - np.uint64(lo)).astype(np.uint64)
+        k = keys[f0:f1]
+        dev = torch.device("cuda", d)
+        src = torch.from_numpy(payload[lo:hi].copy()).to(dev)
+        shards.append((torch.empty_like(src), src, _dev(torch, o, dev), _dev(torch, k, dev)))
+        expect.append(orc.mask_batch(payload[lo:hi], o, k))
+        devs.append(d)
+    nm.mask_batch_multi(shards, synchronize=True)
+    for (dst, _, _, _), e, d in zip(shards, expect, devs):
+        assert dst.device.index == d
         assert np.array_equal(dst.cpu().numpy(), e)
 
 

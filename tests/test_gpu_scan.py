@@ -22,7 +22,9 @@ def frames_from_sizes(sizes, start=0):
     return off
 
 
-def run_scan(torch, wire: np.ndarray, start=0, strict=True, max_frames=None):
+def run_scan(torch, wire: np.ndarray, start=0, strict=True, max_frames=None, parallel=False):
+    """parallel: also require that the scan did not fall back to the serial walk
+    (netc_gpu_scan_diag == 0) -- results are identical either way, so only this sees it."""
     exp_hdr, exp_keys, exp_b0, exp_consumed, exp_err = orc.scan_frames(wire, start=start, strict=strict)
     n = exp_hdr.size
     cap = n if max_frames is None else max_frames
@@ -45,6 +47,9 @@ def run_scan(torch, wire: np.ndarray, start=0, strict=True, max_frames=None):
     assert np.array_equal(b0.cpu().numpy()[:k], exp_b0[:k])
     if n <= cap:
         assert int(got_hdr[n]) == exp_consumed
+    if parallel:
+        why = nm.scan_diag()
+        assert why == 0, f"serial fallback, reason {why:#x}"
     return n
 
 
@@ -62,26 +67,26 @@ def test_mixed_sizes(torch_cuda, seed):
     sizes = np.concatenate([rng.integers(0, 5000, 300), rng.integers(0, 130, 300), [65535, 65536, 200000]])
     rng.shuffle(sizes)
     wire, _ = _stream(rng, sizes)
-    assert run_scan(torch_cuda, wire) == sizes.size
+    assert run_scan(torch_cuda, wire, parallel=True) == sizes.size
 
 
 def test_c2_shape(torch_cuda):
     rng = np.random.default_rng(2)
     wire, _ = _stream(rng, np.full(65536, 1024))
-    assert run_scan(torch_cuda, wire) == 65536
+    assert run_scan(torch_cuda, wire, parallel=True) == 65536
 
 
 def test_c4_shape_64mib(torch_cuda):
     rng = np.random.default_rng(4)
     wire, _ = _stream(rng, rng.integers(256, 65537, 2000))
-    assert run_scan(torch_cuda, wire) == 2000
+    assert run_scan(torch_cuda, wire, parallel=True) == 2000
 
 
 def test_tiny_frames(torch_cuda):
     # 6-byte wire frames (empty masked payloads) and 1-3 byte payloads: long chains inside a chunk
     rng = np.random.default_rng(5)
     wire, _ = _stream(rng, rng.integers(0, 4, 20000))
-    assert run_scan(torch_cuda, wire) == 20000
+    assert run_scan(torch_cuda, wire, parallel=True) == 20000
 
 
 def test_truncated_streams(torch_cuda):
@@ -89,14 +94,14 @@ def test_truncated_streams(torch_cuda):
     wire, wo = _stream(rng, rng.integers(0, 9000, 200))
     for cut in [0, 1, 2, 5, int(wo[50]) - 1, int(wo[50]), int(wo[50]) + 1, int(wo[50]) + 3, int(wo[120]) + 7,
                 wire.size - 1, wire.size]:
-        run_scan(torch_cuda, wire[:cut])
+        run_scan(torch_cuda, wire[:cut], parallel=True)
 
 
 def test_start_offset(torch_cuda):
     rng = np.random.default_rng(7)
     wire, wo = _stream(rng, rng.integers(0, 9000, 200))
     for s in (int(wo[1]), int(wo[77]), int(wo[199]), wire.size):
-        run_scan(torch_cuda, wire, start=s)
+        run_scan(torch_cuda, wire, start=s, parallel=True)
 
 
 def test_unmasked_and_non_strict(torch_cuda):
@@ -132,14 +137,14 @@ def test_header_byte_variants(torch_cuda):
     sizes = rng.integers(0, 125, 500)
     b0 = rng.choice(np.array([0x81, 0x82, 0x01, 0x00, 0x80, 0x89, 0x8A, 0x88], dtype=np.uint8), 500)
     wire, _ = _stream(rng, sizes, b0=b0)
-    assert run_scan(torch_cuda, wire) == 500
+    assert run_scan(torch_cuda, wire, parallel=True) == 500
 
 
 def test_max_frames_cap(torch_cuda):
     rng = np.random.default_rng(11)
     wire, _ = _stream(rng, rng.integers(0, 2000, 400))
-    run_scan(torch_cuda, wire, max_frames=100)
-    run_scan(torch_cuda, wire, max_frames=0)
+    run_scan(torch_cuda, wire, max_frames=100, parallel=True)
+    run_scan(torch_cuda, wire, max_frames=0, parallel=True)
 
 
 def test_scratch_left_clean_between_calls(torch_cuda):
@@ -237,9 +242,9 @@ def test_dense_chunks_parallel_walks(torch_cuda, monkeypatch, masked, strict, sl
     sizes = np.concatenate([np.full(3000, 16), np.full(2500, 8), np.zeros(3000, dtype=np.int64),
                             rng.integers(0, 20, 3000), [70000], np.full(1000, 1)])
     wire, wo = _stream(rng, sizes, masked=masked)
-    assert run_scan(torch_cuda, wire, strict=strict) == sizes.size
+    assert run_scan(torch_cuda, wire, strict=strict, parallel=strict) == sizes.size
     for cut in (int(wo[3100]) + 1, int(wo[6000]), int(wo[9001]) + 3):
-        run_scan(torch_cuda, wire[:cut], strict=strict)
+        run_scan(torch_cuda, wire[:cut], strict=strict, parallel=strict)
     for s in (int(wo[17]), int(wo[5600])):
-        run_scan(torch_cuda, wire, start=s, strict=strict)
+        run_scan(torch_cuda, wire, start=s, strict=strict, parallel=strict)
     run_scan(torch_cuda, wire, strict=strict, max_frames=4123)

@@ -87,6 +87,7 @@ def main():
         print(json.dumps({"workload": wl, "frames": int(n), "wire_bytes": int(wire.size), "us_per_scan": round(us, 2),
                           "wire_GBps": round(wire.size / (us * 1e-6) / 1e9, 1),
                           "frames_per_s": round(n / (us * 1e-6), 1), "matches_oracle": bool(ok),
+                          "serial_fallback": hex(nm.scan_diag(s)),
                           "cpu_serial_us": round(cpu_s * 1e6, 1),
                           "cpu_serial_frames_per_s": round(n / cpu_s, 1)}), flush=True)
         del w
