@@ -88,7 +88,7 @@ struct TileExt {
     uint32_t slot;   // its global node slot
     uint32_t w;      // frames from it to the tile's exit
     int32_t xl;      // the node its path exits to (another tile), or -1: the chain ends in the tile
-    uint32_t pad;
+    uint32_t root;   // it is the stream start
     uint64_t term;   // K2's terminal of the path's last node in the tile
 };
 // K3b -> K4: a tile's true entry
@@ -106,7 +106,9 @@ struct ScanArgs {
     uint64_t start;        // offset of the first header
     uint64_t nc;           // chunks (the last one, index nc, is virtual: positions >= len)
     int strict;
-    uint32_t* flags;       // [0] overflow bits, [1] root slot + 1, [8] K3b -> K4: serial fallback, [9] why
+    uint32_t* flags;       // [8] K3b -> K4: serial fallback (big streams), [9] why the last call walked serially
+    uint32_t* ovf;         // this call's overflow bits (flags[0] / flags[2] on alternate calls: the
+    uint32_t* ovf_prev;    // ... reader is every K4 block, so K4 zeroes the previous call's word instead)
     uint32_t* ccount;      // nc + 1 candidate counters (zero when a call starts; K4 re-zeroes)
     uint8_t* ext;          // (nc + 1) * kCand: slot entered from another tile (or the root); K4 re-zeroes
     uint64_t* cand;        // (nc + 1) * kCand candidate positions
@@ -319,7 +321,7 @@ __device__ __forceinline__ void append_cand(const ScanArgs& a, uint64_t x, bool 
         a.cand[t * kCand + slot] = x;
         if (ext) a.ext[t * kCand + slot] = 1;
     } else {
-        atomicOr(&a.flags[0], kOvfBucket);
+        atomicOr(a.ovf, kOvfBucket);
     }
 }
 
@@ -440,8 +442,9 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
                 ok &= ((m4 * 0x00204081u) & 0x01010101u) << 7;
             }
             // a 7-bit length cannot leave the chunk unless the position is near its end
-            const uint32_t ext_len = (y & 0x7E7E7E7Eu) + 0x02020202u;   // bit 7: byte 1 & 0x7F >= 126
-            ci |= (ok & ((i == 3 && lane >= kNearLane) ? kH : ext_len) & kH) >> (7 - k);
+            // (a per-byte threshold test for those lanes cost more VALU than it saved)
+            const uint32_t sel = ((i == 3 && lane >= kNearLane) ? kH : ((y & 0x7E7E7E7Eu) + 0x02020202u));
+            ci |= (ok & sel & kH) >> (7 - k);
         }
         half[i >> 1] |= ci << (4 * (i & 1));
     }
@@ -456,7 +459,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     }
     const uint32_t total = (uint32_t)__shfl((int)incl, kWave - 1, kWave);
     if (total > (uint32_t)kQCap) {   // wave-uniform (adversarial payloads, non-strict mode)
-        if (lane == 0) atomicOr(&a.flags[0], kOvfQueue);
+        if (lane == 0) atomicOr(a.ovf, kOvfQueue);
         return;
     }
     uint32_t at = incl - mine;
@@ -479,13 +482,12 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         if (!(v & kTerm) && v >= Bend && set_insert(set[wv], v, &ovf) && !quick_reject(a, v))
             append_cand(a, v, v / kChunk / kTileChunks != c / kTileChunks);
     }
-    if (ovf) atomicOr(&a.flags[0], kOvfSet);
+    if (ovf) atomicOr(a.ovf, kOvfSet);
 }
 
 // node -> the candidate its chain exits to (the first slot holding that position, or
 // -1) and the terminal where it ends
 __device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint64_t x, uint64_t v, uint32_t cnt) {
-    if (x == a.start) a.flags[1] = (uint32_t)node + 1;
     int32_t next = -1;
     if (term_type(v) == kExit) {
         const uint64_t y = term_pos(v), t = y / kChunk;
@@ -498,7 +500,7 @@ __device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint
         for (int j = kCand - 1; j >= 0; --j)
             if ((uint32_t)j < n && ts[j] == y) next = (int32_t)(t * kCand + j);   // the first match
         // not a candidate: pruned by K1 (the chain dies at y), or its bucket overflowed
-        if (next < 0 && !quick_reject(a, y)) atomicOr(&a.flags[0], kOvfLink);
+        if (next < 0 && !quick_reject(a, y)) atomicOr(a.ovf, kOvfLink);
     }
     a.link[node] = next;
     a.nterm[node] = v;
@@ -690,10 +692,11 @@ __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
     __shared__ uint32_t W[kTileSlots];     // frames from the node to L's exit
     __shared__ uint32_t bits[kTileSlots];
     __shared__ uint16_t elist[kExt];
+    __shared__ uint8_t eroot[kExt];
     __shared__ int skip;
     const int t = threadIdx.x;
     // overflow: K4 walks serially.  Read once for the block (another tile may set it meanwhile)
-    if (t == 0) skip = __hip_atomic_load(&a.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (t == 0) skip = __hip_atomic_load(a.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
     __syncthreads();
     if (skip) return;
     const uint64_t tile = blockIdx.x, c = tile * kTileChunks + t, s0 = tile * kTileSlots;
@@ -703,10 +706,12 @@ __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
     const uint64_t exf = live ? *(const uint64_t*)(a.ext + c * kCand) : 0;   // kCand == 8 flag bytes
     int32_t lks[kCand];
     uint32_t nws[kCand];
+    uint32_t rootm = 0;   // the slot holding the stream start
 #pragma unroll
     for (int j = 0; j < kCand; ++j) {
         lks[j] = live ? a.link[c * kCand + j] : kDupLink;
         nws[j] = live ? a.ncnt[c * kCand + j] : 0;
+        rootm |= (live && a.cand[c * kCand + j] == a.start ? 1u : 0u) << j;
     }
     uint32_t extm = 0;
 #pragma unroll
@@ -716,7 +721,7 @@ __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
     const uint32_t base = (uint32_t)block_scan<kScanT>(cnt, &V64);
     uint32_t eidx = (uint32_t)block_scan<kScanT>((uint64_t)__popc(extm), &E64);
     if (E64 > (uint64_t)kExt) {   // block-uniform
-        if (t == 0) atomicOr(&a.flags[0], kOvfExt);
+        if (t == 0) atomicOr(a.ovf, kOvfExt);
         return;
     }
     const int V = (int)V64, E = (int)E64;
@@ -736,6 +741,7 @@ __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
         if ((extm >> i) & 1) {
             bits[k] = 1u << eidx;
             elist[eidx] = (uint16_t)k;
+            eroot[eidx] = (rootm >> i) & 1;
             ++eidx;
         } else {
             bits[k] = 0;
@@ -787,172 +793,169 @@ __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
         e.slot = (uint32_t)(s0 + gsl[k]);
         e.w = W[k];
         e.xl = a.link[last];
-        e.pad = 0;
+        e.root = eroot[t];
         e.term = a.nterm[last];
         a.text[tile * kExt + t] = e;
     }
     if (t == 0) a.tcount[tile] = (uint32_t)E;
 }
 
-// K3b: one block.  The external nodes of all tiles into LDS (tile by tile, in bit
-// order); each one's successor is the external node its path exits to; Wyllie
+// Tile resolution (K3b): the external nodes of all tiles into LDS (tile by tile, in
+// bit order); each one's successor is the external node its path exits to; Wyllie
 // pointer jumping gives R = frames from the node to the end of its chain and marks
 // the nodes reachable from the root.  A marked node is its tile's true entry: frames
 // before it = R(root) - R(node).  The one whose path ends inside its tile holds the
-// terminal: the results.  Beyond the capacities (kMaxTiles, kExtCap) -> serial walk.
-// The tile counts and each tile's first two records are read in one trip (a tile
-// rarely has more: the true entry, now and then a garbage one); the rest in a second.
+// terminal: the results.  Beyond the capacities (MAXT tiles, CAP nodes) -> serial
+// walk.  The tile counts and each tile's first two records are read in one trip (a
+// tile rarely has more: the true entry, now and then a garbage one); the rest in a
+// second.  (Tried: every K4 workgroup resolving the tiles itself in its prologue, no
+// launch of its own: C2 51 -> 60 us -- the chain of trips, scans and rounds is paid
+// per workgroup round, and K4 has several.)
 static constexpr int kExtFirst = 2;
 
-__device__ __forceinline__ void put_ext(uint32_t* eslot, uint32_t* ew, int32_t* exl, uint64_t* R, uint32_t idx,
-                                        const TileExt& e) {
+template <int MAXT, int CAP>
+struct ResolveLds {
+    uint32_t toff[MAXT + 1];
+    uint32_t eslot[CAP];
+    uint32_t ew[CAP];
+    int32_t exl[CAP];
+    uint64_t R[CAP];
+    uint16_t succ[CAP];
+    uint8_t mark[CAP];
+    uint8_t islast[CAP];   // its path ends in its tile (no successor)
+    int bad, root_idx;
+    uint32_t M, why;
+};
+
+__device__ __forceinline__ void put_ext(uint32_t* eslot, uint32_t* ew, int32_t* exl, uint64_t* R, uint8_t* mark,
+                                        uint32_t idx, const TileExt& e) {
     eslot[idx] = e.slot;
     ew[idx] = e.w;
     exl[idx] = e.xl;
     R[idx] = e.w;
+    mark[idx] = e.root != 0;
 }
 
-__global__ __launch_bounds__(kResolveT) void scan_resolve(ScanArgs a, uint64_t tiles) {
-    __shared__ uint32_t toff[kMaxTiles + 1];
-    __shared__ uint32_t eslot[kExtCap];
-    __shared__ uint32_t ew[kExtCap];
-    __shared__ int32_t exl[kExtCap];
-    __shared__ uint16_t succ[kExtCap];
-    __shared__ uint64_t R[kExtCap];
-    __shared__ uint8_t mark[kExtCap];
-    __shared__ int bad, root_idx;
-    __shared__ uint32_t root_slot, M;
+// every thread of the block; on return (after a barrier) sm.bad / sm.why say whether the
+// parallel path holds, and R / mark / islast / toff answer per-tile queries
+template <int NT, int MAXT, int CAP>
+__device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT, CAP>& sm) {
     const int t = threadIdx.x;
-    uint32_t ovf = 0, rs = 0;
-    if (t == 0) {
-        ovf = __hip_atomic_load(&a.flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        rs = __hip_atomic_load(&a.flags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (tiles > (uint64_t)kMaxTiles) {   // kernel-uniform
+    if (tiles > (uint64_t)MAXT) {   // kernel-uniform
         if (t == 0) {
-            a.flags[8] = 1u;
-            a.flags[9] = kWhyTiles | ovf;
-            a.flags[0] = 0;
-            a.flags[1] = 0;
+            sm.bad = 1;
+            sm.why = kWhyTiles;
         }
+        __syncthreads();
         return;
     }
-    constexpr int kTR = kMaxTiles / kResolveT;
-    // trip 1: every tile's count, and the first records of the first kResolveT tiles
-    // (1 GiB of stream; issued together, used after the scan)
+    constexpr int kTR = (MAXT + NT - 1) / NT;
+    // trip 1: every tile's count, and the first records of the first NT tiles
+    // (issued together, used after the scan)
     uint32_t tc[kTR];
     TileExt e0, e1;
 #pragma unroll
     for (int r = 0; r < kTR; ++r) {
-        const uint64_t tl = (uint64_t)t + (uint64_t)kResolveT * r;
+        const uint64_t tl = (uint64_t)t + (uint64_t)NT * r;
         tc[r] = tl < tiles ? a.tcount[tl] : 0;
     }
     if ((uint64_t)t < tiles) {
         e0 = a.text[(uint64_t)t * kExt];
         e1 = a.text[(uint64_t)t * kExt + 1];
     }
-    __shared__ uint32_t why;
-    if (t == 0) {
-        bad = ovf != 0 || rs == 0;
-        why = ovf | (rs == 0 ? kWhyRoot : 0u);
-        root_slot = rs - 1;
-        root_idx = -1;
+    if (t == 0) {   // the overflow word in the same trip
+        const uint32_t ovf = __hip_atomic_load(a.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sm.bad = ovf != 0;
+        sm.why = ovf;
+        sm.root_idx = -1;
     }
     uint64_t run = 0;
 #pragma unroll
     for (int r = 0; r < kTR; ++r) {
-        if ((uint64_t)kResolveT * r >= tiles) break;   // block-uniform
-        const uint64_t tl = (uint64_t)t + (uint64_t)kResolveT * r;
+        if ((uint64_t)NT * r >= tiles) break;   // block-uniform
+        const uint64_t tl = (uint64_t)t + (uint64_t)NT * r;
         uint64_t tot;
-        const uint64_t ex = block_scan<kResolveT>(tc[r], &tot);
-        if (tl < tiles) toff[tl] = (uint32_t)(run + ex);
+        const uint64_t ex = block_scan<NT>(tc[r], &tot);
+        if (tl < tiles) sm.toff[tl] = (uint32_t)(run + ex);
         run += tot;
     }
     if (t == 0) {
-        toff[tiles] = (uint32_t)run;
-        M = (uint32_t)run;
-        if (run > (uint64_t)kExtCap) {
-            bad = 1;
-            why |= kWhyExtCap;
+        sm.toff[tiles] = (uint32_t)run;
+        sm.M = (uint32_t)run;
+        if (run > (uint64_t)CAP) {
+            sm.bad = 1;
+            sm.why |= kWhyExtCap;
         }
     }
     __syncthreads();
-    if (bad) {   // block-uniform
-        if (t == 0) {
-            a.flags[8] = 1u;
-            a.flags[9] = why;
-            a.flags[0] = 0;
-            a.flags[1] = 0;
-        }
-        return;
-    }
+    if (sm.bad) return;
     int more = 0;
 #pragma unroll
     for (int r = 0; r < kTR; ++r) {
-        const uint64_t tl = (uint64_t)t + (uint64_t)kResolveT * r;
+        const uint64_t tl = (uint64_t)t + (uint64_t)NT * r;
         if (tl >= tiles) break;
-        const uint32_t o = toff[tl];
+        const uint32_t o = sm.toff[tl];
         if (r == 0) {
-            if (tc[r] > 0) put_ext(eslot, ew, exl, R, o, e0);
-            if (tc[r] > 1) put_ext(eslot, ew, exl, R, o + 1, e1);
+            if (tc[r] > 0) put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, o, e0);
+            if (tc[r] > 1) put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, o + 1, e1);
         } else {
             for (uint32_t j = 0; j < tc[r] && j < (uint32_t)kExtFirst; ++j)
-                put_ext(eslot, ew, exl, R, o + j, a.text[tl * kExt + j]);
+                put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, o + j, a.text[tl * kExt + j]);
         }
         more |= tc[r] > (uint32_t)kExtFirst;
     }
     if (__syncthreads_or(more)) {   // trip 2 (rare): tiles with more than two external nodes
 #pragma unroll
         for (int r = 0; r < kTR; ++r) {
-            const uint64_t tl = (uint64_t)t + (uint64_t)kResolveT * r;
+            const uint64_t tl = (uint64_t)t + (uint64_t)NT * r;
             if (tl >= tiles) break;
-            for (uint32_t j = kExtFirst; j < tc[r]; ++j) put_ext(eslot, ew, exl, R, toff[tl] + j, a.text[tl * kExt + j]);
+            for (uint32_t j = kExtFirst; j < tc[r]; ++j)
+                put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, sm.toff[tl] + j, a.text[tl * kExt + j]);
         }
         __syncthreads();
     }
-    const int m = (int)M;
+    const int m = (int)sm.M;
     // successors: the external node (of a later tile) each path exits to, found in LDS
-    for (int i = t; i < m; i += kResolveT) {
-        const int32_t xl = exl[i];
+    for (int i = t; i < m; i += NT) {
+        const int32_t xl = sm.exl[i];
         uint16_t sx = kNone;
         if (xl >= 0) {
             const uint64_t t2 = (uint64_t)xl / kTileSlots;
-            for (uint32_t u = toff[t2]; u < toff[t2 + 1]; ++u)
-                if (eslot[u] == (uint32_t)xl) sx = (uint16_t)u;
+            for (uint32_t u = sm.toff[t2]; u < sm.toff[t2 + 1]; ++u)
+                if (sm.eslot[u] == (uint32_t)xl) sx = (uint16_t)u;
             if (sx == kNone) {   // an exit onto a node no tile listed (defence in depth)
-                bad = 1;
-                why = kWhySucc;
+                sm.bad = 1;
+                sm.why = kWhySucc;
             }
         }
-        succ[i] = sx;
-        mark[i] = eslot[i] == root_slot;
-        if (eslot[i] == root_slot) root_idx = i;
+        sm.succ[i] = sx;
+        sm.islast[i] = xl < 0;
+        if (sm.mark[i]) sm.root_idx = i;
     }
     __syncthreads();
-    if (bad || root_idx < 0) {   // block-uniform
-        if (t == 0) {
-            a.flags[8] = 1u;
-            a.flags[9] = bad ? why : kWhyRoot;
-            a.flags[0] = 0;
-            a.flags[1] = 0;
+    if (sm.bad || sm.root_idx < 0) {   // block-uniform
+        if (t == 0 && !sm.bad) {
+            sm.bad = 1;
+            sm.why = kWhyRoot;
         }
+        __syncthreads();
         return;
     }
-    constexpr int kR = kExtCap / kResolveT;
+    constexpr int kR = (CAP + NT - 1) / NT;
     for (;;) {
         uint16_t ns[kR];
         uint64_t nr[kR];
         int any = 0;
 #pragma unroll
         for (int r = 0; r < kR; ++r) {
-            const int i = t + kResolveT * r;
+            const int i = t + NT * r;
             ns[r] = kNone;
             if (i < m) {
-                const uint16_t sx = succ[i];
+                const uint16_t sx = sm.succ[i];
                 if (sx != kNone) {
-                    ns[r] = succ[sx];
-                    nr[r] = R[i] + R[sx];
-                    if (mark[i]) mark[sx] = 1;
+                    ns[r] = sm.succ[sx];
+                    nr[r] = sm.R[i] + sm.R[sx];
+                    if (sm.mark[i]) sm.mark[sx] = 1;
                     any |= ns[r] != kNone;
                 }
             }
@@ -960,47 +963,53 @@ __global__ __launch_bounds__(kResolveT) void scan_resolve(ScanArgs a, uint64_t t
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < kR; ++r) {
-            const int i = t + kResolveT * r;
-            if (i < m && succ[i] != kNone) {
-                succ[i] = ns[r];
-                R[i] = nr[r];
+            const int i = t + NT * r;
+            if (i < m && sm.succ[i] != kNone) {
+                sm.succ[i] = ns[r];
+                sm.R[i] = nr[r];
             }
         }
         if (!__syncthreads_or(any)) break;
     }
-    // per tile: its marked external node (at most one: the chain enters a tile once)
-    const uint64_t total = R[root_idx];
-#pragma unroll
-    for (int r = 0; r < kTR; ++r) {
-        const uint64_t tl = (uint64_t)t + (uint64_t)kResolveT * r;
-        if (tl >= tiles) break;
-        TileInfo ti;
-        ti.j = -1;
-        ti.we = 0;
-        ti.base = 0;
-        for (uint32_t i = toff[tl]; i < toff[tl + 1]; ++i)
-            if (mark[i]) {
-                ti.j = (int32_t)(i - toff[tl]);
-                ti.we = ew[i];
-                ti.base = total - R[i];
-                if (exl[i] < 0) {   // the chain ends in this tile
-                    const uint64_t term_v = a.text[tl * kExt + ti.j].term;
-                    const uint64_t ty = term_type(term_v), pos = term_pos(term_v);
-                    // an exit onto a position K1 pruned: the chain dies there
-                    const bool dead = ty == kDead || ty == kExit;
-                    a.result[0] = total;
-                    a.result[1] = pos;
-                    a.result[2] = dead ? pos : ~0ull;
-                    if (total <= a.max_frames) a.hdr[total] = pos;
-                }
+}
+
+// tile tl's true entry (at most one marked node: the chain enters a tile once); if the
+// chain ends in it and `results`, the scan's results too
+template <int MAXT, int CAP>
+__device__ TileInfo tile_info(const ScanArgs& a, const ResolveLds<MAXT, CAP>& sm, uint64_t tl, bool results) {
+    TileInfo ti;
+    ti.j = -1;
+    ti.we = 0;
+    ti.base = 0;
+    const uint64_t total = sm.R[sm.root_idx];
+    for (uint32_t i = sm.toff[tl]; i < sm.toff[tl + 1]; ++i)
+        if (sm.mark[i]) {
+            ti.j = (int32_t)(i - sm.toff[tl]);
+            ti.we = sm.ew[i];
+            ti.base = total - sm.R[i];
+            if (results && sm.islast[i]) {   // the chain ends in this tile
+                const uint64_t term_v = a.text[tl * kExt + ti.j].term;
+                const uint64_t ty = term_type(term_v), pos = term_pos(term_v);
+                // an exit onto a position K1 pruned: the chain dies there
+                const bool dead = ty == kDead || ty == kExit;
+                a.result[0] = total;
+                a.result[1] = pos;
+                a.result[2] = dead ? pos : ~0ull;
+                if (total <= a.max_frames) a.hdr[total] = pos;
             }
-        a.tinfo[tl] = ti;
-    }
-    if (t == 0) {
-        a.flags[8] = 0;
-        a.flags[9] = 0;
-        a.flags[0] = 0;
-        a.flags[1] = 0;
+        }
+    return ti;
+}
+
+// K3b for streams of more than kK4Tiles tiles: one block resolves every tile
+__global__ __launch_bounds__(kResolveT) void scan_resolve(ScanArgs a, uint64_t tiles) {
+    __shared__ ResolveLds<kMaxTiles, kExtCap> sm;
+    resolve_tiles<kResolveT>(a, tiles, sm);
+    if (!sm.bad)
+        for (uint64_t tl = threadIdx.x; tl < tiles; tl += kResolveT) a.tinfo[tl] = tile_info(a, sm, tl, true);
+    if (threadIdx.x == 0) {
+        a.flags[8] = sm.bad ? 1u : 0u;
+        a.flags[9] = sm.bad ? sm.why : 0u;
     }
 }
 
@@ -1046,7 +1055,7 @@ __device__ __forceinline__ void put_frame(const ScanArgs& a, uint64_t k, uint64_
 // an anchor every 16 frames, thread u the 16 frames from anchor u).  Every chunk's
 // candidate counter and external flags are zeroed here, after their last reader:
 // the next call needs no clearing launch.
-__global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a) {
+__global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) {
     __shared__ uint32_t words[kWords];
     __shared__ uint16_t l1[kChunk];    // next header (local index) or kNoLink
     __shared__ uint16_t lj[kChunk];    // 2^k hops (ping)
@@ -1055,19 +1064,26 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a) {
     __shared__ int nanchor, nqa, nqb;
     __shared__ uint32_t qa_node[kBlkChunks], qb_node[kBlkChunks];
     __shared__ uint64_t qa_base[kBlkChunks], qb_base[kBlkChunks];
+    __shared__ TileInfo bti;
+    __shared__ int fbs;
+    (void)tiles;
     const int tid = threadIdx.x;
+    const uint64_t tile = (uint64_t)blockIdx.x * kBlkChunks / kTileChunks;   // kBlkChunks divides kTileChunks
     if (tid == 0) {
+        fbs = __hip_atomic_load(&a.flags[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        bti = a.tinfo[tile];
+        if (blockIdx.x == 0) *a.ovf_prev = 0;   // the previous call's overflow word, for the next call
         nqa = 0;
         nqb = 0;
     }
-    const bool fb = __hip_atomic_load(&a.flags[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
     __syncthreads();
+    const bool fb = fbs != 0;
     if (tid < kBlkChunks) {
         const uint64_t c = (uint64_t)blockIdx.x * kBlkChunks + tid;
         if (c <= a.nc) {
             // the chunk's counter, path bits, W, counts and positions, and its tile's entry, in one trip
             const uint32_t cnt = min(a.ccount[c], (uint32_t)kCand);
-            const TileInfo ti = a.tinfo[c / kTileChunks];
+            const TileInfo ti = bti;
             uint32_t pb[kCand], ws[kCand], nct[kCand];
             uint64_t cd[kCand];
 #pragma unroll
@@ -1190,6 +1206,7 @@ struct ScanScratch {
     uint64_t bytes = 0;
     uint64_t cap = 0;      // chunks the layout is sized for
     bool dirty = false;    // a call did not launch all its kernels: clear before the next
+    uint64_t calls = 0;    // the overflow word alternates per call
     std::vector<void*> retired;   // outgrown allocations (queued work may still use them)
 };
 
@@ -1340,6 +1357,9 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         s.dirty = false;
     }
     a.flags = (uint32_t*)(m + l.flags);
+    a.ovf = a.flags + ((s.calls & 1) ? 2 : 0);
+    a.ovf_prev = a.flags + ((s.calls & 1) ? 0 : 2);
+    ++s.calls;
     a.ccount = (uint32_t*)(m + l.ccount);
     a.ext = m + l.ext;
     a.cand = (uint64_t*)(m + l.cand);
@@ -1366,7 +1386,7 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     hipLaunchKernelGGL(scan_links, dim3(blk), dim3(kScanT), 0, stream, a);
     hipLaunchKernelGGL(scan_tiles, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a);
     hipLaunchKernelGGL(scan_resolve, dim3(1), dim3(kResolveT), 0, stream, a, tiles);
-    hipLaunchKernelGGL(scan_emit, dim3(blk), dim3(kScanT), 0, stream, a);
+    hipLaunchKernelGGL(scan_emit, dim3(blk), dim3(kScanT), 0, stream, a, tiles);
     e = hipGetLastError();
     if (e != hipSuccess) s.dirty = true;   // a launch failed: the flags may be left set (lock still held)
     return e;
