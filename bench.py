@@ -17,7 +17,8 @@ time (the max is the job's; each rank's own rate is reported as per_gpu).
 
 Prints ONE JSON line on rank 0.  Roofline: 2 x payload bytes per launch (read +
 write) / mean kernel duration (HIP events on the launch stream) vs 8.0 TB/s, next
-to in-bench frame-free stream ceilings (hand-written kernels, same rotation).
+to in-bench frame-free stream ceilings (hand-written kernels, same rotation) and the
+same kernel out of place and with src misaligned against dst (roofline.shapes).
 After the timed region: the timed entry is checked (involution + every frame's
 keystream), BASELINE config 5's host-to-host rate is measured (rank 0, N = 1), and
 cpu_baseline times the oracle's restatement of the reference loop on this host,
@@ -148,13 +149,49 @@ def stream_ceilings(torch, batches, total, stream, steps):
     return out
 
 
+def shape_points(torch, entry, local, batches, total, nframes, stream, steps):
+    """The same kernel on the same rotation, other buffer shapes (secondary figures, never
+    `value`): out of place (dst a batch no recent step wrote, 16-B aligned like src) and
+    out of place with src = dst + 3 (every 16-B load unaligned; frames clipped to the
+    3 bytes shorter buffer).  (read + write bytes) / HIP-event time per launch, GB/s."""
+    nb = len(batches)
+    out = {}
+    for name, shift in (("out_of_place_GBps", 0), ("src_misaligned_3_GBps", 3)):
+        n_bytes = total - shift
+        offs = [torch.clamp(o, max=n_bytes) for _, o, _ in batches[:1]][0] if shift else batches[0][1]
+
+        def launch(i):
+            src = batches[i % nb][0]
+            dst = batches[(i + nb // 2) % nb][0]
+            _, o, k = batches[i % nb]
+            rc = entry(local, dst.data_ptr(), src.data_ptr() + shift, n_bytes, (offs if shift else o).data_ptr(),
+                       k.data_ptr(), nframes, stream.cuda_stream)
+            if rc != 0:
+                raise RuntimeError(f"netc_gpu_mask_batch failed ({rc})")
+        for i in range(4):
+            launch(i)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for i in range(steps):
+            launch(4 + i)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        out[name] = round(2.0 * n_bytes / (e0.elapsed_time(e1) / steps * 1e-3) / 1e9, 1)
+    return out
+
+
 def verify_step(torch, nm, batch, total, nframes, off_h, keys_h, stream):
     """Checks what the timed loop ran, after the timed region, with the same C-ABI entry:
       * involution: masking a timed batch twice gives its bytes back, and once changes them;
       * keystream: masking a zero buffer yields, for EVERY frame, its 4 key bytes repeated
         from phase 0 (RFC 6455 §5.3; src/ws/common.c:321) -- checked with numpy here."""
     p, o, k = batch
+    # clone / zeros run on torch's current stream, the masks on `stream`: synchronise
+    # between them (a 1 GiB clone was still reading while the first mask ran)
+    torch.cuda.synchronize()
     before = p.clone()
+    torch.cuda.synchronize()
     nm.mask_batch(p, p, o, k, stream=stream)
     torch.cuda.synchronize()
     once_differs = not torch.equal(p, before)
@@ -162,6 +199,7 @@ def verify_step(torch, nm, batch, total, nframes, off_h, keys_h, stream):
     torch.cuda.synchronize()
     involution = torch.equal(p, before)
     zero = torch.zeros(total, dtype=torch.uint8, device=p.device)
+    torch.cuda.synchronize()
     nm.mask_batch(zero, zero, o, k, stream=stream)
     torch.cuda.synchronize()
     ks = zero.cpu().numpy()
@@ -412,8 +450,10 @@ def main():
         kern_mean = float(kern_ms.mean())
 
     ceilings = None
+    shapes = None
     if rank == 0 and not args.no_copy_ceiling:
         ceilings = stream_ceilings(torch, batches, total, stream, max(20, args.steps))
+        shapes = shape_points(torch, entry, local, batches, total, nframes, stream, max(20, args.steps))
 
     off_h, _, _ = synth_config(args.workload, rank)
     last = batches[(args.warmup + args.steps - 1) % nb]
@@ -471,6 +511,7 @@ def main():
                 "algorithmic_bytes_per_launch": 2 * total,
                 "ceilings": ceilings,
                 "frac_of_xor_stream": round(achieved / ceilings["xor_inplace_GBps"], 4) if ceilings else None,
+                "shapes": shapes,
             },
             "per_gpu": [round(float(total) * args.steps / e / GIB, 3) for e in per_rank_elapsed],
             "verified": check,
