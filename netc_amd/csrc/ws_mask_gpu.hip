@@ -304,6 +304,50 @@ __device__ __forceinline__ u32x4 load_vec(const A& a, uint64_t P) {
     }
 }
 
+// src misaligned against dst by sh = src_base & 15 (uniform over the batch): a lane loads
+// the ALIGNED 16 bytes holding the start of its source vector (P - sh from src_base), and
+// its vector is bytes [sh, sh + 16) of that block and the next lane's (lane 63: the block
+// after the span, one broadcast load).  Every aligned block read holds at least one byte
+// of the vector, so no access leaves the buffer's pages.  (16 global_load_ubyte per lane
+// in round 1; an unaligned global_load_dwordx4 since: 85 % of the aligned rate at C2.)
+template <bool NT, class A>
+__device__ __forceinline__ u32x4 load_block(const A& a, uint64_t off) {   // a.src_base + off is 16-aligned
+    const NETC_GLOBAL u32x4* p = gptr(reinterpret_cast<const u32x4*>(a.src_base + off));
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
+// bytes [sh, sh + 16) of (b, the next lane's block; lane 63: n63) -- every lane executes it
+__device__ __forceinline__ u32x4 shift_in(u32x4 b, u32x4 n63, uint32_t sh, int lane) {
+    uint32_t nb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t x = (uint32_t)__shfl_down((int)b[k], 1, kWave);
+        nb[k] = lane == kWave - 1 ? n63[k] : x;
+    }
+    const uint32_t r = sh & 3;
+    u32x4 o;
+    switch (sh >> 2) {   // uniform: constant register indices in each case
+        case 0:
+            o = u32x4{__builtin_amdgcn_alignbyte(b[1], b[0], r), __builtin_amdgcn_alignbyte(b[2], b[1], r),
+                      __builtin_amdgcn_alignbyte(b[3], b[2], r), __builtin_amdgcn_alignbyte(nb[0], b[3], r)};
+            break;
+        case 1:
+            o = u32x4{__builtin_amdgcn_alignbyte(b[2], b[1], r), __builtin_amdgcn_alignbyte(b[3], b[2], r),
+                      __builtin_amdgcn_alignbyte(nb[0], b[3], r), __builtin_amdgcn_alignbyte(nb[1], nb[0], r)};
+            break;
+        case 2:
+            o = u32x4{__builtin_amdgcn_alignbyte(b[3], b[2], r), __builtin_amdgcn_alignbyte(nb[0], b[3], r),
+                      __builtin_amdgcn_alignbyte(nb[1], nb[0], r), __builtin_amdgcn_alignbyte(nb[2], nb[1], r)};
+            break;
+        default:
+            o = u32x4{__builtin_amdgcn_alignbyte(nb[0], b[3], r), __builtin_amdgcn_alignbyte(nb[1], nb[0], r),
+                      __builtin_amdgcn_alignbyte(nb[2], nb[1], r), __builtin_amdgcn_alignbyte(nb[3], nb[2], r)};
+            break;
+    }
+    return o;
+}
+
 template <bool NT, class A>
 __device__ __forceinline__ void store_vec(const A& a, uint64_t P, u32x4 v) {
     NETC_GLOBAL u32x4* p = gptr(reinterpret_cast<u32x4*>(a.dst_base + P));
@@ -723,9 +767,22 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
         for (int k = 0; k < K; ++k) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, A + (uint64_t)k * kStep, lane);
         return;
     }
-    u32x4 d[U];
+    // src misaligned against dst: aligned blocks + a shift across lanes (shift_in)
+    const uint32_t sh = SRC_ALIGNED ? 0u : (uint32_t)((uintptr_t)a.src_base & 15u);
+    u32x4 d[U], d63[U];
+    auto load_step = [&](uint64_t base) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) d[u] = load_vec<SRC_ALIGNED, NT>(a, A + (uint64_t)u * kSpan + 16ull * lane);
+        for (int u = 0; u < U; ++u) {
+            const uint64_t P = base + (uint64_t)u * kSpan + 16ull * lane;
+            if constexpr (SRC_ALIGNED) {
+                d[u] = load_vec<true, NT>(a, P);
+            } else {
+                d[u] = load_block<NT>(a, P - sh);
+                d63[u] = load_block<NT>(a, base + (uint64_t)(u + 1) * kSpan - sh);
+            }
+        }
+    };
+    load_step(A);
     Table t;
     table_issue(a, t, guess_base(a, 0, a.mis, A), lane);
     np_resolve(a, t, A, lane);
@@ -733,15 +790,14 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint64_t base = A + (uint64_t)k * kStep;
-        if (k > 0) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) d[u] = load_vec<SRC_ALIGNED, NT>(a, base + (uint64_t)u * kSpan + 16ull * lane);
-        }
+        if (k > 0) load_step(base);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t A0 = base + (uint64_t)u * kSpan;
             const u32x4 m = span_mask(a, t, A0, lane);
-            const u32x4 out = d[u] ^ m;
+            u32x4 src = d[u];
+            if constexpr (!SRC_ALIGNED) src = shift_in(d[u], d63[u], sh, lane);
+            const u32x4 out = src ^ m;
             store_vec<NT>(a, A0 + 16ull * lane, out);
             if constexpr (VAL) {
                 const uint32_t up = (uint32_t)__shfl_up((int)out[3], 1, kWave);
