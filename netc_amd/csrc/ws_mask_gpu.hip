@@ -317,33 +317,40 @@ __device__ __forceinline__ u32x4 load_block(const A& a, uint64_t off) {   // a.s
     return *p;
 }
 
-// bytes [sh, sh + 16) of (b, the next lane's block; lane 63: n63) -- every lane executes it
+// bytes [sh, sh + 16) of (b, the next lane's block; lane 63: n63) -- every lane executes it.
+// Only the next block's dwords the shift reaches are fetched across lanes (1 + sh / 4).
 __device__ __forceinline__ u32x4 shift_in(u32x4 b, u32x4 n63, uint32_t sh, int lane) {
-    uint32_t nb[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    auto nb = [&](int k) {
         const uint32_t x = (uint32_t)__shfl_down((int)b[k], 1, kWave);
-        nb[k] = lane == kWave - 1 ? n63[k] : x;
-    }
+        return lane == kWave - 1 ? n63[k] : x;
+    };
     const uint32_t r = sh & 3;
     u32x4 o;
     switch (sh >> 2) {   // uniform: constant register indices in each case
-        case 0:
+        case 0: {
+            const uint32_t n0 = nb(0);
             o = u32x4{__builtin_amdgcn_alignbyte(b[1], b[0], r), __builtin_amdgcn_alignbyte(b[2], b[1], r),
-                      __builtin_amdgcn_alignbyte(b[3], b[2], r), __builtin_amdgcn_alignbyte(nb[0], b[3], r)};
+                      __builtin_amdgcn_alignbyte(b[3], b[2], r), __builtin_amdgcn_alignbyte(n0, b[3], r)};
             break;
-        case 1:
+        }
+        case 1: {
+            const uint32_t n0 = nb(0), n1 = nb(1);
             o = u32x4{__builtin_amdgcn_alignbyte(b[2], b[1], r), __builtin_amdgcn_alignbyte(b[3], b[2], r),
-                      __builtin_amdgcn_alignbyte(nb[0], b[3], r), __builtin_amdgcn_alignbyte(nb[1], nb[0], r)};
+                      __builtin_amdgcn_alignbyte(n0, b[3], r), __builtin_amdgcn_alignbyte(n1, n0, r)};
             break;
-        case 2:
-            o = u32x4{__builtin_amdgcn_alignbyte(b[3], b[2], r), __builtin_amdgcn_alignbyte(nb[0], b[3], r),
-                      __builtin_amdgcn_alignbyte(nb[1], nb[0], r), __builtin_amdgcn_alignbyte(nb[2], nb[1], r)};
+        }
+        case 2: {
+            const uint32_t n0 = nb(0), n1 = nb(1), n2 = nb(2);
+            o = u32x4{__builtin_amdgcn_alignbyte(b[3], b[2], r), __builtin_amdgcn_alignbyte(n0, b[3], r),
+                      __builtin_amdgcn_alignbyte(n1, n0, r), __builtin_amdgcn_alignbyte(n2, n1, r)};
             break;
-        default:
-            o = u32x4{__builtin_amdgcn_alignbyte(nb[0], b[3], r), __builtin_amdgcn_alignbyte(nb[1], nb[0], r),
-                      __builtin_amdgcn_alignbyte(nb[2], nb[1], r), __builtin_amdgcn_alignbyte(nb[3], nb[2], r)};
+        }
+        default: {
+            const uint32_t n0 = nb(0), n1 = nb(1), n2 = nb(2), n3 = nb(3);
+            o = u32x4{__builtin_amdgcn_alignbyte(n0, b[3], r), __builtin_amdgcn_alignbyte(n1, n0, r),
+                      __builtin_amdgcn_alignbyte(n2, n1, r), __builtin_amdgcn_alignbyte(n3, n2, r)};
             break;
+        }
     }
     return o;
 }
@@ -778,7 +785,9 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
                 d[u] = load_vec<true, NT>(a, P);
             } else {
                 d[u] = load_block<NT>(a, P - sh);
-                d63[u] = load_block<NT>(a, base + (uint64_t)(u + 1) * kSpan - sh);
+                // the block after the span: only lane 63 needs it (one lane's request, not 64)
+                d63[u] = u32x4{0, 0, 0, 0};
+                if (lane == kWave - 1) d63[u] = load_block<NT>(a, base + (uint64_t)(u + 1) * kSpan - sh);
             }
         }
     };
