@@ -71,7 +71,7 @@ tools/libdiag_policy.so: tools/diag_policy.hip
 # The instrumented libraries go to build/asan/; Python itself is not instrumented, so the
 # sanitizer runtimes are preloaded and leak checking is off (the interpreter's own).
 ASAN_FLAGS := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined
-ASAN_TESTS := tests/test_host_framing.py tests/test_mask_cpu.py tests/test_oracle.py tests/test_scan_oracle.py \
+ASAN_TESTS := tests/test_host_framing.py tests/test_mask_cpu.py tests/test_oracle.py tests/test_scan_oracle.py tests/test_scan_host.py \
               tests/test_utf8_oracle.py
 build/asan/libnetc.so: $(HOST_SRCS) $(HOST_HDRS)
 	@mkdir -p build/asan

@@ -119,6 +119,16 @@ int netc_gpu_scan_release(int device, void *stream);
 int64_t netc_gpu_scan_diag(int device, void *stream);
 
 /**
+ * The same scan over a stream in host memory, on the calling thread (libnetc.so): the
+ * header walk of ws_parse_frame (src/ws/common.c:146-296) hopping from header to header,
+ * O(frames) instead of O(bytes).  Arguments, outputs (hdr[n] = the consumed offset when
+ * n <= max_frames) and strict checks as netc_gpu_scan_frames, all pointers host memory.
+ * Returns 0 or NETC_GPU_EINVAL.  The ingest ring uses it for slots of large frames.
+ */
+int netc_ws_scan_frames_host(const void *wire, size_t len, uint64_t start, int flags, uint64_t *hdr, uint32_t *keys,
+                             uint8_t *b0, size_t max_frames, uint64_t *result);
+
+/**
  * Unmask, in place, the payloads of the frames a netc_gpu_scan_frames call found
  * in d_wire (the reference's unmask loop, src/ws/common.c:317-323, for every
  * frame of the stream at once); header bytes and bytes past the last recorded

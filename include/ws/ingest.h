@@ -27,6 +27,7 @@
  *   netc_ws_ingest_next_message()  the next reassembled message, in ws_parse_frame's
  *                              form (struct ws_message, 0 / 1 / WS_FRAME_PARSE_ERROR_*)
  *   netc_ws_ingest_destroy()
+ *   netc_ws_ingest_scan_counts()  which scan found the frames of the slots so far
  *   netc_ws_batch_payload()    where frame k's payload lies in a batch
  *
  * Threading: an ingest object serves one connection from one thread at a time,
@@ -48,6 +49,15 @@ struct netc_ws_ingest;
 /** netc_ws_ingest_create flag: reject what RFC 6455 forbids from a client (as NETC_WS_SCAN_STRICT).
  *  Without it (the default, 0) every header is accepted, as the reference's parser does. */
 #define NETC_WS_INGEST_STRICT 1
+
+/** Where a slot's frames are found (netc_ws_ingest_create flags).  Neither flag (the default): the
+ *  host header walk over the pinned slot (netc_ws_scan_frames_host, O(frames)), whose
+ *  descriptors go to the GPU with the bytes for the unmask only -- always without
+ *  NETC_WS_INGEST_STRICT (the GPU scan needs the strict header filter for its parallel path),
+ *  and with it when the previous slot's frames averaged >= 16 KiB; otherwise the GPU frame scan
+ *  (netc_gpu_scan_frames, O(bytes), no host work).  The results are the same either way. */
+#define NETC_WS_INGEST_SCAN_GPU  2   /* always the GPU frame scan */
+#define NETC_WS_INGEST_SCAN_HOST 4   /* always the host header walk */
 
 /* return codes of the ingest entries, besides 0 and the NETC_GPU_E* codes of mask.h */
 #define NETC_WS_INGEST_CLOSED   -20   /* recv: the peer closed the connection (what it sent is submitted) */
@@ -135,6 +145,9 @@ struct ws_message;   /* include/ws/common.h */
  */
 int netc_ws_ingest_next_message(struct netc_ws_ingest *ing, struct ws_message *message, size_t max_payload_length,
                                 int wait);
+
+/** Slots submitted so far whose frames the GPU scan found (*gpu) / the host walk found (*host).  0 or EINVAL. */
+int netc_ws_ingest_scan_counts(const struct netc_ws_ingest *ing, uint64_t *gpu, uint64_t *host);
 
 /** Frame k's payload inside batch->wire: *offset, *length.  0 or NETC_GPU_EINVAL.  Host only. */
 int netc_ws_batch_payload(const struct netc_ws_batch *batch, uint64_t k, uint64_t *offset, uint64_t *length);

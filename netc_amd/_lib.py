@@ -60,6 +60,10 @@ def host() -> ctypes.CDLL:
             lib.ws_send_message.restype = ctypes.c_int
             lib.ws_parse_frame.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
             lib.ws_parse_frame.restype = ctypes.c_int
+            lib.netc_ws_scan_frames_host.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
+                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                     ctypes.c_void_p]
+            lib.netc_ws_scan_frames_host.restype = ctypes.c_int
             _host = lib
         return _host
 

@@ -9,6 +9,8 @@
 //   H2D     the slot's stream bytes: the carry of the previous slot + the new bytes
 //   scan    netc_gpu_scan_frames' kernels -> header offsets, keys, byte 0s, result
 //   D2H     the 3-word result (frames, consumed, error), then event "scanned"
+//           (or, for a slot of large frames: the host header walk over the pinned
+//           slot before the H2D, O(frames), and its descriptors H2D -- see kHostWalkMean)
 //   unmask  every frame the scan found, in place (the batch kernel reads the frame
 //           count on the device: no host round trip between scan and unmask)
 //   D2H     the stream back into the same pinned slot, then event "done"
@@ -49,6 +51,13 @@ namespace {
 
 constexpr int kBadRecv = 10;   // netc's BADRECV reason (include/utils/error.h)
 
+// Default scan choice per slot (strict streams; non-strict ones always take the host
+// walk): the host header walk when the previous slot's frames averaged at least this
+// many bytes.  The walk costs the submitting thread one header
+// parse per frame (<= 1,024 per 16 MiB slot at this size); the GPU scan reads every byte
+// but costs the host nothing, so small frames stay on the GPU.
+constexpr uint64_t kHostWalkMean = 16384;
+
 enum SlotState : int { kFree = 0, kFilling, kInflight, kTaken };
 
 struct IngestSlot {
@@ -73,6 +82,7 @@ struct IngestSlot {
     uint64_t frames = 0;
     uint64_t cut = 0;            // end of the last complete frame (slot coordinates)
     uint64_t err = ~0ull;        // offset of a rejected header (strict), or ~0
+    bool host_walk = false;      // frames found by the host header walk (descriptors already in h_*)
 };
 
 struct DeviceGuard {
@@ -107,6 +117,8 @@ struct MessageState {
 struct netc_ws_ingest {
     int device = 0;
     int strict = 0;
+    int scan_mode = 0;     // 0: per slot by frame size, NETC_WS_INGEST_SCAN_GPU / _HOST: always that
+    uint64_t n_gpu = 0, n_host = 0;   // slots scanned each way
     int nslots = 0;
     uint64_t slot_bytes = 0, carry_cap = 0, cap = 0, max_frames = 0;
     IngestSlot* slots = nullptr;
@@ -223,6 +235,9 @@ int submit_cur(netc_ws_ingest* g) {
     if (s.fill == 0) return 0;   // nothing new: the carry alone cannot complete a frame
     uint64_t carry = 0, pos = 0;
     const uint8_t* carry_src = nullptr;
+    // non-strict streams: the GPU scan's parallel path needs the strict header filter to
+    // prune chains through payload bytes, without it the scan finishes serially on the GPU
+    bool host_walk = g->scan_mode == NETC_WS_INGEST_SCAN_HOST || (g->scan_mode == 0 && !g->strict);
     if (g->prev >= 0) {
         IngestSlot& p = g->slots[g->prev];
         if (int r = resolve(g, p)) return r;
@@ -230,6 +245,8 @@ int submit_cur(netc_ws_ingest* g) {
         carry = p.carry + p.fill - p.cut;
         carry_src = p.h_buf + (g->carry_cap - p.carry) + p.cut;
         pos = p.pos + p.cut;
+        // no complete frame in a whole slot: the frames are larger than a slot
+        if (g->scan_mode == 0) host_walk = !g->strict || p.frames == 0 || p.cut / p.frames >= kHostWalkMean;
     }
     if (carry > g->carry_cap) return set_sticky(g, NETC_WS_INGEST_TOO_BIG, g->prev);
     // the carried bytes are raw in the previous slot (the unmask stops at its last
@@ -241,16 +258,44 @@ int submit_cur(netc_ws_ingest* g) {
     s.resolved = false;
     s.frames = s.cut = 0;
     s.err = ~0ull;
+    s.host_walk = host_walk;
     const uint64_t len = carry + s.fill;
     hipError_t e;
-    if ((e = hipMemcpyAsync(s.d_buf, h, len, hipMemcpyHostToDevice, s.stream)) != hipSuccess)
-        return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: H2D copy", e);
-    if ((e = netc_gpu::launch_scan_frames(s.d_buf, len, 0, g->strict != 0, s.d_hdr, s.d_keys, s.d_b0, g->max_frames,
-                                          s.d_res, s.stream, s.scratch)) != hipSuccess)
-        return api_fail_hip(e == hipErrorOutOfMemory ? NETC_GPU_ENOMEM : NETC_GPU_ELAUNCH, "ingest: frame scan", e);
-    if ((e = hipMemcpyAsync(s.h_res, s.d_res, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
-        (e = hipEventRecord(s.scanned, s.stream)) != hipSuccess)
-        return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: result copy", e);
+    if (host_walk) {
+        // the header walk over the pinned slot, then its descriptors go to the device
+        // behind the bytes (the unmask reads them there, as it reads the GPU scan's)
+        if (netc_ws_scan_frames_host(h, len, 0, g->strict ? NETC_WS_SCAN_STRICT : 0, s.h_hdr, s.h_keys, s.h_b0,
+                                     g->max_frames, s.h_res) != 0)
+            return api_fail(NETC_GPU_ERUNTIME, "ingest: host header walk");
+        const uint64_t n = s.h_res[0];
+        if (n + 1 > g->max_frames || s.h_res[1] > len)
+            return api_fail(NETC_GPU_ERUNTIME, "ingest: host walk result out of range");
+        s.frames = n;
+        s.cut = s.h_res[1];
+        s.err = s.h_res[2];
+        s.resolved = true;
+        if ((e = hipMemcpyAsync(s.d_buf, h, len, hipMemcpyHostToDevice, s.stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(s.d_hdr, s.h_hdr, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream)) !=
+                hipSuccess ||
+            (n && (e = hipMemcpyAsync(s.d_keys, s.h_keys, n * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream)) !=
+                      hipSuccess) ||
+            (e = hipMemcpyAsync(s.d_res, s.h_res, 3 * sizeof(uint64_t), hipMemcpyHostToDevice, s.stream)) !=
+                hipSuccess)
+            return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: H2D copy", e);
+        ++g->n_host;
+    } else {
+        if ((e = hipMemcpyAsync(s.d_buf, h, len, hipMemcpyHostToDevice, s.stream)) != hipSuccess)
+            return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: H2D copy", e);
+        if ((e = netc_gpu::launch_scan_frames(s.d_buf, len, 0, g->strict != 0, s.d_hdr, s.d_keys, s.d_b0,
+                                              g->max_frames, s.d_res, s.stream, s.scratch)) != hipSuccess)
+            return api_fail_hip(e == hipErrorOutOfMemory ? NETC_GPU_ENOMEM : NETC_GPU_ELAUNCH, "ingest: frame scan",
+                                e);
+        if ((e = hipMemcpyAsync(s.h_res, s.d_res, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream)) !=
+                hipSuccess ||
+            (e = hipEventRecord(s.scanned, s.stream)) != hipSuccess)
+            return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: result copy", e);
+        ++g->n_gpu;
+    }
     if ((e = netc_gpu::launch_unmask_scanned(s.d_buf, len, s.d_hdr, s.d_keys, g->max_frames, s.d_res, s.stream,
                                              netc_gpu::api_cfg())) != hipSuccess)
         return api_fail_hip(e == hipErrorOutOfMemory ? NETC_GPU_ENOMEM : NETC_GPU_ELAUNCH, "ingest: unmask", e);
@@ -286,7 +331,9 @@ int netc_ws_ingest_create(struct netc_ws_ingest** out, int device, size_t slot_b
     if (!out) return api_fail(NETC_GPU_EINVAL, "ingest: null output pointer");
     *out = nullptr;
     if (int r = netc_gpu::api_check_device(device)) return r;
-    if (flags & ~NETC_WS_INGEST_STRICT) return api_fail(NETC_GPU_EINVAL, "ingest: unknown flags 0x%x", flags);
+    if (flags & ~(NETC_WS_INGEST_STRICT | NETC_WS_INGEST_SCAN_GPU | NETC_WS_INGEST_SCAN_HOST) ||
+        (flags & NETC_WS_INGEST_SCAN_GPU && flags & NETC_WS_INGEST_SCAN_HOST))
+        return api_fail(NETC_GPU_EINVAL, "ingest: unknown or conflicting flags 0x%x", flags);
     if (!slot_bytes) slot_bytes = 16u << 20;
     if (!nslots) nslots = 4;
     if (!max_frame_bytes) max_frame_bytes = 65536;
@@ -299,6 +346,7 @@ int netc_ws_ingest_create(struct netc_ws_ingest** out, int device, size_t slot_b
     if (!g) return api_fail(NETC_GPU_ENOMEM, "ingest: host allocation");
     g->device = device;
     g->strict = (flags & NETC_WS_INGEST_STRICT) ? 1 : 0;
+    g->scan_mode = flags & (NETC_WS_INGEST_SCAN_GPU | NETC_WS_INGEST_SCAN_HOST);
     g->nslots = nslots;
     g->slot_bytes = slot_bytes;
     g->max_frame = max_frame_bytes;
@@ -528,6 +576,13 @@ int netc_ws_ingest_next_message(struct netc_ws_ingest* g, struct ws_message* mes
         (void)netc_ws_ingest_release(g, &b);
         m.have = false;
     }
+}
+
+int netc_ws_ingest_scan_counts(const struct netc_ws_ingest* g, uint64_t* gpu, uint64_t* host) {
+    if (!g || !gpu || !host) return NETC_GPU_EINVAL;
+    *gpu = g->n_gpu;
+    *host = g->n_host;
+    return 0;
 }
 
 int netc_ws_batch_payload(const struct netc_ws_batch* b, uint64_t k, uint64_t* offset, uint64_t* length) {

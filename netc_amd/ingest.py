@@ -19,6 +19,9 @@ from . import _lib
 from .mask import NetcGpuError
 
 NETC_WS_INGEST_STRICT = 1
+NETC_WS_INGEST_SCAN_GPU = 2
+NETC_WS_INGEST_SCAN_HOST = 4
+_SCAN_FLAGS = {"auto": 0, "gpu": NETC_WS_INGEST_SCAN_GPU, "host": NETC_WS_INGEST_SCAN_HOST}
 NETC_WS_INGEST_CLOSED = -20
 NETC_WS_INGEST_FULL = -21
 NETC_WS_INGEST_TOO_BIG = -22
@@ -68,6 +71,8 @@ def _bind(lib):
     lib.netc_ws_batch_payload.restype = ctypes.c_int
     lib.netc_ws_ingest_next_message.argtypes = [vp, ctypes.POINTER(WsMessage), sz, ctypes.c_int]
     lib.netc_ws_ingest_next_message.restype = ctypes.c_int
+    lib.netc_ws_ingest_scan_counts.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    lib.netc_ws_ingest_scan_counts.restype = ctypes.c_int
     lib._ingest_bound = True
     return lib
 
@@ -117,14 +122,25 @@ class Ingest:
     """netc_ws_ingest_*: one connection's byte stream -> pinned slots -> GPU scan + unmask -> batches."""
 
     def __init__(self, device: int = 0, slot_bytes: int = 16 << 20, nslots: int = 4, max_frame_bytes: int = 65536,
-                 strict: bool = False):
+                 strict: bool = False, scan: str = "auto"):
+        """scan: "auto" (per slot by frame size, the C default), "gpu" or "host" (NETC_WS_INGEST_SCAN_*)."""
+        if scan not in _SCAN_FLAGS:
+            raise ValueError(f"scan must be one of {sorted(_SCAN_FLAGS)}")
         lib = _bind(_lib.gpu())
         h = ctypes.c_void_p(0)
         rc = lib.netc_ws_ingest_create(ctypes.byref(h), device, slot_bytes, nslots, max_frame_bytes,
-                                       NETC_WS_INGEST_STRICT if strict else 0)
+                                       (NETC_WS_INGEST_STRICT if strict else 0) | _SCAN_FLAGS[scan])
         if rc:
             _raise(rc)
         self._lib, self._h = lib, h
+
+    def scan_counts(self) -> Tuple[int, int]:
+        """netc_ws_ingest_scan_counts: (slots the GPU scan framed, slots the host walk framed)."""
+        g, h = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        rc = self._lib.netc_ws_ingest_scan_counts(self._h, ctypes.byref(g), ctypes.byref(h))
+        if rc:
+            _raise(rc)
+        return int(g.value), int(h.value)
 
     def recv(self, fd: int) -> int:
         """netc_ws_ingest_recv: bytes read (> 0), 0 (would block), CLOSED or FULL; raises on other errors."""

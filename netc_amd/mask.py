@@ -249,6 +249,27 @@ def scan_frames(wire, hdr, keys, b0, result, start: int = 0, strict: bool = True
                                            result.data_ptr(), _stream_handle(stream)))
 
 
+def scan_frames_host(wire: np.ndarray, max_frames: int, start: int = 0, strict: bool = True,
+                     length: Optional[int] = None):
+    """netc_ws_scan_frames_host (libnetc.so): the same scan over a host uint8 array, on this thread.
+
+    Returns (hdr uint64 [max_frames + 1], keys uint32 [max_frames], b0 uint8 [max_frames],
+    result uint64 [3] = frames, consumed, error offset or UINT64_MAX).
+    """
+    w = np.ascontiguousarray(wire, dtype=np.uint8)
+    n = w.size if length is None else int(length)
+    if n > w.size:
+        raise ValueError("length past the array")
+    hdr = np.zeros(max_frames + 1, np.uint64)
+    keys = np.zeros(max(max_frames, 1), np.uint32)
+    b0 = np.zeros(max(max_frames, 1), np.uint8)
+    res = np.zeros(3, np.uint64)
+    _check(_lib.host().netc_ws_scan_frames_host(w.ctypes.data, n, start, NETC_WS_SCAN_STRICT if strict else 0,
+                                                hdr.ctypes.data, keys.ctypes.data, b0.ctypes.data, max_frames,
+                                                res.ctypes.data))
+    return hdr, keys[:max_frames], b0[:max_frames], res
+
+
 def scan_diag(stream=None, device: int = 0) -> int:
     """netc_gpu_scan_diag: why the last scan on `stream` took the serial walk (0: it did not; -1: no scan)."""
     r = int(_lib.gpu().netc_gpu_scan_diag(device, _stream_handle(stream)))

@@ -30,6 +30,20 @@ from tests.wsutil import parse_stream
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["auto", "gpu", "host"])
+def scan_mode(request, monkeypatch):
+    """Every ingest case runs with each way of finding a slot's frames (NETC_WS_INGEST_SCAN_*):
+    the per-slot choice (default), always the GPU scan, always the host header walk."""
+    init = ni.Ingest.__init__
+
+    def with_mode(self, *args, **kwargs):
+        kwargs.setdefault("scan", request.param)
+        init(self, *args, **kwargs)
+
+    monkeypatch.setattr(ni.Ingest, "__init__", with_mode)
+    return request.param
+
+
 def frames_from_sizes(sizes):
     off = np.zeros(len(sizes) + 1, dtype=np.uint64)
     off[1:] = np.cumsum(np.asarray(sizes, dtype=np.uint64))
@@ -131,6 +145,38 @@ def test_mixed_frames_any_slot_size(torch_cuda, slot, nslots):
         col = Collector()
         feed(ing, col, wire, random_chunks(rng, wire.size, 20000))
         assert col.check(wire) == sizes.size
+
+
+def test_scan_choice_follows_frame_size(torch_cuda, scan_mode):
+    # 1 KiB frames, then ~60 KiB frames, then 1 KiB frames again, through 1 MiB slots, strict: by
+    # default the ring frames the small-frame slots on the GPU and the large-frame slots on the host
+    rng = np.random.default_rng(77)
+    sizes = np.concatenate([np.full(3000, 1024), rng.integers(50000, 65536, 100), np.full(3000, 1024)])
+    wire, *_ = make_stream(rng, sizes)
+    with ni.Ingest(0, slot_bytes=1 << 20, nslots=3, strict=True) as ing:
+        col = Collector()
+        feed(ing, col, wire, [1 << 20] * (wire.size // (1 << 20) + 1))
+        assert col.check(wire) == sizes.size
+        gpu, host = ing.scan_counts()
+        assert gpu + host == len(col.batches)
+        if scan_mode == "gpu":
+            assert host == 0
+        elif scan_mode == "host":
+            assert gpu == 0
+        else:
+            assert gpu >= 4 and host >= 4, (gpu, host)
+
+
+def test_non_strict_scan_choice(torch_cuda, scan_mode):
+    # without the strict checks the default frames every slot with the host walk
+    rng = np.random.default_rng(78)
+    wire, *_ = make_stream(rng, np.full(3000, 1024))
+    with ni.Ingest(0, slot_bytes=1 << 20, nslots=3, strict=False) as ing:
+        col = Collector()
+        feed(ing, col, wire, [wire.size])
+        assert col.check(wire, strict=False) == 3000
+        gpu, host = ing.scan_counts()
+        assert (gpu, host) == ((len(col.batches), 0) if scan_mode == "gpu" else (0, len(col.batches)))
 
 
 def test_c5_shape_4k_frames(torch_cuda):

@@ -114,7 +114,7 @@ def run_socket_ingest(args, base, wo, plain, off, total):
 
     a, b = socketpair()
     chk = Checker(base, wo, plain, off, args.sample_every)
-    with ni.Ingest(0, slot_bytes=args.slot_mib << 20, nslots=args.slots) as ing:
+    with ni.Ingest(0, slot_bytes=args.slot_mib << 20, nslots=args.slots, scan=args.scan, strict=args.strict) as ing:
         t = threading.Thread(target=writer_thread, args=(a, base, total, args.piece_kib << 10))
         t0 = time.perf_counter()
         t.start()
@@ -129,6 +129,7 @@ def run_socket_ingest(args, base, wo, plain, off, total):
                 drain(ing, chk, False)
         drain(ing, chk, True)
         secs = time.perf_counter() - t0
+        chk.scan_counts = ing.scan_counts()
         t.join()
     a.close()
     b.close()
@@ -139,7 +140,7 @@ def run_memory_ingest(args, base, wo, plain, off, total):
     from netc_amd import ingest as ni
 
     chk = Checker(base, wo, plain, off, args.sample_every)
-    with ni.Ingest(0, slot_bytes=args.slot_mib << 20, nslots=args.slots) as ing:
+    with ni.Ingest(0, slot_bytes=args.slot_mib << 20, nslots=args.slots, scan=args.scan, strict=args.strict) as ing:
         t0 = time.perf_counter()
         sent = 0
         while sent < total:
@@ -153,6 +154,7 @@ def run_memory_ingest(args, base, wo, plain, off, total):
         ing.submit()
         drain(ing, chk, True)
         secs = time.perf_counter() - t0
+        chk.scan_counts = ing.scan_counts()
     return secs, chk
 
 
@@ -203,6 +205,9 @@ def main():
     ap.add_argument("--frame", type=int, default=4096)
     ap.add_argument("--base-mib", type=int, default=256, help="distinct stream bytes (repeated to --gib)")
     ap.add_argument("--slot-mib", type=int, default=16)
+    ap.add_argument("--scan", default="auto", choices=["auto", "gpu", "host"], help="NETC_WS_INGEST_SCAN_*")
+    ap.add_argument("--skip-cpu", action="store_true", help="no reference / oracle CPU legs")
+    ap.add_argument("--strict", action="store_true", help="NETC_WS_INGEST_STRICT (RFC 6455 client checks)")
     ap.add_argument("--slots", type=int, default=4)
     ap.add_argument("--piece-kib", type=int, default=4096, help="writer's sendall size")
     ap.add_argument("--sample-every", type=int, default=4, help="check 8 frames of every n-th batch")
@@ -234,7 +239,13 @@ def main():
         out[name] = {"wire_GiBps": round(total / secs / GIB, 3), "payload_GiBps": round(payload_total / secs / GIB, 3),
                      "seconds": round(secs, 3), "batches": chk.batches, "frames": chk.frames,
                      "frames_checked": chk.checked, "frames_wrong": chk.bad,
+                     "slots_gpu_scan_host_walk": list(chk.scan_counts),
                      "ok": chk.frames == frames_total and chk.bytes == total and chk.bad == 0}
+    out["scan"] = args.scan
+    out["strict"] = args.strict
+    if args.skip_cpu:
+        print(json.dumps(out), flush=True)
+        return
 
     # CPU legs on a bounded sample of the same stream
     nref = int(np.searchsorted(wo, min(base.size, args.ref_mib << 20), side="right")) - 1

@@ -21,7 +21,9 @@ import shutil
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "mask_np_kernel"
+KERNEL = "mask_np_kernel<1, 2, true, true, false, netc_gpu::Args>"   # the headline instantiation
+# (bench.py's shape points launch other instantiations; the out-of-place point runs this one,
+# after the timed launches)
 
 
 def pmc(path, counter):
@@ -54,11 +56,12 @@ def main():
                      "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in
             csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))) if KERNEL in r["Kernel_Name"]]
-    timed = durs[args.warmup: args.warmup + args.steps]
+    first = 1 + args.warmup   # bench.py: one validated call through the Python mirror, then the warmup
+    timed = durs[first: first + args.steps]
     fetch = pmc(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = pmc(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
-    ft = fetch[args.warmup: args.warmup + args.steps]
-    wt = write[args.warmup: args.warmup + args.steps]
+    ft = fetch[first: first + args.steps]
+    wt = write[first: first + args.steps]
     hbm = 2 * statistics.mean(ft) * 1024 + statistics.mean(wt) * 1024
     out = {
         "tag": args.tag, "workload": wl, "kernel": stats.get("name"),
