@@ -113,8 +113,11 @@ int netc_gpu_scan_release(int device, void *stream);
  * call on it finished with the serial walk instead of the parallel scan (0: it
  * did not; bits 0-7: a capacity overflowed — a chunk's candidate bucket, a
  * chunk's exit set, an exit onto no candidate, a tile's external list; 256+: the
- * tile resolution), -1 when no scan ran on that stream, or a negative code.
- * The results are the same either way; only the speed differs.
+ * tile resolution; 65536: a scan without NETC_WS_SCAN_STRICT -- which runs its
+ * parallel pass with the strict checks except MASK, speculatively -- met a header
+ * those checks reject and walked on serially from it), -1 when no scan ran on that
+ * stream, or a negative code.  The results are the same either way; only the
+ * speed differs.
  */
 int64_t netc_gpu_scan_diag(int device, void *stream);
 

@@ -50,12 +50,13 @@ struct netc_ws_ingest;
  *  Without it (the default, 0) every header is accepted, as the reference's parser does. */
 #define NETC_WS_INGEST_STRICT 1
 
-/** Where a slot's frames are found (netc_ws_ingest_create flags).  Neither flag (the default): the
- *  host header walk over the pinned slot (netc_ws_scan_frames_host, O(frames)), whose
- *  descriptors go to the GPU with the bytes for the unmask only -- always without
- *  NETC_WS_INGEST_STRICT (the GPU scan needs the strict header filter for its parallel path),
- *  and with it when the previous slot's frames averaged >= 16 KiB; otherwise the GPU frame scan
- *  (netc_gpu_scan_frames, O(bytes), no host work).  The results are the same either way. */
+/** Where a slot's frames are found (netc_ws_ingest_create flags).  Neither flag (the default):
+ *  per slot, from the previous slot -- the host header walk over the pinned slot
+ *  (netc_ws_scan_frames_host, O(frames)), whose descriptors go to the GPU with the bytes for
+ *  the unmask only, when its frames averaged >= 16 KiB or (without NETC_WS_INGEST_STRICT) it
+ *  held headers with RSV bits, reserved opcodes or fragmented control frames (the GPU scan's
+ *  parallel pass stops at those); otherwise the GPU frame scan (netc_gpu_scan_frames,
+ *  O(bytes), no host work).  The results are the same either way. */
 #define NETC_WS_INGEST_SCAN_GPU  2   /* always the GPU frame scan */
 #define NETC_WS_INGEST_SCAN_HOST 4   /* always the host header walk */
 

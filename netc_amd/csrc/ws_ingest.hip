@@ -51,9 +51,8 @@ namespace {
 
 constexpr int kBadRecv = 10;   // netc's BADRECV reason (include/utils/error.h)
 
-// Default scan choice per slot (strict streams; non-strict ones always take the host
-// walk): the host header walk when the previous slot's frames averaged at least this
-// many bytes.  The walk costs the submitting thread one header
+// Default scan choice per slot: the host header walk when the previous slot's frames
+// averaged at least this many bytes.  The walk costs the submitting thread one header
 // parse per frame (<= 1,024 per 16 MiB slot at this size); the GPU scan reads every byte
 // but costs the host nothing, so small frames stay on the GPU.
 constexpr uint64_t kHostWalkMean = 16384;
@@ -207,6 +206,19 @@ int resolve(netc_ws_ingest* g, IngestSlot& s) {
     return 0;
 }
 
+// A non-strict stream whose previous slot held headers a client must not send (RSV set:
+// an extension such as permessage-deflate; a reserved opcode; a fragmented control frame):
+// the GPU scan's parallel pass filters like strict mode except for MASK and would stop at
+// the first of them and walk on serially, so such streams go to the host walk.
+bool unchecked_headers(const IngestSlot& p) {
+    uint32_t bad = 0;
+    for (uint64_t k = 0; k < p.frames; ++k) {
+        const uint32_t b = p.h_b0[k], op = b & 0x0F;
+        bad |= (b & 0x70) | (op - 3 <= 4) | (op >= 11) | ((op >= 8) & !(b & 0x80));
+    }
+    return bad != 0;
+}
+
 int set_sticky(netc_ws_ingest* g, int code, int after_slot) {
     if (!g->sticky) {
         g->sticky = code;
@@ -235,9 +247,7 @@ int submit_cur(netc_ws_ingest* g) {
     if (s.fill == 0) return 0;   // nothing new: the carry alone cannot complete a frame
     uint64_t carry = 0, pos = 0;
     const uint8_t* carry_src = nullptr;
-    // non-strict streams: the GPU scan's parallel path needs the strict header filter to
-    // prune chains through payload bytes, without it the scan finishes serially on the GPU
-    bool host_walk = g->scan_mode == NETC_WS_INGEST_SCAN_HOST || (g->scan_mode == 0 && !g->strict);
+    bool host_walk = g->scan_mode == NETC_WS_INGEST_SCAN_HOST;
     if (g->prev >= 0) {
         IngestSlot& p = g->slots[g->prev];
         if (int r = resolve(g, p)) return r;
@@ -246,7 +256,8 @@ int submit_cur(netc_ws_ingest* g) {
         carry_src = p.h_buf + (g->carry_cap - p.carry) + p.cut;
         pos = p.pos + p.cut;
         // no complete frame in a whole slot: the frames are larger than a slot
-        if (g->scan_mode == 0) host_walk = !g->strict || p.frames == 0 || p.cut / p.frames >= kHostWalkMean;
+        if (g->scan_mode == 0)
+            host_walk = p.frames == 0 || p.cut / p.frames >= kHostWalkMean || (!g->strict && unchecked_headers(p));
     }
     if (carry > g->carry_cap) return set_sticky(g, NETC_WS_INGEST_TOO_BIG, g->prev);
     // the carried bytes are raw in the previous slot (the unmask stops at its last

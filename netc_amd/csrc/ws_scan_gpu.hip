@@ -78,6 +78,8 @@ static constexpr uint32_t kH = 0x80808080u;
 // external list full, K1 candidate queue full), 8+ K3b's own reason
 enum : uint32_t { kOvfBucket = 1, kOvfSet = 2, kOvfLink = 4, kOvfExt = 8, kOvfQueue = 16 };
 enum : uint32_t { kWhyRoot = 1u << 8, kWhyTiles = 2u << 8, kWhyExtCap = 3u << 8, kWhySucc = 4u << 8 };
+// bit 16: a speculative (non-strict) pass stopped at a header the filter rejects; the rest was walked serially
+enum : uint32_t { kWhySpec = 1u << 16 };
 
 __device__ __forceinline__ uint64_t term(uint64_t type, uint64_t pos) { return kTerm | type << 61 | pos; }
 __device__ __forceinline__ uint64_t term_type(uint64_t v) { return (v >> 61) & 3; }
@@ -105,7 +107,10 @@ struct ScanArgs {
     uint64_t len;          // stream bytes
     uint64_t start;        // offset of the first header
     uint64_t nc;           // chunks (the last one, index nc, is virtual: positions >= len)
-    int strict;
+    int strict;            // the header filter is on (always, see spec)
+    int spec;              // the caller asked for no checks: the parallel pass runs with the strict
+                           // filter minus the MASK check, and K4 walks on serially, unchecked, from
+                           // a header that filter rejects (speculative: RFC-clean streams never stop)
     uint32_t* flags;       // [8] K3b -> K4: serial fallback (big streams), [9] why the last call walked serially
     uint32_t* ovf;         // this call's overflow bits (flags[0] / flags[2] on alternate calls: the
     uint32_t* ovf_prev;    // ... reader is every K4 block, so K4 zeroes the previous call's word instead)
@@ -151,7 +156,8 @@ __device__ __forceinline__ uint64_t parse_at(const ScanArgs& a, uint64_t p, cons
     if (a.strict) {
         const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
         const bool control = opcode >= 8;
-        if (!mask || (first & 0x70) || reserved || (control && (!(first & 0x80) || plen > 125)) || (plen >> 63))
+        if ((!mask && !a.spec) || (first & 0x70) || reserved || (control && (!(first & 0x80) || plen > 125)) ||
+            (plen >> 63))
             return term(kDead, p);
     }
     const uint64_t hl = 2 + ext + (mask ? 4 : 0);
@@ -173,7 +179,7 @@ __device__ __forceinline__ bool quick_reject(const ScanArgs& a, uint64_t x) {
     const uint32_t first = gptr(a.wire)[x], second = gptr(a.wire)[x + 1];
     const uint32_t opcode = first & 0x0F;
     const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
-    return !(second & 0x80) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80));
+    return (!(second & 0x80) && !a.spec) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80));
 }
 
 // 16 stream bytes from LDS position i as 4 dwords (5 dword reads + v_alignbyte),
@@ -212,7 +218,7 @@ __device__ __forceinline__ uint64_t parse_at(const ScanArgs& a, uint64_t p, cons
     const bool hdr_short = p + 2 + ext > a.len;
     const bool reserved = (opcode >= 3) & ((opcode <= 7) | (opcode >= 11));
     const bool control = opcode >= 8;
-    const bool dead = (a.strict != 0) & ((mask == 0) | ((first & 0x70) != 0) | reserved |
+    const bool dead = (a.strict != 0) & (((mask == 0) & (a.spec == 0)) | ((first & 0x70) != 0) | reserved |
                                          (control & (((first & 0x80) == 0) | (plen > 125))) | ((plen >> 63) != 0));
     const bool pay_short = (p + hl > a.len) | (plen > a.len - (p + hl));
     if (key_out) {
@@ -436,7 +442,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         for (int k = 0; k < 4; ++k) {
             const uint32_t x = d[i][k];
             const uint32_t y = __builtin_amdgcn_alignbyte(k < 3 ? d[i][k + 1] : nb[i], x, 1);
-            uint32_t ok = a.strict ? quick_ok4(x, y) : kH;
+            uint32_t ok = a.strict ? quick_ok4(x, y | (a.spec ? kH : 0u)) : kH;
             if (!fast) {   // positions before the start or at / past the end are not candidates
                 const uint32_t m4 = (valid[i] >> (4 * k)) & 0xFu;   // byte j valid <-> bit j
                 ok &= ((m4 * 0x00204081u) & 0x01010101u) << 7;
@@ -529,7 +535,8 @@ __device__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const ui
     uint32_t cand = 0;   // this thread's positions that can start a header
 #pragma unroll
     for (int k = 0; k < kPer / 4; ++k) {
-        const uint32_t ok = a.strict ? quick_ok4(w[k], __builtin_amdgcn_alignbyte(w[k + 1], w[k], 1)) : kH;
+        const uint32_t ok =
+            a.strict ? quick_ok4(w[k], __builtin_amdgcn_alignbyte(w[k + 1], w[k], 1) | (a.spec ? kH : 0u)) : kH;
 #pragma unroll
         for (int j = 0; j < 4; ++j) cand |= ((ok >> (8 * j + 7)) & 1u) << (4 * k + j);
     }
@@ -1014,7 +1021,9 @@ __global__ __launch_bounds__(kResolveT) void scan_resolve(ScanArgs a, uint64_t t
 }
 
 // K4, serial fallback (capacities overflowed): one thread walks the whole stream.
-__device__ void serial_walk(const ScanArgs& a) {
+__device__ void serial_walk(const ScanArgs& args) {
+    ScanArgs a = args;
+    if (a.spec) a.strict = 0;   // the caller's semantics: no checks
     uint64_t p = a.start, n = 0, err = ~0ull;
     for (;;) {
         uint32_t key;
@@ -1036,6 +1045,35 @@ __device__ void serial_walk(const ScanArgs& a) {
     a.result[0] = n;
     a.result[1] = p;
     a.result[2] = err;
+}
+
+// K4, speculative pass (spec): the parallel pass stopped at a header the strict filter
+// (minus the MASK check) rejects, which the caller accepts: one thread walks on from
+// there, unchecked, appending frames after the ones found in parallel.
+__device__ void spec_continue(const ScanArgs& args) {
+    const uint64_t stop = args.result[2];
+    if (stop == ~0ull) return;
+    ScanArgs a = args;
+    a.strict = 0;
+    uint64_t p = stop, n = a.result[0];
+    for (;;) {
+        uint32_t key;
+        uint8_t b0;
+        const uint64_t v = parse_at(a, p, window_global(a, p), &key, &b0);
+        if (v & kTerm) break;
+        if (n < a.max_frames) {
+            a.hdr[n] = p;
+            a.keys[n] = key;
+            a.b0[n] = b0;
+        }
+        ++n;
+        p = v;
+    }
+    if (n <= a.max_frames) a.hdr[n] = p;
+    a.result[0] = n;
+    a.result[1] = p;
+    a.result[2] = ~0ull;
+    a.flags[9] |= kWhySpec;
 }
 
 // Write frame k's descriptors (if recorded)
@@ -1186,6 +1224,7 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
         }
         __syncthreads();
     }
+    if (a.spec && blockIdx.x == 0 && tid == 0) spec_continue(a);   // after this block's own frames
 }
 
 // In-place unmask of scanned frames: the batch kernel reads each frame's header
@@ -1325,7 +1364,8 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.wire = wire;
     a.len = len;
     a.start = start;
-    a.strict = strict ? 1 : 0;
+    a.strict = 1;
+    a.spec = strict ? 0 : 1;
     a.nc = (len + kChunk - 1) / kChunk;   // real chunks 0 .. nc-1; chunk nc is virtual (positions >= len)
     const uint64_t chunks = a.nc + 1, tiles = (chunks + kTileChunks - 1) / kTileChunks;
     a.hdr = hdr;

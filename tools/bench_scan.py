@@ -2,7 +2,7 @@
 """Device frame-boundary scan (netc_gpu_scan_frames) throughput, one GPU.
 
 Wire streams of configs 2 and 4 shape (masked client frames, built on the host by
-the oracle encoder), strict mode.  Per step: one full scan of the stream (all of
+the oracle encoder), strict mode (--non-strict: the reference's semantics; --unmasked).  Per step: one full scan of the stream (all of
 its kernels).  Bytes = wire bytes read by the scan's per-chunk passes (reported as
 GB/s of stream scanned).  GPU time from two events around K steps on one stream.
 The result of the last step is checked against the oracle scan.
@@ -23,7 +23,10 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workloads", default="c2,c4")
+    ap.add_argument("--non-strict", action="store_true", help="flags 0: the reference's semantics (speculative pass)")
+    ap.add_argument("--unmasked", action="store_true", help="unmasked frames (server-to-client direction)")
     args = ap.parse_args()
+    flags = 0 if args.non_strict else 1
 
     import torch
 
@@ -42,7 +45,9 @@ def main():
             off, keys = off[: cut + 1], keys[:cut]
         rng = np.random.default_rng(5)
         payload = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
-        wire, wo = orc.encode_batch(payload, off, keys, None, True)
+        wire, wo = orc.encode_batch(payload, off, keys, None, not args.unmasked)
+        if args.unmasked:
+            keys = np.zeros_like(keys)
         n = keys.size
         w = torch.from_numpy(wire).to(dev)
         hdr = torch.empty(n + 1, dtype=torch.int64, device=dev)
@@ -52,7 +57,7 @@ def main():
         torch.cuda.synchronize()
 
         def step():
-            rc = entry(0, w.data_ptr(), wire.size, 0, 1, hdr.data_ptr(), kk.data_ptr(), b0.data_ptr(), n,
+            rc = entry(0, w.data_ptr(), wire.size, 0, flags, hdr.data_ptr(), kk.data_ptr(), b0.data_ptr(), n,
                        res.data_ptr(), sh)
             if rc:
                 raise RuntimeError(_lib.gpu().netc_gpu_strerror())
@@ -80,16 +85,26 @@ def main():
         cons, err = ctypes.c_uint64(0), ctypes.c_uint64(0)
         reps, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < 2.0:
-            orc.lib().oracle_scan_frames(wire.ctypes.data, wire.size, 0, 1, ch.ctypes.data, ck.ctypes.data,
+            orc.lib().oracle_scan_frames(wire.ctypes.data, wire.size, 0, flags, ch.ctypes.data, ck.ctypes.data,
                                          cb.ctypes.data, n + 1, ctypes.addressof(cons), ctypes.addressof(err))
             reps += 1
         cpu_s = (time.perf_counter() - t0) / reps
-        print(json.dumps({"workload": wl, "frames": int(n), "wire_bytes": int(wire.size), "us_per_scan": round(us, 2),
+        # the product's host walk (netc_ws_scan_frames_host, libnetc.so -O3): what the ingest ring uses
+        hres = np.zeros(3, dtype=np.uint64)
+        hl = _lib.host().netc_ws_scan_frames_host
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 2.0:
+            hl(wire.ctypes.data, wire.size, 0, flags, ch.ctypes.data, ck.ctypes.data, cb.ctypes.data, n + 1,
+               hres.ctypes.data)
+            reps += 1
+        host_s = (time.perf_counter() - t0) / reps
+        print(json.dumps({"workload": wl, "strict": bool(flags), "masked": not args.unmasked, "frames": int(n), "wire_bytes": int(wire.size), "us_per_scan": round(us, 2),
                           "wire_GBps": round(wire.size / (us * 1e-6) / 1e9, 1),
                           "frames_per_s": round(n / (us * 1e-6), 1), "matches_oracle": bool(ok),
                           "serial_fallback": hex(nm.scan_diag(s)),
                           "cpu_serial_us": round(cpu_s * 1e6, 1),
-                          "cpu_serial_frames_per_s": round(n / cpu_s, 1)}), flush=True)
+                          "cpu_serial_frames_per_s": round(n / cpu_s, 1),
+                          "host_walk_us": round(host_s * 1e6, 1), "host_walk_ok": int(hres[0]) == n}), flush=True)
         del w
         torch.cuda.empty_cache()
 
