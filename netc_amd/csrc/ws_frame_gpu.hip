@@ -680,8 +680,24 @@ __device__ __forceinline__ void fix_frame(const EncArgs& a, uint64_t k) {
         dlo ^= k2;
         dhi ^= k2;
     }
-    for (uint64_t i = 0; i < hl; ++i) w[i] = (uint8_t)(i < 8 ? lo >> (8 * i) : hi >> (8 * (i - 8)));
-    for (uint64_t i = 0; i < m; ++i) w[hl + i] = (uint8_t)(i < 8 ? dlo >> (8 * i) : dhi >> (8 * (i - 8)));
+    // header then payload bytes, hl + m <= 16 of them inside one 16-byte wire vector, written
+    // with the widest naturally aligned stores (at most 5, was one store per byte)
+    typedef unsigned __int128 u128;
+    const u128 hmask = hl >= 16 ? ~(u128)0 : (((u128)1 << (8 * hl)) - 1);
+    const u128 pay = (u128)dhi << 64 | dlo;
+    u128 v = (((u128)hi << 64 | lo) & hmask) | (hl < 16 ? pay << (8 * hl) : (u128)0);
+    uint64_t addr = (uint64_t)(uintptr_t)w, left = hl + m;
+    while (left) {
+        const uint64_t sz = (addr & 1) || left < 2 ? 1 : (addr & 2) || left < 4 ? 2 : (addr & 4) || left < 8 ? 4 : 8;
+        NETC_GLOBAL uint8_t* q = (NETC_GLOBAL uint8_t*)addr;
+        if (sz == 8) *(NETC_GLOBAL uint64_t*)q = (uint64_t)v;
+        else if (sz == 4) *(NETC_GLOBAL uint32_t*)q = (uint32_t)v;
+        else if (sz == 2) *(NETC_GLOBAL uint16_t*)q = (uint16_t)v;
+        else *q = (uint8_t)v;
+        v >>= 8 * sz;
+        addr += sz;
+        left -= sz;
+    }
 }
 
 // The queued spans: each wavefront takes queue entries in turn and composes them;
@@ -714,6 +730,11 @@ __global__ __launch_bounds__(256) void encode_queued_kernel(EncArgs a) {
         }
         return;
     }
+    // the header fixups first: their loads need nothing from the queue counter, so the
+    // dependent trips (frame descriptors, then the payload bytes after each header) do
+    // not wait behind the counter's
+    const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.n; k += nth) fix_frame(a, k);
     for (uint64_t q = wave; q < count; q += nwaves) {
         const uint64_t A0 = a.defer[q];
         if (!ENC_OK(3, A0, whi)) continue;
@@ -723,8 +744,6 @@ __global__ __launch_bounds__(256) void encode_queued_kernel(EncArgs a) {
         const u32x4 v = compose_vec(a, t, A0, W, lane);
         if (W < whi) store_wire<false>(a, W, v, wlo, whi);
     }
-    const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.n; k += nth) fix_frame(a, k);
 }
 
 template <int U, bool NT>
