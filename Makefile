@@ -58,7 +58,7 @@ diag: tools/libdiag_stream.so tools/libnetc_ws_gpu_stamps.so tools/libdiag_order
 tools/libdiag_stream.so: tools/diag_stream.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 tools/libnetc_ws_gpu_stamps.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
-	$(HIPCC) $(HIPFLAGS) -DNETC_MASK_STAMPS -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
+	$(HIPCC) $(HIPFLAGS) -DNETC_MASK_STAMPS -DNETC_SCAN_STAMPS -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 tools/libnetc_ws_gpu_checks.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
 	$(HIPCC) $(HIPFLAGS) -DNETC_ENC_CHECKS -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 tools/libdiag_order.so: tools/diag_order.hip

@@ -81,6 +81,36 @@ enum : uint32_t { kWhyRoot = 1u << 8, kWhyTiles = 2u << 8, kWhyExtCap = 3u << 8,
 // bit 16: a speculative (non-strict) pass stopped at a header the filter rejects; the rest was walked serially
 enum : uint32_t { kWhySpec = 1u << 16 };
 
+#ifdef NETC_SCAN_STAMPS
+// diagnostic build only (tools/scan_stamps.py): per kernel k (K1..K4 = 0..4) and block b
+// < kStampBlocks, 8 wall-clock stamps (100 MHz): [0] start, [1..6] phases, [7] end
+static constexpr int kStampBlocks = 8192;
+__device__ uint64_t* g_scan_stamps;
+extern "C" int netc_gpu_debug_scan_stamps(void* d_buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_scan_stamps), &d_buf, sizeof(d_buf));
+}
+__device__ __forceinline__ void scan_stamp(int k, int i) {
+    if (threadIdx.x == 0 && g_scan_stamps && blockIdx.x < (unsigned)kStampBlocks)
+        g_scan_stamps[((uint64_t)k * kStampBlocks + blockIdx.x) * 8 + i] = __builtin_amdgcn_s_memrealtime();
+}
+struct ScanStampScope {
+    int k;
+    __device__ explicit ScanStampScope(int kk) : k(kk) { scan_stamp(k, 0); }
+    __device__ ~ScanStampScope() { scan_stamp(k, 7); }
+};
+__device__ __forceinline__ void scan_value(int k, int i, uint64_t v) {   // a count instead of a time (slots 5, 6)
+    if (threadIdx.x == 0 && g_scan_stamps && blockIdx.x < (unsigned)kStampBlocks)
+        g_scan_stamps[((uint64_t)k * kStampBlocks + blockIdx.x) * 8 + i] = v;
+}
+#define SCAN_SCOPE(k) ScanStampScope scan_scope_guard(k)
+#define SCAN_STAMP(k, i) scan_stamp(k, i)
+#define SCAN_VALUE(k, i, v) scan_value(k, i, v)
+#else
+#define SCAN_SCOPE(k) ((void)0)
+#define SCAN_STAMP(k, i) ((void)0)
+#define SCAN_VALUE(k, i, v) ((void)0)
+#endif
+
 __device__ __forceinline__ uint64_t term(uint64_t type, uint64_t pos) { return kTerm | type << 61 | pos; }
 __device__ __forceinline__ uint64_t term_type(uint64_t v) { return (v >> 61) & 3; }
 __device__ __forceinline__ uint64_t term_pos(uint64_t v) { return v & kPosMask; }
@@ -363,6 +393,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     __shared__ uint32_t stage[4][kWords];      // per wave: its chunk's bytes (+ 32 after)
     __shared__ unsigned long long set[4][kSet];
     __shared__ uint16_t queue[4][kQCap];
+    SCAN_SCOPE(0);
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     if (c > a.nc) return;
@@ -584,6 +615,7 @@ __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
     __shared__ uint16_t lk16[kChunk];
     __shared__ uint32_t queue[kBlkChunks * kCand];
     __shared__ int nq;
+    SCAN_SCOPE(1);
     const int tid = threadIdx.x;
     if (tid == 0) nq = 0;
     __syncthreads();
@@ -621,6 +653,7 @@ __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
         }
     }
     __syncthreads();
+    SCAN_STAMP(1, 1);
     const int n = nq;
     for (int qi = 0; qi < n; ++qi) {
         const uint64_t node = queue[qi], chunk = node / kCand, B = chunk * kChunk;
@@ -690,6 +723,69 @@ __device__ uint64_t block_scan(uint64_t v, uint64_t* total) {
 // its current jump; after round r every node holds the bits of the nodes up to 2^(r+1)
 // - 1 links before it).  ~log2(path) rounds of a few LDS operations per node.
 static constexpr uint16_t kNone = 0xFFFF;
+static constexpr int kFastNodes = 2 * kScanT;   // K3a: up to this many nodes, each thread holds two
+
+// Rounds of pointer jumping that finish every path among n nodes: a path has at most
+// n - 1 links, and round r doubles the links a jump covers.
+__device__ __forceinline__ int jump_rounds(int n) { return n <= 1 ? 0 : 32 - __clz(n - 1); }
+
+// K3a's ranking for V <= kFastNodes, the usual tile: thread t holds nodes t and t +
+// kScanT in registers; a round reads the jump targets from one half of a ping-pong
+// pair in LDS and writes the thread's own nodes into the other, so a round is ONE
+// barrier, and the round count is fixed (no block-wide OR to stop).  bits (monotone)
+// is one array, as in the generic loop.  The results end in P / L / W.  (One
+// wavefront doing all the rounds with no barriers was slower: a lone wavefront is
+// instruction-issue-bound, 8 us at config-2 shape against 5.6 for the generic loop.)
+__device__ void rank_tile_fast(uint16_t* P, uint16_t* L, uint32_t* W, uint32_t* bits, uint16_t* P2, uint16_t* L2,
+                               uint32_t* W2, int n, int t) {
+    uint16_t mp[2], ml[2];
+    uint32_t mw[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int k = t + kScanT * r;
+        mp[r] = k < n ? P[k] : kNone;
+        ml[r] = k < n ? L[k] : 0;
+        mw[r] = k < n ? W[k] : 0;
+    }
+    const int rounds = jump_rounds(n);
+    for (int i = 0; i < rounds; ++i) {
+        const uint16_t* sp = (i & 1) ? P2 : P;
+        const uint16_t* sl = (i & 1) ? L2 : L;
+        const uint32_t* sw = (i & 1) ? W2 : W;
+        uint16_t* dp = (i & 1) ? P : P2;
+        uint16_t* dl = (i & 1) ? L : L2;
+        uint32_t* dw = (i & 1) ? W : W2;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int k = t + kScanT * r;
+            if (k < n) {
+                const uint16_t p = mp[r];
+                if (p != kNone) {
+                    atomicOr(&bits[p], bits[k]);
+                    mp[r] = sp[p];
+                    ml[r] = sl[p];
+                    mw[r] += sw[p];
+                }
+                dp[k] = mp[r];
+                dl[k] = ml[r];
+                dw[k] = mw[r];
+            }
+        }
+        __syncthreads();
+    }
+    if (rounds & 1) {   // the last round wrote the second halves: the results go to P / L / W
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int k = t + kScanT * r;
+            if (k < n) {
+                P[k] = mp[r];
+                L[k] = ml[r];
+                W[k] = mw[r];
+            }
+        }
+        __syncthreads();
+    }
+}
 
 __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
     __shared__ uint16_t cid[kTileSlots];   // tile slot -> compact node
@@ -698,14 +794,16 @@ __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
     __shared__ uint16_t L[kTileSlots];     // last node reached
     __shared__ uint32_t W[kTileSlots];     // frames from the node to L's exit
     __shared__ uint32_t bits[kTileSlots];
+    __shared__ uint16_t P2[kFastNodes], L2[kFastNodes];   // rank_tile_fast: the ping-pong halves
+    __shared__ uint32_t W2[kFastNodes];
     __shared__ uint16_t elist[kExt];
     __shared__ uint8_t eroot[kExt];
     __shared__ int skip;
+    SCAN_SCOPE(2);
     const int t = threadIdx.x;
-    // overflow: K4 walks serially.  Read once for the block (another tile may set it meanwhile)
-    if (t == 0) skip = __hip_atomic_load(a.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-    __syncthreads();
-    if (skip) return;
+    // overflow: K4 walks serially.  Read once for the block (another tile may set it
+    // meanwhile), in the same trip as the chunk data below; checked after the scans
+    const uint32_t ovf0 = t == 0 ? __hip_atomic_load(a.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     const uint64_t tile = blockIdx.x, c = tile * kTileChunks + t, s0 = tile * kTileSlots;
     // the chunk's counter, external flags, links and counts in one trip
     const bool live = c <= a.nc;
@@ -726,12 +824,16 @@ __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
         if ((uint32_t)j < cnt && ((exf >> (8 * j)) & 0xFF) && lks[j] != kDupLink) extm |= 1u << j;
     uint64_t V64, E64;
     const uint32_t base = (uint32_t)block_scan<kScanT>(cnt, &V64);
-    uint32_t eidx = (uint32_t)block_scan<kScanT>((uint64_t)__popc(extm), &E64);
+    if (t == 0) skip = ovf0 != 0;
+    uint32_t eidx = (uint32_t)block_scan<kScanT>((uint64_t)__popc(extm), &E64);   // its barriers publish skip
+    SCAN_STAMP(2, 2);
+    if (skip) return;   // block-uniform
     if (E64 > (uint64_t)kExt) {   // block-uniform
         if (t == 0) atomicOr(a.ovf, kOvfExt);
         return;
     }
     const int V = (int)V64, E = (int)E64;
+    SCAN_VALUE(2, 5, V);
     for (uint32_t i = 0; i < cnt; ++i) {
         cid[t * kCand + i] = (uint16_t)(base + i);
         gsl[base + i] = (uint16_t)(t * kCand + i);
@@ -755,8 +857,12 @@ __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
         }
     }
     __syncthreads();
+    SCAN_STAMP(2, 3);
     constexpr int kR = (int)(kTileSlots / kScanT);
-    for (;;) {
+    if (V <= kFastNodes) {   // block-uniform: the usual tile (strict: about one node per chunk)
+        rank_tile_fast(P, L, W, bits, P2, L2, W2, V, t);
+        SCAN_VALUE(2, 6, jump_rounds(V));
+    } else for (;;) {
         uint16_t np[kR], nl[kR];
         uint32_t nw[kR];
         int any = 0;
@@ -787,6 +893,7 @@ __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
         }
         if (!__syncthreads_or(any)) break;
     }
+    SCAN_STAMP(2, 4);
     for (uint32_t i = 0; i < cnt; ++i) {
         const uint64_t gs = c * kCand + i;
         const uint32_t k = base + i;
@@ -828,6 +935,8 @@ struct ResolveLds {
     int32_t exl[CAP];
     uint64_t R[CAP];
     uint16_t succ[CAP];
+    uint64_t R2[kResolveT];      // resolve_fast: the ping-pong halves
+    uint16_t succ2[kResolveT];
     uint8_t mark[CAP];
     uint8_t islast[CAP];   // its path ends in its tile (no successor)
     int bad, root_idx;
@@ -841,6 +950,41 @@ __device__ __forceinline__ void put_ext(uint32_t* eslot, uint32_t* ew, int32_t* 
     exl[idx] = e.xl;
     R[idx] = e.w;
     mark[idx] = e.root != 0;
+}
+
+// K3b's ranking for m <= NT nodes (the usual stream: a few external nodes per tile):
+// thread i holds node i in registers, one barrier per round over ping-pong halves, a
+// fixed round count -- as rank_tile_fast.  The results end in succ / R; mark
+// (monotone) is one array.
+template <int NT>
+__device__ void resolve_fast(uint16_t* succ, uint64_t* R, uint16_t* succ2, uint64_t* R2, uint8_t* mark, int m) {
+    const int i = threadIdx.x;
+    uint16_t ms = i < m ? succ[i] : kNone;
+    uint64_t mr = i < m ? R[i] : 0;
+    const int rounds = jump_rounds(m);
+    for (int r = 0; r < rounds; ++r) {
+        const uint16_t* ss = (r & 1) ? succ2 : succ;
+        const uint64_t* sr = (r & 1) ? R2 : R;
+        uint16_t* ds = (r & 1) ? succ : succ2;
+        uint64_t* dr = (r & 1) ? R : R2;
+        if (i < m) {
+            if (ms != kNone) {
+                if (mark[i]) mark[ms] = 1;
+                mr += sr[ms];
+                ms = ss[ms];
+            }
+            ds[i] = ms;
+            dr[i] = mr;
+        }
+        __syncthreads();
+    }
+    if (rounds & 1) {
+        if (i < m) {
+            succ[i] = ms;
+            R[i] = mr;
+        }
+        __syncthreads();
+    }
 }
 
 // every thread of the block; on return (after a barrier) sm.bad / sm.why say whether the
@@ -886,6 +1030,7 @@ __device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT
         if (tl < tiles) sm.toff[tl] = (uint32_t)(run + ex);
         run += tot;
     }
+    SCAN_STAMP(3, 1);
     if (t == 0) {
         sm.toff[tiles] = (uint32_t)run;
         sm.M = (uint32_t)run;
@@ -921,7 +1066,9 @@ __device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT
         }
         __syncthreads();
     }
+    SCAN_STAMP(3, 2);
     const int m = (int)sm.M;
+    SCAN_VALUE(3, 5, m);
     // successors: the external node (of a later tile) each path exits to, found in LDS
     for (int i = t; i < m; i += NT) {
         const int32_t xl = sm.exl[i];
@@ -940,12 +1087,19 @@ __device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT
         if (sm.mark[i]) sm.root_idx = i;
     }
     __syncthreads();
+    SCAN_STAMP(3, 3);
     if (sm.bad || sm.root_idx < 0) {   // block-uniform
         if (t == 0 && !sm.bad) {
             sm.bad = 1;
             sm.why = kWhyRoot;
         }
         __syncthreads();
+        return;
+    }
+    if (m <= NT) {   // block-uniform: the usual stream (a few external nodes per tile)
+        resolve_fast<NT>(sm.succ, sm.R, sm.succ2, sm.R2, sm.mark, m);
+        SCAN_VALUE(3, 6, jump_rounds(m));
+        SCAN_STAMP(3, 4);
         return;
     }
     constexpr int kR = (CAP + NT - 1) / NT;
@@ -978,6 +1132,7 @@ __device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT
         }
         if (!__syncthreads_or(any)) break;
     }
+    SCAN_STAMP(3, 4);
 }
 
 // tile tl's true entry (at most one marked node: the chain enters a tile once); if the
@@ -1011,6 +1166,7 @@ __device__ TileInfo tile_info(const ScanArgs& a, const ResolveLds<MAXT, CAP>& sm
 // K3b for streams of more than kK4Tiles tiles: one block resolves every tile
 __global__ __launch_bounds__(kResolveT) void scan_resolve(ScanArgs a, uint64_t tiles) {
     __shared__ ResolveLds<kMaxTiles, kExtCap> sm;
+    SCAN_SCOPE(3);
     resolve_tiles<kResolveT>(a, tiles, sm);
     if (!sm.bad)
         for (uint64_t tl = threadIdx.x; tl < tiles; tl += kResolveT) a.tinfo[tl] = tile_info(a, sm, tl, true);
@@ -1104,6 +1260,7 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
     __shared__ uint64_t qa_base[kBlkChunks], qb_base[kBlkChunks];
     __shared__ TileInfo bti;
     __shared__ int fbs;
+    SCAN_SCOPE(4);
     (void)tiles;
     const int tid = threadIdx.x;
     const uint64_t tile = (uint64_t)blockIdx.x * kBlkChunks / kTileChunks;   // kBlkChunks divides kTileChunks
@@ -1171,6 +1328,7 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
         return;
     }
     __syncthreads();
+    SCAN_STAMP(4, 1);
     // anchored chunks: one wavefront each
     const int lane = tid & (kWave - 1), wv = tid / kWave;
     for (int q = wv; q < nqa; q += kScanT / kWave) {
