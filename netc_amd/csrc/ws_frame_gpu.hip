@@ -49,8 +49,6 @@ __device__ __forceinline__ uint32_t ext_len(uint64_t len) { return len < 126 ? 0
 // ------------------------------------------------------------ wire offsets --
 
 static constexpr int kScanThreads = 256;
-static constexpr int kScanPer = 16;
-static constexpr uint64_t kScanBlock = (uint64_t)kScanThreads * kScanPer;   // frames per tile
 
 // exclusive prefix sum over the block (kScanThreads threads); returns the block total in *total
 __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total) {
@@ -79,9 +77,11 @@ __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total) {
 // global access is coalesced (thread t owns frames t*16 .. t*16+15 of the tile: read
 // straight from HBM, each load instruction would touch 64 cache lines, and with one
 // tile per CU that strided traffic, not the scan, set the kernel's time).
+template <int kScanPer>
 __global__ __launch_bounds__(kScanThreads) void wire_offsets_chained(const uint64_t* off, uint64_t n, uint32_t fixed,
                                                                      uint64_t* wo, uint64_t* status, uint32_t epoch,
                                                                      uint32_t* defer_count) {
+    constexpr uint64_t kScanBlock = (uint64_t)kScanThreads * kScanPer;   // frames per tile
     __shared__ uint64_t tile_prefix;
     __shared__ uint64_t v[kScanBlock + kScanBlock / kScanPer + 1];   // entry j at j + j / kScanPer
     auto pos = [](uint32_t j) { return j + j / kScanPer; };
@@ -809,23 +809,46 @@ static hipError_t scratch_for(hipStream_t stream, uint64_t tiles, uint64_t spans
     return hipSuccess;
 }
 
-static hipError_t launch_scan(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream,
-                              const EncScratch& sc) {
-    const uint64_t tiles = n / kScanBlock + 1;   // frames 0 .. n inclusive
-    hipLaunchKernelGGL(wire_offsets_chained, dim3((unsigned)tiles), dim3(kScanThreads), 0, stream, off, n,
+// frames per thread of the wire-offsets scan (NETC_ENC_SCAN_PER = 1, 2, 4, 8 or 16
+// overrides, read per call: measurement)
+static int scan_per() {
+    const char* e = getenv("NETC_ENC_SCAN_PER");
+    const int v = e ? atoi(e) : 16;
+    return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : 16;
+}
+
+static uint64_t scan_tiles_for(uint64_t n, int per) { return n / ((uint64_t)kScanThreads * per) + 1; }   // frames 0 .. n
+
+template <int PER>
+static hipError_t launch_scan_per(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream,
+                                  const EncScratch& sc) {
+    const uint64_t tiles = scan_tiles_for(n, PER);
+    hipLaunchKernelGGL((wire_offsets_chained<PER>), dim3((unsigned)tiles), dim3(kScanThreads), 0, stream, off, n,
                        (uint32_t)(2 + (masked ? 4 : 0)), wo, sc.status, sc.epoch,
                        (uint32_t*)(sc.defer + sc.defer_cap));
     return hipGetLastError();
 }
 
+static hipError_t launch_scan(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream,
+                              const EncScratch& sc, int per) {
+    switch (per) {
+        case 1: return launch_scan_per<1>(off, n, masked, wo, stream, sc);
+        case 2: return launch_scan_per<2>(off, n, masked, wo, stream, sc);
+        case 4: return launch_scan_per<4>(off, n, masked, wo, stream, sc);
+        case 8: return launch_scan_per<8>(off, n, masked, wo, stream, sc);
+        default: return launch_scan_per<16>(off, n, masked, wo, stream, sc);
+    }
+}
+
 hipError_t launch_wire_offsets(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream) {
     if (n == 0) return hipMemsetAsync(wo, 0, sizeof(uint64_t), stream);
-    const uint64_t tiles = n / kScanBlock + 1;
+    const int per = scan_per();
+    const uint64_t tiles = scan_tiles_for(n, per);
     if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
     EncScratch sc;
     hipError_t e = scratch_for(stream, tiles, 1, sc);
     if (e != hipSuccess) return e;
-    return launch_scan(off, n, masked, wo, stream, sc);
+    return launch_scan(off, n, masked, wo, stream, sc, per);
 }
 
 // mean payload bytes per frame under which a batch takes the dense compose path
@@ -864,14 +887,15 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
                                 const uint64_t* off, const uint32_t* keys, const uint8_t* b0, uint64_t n, bool masked,
                                 uint64_t* wo, hipStream_t stream, const LaunchCfg& cfg) {
     if (n == 0) return hipMemsetAsync(wo, 0, sizeof(uint64_t), stream);
-    const uint64_t tiles = n / kScanBlock + 1;
+    const int per = scan_per();
+    const uint64_t tiles = scan_tiles_for(n, per);
     if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
     const uint64_t wmis = (uint64_t)(uintptr_t)wire & 15u;
     const uint64_t spans = (wmis + wire_bound + kSpan - 1) / kSpan + 8;   // every span could be queued
     EncScratch sc;
     hipError_t e = scratch_for(stream, tiles, spans, sc);
     if (e != hipSuccess) return e;
-    if ((e = launch_scan(off, n, masked, wo, stream, sc)) != hipSuccess) return e;
+    if ((e = launch_scan(off, n, masked, wo, stream, sc, per)) != hipSuccess) return e;
     EncArgs a;
     a.wmis = wmis;
     a.wire_base = wire - a.wmis;

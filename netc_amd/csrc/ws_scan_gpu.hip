@@ -72,6 +72,8 @@ static constexpr int kMaxTiles = 8192;                        // K3b: tiles (8 G
 static constexpr int kBlkChunks = 16;                         // K2 / K4: chunks per block
 static constexpr int32_t kDupLink = -2;                       // K2: slot repeats an earlier slot's position
 static constexpr int kWalkHops = 64;                          // K2 / K4: frames walked one by one
+static constexpr int kList = 8;                               // K2 -> K4: frames recorded per node
+static constexpr int kListSlots = 4;                          // ... for node slots 0..3 of a chunk
 static constexpr uint32_t kH = 0x80808080u;
 // why a scan fell back to the serial walk (flags[9], read by netc_gpu_scan_diag): bits
 // 0-7 flags[0] (K1 bucket full, K1 exit set full, K2 exit onto no candidate, K3a tile
@@ -158,6 +160,9 @@ struct ScanArgs {
     uint16_t* anc;         // K2' -> K4: 8-frame anchors of anchor slot q at anc[q * kAncSlot]
     uint32_t* anc_n;       // anchors in slot q
     uint32_t* anq;         // per node: its anchor slot, or ~0 when none was left
+    uint64_t* flist;       // K2 -> K4: the frames of node slots 0..kListSlots-1 of each chunk, when
+                           // the node's walk has at most kList of them: {offset in the chunk,
+                           // header byte 0 << 16, key << 32} per frame
     uint64_t anc_cap;      // anchor slots
     uint64_t* hdr;         // outputs
     uint32_t* keys;
@@ -640,9 +645,19 @@ __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
             } else {
                 const uint64_t B = c * kChunk;
                 uint32_t cnt = 0;
-                const uint64_t v = x - B < kChunk ? walk_frames<false>(a, B, nullptr, x, kWalkHops,
-                                                                       [&](uint64_t, uint32_t, uint8_t) { ++cnt; })
-                                                  : term(kEnd, x);   // x == len on a chunk edge
+                // the walk's first kList frames, for K4 (read only if this node is the
+                // chunk's true entry and its walk has at most kList frames)
+                uint64_t* fl = a.flist + (c * kListSlots + (i < (uint32_t)kListSlots ? i : 0)) * kList;
+                const bool rec = i < (uint32_t)kListSlots;
+                const uint64_t v = x - B < kChunk
+                                       ? walk_frames<false>(a, B, nullptr, x, kWalkHops,
+                                                            [&](uint64_t p, uint32_t key, uint8_t b0) {
+                                                                if (rec && cnt < (uint32_t)kList)
+                                                                    fl[cnt] = (p - B) | (uint64_t)b0 << 16 |
+                                                                              (uint64_t)key << 32;
+                                                                ++cnt;
+                                                            })
+                                       : term(kEnd, x);   // x == len on a chunk edge
                 if (v == 0) {
                     queue[atomicAdd(&nq, 1)] = (uint32_t)s;
                 } else {
@@ -816,7 +831,10 @@ __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
     for (int j = 0; j < kCand; ++j) {
         lks[j] = live ? a.link[c * kCand + j] : kDupLink;
         nws[j] = live ? a.ncnt[c * kCand + j] : 0;
-        rootm |= (live && a.cand[c * kCand + j] == a.start ? 1u : 0u) << j;
+    }
+    if (live && c == a.start / kChunk) {   // only the stream start's chunk holds the root
+#pragma unroll
+        for (int j = 0; j < kCand; ++j) rootm |= (a.cand[c * kCand + j] == a.start ? 1u : 0u) << j;
     }
     uint32_t extm = 0;
 #pragma unroll
@@ -1313,6 +1331,20 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
                         qb_node[q] = (uint32_t)e;
                         qb_base[q] = base;
                     }
+                } else if (ie < kListSlots && count <= (uint32_t)kList) {
+                    // K2 recorded the frames: one trip for the list instead of a walk of
+                    // dependent header reads
+                    const NETC_GLOBAL u32x4* fl = (const NETC_GLOBAL u32x4*)(a.flist + (c * kListSlots + ie) * kList);
+                    u32x4 r[kList / 2];
+#pragma unroll
+                    for (int h = 0; h < kList / 2; ++h)
+                        if ((uint32_t)(2 * h) < count) r[h] = fl[h];
+#pragma unroll
+                    for (int h = 0; h < kList; ++h)
+                        if ((uint32_t)h < count) {
+                            const uint32_t lo = r[h / 2][2 * (h & 1)], hi = r[h / 2][2 * (h & 1) + 1];
+                            put_frame(a, base + h, c * kChunk + (lo & 0xFFFFu), hi, (uint8_t)(lo >> 16));
+                        }
                 } else {
                     uint64_t k = base;
                     walk_frames<false>(a, c * kChunk, nullptr, x, -1,
@@ -1430,7 +1462,7 @@ std::mutex& stream_scratch_mu() {
 // The scratch layout for `cap` chunks (cap a multiple of kTileChunks): offsets of the
 // regions; flags, ccount and ext first -- the region every call leaves zeroed.
 struct Layout {
-    uint64_t flags, ccount, ext, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, text, tcount, tinfo,
+    uint64_t flags, ccount, ext, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, flist, text, tcount, tinfo,
         total;
 };
 Layout layout_for(uint64_t cap) {
@@ -1451,6 +1483,7 @@ Layout layout_for(uint64_t cap) {
     l.anq = o;     o = align(o + slots * 4);
     l.anc = o;     o = align(o + cap * kAncSlot * 2);
     l.anc_n = o;   o = align(o + cap * 4);
+    l.flist = o;   o = align(o + cap * kListSlots * kList * 8);
     l.text = o;    o = align(o + tiles * kExt * sizeof(TileExt));
     l.tcount = o;  o = align(o + tiles * 4);
     l.tinfo = o;   o = align(o + tiles * sizeof(TileInfo));
@@ -1569,6 +1602,7 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.anq = (uint32_t*)(m + l.anq);
     a.anc = (uint16_t*)(m + l.anc);
     a.anc_n = (uint32_t*)(m + l.anc_n);
+    a.flist = (uint64_t*)(m + l.flist);
     a.text = (TileExt*)(m + l.text);
     a.tcount = (uint32_t*)(m + l.tcount);
     a.tinfo = (TileInfo*)(m + l.tinfo);
