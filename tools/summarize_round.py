@@ -47,7 +47,10 @@ def main():
     wl = args.workload
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(prof, f"{args.tag}_{wl}_kernel_stats.csv"))
-    bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
+    bpath = os.path.join(src, "bench.json")
+    if not os.path.exists(bpath):   # tools/gpu_round2.sh names it per workload
+        bpath = os.path.join(src, f"bench_{wl}.json")
+    bench = json.loads(open(bpath).read().strip().splitlines()[-1])
     total = bench["config"]["batch_bytes_per_gpu"]
     stats = {}
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
