@@ -169,6 +169,8 @@ struct ScanArgs {
     uint8_t* b0;
     uint64_t max_frames;
     uint64_t* result;      // [0] frames, [1] consumed, [2] error offset or ~0
+    int fast_rank;         // K3a / K3b may take their one-barrier-per-round ranking (0: the generic
+                           // loop always; NETC_SCAN_FAST_RANK=0, tests)
 };
 
 // One header at stream position p (bytes b[0..13] from p; bytes past len unused).
@@ -877,7 +879,7 @@ __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
     __syncthreads();
     SCAN_STAMP(2, 3);
     constexpr int kR = (int)(kTileSlots / kScanT);
-    if (V <= kFastNodes) {   // block-uniform: the usual tile (strict: about one node per chunk)
+    if (a.fast_rank && V <= kFastNodes) {   // block-uniform: the usual tile (strict: about one node per chunk)
         rank_tile_fast(P, L, W, bits, P2, L2, W2, V, t);
         SCAN_VALUE(2, 6, jump_rounds(V));
     } else for (;;) {
@@ -1114,7 +1116,7 @@ __device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT
         __syncthreads();
         return;
     }
-    if (m <= NT) {   // block-uniform: the usual stream (a few external nodes per tile)
+    if (a.fast_rank && m <= NT) {   // block-uniform: the usual stream (a few external nodes per tile)
         resolve_fast<NT>(sm.succ, sm.R, sm.succ2, sm.R2, sm.mark, m);
         SCAN_VALUE(3, 6, jump_rounds(m));
         SCAN_STAMP(3, 4);
@@ -1607,6 +1609,10 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.tcount = (uint32_t*)(m + l.tcount);
     a.tinfo = (TileInfo*)(m + l.tinfo);
     a.anc_cap = s.cap;
+    {   // tests: NETC_SCAN_FAST_RANK=0 sends every tile and stream through the generic ranking loop
+        const char* env = getenv("NETC_SCAN_FAST_RANK");
+        a.fast_rank = env && env[0] == '0' ? 0 : 1;
+    }
     if (const char* env = getenv("NETC_SCAN_ANCHOR_SLOTS")) {   // tests: fewer slots (0: none)
         const uint64_t v = (uint64_t)strtoull(env, nullptr, 10);
         a.anc_cap = v < a.anc_cap ? v : a.anc_cap;

@@ -253,3 +253,19 @@ def test_dense_chunks_parallel_walks(torch_cuda, monkeypatch, masked, strict, sl
     for s in (int(wo[17]), int(wo[5600])):
         run_scan(torch_cuda, wire, start=s, strict=strict, parallel=strict)
     run_scan(torch_cuda, wire, strict=strict, max_frames=4123)
+
+
+@pytest.mark.parametrize("fast", ["1", "0"])
+def test_ranking_paths(torch_cuda, monkeypatch, fast):
+    # K3a / K3b rank a tile's nodes (and the tiles' external nodes) with one barrier per
+    # round when they fit (512 / 1,024 nodes), else with the generic loop; both on the
+    # same streams (NETC_SCAN_FAST_RANK=0 forces the generic loop)
+    monkeypatch.setenv("NETC_SCAN_FAST_RANK", fast)
+    rng = np.random.default_rng(31)
+    wire, _ = _stream(rng, np.full(16384, 1024))   # 16 MiB: 16 full tiles of ~262 nodes
+    assert run_scan(torch_cuda, wire, parallel=True) == 16384
+    sizes = np.concatenate([rng.integers(0, 5000, 2000), rng.integers(0, 130, 2000), [65535, 65536, 300000]])
+    rng.shuffle(sizes)
+    wire, _ = _stream(rng, sizes)
+    assert run_scan(torch_cuda, wire, parallel=True) == sizes.size
+    assert run_scan(torch_cuda, wire, strict=False, parallel=True) == sizes.size
