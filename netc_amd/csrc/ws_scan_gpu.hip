@@ -444,6 +444,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     for (int i = 0; i < 4; ++i)
         *(u32x4*)&st[(1024 * i + 16 * lane) / 4] = u32x4{d[i][0], d[i][1], d[i][2], d[i][3]};
     if (lane < 4) st[kChunk / 4 + lane] = nx[lane];
+    SCAN_STAMP(0, 1);   // the chunk's bytes have arrived
     set[wv][lane] = ~0ull;   // the wave's exit set
     // the dword after each lane's 16 bytes (readfirstlane outside the lane-63 branch:
     // inside it lane 63 is the first active lane)
@@ -516,6 +517,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    SCAN_STAMP(0, 2);   // quick check done, candidates queued
     bool ovf = false;
     for (uint32_t e = lane; e < total; e += kWave) {
         const uint32_t off = queue[wv][e];
@@ -526,6 +528,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         if (!(v & kTerm) && v >= Bend && set_insert(set[wv], v, &ovf) && !quick_reject(a, v))
             append_cand(a, v, v / kChunk / kTileChunks != c / kTileChunks);
     }
+    SCAN_STAMP(0, 3);   // parsed, exits checked and appended
     if (ovf) atomicOr(a.ovf, kOvfSet);
 }
 
