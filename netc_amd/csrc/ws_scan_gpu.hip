@@ -48,6 +48,7 @@
 #include <mutex>
 #include <new>
 #include <vector>
+#include <type_traits>
 #include <utility>
 
 #include "gpu_util.h"
@@ -401,7 +402,9 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     __shared__ unsigned long long set[4][kSet];
     __shared__ uint16_t queue[4][kQCap];
     SCAN_SCOPE(0);
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    // wv through readfirstlane: the chunk index, its bounds and the edge test below are
+    // then scalar (SGPR arithmetic, scalar branches) instead of per-lane VALU
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(tid / kWave);
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     if (c > a.nc) return;
     const uint64_t B = c * kChunk, Bend = B + kChunk;
@@ -460,38 +463,46 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         nb[2] = f3;
         nb[3] = nx[0];
     }
-    // edge chunks: the lane's valid positions [start, len) per vector, bit b <-> byte b
-    uint32_t valid[4] = {0xFFFFu, 0xFFFFu, 0xFFFFu, 0xFFFFu};
-    if (!fast) {
+    // exit-capable candidates: bit 32 h + 8 j + 4 (i & 1) + k <-> vector i = 2 h + (i & 1),
+    // dword k, byte j.  The strict filter (always on: see ScanArgs::spec) is one branch
+    // for the whole pass, not one per dword.
+    uint32_t half[2] = {0, 0};
+    const uint32_t specH = a.spec ? kH : 0u;
+    auto pass = [&](auto strict_c) {
+        constexpr bool kStrict = decltype(strict_c)::value;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint32_t ci = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t x = d[i][k];
+                const uint32_t y = __builtin_amdgcn_alignbyte(k < 3 ? d[i][k + 1] : nb[i], x, 1);
+                const uint32_t ok = kStrict ? quick_ok4(x, y | specH) : kH;
+                // a 7-bit length cannot leave the chunk unless the position is near its end
+                // (a per-byte threshold test for those lanes cost more VALU than it saved)
+                const uint32_t sel = ((i == 3 && lane >= kNearLane) ? kH : ((y & 0x7E7E7E7Eu) + 0x02020202u));
+                ci |= (ok & sel & kH) >> (7 - k);
+            }
+            half[i >> 1] |= ci << (4 * (i & 1));
+        }
+    };
+    if (a.strict) pass(std::integral_constant<bool, true>{});
+    else pass(std::integral_constant<bool, false>{});
+    if (!fast) {   // wave-uniform: an edge chunk; positions before the start or at / past the end are not candidates
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint64_t q0 = B + 1024 * i + 16 * (uint64_t)lane;
             const uint64_t lo = a.start <= q0 ? 0 : (a.start - q0 < 16 ? a.start - q0 : 16);
             const uint64_t hi = a.len <= q0 ? 0 : (a.len - q0 < 16 ? a.len - q0 : 16);
-            valid[i] = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
-        }
-    }
-    // exit-capable candidates: bit 32 h + 8 j + 4 (i & 1) + k <-> vector i = 2 h + (i & 1),
-    // dword k, byte j
-    uint32_t half[2] = {0, 0};
+            const uint32_t valid = ((1u << hi) - 1u) & ~((1u << lo) - 1u);   // byte b <-> bit b
+            uint32_t vm = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        uint32_t ci = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t x = d[i][k];
-            const uint32_t y = __builtin_amdgcn_alignbyte(k < 3 ? d[i][k + 1] : nb[i], x, 1);
-            uint32_t ok = a.strict ? quick_ok4(x, y | (a.spec ? kH : 0u)) : kH;
-            if (!fast) {   // positions before the start or at / past the end are not candidates
-                const uint32_t m4 = (valid[i] >> (4 * k)) & 0xFu;   // byte j valid <-> bit j
-                ok &= ((m4 * 0x00204081u) & 0x01010101u) << 7;
+            for (int k = 0; k < 4; ++k) {   // byte j of dword k <-> bit 8 j + k
+                const uint32_t m4 = (valid >> (4 * k)) & 0xFu;
+                vm |= (((m4 * 0x00204081u) & 0x01010101u)) << k;
             }
-            // a 7-bit length cannot leave the chunk unless the position is near its end
-            // (a per-byte threshold test for those lanes cost more VALU than it saved)
-            const uint32_t sel = ((i == 3 && lane >= kNearLane) ? kH : ((y & 0x7E7E7E7Eu) + 0x02020202u));
-            ci |= (ok & sel & kH) >> (7 - k);
+            half[i >> 1] &= ~(0x0F0F0F0Fu << (4 * (i & 1))) | (vm << (4 * (i & 1)));
         }
-        half[i >> 1] |= ci << (4 * (i & 1));
     }
     uint64_t rel = (uint64_t)half[1] << 32 | half[0];
     // queue them (chunk offsets), then parse round-robin
