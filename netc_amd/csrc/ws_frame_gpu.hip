@@ -809,13 +809,16 @@ static hipError_t scratch_for(hipStream_t stream, uint64_t tiles, uint64_t spans
     return hipSuccess;
 }
 
-// frames per thread of the wire-offsets scan: tiles of 1,024 frames (C2 shape, one
-// box: 1 / 2 / 4 / 8 / 16 frames per thread gave 43.9 / 43.2 / 42.3 / 42.8 / 44.2 us
-// per call; NETC_ENC_SCAN_PER overrides, read per call: measurement)
-static int scan_per() {
+// frames per thread of the wire-offsets scan: tiles of 1,024 frames up to 256 Ki frames
+// (C2 shape, one box: 1 / 2 / 4 / 8 / 16 frames per thread gave 43.9 / 43.2 / 42.3 /
+// 42.8 / 44.2 us per call), tiles of 4,096 frames above (1-8 Mi frames of 8-64 B: the
+// look-back over 4x the tiles cost more than the shorter tiles saved).
+// NETC_ENC_SCAN_PER overrides, read per call: measurement.
+static int scan_per(uint64_t n) {
     const char* e = getenv("NETC_ENC_SCAN_PER");
-    const int v = e ? atoi(e) : 4;
-    return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : 4;
+    const int dflt = n <= (256u << 10) ? 4 : 16;
+    const int v = e ? atoi(e) : dflt;
+    return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : dflt;
 }
 
 static uint64_t scan_tiles_for(uint64_t n, int per) { return n / ((uint64_t)kScanThreads * per) + 1; }   // frames 0 .. n
@@ -843,7 +846,7 @@ static hipError_t launch_scan(const uint64_t* off, uint64_t n, bool masked, uint
 
 hipError_t launch_wire_offsets(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream) {
     if (n == 0) return hipMemsetAsync(wo, 0, sizeof(uint64_t), stream);
-    const int per = scan_per();
+    const int per = scan_per(n);
     const uint64_t tiles = scan_tiles_for(n, per);
     if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
     EncScratch sc;
@@ -888,7 +891,7 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
                                 const uint64_t* off, const uint32_t* keys, const uint8_t* b0, uint64_t n, bool masked,
                                 uint64_t* wo, hipStream_t stream, const LaunchCfg& cfg) {
     if (n == 0) return hipMemsetAsync(wo, 0, sizeof(uint64_t), stream);
-    const int per = scan_per();
+    const int per = scan_per(n);
     const uint64_t tiles = scan_tiles_for(n, per);
     if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
     const uint64_t wmis = (uint64_t)(uintptr_t)wire & 15u;
