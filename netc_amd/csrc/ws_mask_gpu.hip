@@ -355,6 +355,64 @@ __device__ __forceinline__ u32x4 shift_in(u32x4 b, u32x4 n63, uint32_t sh, int l
     return o;
 }
 
+// ---------------------------------------------------------------------------
+// Line-aligned source (one-window-per-wave walk, src misaligned against dst).
+// A wave's 1 KiB span read at a 16-B but not 128-B aligned address touches 9 lines,
+// not 8; a plain float4 copy from such a source runs 3.5 % slower
+// (profiles/r02j_probe_lineoff.jsonl), and round 2's form -- aligned 16-B blocks at
+// P - sh plus a one-lane load of the block after each span -- touched 10 lines per
+// span.  Here a window of M spans loads its source as M whole-line spans from the
+// line holding its first byte (c[0..M-1], 8 lines each) plus the <= 8 blocks of the
+// line after them (c[M], one line), and each output vector is assembled across lanes:
+// span m's lane i takes bytes [o + 16 i, o + 16 i + 16) of c[m]:c[m+1], o = the source
+// line offset, i.e. blocks j = i + o/16 and j + 1 (from c[m+1] once j >= 64), shifted
+// by o & 15 bytes.  The permutes (ds_bpermute) of each c[m] are shared by spans m - 1
+// and m.  Every line read holds a byte of the window's source, so no access leaves the
+// source's pages.
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t lane_pick(int idx4, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(idx4, (int)v);
+}
+
+// bytes [4 D + r, 4 D + r + 16) of the 32 bytes X:Y
+template <int D>
+__device__ __forceinline__ u32x4 join_shift(u32x4 X, u32x4 Y, uint32_t r) {
+    uint32_t w[8] = {X[0], X[1], X[2], X[3], Y[0], Y[1], Y[2], Y[3]};
+    return u32x4{__builtin_amdgcn_alignbyte(w[D + 1], w[D], r), __builtin_amdgcn_alignbyte(w[D + 2], w[D + 1], r),
+                 __builtin_amdgcn_alignbyte(w[D + 3], w[D + 2], r), __builtin_amdgcn_alignbyte(w[D + 4], w[D + 3], r)};
+}
+
+// the source vectors of the window's M spans, from c[0..M] (see above); o = line offset
+template <int M, int D>
+__device__ __forceinline__ void shift_window(const u32x4 (&c)[M + 1], u32x4 (&v)[M], uint32_t o, int lane) {
+    const uint32_t q = o >> 4, r = o & 3;
+    const int j0 = (int)(((uint32_t)lane + q) & 63u) * 4, j1 = (int)(((uint32_t)lane + q + 1) & 63u) * 4;
+    const bool lo0 = (uint32_t)lane + q < 64u, lo1 = (uint32_t)lane + q + 1 < 64u;
+    u32x4 px[M + 1], py[M + 1];
+#pragma unroll
+    for (int m = 0; m <= M; ++m) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {   // X needs dwords D..3, Y dwords 0..D
+            px[m][k] = k >= D ? lane_pick(j0, c[m][k]) : 0u;
+            py[m][k] = k <= D ? lane_pick(j1, c[m][k]) : 0u;
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        const u32x4 X = lo0 ? px[m] : px[m + 1];
+        const u32x4 Y = lo1 ? py[m] : py[m + 1];
+        v[m] = join_shift<D>(X, Y, r);
+    }
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 load_line_block(const uint8_t* p) {   // p 16-aligned
+    const NETC_GLOBAL u32x4* g = gptr(reinterpret_cast<const u32x4*>(p));
+    if constexpr (NT) return __builtin_nontemporal_load(g);
+    return *g;
+}
+
 template <bool NT, class A>
 __device__ __forceinline__ void store_vec(const A& a, uint64_t P, u32x4 v) {
     NETC_GLOBAL u32x4* p = gptr(reinterpret_cast<u32x4*>(a.dst_base + P));
@@ -535,6 +593,32 @@ __device__ __forceinline__ void validate_span(const Args& a, const Table& t, uin
     }
 }
 
+template <class A>
+__device__ __forceinline__ int64_t clamp_base(const A& a, int64_t g) {
+    g = g < -1 ? -1 : g;
+    return g > (int64_t)a.n ? (int64_t)a.n : g;
+}
+
+// make t (issued at a guessed base) hold the frame containing A
+template <class AT>
+__device__ __forceinline__ void np_resolve(const AT& a, Table& t, uint64_t A, int lane) {
+    table_finish(t);
+#pragma unroll 1
+    for (int step = 0; step < 2; ++step) {
+        const uint64_t m = __ballot(t.start <= A);
+        if (m != 0 && (t.tail || m != ~0ull)) return;   // brackets A
+        int64_t g;
+        if (m == 0) {   // every entry starts after A: step back by the distance from entry 0
+            const uint64_t s0 = readlane64(t.start, 0);
+            g = t.kb - (int64_t)((double)(s0 - A) * a.density) - 40;
+        } else {        // every entry starts at or before A: step on from entry 63
+            g = t.kb + (kWave - 1) + (int64_t)((double)(A - t.last) * a.density) - 24;
+        }
+        table_load(a, t, clamp_base(a, g), lane);
+    }
+    if (!table_brackets(t, A)) table_load(a, t, locate(a, A, lane), lane);
+}
+
 template <int U, bool SRC_ALIGNED, bool NT, bool VAL, class AT>
 __device__ __forceinline__ void edge_chunk(const AT& a, uint64_t A, int lane) {
     const uint64_t full_lo = a.mis ? 16 : 0;
@@ -709,32 +793,6 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
 // the table carried across them.
 // ---------------------------------------------------------------------------
 
-template <class A>
-__device__ __forceinline__ int64_t clamp_base(const A& a, int64_t g) {
-    g = g < -1 ? -1 : g;
-    return g > (int64_t)a.n ? (int64_t)a.n : g;
-}
-
-// make t (issued at a guessed base) hold the frame containing A
-template <class AT>
-__device__ __forceinline__ void np_resolve(const AT& a, Table& t, uint64_t A, int lane) {
-    table_finish(t);
-#pragma unroll 1
-    for (int step = 0; step < 2; ++step) {
-        const uint64_t m = __ballot(t.start <= A);
-        if (m != 0 && (t.tail || m != ~0ull)) return;   // brackets A
-        int64_t g;
-        if (m == 0) {   // every entry starts after A: step back by the distance from entry 0
-            const uint64_t s0 = readlane64(t.start, 0);
-            g = t.kb - (int64_t)((double)(s0 - A) * a.density) - 40;
-        } else {        // every entry starts at or before A: step on from entry 63
-            g = t.kb + (kWave - 1) + (int64_t)((double)(A - t.last) * a.density) - 24;
-        }
-        table_load(a, t, clamp_base(a, g), lane);
-    }
-    if (!table_brackets(t, A)) table_load(a, t, locate(a, A, lane), lane);
-}
-
 // the frame count when it is produced on the device by an earlier kernel (scan -> unmask)
 __device__ __forceinline__ void init_frames(Args& a) {
     if (a.n_dev) {
@@ -774,46 +832,55 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
         for (int k = 0; k < K; ++k) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, A + (uint64_t)k * kStep, lane);
         return;
     }
-    // src misaligned against dst: aligned blocks + a shift across lanes (shift_in)
-    const uint32_t sh = SRC_ALIGNED ? 0u : (uint32_t)((uintptr_t)a.src_base & 15u);
-    u32x4 d[U], d63[U];
-    auto load_step = [&](uint64_t base) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t P = base + (uint64_t)u * kSpan + 16ull * lane;
-            if constexpr (SRC_ALIGNED) {
-                d[u] = load_vec<true, NT>(a, P);
-            } else {
-                d[u] = load_block<NT>(a, P - sh);
-                // the block after the span: only lane 63 needs it (one lane's request, not 64)
-                d63[u] = u32x4{0, 0, 0, 0};
-                if (lane == kWave - 1) d63[u] = load_block<NT>(a, base + (uint64_t)(u + 1) * kSpan - sh);
-            }
+    uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
+    Table t;
+    auto emit = [&](uint64_t A0, u32x4 src, bool first) {
+        const u32x4 m = span_mask(a, t, A0, lane);
+        const u32x4 out = src ^ m;
+        store_vec<NT>(a, A0 + 16ull * lane, out);
+        if constexpr (VAL) {
+            const uint32_t up = (uint32_t)__shfl_up((int)out[3], 1, kWave);
+            validate_span(a, t, A0, out, lane ? up : carry, first, lane);
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1);
         }
     };
+    if constexpr (!SRC_ALIGNED) {
+        // src misaligned against dst: whole source lines + a shift across lanes (shift_window)
+        constexpr int M = U * K;
+        const uint8_t* S = a.src_base + A;                       // the window's first source byte
+        const uint32_t o = (uint32_t)((uintptr_t)S & 127u);      // uniform over the batch
+        const uint8_t* L = S - o + 16 * lane;
+        u32x4 c[M + 1], v[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) c[m] = load_line_block<NT>(L + (uint64_t)m * kSpan);
+        c[M] = u32x4{0, 0, 0, 0};
+        if ((uint32_t)lane <= (o >> 4)) c[M] = load_line_block<NT>(L + (uint64_t)M * kSpan);
+        table_issue(a, t, guess_base(a, 0, a.mis, A), lane);
+        np_resolve(a, t, A, lane);
+        switch ((o >> 2) & 3) {   // uniform: constant register indices in each case
+            case 0: shift_window<M, 0>(c, v, o, lane); break;
+            case 1: shift_window<M, 1>(c, v, o, lane); break;
+            case 2: shift_window<M, 2>(c, v, o, lane); break;
+            default: shift_window<M, 3>(c, v, o, lane); break;
+        }
+#pragma unroll
+        for (int m = 0; m < M; ++m) emit(A + (uint64_t)m * kSpan, v[m], m == 0);
+        return;
+    }
+    u32x4 d[U];
+    auto load_step = [&](uint64_t base) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) d[u] = load_vec<true, NT>(a, base + (uint64_t)u * kSpan + 16ull * lane);
+    };
     load_step(A);
-    Table t;
     table_issue(a, t, guess_base(a, 0, a.mis, A), lane);
     np_resolve(a, t, A, lane);
-    uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint64_t base = A + (uint64_t)k * kStep;
         if (k > 0) load_step(base);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t A0 = base + (uint64_t)u * kSpan;
-            const u32x4 m = span_mask(a, t, A0, lane);
-            u32x4 src = d[u];
-            if constexpr (!SRC_ALIGNED) src = shift_in(d[u], d63[u], sh, lane);
-            const u32x4 out = src ^ m;
-            store_vec<NT>(a, A0 + 16ull * lane, out);
-            if constexpr (VAL) {
-                const uint32_t up = (uint32_t)__shfl_up((int)out[3], 1, kWave);
-                validate_span(a, t, A0, out, lane ? up : carry, k == 0 && u == 0, lane);
-                carry = (uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1);
-            }
-        }
+        for (int u = 0; u < U; ++u) emit(base + (uint64_t)u * kSpan, d[u], k == 0 && u == 0);
     }
 }
 
@@ -962,10 +1029,13 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
     // frame-free and with frames, at 64 MiB and at 1 GiB)
     const bool two = flags < 0 || (flags & kTwoSteps);
     a.xcd_remap = (flags >= 0 && (flags & kXcdRemap)) ? 1 : 0;
-    const uint64_t win_vec = 64ull * (uint64_t)cfg.unroll * (two ? 2 : 1);
+    // src misaligned against dst, auto, >= 256 MiB: windows of 4 x 1 KiB (33 source lines per
+    // 4 spans, not 17 per 2): 1 GiB mixed frames 0.88 -> 0.97 of the aligned rate; at 64 MiB
+    // 2 x 1 KiB stays ahead (profiles/r02j_misaligned_sweep.jsonl)
+    const int U = (!aligned && flags < 0 && total >= (256ull << 20)) ? 2 : cfg.unroll;
+    const uint64_t win_vec = 64ull * (uint64_t)U * (two ? 2 : 1);
     a.nwin = (nvec + win_vec - 1) / win_vec;
-    return aligned ? launch_np_u<true>(a, cfg.unroll, nt, two, stream)
-                   : launch_np_u<false>(a, cfg.unroll, nt, two, stream);
+    return aligned ? launch_np_u<true>(a, U, nt, two, stream) : launch_np_u<false>(a, U, nt, two, stream);
 }
 
 

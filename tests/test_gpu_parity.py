@@ -248,6 +248,19 @@ def test_c4_shard_full_exact(torch_cuda):
 
 
 @pytest.mark.slow
+@pytest.mark.parametrize("dst_shift,src_shift", [(0, 3), (5, 12), (0, 9)])
+def test_misaligned_large_batch_exact(torch_cuda, dst_shift, src_shift):
+    """src misaligned against dst at >= 256 MiB (the 4 x 1 KiB line-aligned source windows):
+    320 MiB of C4's mixed frames, out of place, every byte and the guard bytes."""
+    off, keys, _ = synth.config("c4", shard=1)
+    n = int(np.searchsorted(off, 320 << 20, side="right")) - 1
+    off, keys = off[:n + 1].copy(), keys[:n].copy()
+    total = int(off[-1]) + 5                       # a ragged tail after the last frame
+    payload = synth.host_payload(total, synth.SEED, 9)
+    run_case(torch_cuda, payload, off, keys, dst_shift, src_shift)
+
+
+@pytest.mark.slow
 def test_c3_full_properties(torch_cuda):
     """1 GiB: involution over the whole buffer, keystream linearity, oracle on sampled frames."""
     torch = torch_cuda

@@ -24,8 +24,8 @@ for s in $STEPS; do
         timeout -k 10 400 python3 bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err"
         rc=$?
         cat "$OUT/bench.json"; tail -3 "$OUT/bench.err" ;;
-    tests/*)
-        timeout -k 10 ${SUITE_TIMEOUT:-400} python3 -u -m pytest "$s" -x -v --timeout 120 --timeout-method thread \
+    tests|tests/*)
+        timeout -k 10 ${SUITE_TIMEOUT:-400} python3 -u -m pytest "$s" -m gpu -x -v --timeout 120 --timeout-method thread \
             > "$OUT/$name.log" 2>&1
         rc=$?
         tail -3 "$OUT/$name.log" ;;
