@@ -853,8 +853,11 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
         u32x4 c[M + 1], v[M];
 #pragma unroll
         for (int m = 0; m < M; ++m) c[m] = load_line_block<NT>(L + (uint64_t)m * kSpan);
-        c[M] = u32x4{0, 0, 0, 0};
-        if ((uint32_t)lane <= (o >> 4)) c[M] = load_line_block<NT>(L + (uint64_t)M * kSpan);
+        // the line after: lanes 0 .. o/16 hold its blocks; the others re-read lane o/16's
+        // block (same line) instead of branching -- a load under a lane branch is followed
+        // by vmcnt(0), which held the table's trip behind the payload's
+        const uint32_t lm = min((uint32_t)lane, o >> 4);
+        c[M] = load_line_block<NT>(S - o + 16 * lm + (uint64_t)M * kSpan);
         table_issue(a, t, guess_base(a, 0, a.mis, A), lane);
         np_resolve(a, t, A, lane);
         switch ((o >> 2) & 3) {   // uniform: constant register indices in each case
