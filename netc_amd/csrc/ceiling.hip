@@ -42,7 +42,7 @@ __global__ __launch_bounds__(1024) void stream_kernel(u32x4* dst_, const u32x4* 
     const u32x4 k = {key, key, key, key};
     const int lane = threadIdx.x & 63;
     const uint32_t wpb = blockDim.x >> 6;
-    const uint64_t wave = (uint64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     u32x4 acc = {0, 0, 0, 0};
     auto loadc = [&](u32x4(&d)[U], uint64_t c) {
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(1024) void walk_kernel(u32x4* dst_, const u32x4* sr
     const u32x4 kk = {key, key, key, key};
     const int lane = threadIdx.x & 63;
     const uint32_t wpb = blockDim.x >> 6;
-    const uint64_t wave = (uint64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     u32x4 acc = {0, 0, 0, 0};
     uint64_t c, stride, end;

@@ -598,7 +598,7 @@ __global__ __launch_bounds__(256) void encode_frames_kernel(EncArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wpb = blockDim.x / kWave;
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
-    const uint64_t wave = (uint64_t)blockIdx.x * wpb + (threadIdx.x / kWave);
+    const uint64_t wave = (uint64_t)blockIdx.x * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // uniform: scalar branches, exact vmcnt waits
     const uint64_t wire_total = gptr(a.wo)[a.n];
     const uint64_t wlo = a.wmis, whi = a.wmis + wire_total;
     const uint64_t nwin = (whi + kWin - 1) / kWin;
@@ -705,7 +705,7 @@ __device__ __forceinline__ void fix_frame(const EncArgs& a, uint64_t k) {
 __global__ __launch_bounds__(256) void encode_queued_kernel(EncArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / kWave);
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint64_t count = min((uint64_t)*a.defer_count, a.defer_cap);
     const uint64_t wire_total = gptr(a.wo)[a.n];
     const uint64_t wlo = a.wmis, whi = a.wmis + wire_total;

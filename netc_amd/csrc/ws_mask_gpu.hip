@@ -684,7 +684,7 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wpb = blockDim.x / kWave;                     // wavefronts per block
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
-    const uint64_t wave = (uint64_t)blockIdx.x * wpb + (threadIdx.x / kWave);
+    const uint64_t wave = (uint64_t)blockIdx.x * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     if (a.n_dev) {   // frame count produced on the device by an earlier kernel (scan -> unmask)
         a.n = *gptr(a.n_dev);
         a.density = a.total ? (double)a.n / (double)a.total : 0.0;
@@ -819,7 +819,7 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
         const uint64_t nb = gridDim.x, per = nb / 8;
         if (block < per * 8) block = (block % 8) * per + block / 8;
     }
-    const uint64_t wave = block * wpb + (threadIdx.x / kWave);
+    const uint64_t wave = block * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // uniform: scalar branches
     if (wave >= a.nwin) return;
     extern __shared__ uint32_t lds_occupancy_pad[];   // dynamic LDS only limits workgroups per CU
     (void)lds_occupancy_pad;
