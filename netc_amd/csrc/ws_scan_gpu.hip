@@ -1378,7 +1378,7 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
     __syncthreads();
     SCAN_STAMP(4, 1);
     // anchored chunks: one wavefront each
-    const int lane = tid & (kWave - 1), wv = tid / kWave;
+    const int lane = tid & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(tid / kWave);
     for (int q = wv; q < nqa; q += kScanT / kWave) {
         const uint64_t node = qa_node[q], chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
         const uint32_t slot = a.anq[node];
