@@ -592,8 +592,9 @@ __device__ __forceinline__ void finish_chunk(const EncArgs& a, const EncTable& t
 // Chunk = U spans.  Wavefront w of W takes chunks w, w+W, ...  Per trip: the table
 // of chunk c+W (issued a trip ago) is resolved and chunk c+W's loads are issued,
 // chunk c+2W's table is issued, then chunk c (loaded a trip ago) is stored.
-template <int U, bool NT>
-__global__ __launch_bounds__(256) void encode_frames_kernel(EncArgs a) {
+// W: wavefronts per SIMD the register budget must allow (launch_enc_u picks it per batch)
+template <int U, bool NT, int W>
+__global__ __launch_bounds__(256, W) void encode_frames_kernel(EncArgs a) {
     constexpr uint64_t kWin = kSpan * U;
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wpb = blockDim.x / kWave;
@@ -746,14 +747,14 @@ __global__ __launch_bounds__(256) void encode_queued_kernel(EncArgs a) {
     }
 }
 
-template <int U, bool NT>
+template <int U, bool NT, int W>
 static int enc_resident_blocks() {
     static int cache[64] = {0};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
     if (cache[dev] > 0) return cache[dev];
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, encode_frames_kernel<U, NT>, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, encode_frames_kernel<U, NT, W>, 256, 0) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 || cus <= 0)
         return 1024;
     cache[dev] = per_cu * cus;
@@ -863,11 +864,11 @@ static uint64_t dense_bytes() {
     return e ? (uint64_t)strtoull(e, nullptr, 10) : (uint64_t)80;
 }
 
-template <int U>
+template <int U, int W>
 static hipError_t launch_enc_u(EncArgs a, uint64_t wire_bound, bool nt, int max_blocks, hipStream_t stream) {
     const uint64_t nwin = (a.wmis + wire_bound + kSpan * U - 1) / (kSpan * U);
     const uint64_t cap = (uint64_t)(max_blocks > 0 ? max_blocks
-                                                  : (nt ? enc_resident_blocks<U, true>() : enc_resident_blocks<U, false>()));
+                                                  : (nt ? enc_resident_blocks<U, true, W>() : enc_resident_blocks<U, false, W>()));
     const uint64_t want = (nwin + 3) / 4;
     const int blocks = (int)(want < cap ? want : cap);
     if (blocks <= 0) return hipSuccess;
@@ -877,8 +878,8 @@ static hipError_t launch_enc_u(EncArgs a, uint64_t wire_bound, bool nt, int max_
         hipLaunchKernelGGL(encode_queued_kernel, dim3((unsigned)(gb < 8192 ? gb : 8192)), dim3(256), 0, stream, a);
         return hipGetLastError();
     }
-    if (nt) hipLaunchKernelGGL((encode_frames_kernel<U, true>), dim3(blocks), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((encode_frames_kernel<U, false>), dim3(blocks), dim3(256), 0, stream, a);
+    if (nt) hipLaunchKernelGGL((encode_frames_kernel<U, true, W>), dim3(blocks), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((encode_frames_kernel<U, false, W>), dim3(blocks), dim3(256), 0, stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint64_t fix_blocks = (a.n + 255) / 256;   // one thread per frame, up to 64 frames each
@@ -918,10 +919,13 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     // (the vector path would queue most spans and leave a header fixup per frame)
     a.all_spans = src_total < dense_bytes() * n ? 1u : 0u;
     const bool nt = cfg.flags < 0 || (cfg.flags & (kNtLoads | kNtStores));
-    // U = 2 KiB chunks (124 VGPRs: 4 wavefronts per SIMD; measured faster than 4 KiB at
-    // configs 2 and 4) unless netc_gpu_tune's unroll is 8, which selects 4 KiB
-    if (cfg.unroll >= 8) return launch_enc_u<4>(a, wire_bound, nt, cfg.max_blocks, stream);
-    return launch_enc_u<2>(a, wire_bound, nt, cfg.max_blocks, stream);
+    // U = 2 KiB chunks (measured faster than 4 KiB at configs 2 and 4) unless netc_gpu_tune's
+    // unroll is 8, which selects 4 KiB.  Wire up to 256 MiB: 7 wavefronts per SIMD (72 VGPRs;
+    // C2 40.1 -> 39.3 us); larger: 6 (76 VGPRs; C4 418 vs 425 us at 7, 424 at 8 with spills;
+    // profiles/r02k_ab_enc_occupancy.json)
+    if (cfg.unroll >= 8) return launch_enc_u<4, 5>(a, wire_bound, nt, cfg.max_blocks, stream);
+    if (wire_bound <= (256ull << 20)) return launch_enc_u<2, 7>(a, wire_bound, nt, cfg.max_blocks, stream);
+    return launch_enc_u<2, 6>(a, wire_bound, nt, cfg.max_blocks, stream);
 }
 
 }  // namespace netc_gpu
