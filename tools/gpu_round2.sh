@@ -22,6 +22,7 @@ PROFCMD="python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --c5-gib 0 --cpu-sec
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $PROFCMD > $OUT/trace.log 2>&1 || { echo TRACEFAIL; tail -20 $OUT/trace.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "mask_np_kernel" --output-format csv -d $OUT/pmc_fetch -o run -- $PROFCMD --no-copy-ceiling > $OUT/pmc_fetch.log 2>&1 || { echo FETCHFAIL; tail -20 $OUT/pmc_fetch.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "mask_np_kernel" --output-format csv -d $OUT/pmc_write -o run -- $PROFCMD --no-copy-ceiling > $OUT/pmc_write.log 2>&1 || { echo WRITEFAIL; tail -20 $OUT/pmc_write.log; exit 1; }
+[ "${ROWS:-1}" = 0 ] && { echo done; exit 0; }
 cd $R && TAG=$TAG bash tools/prof_rows.sh > $OUT/rows.log 2>&1 || { echo ROWSFAIL; tail -20 $OUT/rows.log; exit 1; }
 tail -3 $OUT/rows.log
 echo done
