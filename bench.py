@@ -10,10 +10,15 @@ in place (the reference's receive direction, src/ws/common.c:317-323).  Each ste
 uses the next of R distinct batches (>= 1 GiB in total) so the 256 MiB Infinity
 Cache cannot serve a batch from the previous touch.
 
-Multi-GPU: one process per GPU (torchrun); every rank masks its own shard of
-frames -- no data-path collective (frames are independent); the
-only collectives are the timing barrier and the gather of every rank's elapsed
-time (the max is the job's; each rank's own rate is reported as per_gpu).
+Multi-GPU: one process per GPU.  Under torchrun WORLD_SIZE must equal --gpus; a
+plain `python bench.py --gpus N` (N > 1) starts torch.distributed.run as a child
+process before anything touches the GPU and exits with its code, and exits 2 when
+fewer than N GPUs are visible -- it never prints an n_gpus = 1 line for N > 1.
+Every rank masks its own shard of frames -- no data-path collective (frames are
+independent); the only collectives are the timing barrier and the
+gather of every rank's elapsed time (the max is the job's; each rank's own rate is
+reported as per_gpu).  At N > 1 a second leg (c4_shards) runs BASELINE config 4:
+a 1 GiB mixed-frame shard per GPU, aggregate and per-GPU GiB/s.
 
 Prints ONE JSON line on rank 0.  Roofline: 2 x payload bytes per launch (read +
 write) / mean kernel duration (HIP events on the launch stream) vs 8.0 TB/s, next
@@ -68,6 +73,8 @@ def parse_args():
     p.add_argument("--pipelined-probe", action="store_true",
                    help="also time two independent batches in flight on two streams (secondary figure; its "
                         "overlapping launches would inflate a rocprof average of the kernel, so it is off by default)")
+    p.add_argument("--no-shard-leg", dest="shard_leg", action="store_false",
+                   help="at N > 1, skip the BASELINE config 4 leg (8 x 1 GiB mixed-frame shards, c4_shards)")
     return p.parse_args()
 
 
@@ -348,16 +355,127 @@ def build_wire(buf, off, keys, limit_frames):
     return np.frombuffer(b"".join(out), dtype=np.uint8)
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N > 1` outside torchrun: one process per GPU.  This process never touches the
+    GPU (device_count() does not initialise HIP on this image); it starts
+    torch.distributed.run as a CHILD with the same arguments and returns the child's exit
+    code, so the driver's `python bench.py --gpus N` yields an n_gpus = N line or fails."""
+    import subprocess
+
+    if "NETC_BENCH_DEVICE" not in os.environ:     # rehearsal (all ranks on one GPU) skips the count
+        import torch
+
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but {have} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def timed_steps(torch, step, steps: int, warmup: int, stream, device, world: int):
+    """W untimed steps, then exactly K steps bracketed by barrier + synchronize on both sides.
+    Returns (this rank's elapsed seconds, mean launch duration in ms from two HIP events on the
+    launch stream).  Per-launch event pairs are NOT recorded inside the region: each event
+    packet breaks the back-to-back dispatch and cost 7-9 us per step on this path
+    (tools/launch_probe.py), which would be measuring the events, not the kernel."""
+    sh = stream.cuda_stream
+    for i in range(warmup):
+        step(i, sh)
+    torch.cuda.synchronize(device)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(steps):
+        step(warmup + i, sh)
+    ev1.record(stream)
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0            # this rank's K steps, sync to sync
+    if world > 1:
+        torch.distributed.barrier()               # closing bracket; the max over ranks follows
+    return elapsed, ev0.elapsed_time(ev1) / steps
+
+
+def gather_max(torch, values, world: int, coll_dev):
+    """all_gather one float64 vector per rank; returns the list of per-rank vectors."""
+    if world == 1:
+        return [list(values)]
+    mine = torch.tensor(values, dtype=torch.float64, device=coll_dev)
+    gathered = [torch.zeros_like(mine) for _ in range(world)]
+    torch.distributed.all_gather(gathered, mine)
+    return [[float(x) for x in g] for g in gathered]
+
+
+def shard_leg(torch, nm, entry, local, rank, world, device, stream, coll_dev, args):
+    """BASELINE config 4 at N GPUs: every rank masks its own 1 GiB shard of mixed 256 B - 64 KiB
+    frames (own seed per rank), rotating over 2 such batches, K steps timed as the headline.
+    Aggregate = all ranks' payload bytes / the slowest rank's time; per-GPU rates beside it;
+    every rank's last batch checked (involution + every frame's keystream)."""
+    batches, total, nframes = make_batches(torch, "c4", rank, 2 << 30, device)
+    prepared = [(p.data_ptr(), o.data_ptr(), k.data_ptr()) for p, o, k in batches]
+
+    def step(i, s_handle):
+        p, o, k = prepared[i % len(prepared)]
+        rc = entry(local, p, p, total, o, k, nframes, s_handle)
+        if rc != 0:
+            raise nm.NetcGpuError(rc, "c4 shard leg")
+
+    steps = max(5, args.steps // 4)
+    elapsed, kern = timed_steps(torch, step, steps, 2, stream, device, world)
+    off_h, _, _ = synth_config("c4", rank)
+    last = batches[(2 + steps - 1) % len(batches)]
+    check = verify_step(torch, nm, last, total, nframes, off_h, last[2].cpu().numpy().view(np.uint32), stream)
+    ok = int(check["involution"] and check["keystream_all_frames"])
+    rows = gather_max(torch, [elapsed, kern, float(total), float(ok)], world, coll_dev)
+    del batches, prepared
+    torch.cuda.empty_cache()
+    t_max = max(r[0] for r in rows)
+    return {
+        "workload": "c4: " + WORKLOADS["c4"],
+        "value": round(sum(r[2] for r in rows) * steps / t_max / GIB, 3),
+        "unit": "GiB/s aggregate",
+        "steps": steps,
+        "per_gpu": [round(r[2] * steps / r[0] / GIB, 3) for r in rows],
+        "kernel_frac_of_hbm": [round(2.0 * r[2] / (r[1] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) for r in rows],
+        "verified_all_ranks": all(r[3] == 1.0 for r in rows),
+        "note": "BASELINE config 4 (8 x 1 GiB independent shards, no collective); secondary to the headline",
+    }
+
+
 def main():
     args = parse_args()
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world, rank, local = dist_env()
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr, flush=True)
+        sys.exit(2)
     import torch
 
     # NETC_BENCH_DEVICE / NETC_BENCH_BACKEND=gloo: rehearsal of the N-rank path on a
     # one-GPU box (every rank on one device, timing collectives on the CPU); the
     # real multi-GPU run uses one GPU per rank and RCCL ("nccl") for the barrier.
+    rehearsal = "NETC_BENCH_DEVICE" in os.environ
     local = int(os.environ.get("NETC_BENCH_DEVICE", local))
     backend = os.environ.get("NETC_BENCH_BACKEND", "nccl")
+    if not rehearsal and torch.cuda.device_count() < world:
+        print(f"bench.py: {world} ranks but {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr, flush=True)
+        sys.exit(2)
     if world > 1:
         import torch.distributed as dist
 
@@ -393,31 +511,8 @@ def main():
         if rc != 0:
             raise nm.NetcGpuError(rc, _lib.gpu().netc_gpu_strerror().decode())
 
-    sh = stream.cuda_stream
-    for i in range(args.warmup):
-        step(i, sh)
-    torch.cuda.synchronize(device)
-
-    # Timed region: K back-to-back launches on one stream.  Two HIP events on that
-    # stream bracket the launches: (end - start) / K is the average launch duration
-    # on the GPU (kernel time plus the dependent-launch boundary, no host time).
-    # Per-launch event pairs are NOT recorded inside the region: each event packet
-    # breaks the back-to-back dispatch and cost 7-9 us per step on this path
-    # (tools/launch_probe.py), which would be measuring the events, not the kernel.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        step(args.warmup + i, sh)
-    ev1.record(stream)
-    torch.cuda.synchronize(device)
-    elapsed = time.perf_counter() - t0            # this rank's K steps, sync to sync
-    if world > 1:
-        torch.distributed.barrier()               # closing bracket; the max over ranks follows
-    kern_ms = np.array([ev0.elapsed_time(ev1) / args.steps])
+    # Timed region: K back-to-back launches on one stream (timed_steps).
+    elapsed, kern_own = timed_steps(torch, step, args.steps, args.warmup, stream, device, world)
 
     # secondary figure: the same steps with two batches in flight on two HIP streams
     # (independent batches, as a serving loop would pipeline them); not the headline
@@ -437,17 +532,11 @@ def main():
         if world > 1:
             torch.distributed.barrier()
 
-    per_rank_elapsed = [elapsed]
-    if world > 1:
-        mine = torch.tensor([elapsed, kern_ms.mean(), pipelined or 0.0], dtype=torch.float64, device=coll_dev)
-        gathered = [torch.zeros_like(mine) for _ in range(world)]
-        torch.distributed.all_gather(gathered, mine)
-        per_rank_elapsed = [float(g[0]) for g in gathered]
-        elapsed = max(per_rank_elapsed)
-        kern_mean = max(float(g[1]) for g in gathered)
-        pipelined = max(float(g[2]) for g in gathered) or None
-    else:
-        kern_mean = float(kern_ms.mean())
+    rows = gather_max(torch, [elapsed, kern_own, pipelined or 0.0], world, coll_dev)
+    per_rank_elapsed = [r[0] for r in rows]
+    elapsed = max(per_rank_elapsed)
+    kern_mean = max(r[1] for r in rows)
+    pipelined = max(r[2] for r in rows) or None
 
     ceilings = None
     shapes = None
@@ -459,10 +548,15 @@ def main():
     last = batches[(args.warmup + args.steps - 1) % nb]
     keys_h = last[2].cpu().numpy().view(np.uint32)   # this batch's own keys
     check = verify_step(torch, nm, last, total, nframes, off_h, keys_h, stream)
-    if world > 1:
-        ok = torch.tensor([int(check["involution"] and check["keystream_all_frames"])], device=coll_dev)
-        torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
-        check["all_ranks_ok"] = bool(ok.item())
+    ok_rows = gather_max(torch, [float(check["involution"] and check["keystream_all_frames"])], world, coll_dev)
+    check["ranks_verified"] = int(sum(r[0] for r in ok_rows))
+    check["all_ranks_ok"] = check["ranks_verified"] == world
+
+    shards = None
+    if world > 1 and args.shard_leg:
+        del batches, prepared
+        torch.cuda.empty_cache()
+        shards = shard_leg(torch, nm, entry, local, rank, world, device, stream, coll_dev, args)
 
     cpu = None
     c5 = None
@@ -496,8 +590,9 @@ def main():
                 "frames_per_gpu": nframes,
                 "batch_bytes_per_gpu": total,
                 "rotation_batches": args.rotation_bytes and max(2, -(-args.rotation_bytes // total)),
-                "parallelism": f"shard{world} (independent frames, no collective)",
+                "parallelism": f"shard{world} (independent frames, one process per GPU, no collective)",
                 "entry": "netc_gpu_mask_batch (include/ws/mask.h)",
+                "devices": "rehearsal: every rank on one GPU" if rehearsal else "one GPU per rank",
             },
             "roofline": {
                 "bound": "hbm",
@@ -507,7 +602,8 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic_per_launch(args.workload),
                 "kernel_ms_mean": round(kern_mean, 5),
-                "kernel_timing": "HIP events on the launch stream around the K timed launches, / K",
+                "kernel_timing": "HIP events on the launch stream around the K timed launches, / K "
+                                 "(slowest rank)",
                 "algorithmic_bytes_per_launch": 2 * total,
                 "ceilings": ceilings,
                 "frac_of_xor_stream": round(achieved / ceilings["xor_inplace_GBps"], 4) if ceilings else None,
@@ -515,6 +611,7 @@ def main():
             },
             "per_gpu": [round(float(total) * args.steps / e / GIB, 3) for e in per_rank_elapsed],
             "verified": check,
+            "c4_shards": shards,
             "c5_host_to_host": c5,
             "cpu_baseline": cpu,
             "pipelined_2stream": None if not pipelined else {

@@ -99,13 +99,14 @@ int netc_gpu_encode_frames(int device, void *d_wire, size_t wire_capacity, uint6
  * (ERROR = CONSUMED = its offset).  Frames past max_frames are counted but not
  * recorded.  Asynchronous on `stream`; read d_result after synchronising.
  * Scratch memory is allocated on first use per (device, stream) and reused until
- * netc_gpu_scan_release(device, stream) frees it (call that before destroying a
- * stream the scan ran on).
+ * netc_gpu_stream_release(device, stream) (include/ws/mask.h) frees it: call that
+ * before destroying a stream the scan ran on.
  */
 int netc_gpu_scan_frames(int device, const void *d_wire, size_t len, uint64_t start, int flags, uint64_t *d_hdr,
                          uint32_t *d_keys, uint8_t *d_b0, size_t max_frames, uint64_t *d_result, void *stream);
 
-/** Frees the scan scratch kept for (device, stream); waits for that stream first.  0 or a code. */
+/** Same as netc_gpu_stream_release (include/ws/mask.h): frees ALL scratch kept for
+ *  (device, stream) -- scan, assembly, UTF-8 flags; waits for that stream first.  0 or a code. */
 int netc_gpu_scan_release(int device, void *stream);
 
 /**

@@ -102,8 +102,9 @@ int netc_gpu_init(int device);
  * chunks — where max_blocks caps the workgroups (0 = exactly the workgroups the
  * device holds at once); max_blocks is ignored otherwise.  The frame assembly of
  * include/ws/frame.h reads the same knob: unroll 8 selects 4 KiB chunks there,
- * anything else 2 KiB, and it always walks persistently.  Diagnostic knob: call
- * before launching work; it is not synchronised with concurrent launches.
+ * anything else 2 KiB, and it always walks persistently.  Diagnostic knob.  The
+ * shape is one atomic word: a launch on another thread sees the old shape or the
+ * new one, never a mix.
  */
 #define NETC_GPU_TUNE_AUTO       -1
 #define NETC_GPU_TUNE_NT_LOADS    1   /* non-temporal payload loads                        */
@@ -112,6 +113,34 @@ int netc_gpu_init(int device);
 #define NETC_GPU_TUNE_TWO_STEPS   8   /* a wavefront's window is two steps of unroll KiB   */
 #define NETC_GPU_TUNE_XCD_ORDER  16   /* each XCD takes a contiguous share of the windows  */
 int netc_gpu_tune(int unroll, int max_blocks, int flags);
+
+/**
+ * Measurement / test knobs of the §8(f) kernels (defaults in brackets).  Each is one
+ * atomic word, seeded once per process from the environment variable named beside
+ * it; value < 0 restores the default.  Returns 0 or NETC_GPU_EINVAL.
+ *   ENC_DENSE_BYTES    mean payload bytes per frame under which netc_gpu_encode_frames
+ *                      composes every span per lane [80]          (NETC_ENC_DENSE_BYTES)
+ *   ENC_SCAN_PER       frames per thread of the wire-offsets scan, 1/2/4/8/16
+ *                      [4 up to 256 Ki frames, else 16]            (NETC_ENC_SCAN_PER)
+ *   SCAN_FAST_RANK     0 sends the frame scan's list ranking through the generic
+ *                      loop [1]                                     (NETC_SCAN_FAST_RANK)
+ *   SCAN_ANCHOR_SLOTS  cap on the frame scan's anchor slots [all]  (NETC_SCAN_ANCHOR_SLOTS)
+ */
+#define NETC_GPU_KNOB_ENC_DENSE_BYTES   1
+#define NETC_GPU_KNOB_ENC_SCAN_PER      2
+#define NETC_GPU_KNOB_SCAN_FAST_RANK    3
+#define NETC_GPU_KNOB_SCAN_ANCHOR_SLOTS 4
+int netc_gpu_knob(int knob, int64_t value);
+
+/**
+ * Free every piece of scratch this library keeps for (device, stream): the frame
+ * scan's (netc_gpu_scan_frames, include/ws/frame.h), the frame assembly's
+ * (netc_gpu_encode_frames) and the UTF-8 flags of netc_gpu_unmask_validate.  It
+ * synchronises the stream first.  Call it before destroying a stream those entries
+ * ran on; a later call on the stream allocates afresh.  netc_gpu_scan_release is
+ * the same call under its round-1 name.
+ */
+int netc_gpu_stream_release(int device, void *stream);
 
 /** Message for the last failing netc_gpu_* call on this thread ("" if none). */
 const char *netc_gpu_strerror(void);

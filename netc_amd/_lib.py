@@ -115,6 +115,10 @@ def gpu() -> ctypes.CDLL:
             lib.netc_gpu_scan_frames.restype = ctypes.c_int
             lib.netc_gpu_scan_release.argtypes = [ctypes.c_int, vp]
             lib.netc_gpu_scan_release.restype = ctypes.c_int
+            lib.netc_gpu_stream_release.argtypes = [ctypes.c_int, vp]
+            lib.netc_gpu_stream_release.restype = ctypes.c_int
+            lib.netc_gpu_knob.argtypes = [ctypes.c_int, ctypes.c_int64]
+            lib.netc_gpu_knob.restype = ctypes.c_int
             lib.netc_gpu_scan_diag.argtypes = [ctypes.c_int, vp]
             lib.netc_gpu_scan_diag.restype = ctypes.c_int64
             lib.netc_gpu_unmask_frames.argtypes = [ctypes.c_int, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp, vp]

@@ -35,6 +35,7 @@
 #include <mutex>
 #include <type_traits>
 #include <utility>
+#include <vector>
 
 #include "gpu_util.h"
 #include "ws_mask_gpu.h"
@@ -764,14 +765,16 @@ static int enc_resident_blocks() {
 // Per (device, stream) scratch: the scan's status words (one per tile) and the
 // span queue.  Work queued on one stream runs in order, so it can share them (the
 // epoch tells scans apart); streams may run concurrently and get their own.
-// Arrays grow geometrically and are never freed: an outgrown one may still be
-// read by work queued before the growth.
+// Arrays grow geometrically; an outgrown one may still be read by work queued
+// before the growth, so it is kept (retired) until netc_gpu_stream_release frees
+// the stream's scratch, after synchronising it.
 struct EncScratch {
     uint64_t* status = nullptr;
     uint64_t tiles = 0;
     uint32_t epoch = 0;
     uint64_t* defer = nullptr;   // defer[0 .. cap), then the counter word
     uint64_t defer_cap = 0;
+    std::vector<void*> retired;
 };
 
 static std::map<std::pair<int, hipStream_t>, EncScratch> g_scratch;
@@ -788,7 +791,11 @@ static hipError_t scratch_for(hipStream_t stream, uint64_t tiles, uint64_t spans
         uint64_t want = sc.tiles ? 2 * sc.tiles : 1024;
         while (want < tiles) want *= 2;
         if ((e = hipMalloc(&p, want * sizeof(uint64_t))) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(p, 0, want * sizeof(uint64_t), stream)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(p, 0, want * sizeof(uint64_t), stream)) != hipSuccess) {
+            (void)hipFree(p);
+            return e;
+        }
+        if (sc.status) sc.retired.push_back(sc.status);
         sc.status = p;
         sc.tiles = want;
         sc.epoch = 0;
@@ -798,6 +805,7 @@ static hipError_t scratch_for(hipStream_t stream, uint64_t tiles, uint64_t spans
         uint64_t want = sc.defer_cap ? 2 * sc.defer_cap : 4096;
         while (want < spans) want *= 2;
         if ((e = hipMalloc(&p, (want + 1) * sizeof(uint64_t))) != hipSuccess) return e;
+        if (sc.defer) sc.retired.push_back(sc.defer);
         sc.defer = p;
         sc.defer_cap = want;
     }
@@ -806,19 +814,38 @@ static hipError_t scratch_for(hipStream_t stream, uint64_t tiles, uint64_t spans
         if ((e = hipMemsetAsync(sc.status, 0, sc.tiles * sizeof(uint64_t), stream)) != hipSuccess) return e;
         sc.epoch = 1;
     }
-    out = sc;
+    out.status = sc.status;
+    out.tiles = sc.tiles;
+    out.epoch = sc.epoch;
+    out.defer = sc.defer;
+    out.defer_cap = sc.defer_cap;
     return hipSuccess;
+}
+
+int release_enc_scratch(int device, hipStream_t stream) {   // the stream is synchronised
+    EncScratch sc;
+    {
+        std::lock_guard<std::mutex> g(g_scratch_mu);
+        auto it = g_scratch.find({device, stream});
+        if (it == g_scratch.end()) return 0;
+        sc = std::move(it->second);
+        g_scratch.erase(it);
+    }
+    if (sc.status) (void)hipFree(sc.status);
+    if (sc.defer) (void)hipFree(sc.defer);
+    for (void* p : sc.retired) (void)hipFree(p);
+    return 1;
 }
 
 // frames per thread of the wire-offsets scan: tiles of 1,024 frames up to 256 Ki frames
 // (C2 shape, one box: 1 / 2 / 4 / 8 / 16 frames per thread gave 43.9 / 43.2 / 42.3 /
 // 42.8 / 44.2 us per call), tiles of 4,096 frames above (1-8 Mi frames of 8-64 B: the
 // look-back over 4x the tiles cost more than the shorter tiles saved).
-// NETC_ENC_SCAN_PER overrides, read per call: measurement.
+// NETC_GPU_KNOB_ENC_SCAN_PER (env NETC_ENC_SCAN_PER) overrides: measurement.
 static int scan_per(uint64_t n) {
-    const char* e = getenv("NETC_ENC_SCAN_PER");
+    const int64_t k = knob(NETC_GPU_KNOB_ENC_SCAN_PER);
     const int dflt = n <= (256u << 10) ? 4 : 16;
-    const int v = e ? atoi(e) : dflt;
+    const int v = k >= 0 ? (int)k : dflt;
     return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : dflt;
 }
 
@@ -857,11 +884,11 @@ hipError_t launch_wire_offsets(const uint64_t* off, uint64_t n, bool masked, uin
 }
 
 // mean payload bytes per frame under which a batch takes the dense compose path
-// (NETC_ENC_DENSE_BYTES overrides, read per call: measurement and the parity tests
-// run both paths over the same batches; 0 = never dense)
+// (NETC_GPU_KNOB_ENC_DENSE_BYTES overrides: measurement, and the parity tests run both
+// paths over the same batches; 0 = never dense)
 static uint64_t dense_bytes() {
-    const char* e = getenv("NETC_ENC_DENSE_BYTES");
-    return e ? (uint64_t)strtoull(e, nullptr, 10) : (uint64_t)80;
+    const int64_t k = knob(NETC_GPU_KNOB_ENC_DENSE_BYTES);
+    return k >= 0 ? (uint64_t)k : (uint64_t)80;
 }
 
 template <int U, int W>

@@ -69,7 +69,7 @@ struct IngestSlot {
     uint64_t* h_hdr = nullptr;   // pinned descriptor copies
     uint32_t* h_keys = nullptr;
     uint8_t* h_b0 = nullptr;
-    uint64_t* h_res = nullptr;   // pinned: frames, consumed, error
+    uint64_t* h_res = nullptr;   // pinned: frames, consumed, error, then the scan's diag word (GPU scan)
     hipStream_t stream = nullptr;
     hipEvent_t scanned = nullptr, done = nullptr;
     netc_gpu::ScanScratch* scratch = nullptr;   // the frame scan's device scratch, sized for the slot
@@ -82,6 +82,7 @@ struct IngestSlot {
     uint64_t cut = 0;            // end of the last complete frame (slot coordinates)
     uint64_t err = ~0ull;        // offset of a rejected header (strict), or ~0
     bool host_walk = false;      // frames found by the host header walk (descriptors already in h_*)
+    bool slow_scan = false;      // the GPU scan walked part of the slot serially (diag != 0, e.g. RSV headers)
 };
 
 struct DeviceGuard {
@@ -165,7 +166,7 @@ int alloc_slot(const netc_ws_ingest* g, IngestSlot& s) {
         (e = hipHostMalloc((void**)&s.h_hdr, (mf + 1) * sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc((void**)&s.h_keys, mf * sizeof(uint32_t), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc((void**)&s.h_b0, mf, hipHostMallocDefault)) != hipSuccess ||
-        (e = hipHostMalloc((void**)&s.h_res, 3 * sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess)
+        (e = hipHostMalloc((void**)&s.h_res, 4 * sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess)
         return api_fail_hip(NETC_GPU_ENOMEM, "ingest: pinned host allocation", e);
     if ((e = hipMalloc((void**)&s.d_buf, g->cap)) != hipSuccess ||
         (e = hipMalloc((void**)&s.d_hdr, (mf + 1) * sizeof(uint64_t))) != hipSuccess ||
@@ -195,6 +196,7 @@ int resolve(netc_ws_ingest* g, IngestSlot& s) {
     s.frames = n;
     s.cut = consumed;
     s.err = s.h_res[2];
+    s.slow_scan = (uint32_t)s.h_res[3] != 0;   // copied behind the result, before "scanned"
     if ((e = hipMemcpyAsync(s.h_hdr, s.d_hdr, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream)) !=
             hipSuccess ||
         (n && (e = hipMemcpyAsync(s.h_keys, s.d_keys, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream)) !=
@@ -210,7 +212,13 @@ int resolve(netc_ws_ingest* g, IngestSlot& s) {
 // an extension such as permessage-deflate; a reserved opcode; a fragmented control frame):
 // the GPU scan's parallel pass filters like strict mode except for MASK and would stop at
 // the first of them and walk on serially, so such streams go to the host walk.
+//   * GPU-scanned slot: the scan says so itself -- its diag word (nonzero when any part
+//     of the slot was walked serially) is copied to h_res[3] before "scanned", so
+//     resolve() reads it with the result.  The slot's descriptors (h_b0) are NOT read
+//     here: their copy back is queued behind the unmask and may still be running.
+//   * host-walked slot: h_b0 was written by the walk itself, before the submission.
 bool unchecked_headers(const IngestSlot& p) {
+    if (!p.host_walk) return p.slow_scan;
     uint32_t bad = 0;
     for (uint64_t k = 0; k < p.frames; ++k) {
         const uint32_t b = p.h_b0[k], op = b & 0x0F;
@@ -270,6 +278,7 @@ int submit_cur(netc_ws_ingest* g) {
     s.frames = s.cut = 0;
     s.err = ~0ull;
     s.host_walk = host_walk;
+    s.slow_scan = false;
     const uint64_t len = carry + s.fill;
     hipError_t e;
     if (host_walk) {
@@ -301,8 +310,11 @@ int submit_cur(netc_ws_ingest* g) {
                                               g->max_frames, s.d_res, s.stream, s.scratch)) != hipSuccess)
             return api_fail_hip(e == hipErrorOutOfMemory ? NETC_GPU_ENOMEM : NETC_GPU_ELAUNCH, "ingest: frame scan",
                                 e);
+        s.h_res[3] = 0;
         if ((e = hipMemcpyAsync(s.h_res, s.d_res, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream)) !=
                 hipSuccess ||
+            (e = hipMemcpyAsync(s.h_res + 3, netc_gpu::scan_scratch_diag_word(s.scratch), sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
             (e = hipEventRecord(s.scanned, s.stream)) != hipSuccess)
             return api_fail_hip(NETC_GPU_ERUNTIME, "ingest: result copy", e);
         ++g->n_gpu;

@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <utility>
@@ -25,7 +26,38 @@ extern __thread int netc_errno_reason;
 namespace {
 
 thread_local char g_err[512];
-netc_gpu::LaunchCfg g_cfg;   // process-wide tuning (netc_gpu_tune); read-mostly
+
+// Process-wide launch shape (netc_gpu_tune) as ONE atomic word, so a launch on another
+// thread reads either the old shape or the new one, never a mix: bits 0-7 unroll, 8-39
+// max_blocks, 40-63 flags + 1 (flags is -1 for auto).
+uint64_t pack_cfg(int unroll, int max_blocks, int flags) {
+    return (uint64_t)(uint8_t)unroll | ((uint64_t)(uint32_t)max_blocks << 8) | ((uint64_t)(uint32_t)(flags + 1) << 40);
+}
+std::atomic<uint64_t> g_cfg_word{pack_cfg(1, 0, -1)};
+
+netc_gpu::LaunchCfg cfg_now() {
+    const uint64_t w = g_cfg_word.load(std::memory_order_acquire);
+    netc_gpu::LaunchCfg c;
+    c.unroll = (int)(w & 0xFF);
+    c.max_blocks = (int)((w >> 8) & 0xFFFFFFFFu);
+    c.flags = (int)((w >> 40) & 0xFFFFFF) - 1;
+    return c;
+}
+
+// Measurement / test knobs (netc_gpu_knob).  Seeded once per process from the environment
+// (tools/ sweeps set NETC_ENC_SCAN_PER=...), then changed only through netc_gpu_knob; the
+// launch paths read one atomic word, never getenv.
+constexpr int kKnobs = 8;
+std::atomic<int64_t> g_knob[kKnobs];
+std::once_flag g_knob_once;
+void knobs_init() {
+    static const char* const env[kKnobs] = {nullptr, "NETC_ENC_DENSE_BYTES", "NETC_ENC_SCAN_PER", "NETC_SCAN_FAST_RANK",
+                                            "NETC_SCAN_ANCHOR_SLOTS", nullptr, nullptr, nullptr};
+    for (int k = 0; k < kKnobs; ++k) {
+        const char* e = env[k] ? getenv(env[k]) : nullptr;
+        g_knob[k].store(e && *e ? (int64_t)strtoll(e, nullptr, 10) : -1, std::memory_order_relaxed);
+    }
+}
 
 int fail(int code, const char* fmt, ...) {
     va_list ap;
@@ -94,9 +126,68 @@ int mask_batch_on_current(void* d_dst, const void* d_src, size_t total, const ui
     if (nframes && !d_keys) return fail(NETC_GPU_EINVAL, "null keys with %zu frames", nframes);
     if (partial_overlap(d_dst, d_src, total)) return fail(NETC_GPU_EINVAL, "dst and src partially overlap");
     hipError_t e = netc_gpu::launch_mask_frames((uint8_t*)d_dst, (const uint8_t*)d_src, total, d_off, d_keys,
-                                                nframes, stream, g_cfg);
+                                                nframes, stream, cfg_now());
     if (e != hipSuccess) return fail_hip(NETC_GPU_ELAUNCH, "mask kernel launch", e);
     return 0;
+}
+
+// Per (device, stream) flag scratch of netc_gpu_unmask_validate, grown geometrically.
+// A call flags frames with its own tag (1..255), so the flags need clearing only when
+// the scratch is new and when the tags wrap.  Outgrown arrays are kept (work queued
+// before the growth may still use them) until netc_gpu_stream_release frees them all.
+struct FlagScratch {
+    int device;
+    hipStream_t stream;
+    uint8_t* p;
+    size_t cap;
+    uint8_t tag;
+    std::vector<void*> retired;
+};
+std::mutex g_flag_mu;
+std::vector<FlagScratch> g_flags;
+
+int validate_scratch(int device, hipStream_t stream, size_t nframes, uint8_t** verr, uint8_t* tag) {
+    std::lock_guard<std::mutex> lk(g_flag_mu);
+    auto it = std::find_if(g_flags.begin(), g_flags.end(),
+                           [&](const FlagScratch& f) { return f.device == device && f.stream == stream; });
+    if (it == g_flags.end()) {
+        g_flags.push_back({device, stream, nullptr, 0, 0, {}});
+        it = g_flags.end() - 1;
+    }
+    bool clear = false;
+    if (it->cap < nframes) {
+        size_t want = it->cap ? 2 * it->cap : 65536;
+        while (want < nframes) want *= 2;
+        void* p = nullptr;
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) return fail_hip(NETC_GPU_ENOMEM, "validation scratch", e);
+        if (it->p) it->retired.push_back(it->p);
+        it->p = (uint8_t*)p;
+        it->cap = want;
+        it->tag = 0;
+    }
+    if (it->tag == 0xFF || it->tag == 0) {
+        it->tag = 0;
+        clear = true;
+    }
+    *tag = ++it->tag;
+    *verr = it->p;
+    if (clear) {
+        hipError_t e = hipMemsetAsync(it->p, 0, it->cap, stream);
+        if (e != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "validation scratch clear", e);
+    }
+    return 0;
+}
+
+int validate_scratch_release(int device, hipStream_t stream) {   // the stream is synchronised
+    std::lock_guard<std::mutex> lk(g_flag_mu);
+    auto it = std::find_if(g_flags.begin(), g_flags.end(),
+                           [&](const FlagScratch& f) { return f.device == device && f.stream == stream; });
+    if (it == g_flags.end()) return 0;
+    if (it->p) (void)hipFree(it->p);
+    for (void* q : it->retired) (void)hipFree(q);
+    g_flags.erase(it);
+    return 1;
 }
 
 }  // namespace
@@ -113,7 +204,11 @@ int api_fail(int code, const char* fmt, ...) {
 }
 int api_fail_hip(int code, const char* what, hipError_t e) { return fail_hip(code, what, e); }
 int api_check_device(int device) { return check_device(device); }
-const LaunchCfg& api_cfg() { return g_cfg; }
+LaunchCfg api_cfg() { return cfg_now(); }
+int64_t knob(int k) {
+    std::call_once(g_knob_once, knobs_init);
+    return k > 0 && k < kKnobs ? g_knob[k].load(std::memory_order_relaxed) : -1;
+}
 }  // namespace netc_gpu
 
 extern "C" {
@@ -139,9 +234,15 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags) {
         (flags & ~(NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES | NETC_GPU_TUNE_PERSISTENT |
                    NETC_GPU_TUNE_TWO_STEPS | NETC_GPU_TUNE_XCD_ORDER)))
         return fail(NETC_GPU_EINVAL, "unknown tune flags");
-    g_cfg.unroll = unroll;
-    g_cfg.max_blocks = max_blocks;
-    g_cfg.flags = flags;
+    g_cfg_word.store(pack_cfg(unroll, max_blocks, flags), std::memory_order_release);
+    return 0;
+}
+
+int netc_gpu_knob(int knob, int64_t value) {
+    if (knob < NETC_GPU_KNOB_ENC_DENSE_BYTES || knob > NETC_GPU_KNOB_SCAN_ANCHOR_SLOTS)
+        return fail(NETC_GPU_EINVAL, "unknown knob %d", knob);
+    std::call_once(g_knob_once, knobs_init);
+    g_knob[knob].store(value < 0 ? -1 : value, std::memory_order_relaxed);
     return 0;
 }
 
@@ -164,53 +265,12 @@ int netc_gpu_unmask_validate(int device, void* d_dst, const void* d_src, size_t 
     if (partial_overlap(d_dst, d_src, total_bytes)) return fail(NETC_GPU_EINVAL, "dst and src partially overlap");
     DeviceGuard g(device);
     if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
-    // per (device, stream) flag scratch, grown geometrically, never freed (queued work
-    // may still use it).  A call flags frames with its own tag (1..255), so the flags
-    // need clearing only when the scratch is new and when the tags wrap.
-    struct FlagScratch {
-        int device;
-        void* stream;
-        uint8_t* p;
-        size_t cap;
-        uint8_t tag;
-    };
-    static std::mutex mu;
-    static std::vector<FlagScratch> scratch;
     uint8_t* verr = nullptr;
     uint8_t tag = 0;
-    bool clear = false;
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        auto it = std::find_if(scratch.begin(), scratch.end(),
-                               [&](const FlagScratch& f) { return f.device == device && f.stream == stream; });
-        if (it == scratch.end()) {
-            scratch.push_back({device, stream, nullptr, 0, 0});
-            it = scratch.end() - 1;
-        }
-        if (it->cap < nframes) {
-            size_t want = it->cap ? 2 * it->cap : 65536;
-            while (want < nframes) want *= 2;
-            void* p = nullptr;
-            hipError_t e = hipMalloc(&p, want);
-            if (e != hipSuccess) return fail_hip(NETC_GPU_ENOMEM, "validation scratch", e);
-            it->p = (uint8_t*)p;
-            it->cap = want;
-            it->tag = 0;
-        }
-        if (it->tag == 0xFF || it->tag == 0) {
-            it->tag = 0;
-            clear = true;
-        }
-        tag = ++it->tag;
-        verr = it->p;
-        if (clear) {
-            hipError_t e = hipMemsetAsync(verr, 0, it->cap, (hipStream_t)stream);
-            if (e != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "validation scratch clear", e);
-        }
-    }
+    if (int r = validate_scratch(device, (hipStream_t)stream, nframes, &verr, &tag)) return r;
     hipError_t e = netc_gpu::launch_mask_validate((uint8_t*)d_dst, (const uint8_t*)d_src, total_bytes,
                                                   d_frame_offsets, d_keys, d_header0, nframes, verr, tag, d_valid,
-                                                  (hipStream_t)stream, g_cfg);
+                                                  (hipStream_t)stream, cfg_now());
     if (e != hipSuccess) return fail_hip(NETC_GPU_ELAUNCH, "unmask + validate launch", e);
     return 0;
 }
@@ -272,7 +332,7 @@ int netc_gpu_encode_frames(int device, void* d_wire, size_t wire_capacity, uint6
     if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
     hipError_t e = netc_gpu::launch_encode_frames((uint8_t*)d_wire, bound, (const uint8_t*)d_payload, total_bytes,
                                                   d_frame_offsets, d_keys, d_header0, nframes, masked != 0,
-                                                  d_wire_offsets, (hipStream_t)stream, g_cfg);
+                                                  d_wire_offsets, (hipStream_t)stream, cfg_now());
     if (e != hipSuccess) return fail_hip(NETC_GPU_ELAUNCH, "frame assembly launch", e);
     return 0;
 }
@@ -294,16 +354,20 @@ int netc_gpu_scan_frames(int device, const void* d_wire, size_t len, uint64_t st
     return 0;
 }
 
-int netc_gpu_scan_release(int device, void* stream) {
+int netc_gpu_stream_release(int device, void* stream) {
     if (int r = check_device(device)) return r;
     DeviceGuard g(device);
     if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
-    // queued scans on that stream may still use the scratch
+    // work queued on that stream may still use the scratch
     hipError_t e = hipStreamSynchronize((hipStream_t)stream);
     if (e != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipStreamSynchronize", e);
-    (void)netc_gpu::release_stream_scratch(device, (hipStream_t)stream);
+    (void)netc_gpu::release_stream_scratch(device, (hipStream_t)stream);   // frame scan
+    (void)netc_gpu::release_enc_scratch(device, (hipStream_t)stream);      // frame assembly
+    (void)validate_scratch_release(device, (hipStream_t)stream);           // UTF-8 flags
     return 0;
 }
+
+int netc_gpu_scan_release(int device, void* stream) { return netc_gpu_stream_release(device, stream); }
 
 int64_t netc_gpu_scan_diag(int device, void* stream) {
     if (int r = check_device(device)) return r;
@@ -323,7 +387,7 @@ int netc_gpu_unmask_frames(int device, void* d_wire, size_t len, const uint64_t*
     DeviceGuard g(device);
     if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
     hipError_t e = netc_gpu::launch_unmask_scanned((uint8_t*)d_wire, len, d_hdr, d_keys, max_frames, d_result,
-                                                   (hipStream_t)stream, g_cfg);
+                                                   (hipStream_t)stream, cfg_now());
     if (e != hipSuccess) return fail_hip(NETC_GPU_ELAUNCH, "unmask launch", e);
     return 0;
 }

@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/ws/mask.h"   // NETC_GPU_KNOB_*
+
 namespace netc_gpu {
 
 // Kernel arguments (passed by value in the kernarg segment).
@@ -57,6 +59,7 @@ struct ScanScratch;
 ScanScratch* scan_scratch_new();
 void scan_scratch_free(ScanScratch* s);   // no work using it may be queued
 hipError_t scan_scratch_reserve(ScanScratch* s, uint64_t len, hipStream_t stream);   // sized for a len-byte stream
+const uint32_t* scan_scratch_diag_word(const ScanScratch* s);   // device: why the last scan walked serially (0: it did not)
 int release_stream_scratch(int device, hipStream_t stream);   // 1 if there was a cached entry
 int64_t scan_diag(int device, hipStream_t stream);            // why the last scan walked serially (0: it did not)
 hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start, bool strict, uint64_t* hdr,
@@ -73,7 +76,12 @@ hipError_t launch_mask_scanned(uint8_t* wire, uint64_t len, const uint64_t* hdr,
 int api_fail(int code, const char* fmt, ...);                 // sets the message + netc_errno_reason, returns code
 int api_fail_hip(int code, const char* what, hipError_t e);
 int api_check_device(int device);                            // 0 or NETC_GPU_ENODEV (message set)
-const LaunchCfg& api_cfg();
+LaunchCfg api_cfg();                                         // snapshot of netc_gpu_tune's shape (one atomic word)
+// measurement / test knobs (netc_gpu_knob, include/ws/mask.h NETC_GPU_KNOB_*): one atomic
+// word each, seeded once from the environment; < 0 = the built-in default
+int64_t knob(int k);
+// per-(device, stream) scratch of the public entries, released by netc_gpu_stream_release
+int release_enc_scratch(int device, hipStream_t stream);     // ws_frame_gpu.hip
 
 hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_t* src, uint64_t src_total,
                                 const uint64_t* off, const uint32_t* keys, const uint8_t* b0, uint64_t n, bool masked,

@@ -1534,16 +1534,21 @@ hipError_t scan_scratch_reserve(ScanScratch* s, uint64_t len, hipStream_t stream
     return scratch_grow(*s, (len + kChunk - 1) / kChunk + 1, stream);
 }
 
+// the word netc_gpu_scan_diag reads (flags[9]): written by every call's K3b, OR'd by K4's
+// speculative continuation; valid until the scratch grows (ingest slots reserve up front)
+const uint32_t* scan_scratch_diag_word(const ScanScratch* s) {
+    return s && s->mem ? (const uint32_t*)((const uint8_t*)s->mem + 9 * sizeof(uint32_t)) : nullptr;
+}
+
 // Why the last scan on (device, stream) took the serial walk (0: it did not); the
 // caller has synchronised the stream.  -1: no scratch for that stream.
 int64_t scan_diag(int device, hipStream_t stream) {
-    ScanScratch* s = nullptr;
-    {
-        std::lock_guard<std::mutex> g(stream_scratch_mu());
-        auto it = stream_scratch().find({device, stream});
-        if (it == stream_scratch().end()) return -1;
-        s = it->second;
-    }
+    // the lock is held across the read: a concurrent release (or a growing scan) of the same
+    // (device, stream) must not free or replace s->mem under it
+    std::lock_guard<std::mutex> g(stream_scratch_mu());
+    auto it = stream_scratch().find({device, stream});
+    if (it == stream_scratch().end()) return -1;
+    ScanScratch* s = it->second;
     uint32_t why = 0;
     if (!s->mem || hipMemcpy(&why, (uint8_t*)s->mem + 9 * sizeof(uint32_t), sizeof(why), hipMemcpyDeviceToHost) !=
                        hipSuccess)
@@ -1623,14 +1628,11 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.tcount = (uint32_t*)(m + l.tcount);
     a.tinfo = (TileInfo*)(m + l.tinfo);
     a.anc_cap = s.cap;
-    {   // tests: NETC_SCAN_FAST_RANK=0 sends every tile and stream through the generic ranking loop
-        const char* env = getenv("NETC_SCAN_FAST_RANK");
-        a.fast_rank = env && env[0] == '0' ? 0 : 1;
-    }
-    if (const char* env = getenv("NETC_SCAN_ANCHOR_SLOTS")) {   // tests: fewer slots (0: none)
-        const uint64_t v = (uint64_t)strtoull(env, nullptr, 10);
-        a.anc_cap = v < a.anc_cap ? v : a.anc_cap;
-    }
+    // tests: NETC_GPU_KNOB_SCAN_FAST_RANK = 0 sends every tile and stream through the generic
+    // ranking loop; NETC_GPU_KNOB_SCAN_ANCHOR_SLOTS caps the anchor slots (0: none)
+    a.fast_rank = knob(NETC_GPU_KNOB_SCAN_FAST_RANK) == 0 ? 0 : 1;
+    if (const int64_t v = knob(NETC_GPU_KNOB_SCAN_ANCHOR_SLOTS); v >= 0)
+        a.anc_cap = (uint64_t)v < a.anc_cap ? (uint64_t)v : a.anc_cap;
     a.pf_base = len >= 16 ? wire : m + l.flags;
     a.pf_lim = len >= 16 ? len - 16 : 0;
     const unsigned blk = (unsigned)((chunks + kBlkChunks - 1) / kBlkChunks);

@@ -10,6 +10,8 @@ GPU entries.
 
 from __future__ import annotations
 
+import contextlib
+
 import ctypes
 from typing import Optional, Sequence, Tuple
 
@@ -104,6 +106,33 @@ def tune(unroll: int = 1, max_blocks: int = 0, flags: int = NETC_GPU_TUNE_AUTO) 
     """netc_gpu_tune: process-wide launch shape (KiB a wavefront loads at once, workgroup cap of the
     persistent walk, cache / walk flags); the defaults are the C library's."""
     _check(_lib.gpu().netc_gpu_tune(unroll, max_blocks, flags))
+
+
+KNOBS = {"ENC_DENSE_BYTES": 1, "ENC_SCAN_PER": 2, "SCAN_FAST_RANK": 3, "SCAN_ANCHOR_SLOTS": 4}
+
+
+def set_knob(name: str, value: int) -> None:
+    """netc_gpu_knob: a measurement / test knob of the frame assembly or scan (value < 0 = default)."""
+    _check(_lib.gpu().netc_gpu_knob(KNOBS[name], int(value)))
+
+
+@contextlib.contextmanager
+def knob(name: str, value):
+    """Sets a knob for the duration of a `with` block (None: leave the default), then restores it."""
+    if value is None:
+        yield
+        return
+    set_knob(name, value)
+    try:
+        yield
+    finally:
+        set_knob(name, -1)
+
+
+def stream_release(stream=None, device: int = 0) -> None:
+    """netc_gpu_stream_release: synchronise `stream`, then free every scratch array the library
+    keeps for it (scan, frame assembly, UTF-8 flags)."""
+    _check(_lib.gpu().netc_gpu_stream_release(device, _stream_handle(stream)))
 
 
 def _stream_handle(stream) -> int:

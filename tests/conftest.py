@@ -30,3 +30,22 @@ def torch_cuda():
     if not torch.cuda.is_available():
         pytest.fail("GPU test selected but torch sees no GPU (run with -m 'not gpu' on a CPU-only host)")
     return torch
+
+
+@pytest.fixture
+def gpu_knob():
+    """set(name, value): a netc_gpu_knob (include/ws/mask.h) for this test, restored to its
+    default afterwards (None leaves it alone)."""
+    from netc_amd import mask as nm
+
+    touched = []
+
+    def set_(name, value):
+        if value is None:
+            return
+        nm.set_knob(name, int(value))
+        touched.append(name)
+
+    yield set_
+    for name in touched:
+        nm.set_knob(name, -1)

@@ -25,6 +25,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference"
 ORACLE = os.path.join(ROOT, "oracle")
+DROPIN_DIR = "/tmp/netc_dropin"   # oracle/Makefile DROPIN_DIR: outside the repository
 LIBNETC = os.path.join(ROOT, "netc_amd", "lib", "libnetc.so")
 
 pytestmark = pytest.mark.skipif(not os.path.isfile(os.path.join(REF, "tests", "ws", "test001.c")),
@@ -39,7 +40,7 @@ CHECKS = ["on_connect_server", "send_basic_server", "send_multiple_frames_server
 @pytest.fixture(scope="module")
 def built():
     subprocess.run(["make", "-C", ORACLE, "dropin"], check=True, capture_output=True, text=True)
-    return {k: os.path.join(ORACLE, "_ref", f"ws_test001_{k}") for k in ("reference", "libnetc")}
+    return {k: os.path.join(DROPIN_DIR, f"ws_test001_{k}") for k in ("reference", "libnetc")}
 
 
 def run(exe, env=None):

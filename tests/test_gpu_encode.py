@@ -220,11 +220,11 @@ def test_launch_shapes(torch_cuda, unroll, max_blocks):
 
 @pytest.mark.parametrize("dense", ["0", "100000"])
 @pytest.mark.parametrize("masked", [True, False])
-def test_both_compose_paths(torch_cuda, monkeypatch, dense, masked):
-    # the same batches through the vector path + queued compose (NETC_ENC_DENSE_BYTES=0)
+def test_both_compose_paths(torch_cuda, gpu_knob, dense, masked):
+    # the same batches through the vector path + queued compose (knob ENC_DENSE_BYTES = 0)
     # and through the dense per-lane compose of every span (threshold above any mean):
     # uniform 16 / 8 / 1 B frames, empty frames, 0..30 B mixes, and long frames between
-    monkeypatch.setenv("NETC_ENC_DENSE_BYTES", dense)
+    gpu_knob("ENC_DENSE_BYTES", dense)
     rng = np.random.default_rng(21)
     parts = [np.full(3000, 16), np.full(2000, 8), rng.integers(0, 31, 4000), np.full(1500, 1),
              np.array([126, 65536, 0, 0, 125, 3000]), np.zeros(700, dtype=np.int64), rng.integers(100, 300, 200)]

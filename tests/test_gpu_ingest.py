@@ -186,6 +186,41 @@ def test_non_strict_scan_choice(torch_cuda, scan_mode):
             assert (gpu, host) == ((nb, 0) if scan_mode == "gpu" else (0, nb))
 
 
+def test_non_strict_choice_several_slots_one_write(torch_cuda, scan_mode):
+    # one write() that fills several slots submits each slot right after the
+    # previous one, while the previous slot's descriptor copy back is still queued.  The choice
+    # must come from the scan's own diag word (copied with its result), not from those
+    # descriptors: slot 0 (no history) is GPU-scanned and meets RSV1 headers, so with the
+    # per-slot choice every later slot takes the host walk -- exactly, whatever the timing.
+    rng = np.random.default_rng(79)
+    n = 800
+    wire, *_ = make_stream(rng, np.full(n, 1024), b0=np.full(n, 0xC2, dtype=np.uint8))
+    with ni.Ingest(0, slot_bytes=256 << 10, nslots=4, strict=False) as ing:
+        assert ing.write(wire) == wire.size   # ~806 KiB: four slots, all in one call
+        ing.submit()
+        col = Collector()
+        col.take(ing, wait=True)
+        assert col.check(wire, strict=False) == n
+        gpu, host = ing.scan_counts()
+        nb = len(col.batches)
+        assert nb == 4
+        if scan_mode == "auto":
+            assert (gpu, host) == (1, nb - 1)
+        else:
+            assert (gpu, host) == ((nb, 0) if scan_mode == "gpu" else (0, nb))
+
+
+def test_python_default_is_non_strict(torch_cuda):
+    # the Python mirror follows the C default (flags 0: every header accepted, as the
+    # reference's ws_parse_frame): an unmasked client frame is delivered, not rejected
+    rng = np.random.default_rng(80)
+    wire, *_ = make_stream(rng, np.full(10, 100), masked=False)
+    with ni.Ingest(0, slot_bytes=4096, nslots=2) as ing:
+        col = Collector()
+        feed(ing, col, wire, [wire.size])
+        assert col.check(wire, strict=False) == 10
+
+
 def test_c5_shape_4k_frames(torch_cuda):
     # BASELINE config 5's frame shape: 4 KiB masked BINARY frames, 16 MiB through 1 MiB slots
     rng = np.random.default_rng(5)

@@ -234,15 +234,14 @@ def test_repeat_calls_same_stream(torch_cuda):
 
 @pytest.mark.parametrize("slots", [None, "0", "3"])
 @pytest.mark.parametrize("masked,strict", [(True, True), (False, False)])
-def test_dense_chunks_parallel_walks(torch_cuda, monkeypatch, masked, strict, slots):
+def test_dense_chunks_parallel_walks(torch_cuda, gpu_knob, masked, strict, slots):
     # chunks of 64+ frames (K2' and K4b': 16-hop links, anchored emit): uniform 16 / 8 B
     # payloads, empty frames (2-byte unmasked / 6-byte masked wire frames: up to 2,048
     # per chunk), mixes, and a long frame between; then truncations and start offsets
     # inside the dense stretch and a frame cap that ends inside an anchor's run.  slots:
     # K2' anchor slots (None: one per chunk, K4b' emits from them; "0": none, every
     # dense chunk goes through the LDS emit; "3": both paths in one call)
-    if slots is not None:
-        monkeypatch.setenv("NETC_SCAN_ANCHOR_SLOTS", slots)
+    gpu_knob("SCAN_ANCHOR_SLOTS", slots)
     rng = np.random.default_rng(41 + masked)
     sizes = np.concatenate([np.full(3000, 16), np.full(2500, 8), np.zeros(3000, dtype=np.int64),
                             rng.integers(0, 20, 3000), [70000], np.full(1000, 1)])
@@ -256,11 +255,11 @@ def test_dense_chunks_parallel_walks(torch_cuda, monkeypatch, masked, strict, sl
 
 
 @pytest.mark.parametrize("fast", ["1", "0"])
-def test_ranking_paths(torch_cuda, monkeypatch, fast):
+def test_ranking_paths(torch_cuda, gpu_knob, fast):
     # K3a / K3b rank a tile's nodes (and the tiles' external nodes) with one barrier per
     # round when they fit (512 / 1,024 nodes), else with the generic loop; both on the
-    # same streams (NETC_SCAN_FAST_RANK=0 forces the generic loop)
-    monkeypatch.setenv("NETC_SCAN_FAST_RANK", fast)
+    # same streams (knob SCAN_FAST_RANK = 0 forces the generic loop)
+    gpu_knob("SCAN_FAST_RANK", fast)
     rng = np.random.default_rng(31)
     wire, _ = _stream(rng, np.full(16384, 1024))   # 16 MiB: 16 full tiles of ~262 nodes
     assert run_scan(torch_cuda, wire, parallel=True) == 16384
