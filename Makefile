@@ -25,7 +25,7 @@ GPU_HDRS   := netc_amd/csrc/ws_mask_gpu.h netc_amd/csrc/gpu_util.h include/ws/ma
 .PHONY: all host gpu oracle diag clean asan
 all: host gpu oracle
 host: $(LIBDIR)/libnetc.so
-gpu: $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc_ceiling.so
+gpu: $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc_ceiling.so tests/bin/ws_gpu_epoll
 
 $(LIBDIR)/libnetc.so: $(HOST_SRCS) $(HOST_HDRS)
 	@mkdir -p $(LIBDIR)
@@ -45,11 +45,18 @@ $(LIBDIR)/libnetc_ceiling.so: netc_amd/csrc/ceiling.hip
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 
+# the GPU receive route under netc's caller contract (tests/test_gpu_epoll.py): a C program,
+# epoll + TCP loopback, linked against both libraries as a netc server would be
+tests/bin/ws_gpu_epoll: tests/drivers/ws_gpu_epoll.c $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc.so $(HOST_HDRS)
+	@mkdir -p tests/bin
+	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -L$(LIBDIR) -lnetc_ws_gpu -lnetc -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib -lpthread
+
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(LIBDIR)/*.so build/*.o
+	rm -f $(LIBDIR)/*.so build/*.o tests/bin/ws_gpu_epoll
 	$(MAKE) -C oracle clean
 
 # diagnostics (tools/, not part of the product)

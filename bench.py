@@ -230,17 +230,29 @@ def c5_host_to_host(nm, gib: float):
     """BASELINE config 5: `gib` GiB of 4 KiB frames in a pinned host ring, streamed through the
     default persistent handle (2 x 512 MiB device slots, H2D / kernel / D2H overlapped) into a
     pinned output ring (the ring -> parser hand-off), and once more in place.  Host-to-host GiB/s,
-    best of 2 passes each (the first pass also touches the slots); never `value`."""
+    best of 2 passes each (the first pass also touches the slots); never `value`.
+
+    Checked after the timing, through the oracle (the reference's expression, src/ws/common.c:321):
+    the frames on both sides of every slot edge (where the pipeline cuts) and 256 random frames
+    of the out-of-place output; and, since the ring was masked in place an even number of times,
+    that the same frames of the ring are back to their original bytes."""
     from netc_amd import synth
+    from oracle import oracle as orc
 
     total = int(gib * (1 << 30)) // 4096 * 4096
     nframes = total // 4096
     off = synth.uniform_offsets(nframes, 4096)
     keys = synth.random_keys(nframes, stream=900)
     ring, out = nm.PinnedArray(total), nm.PinnedArray(total)
+    slot = 512 << 20
+    edges = [e // 4096 + d for e in range(slot, total, slot) for d in (-1, 0)]
+    picks = sorted(set(edges) | set(int(k) for k in synth.rng(901).choice(nframes, size=min(256, nframes),
+                                                                         replace=False)))
+    picks = [k for k in picks if 0 <= k < nframes]
     rates = {}
     try:
         synth.fill_payload(ring.array)
+        orig = {k: ring.array[k * 4096:(k + 1) * 4096].copy() for k in picks}
         with nm.HostStream(0) as hs:
             for name, dst in (("out_of_place", out.array), ("in_place", ring.array)):
                 best = None
@@ -250,11 +262,18 @@ def c5_host_to_host(nm, gib: float):
                     dt = time.perf_counter() - t0
                     best = dt if best is None else min(best, dt)
                 rates[name] = round(total / best / GIB, 2)
+        bad = 0
+        for k in picks:
+            exp = orc.mask_batch(orig[k], np.array([0, 4096], dtype=np.uint64), keys[k:k + 1])
+            bad += int(not np.array_equal(out.array[k * 4096:(k + 1) * 4096], exp))
+            bad += int(not np.array_equal(ring.array[k * 4096:(k + 1) * 4096], orig[k]))
     finally:
         ring.close()
         out.close()
     return {"value": rates["out_of_place"], "unit": "GiB/s host to host", "in_place": rates["in_place"],
             "bytes": total, "frames": nframes, "slots": "2 x 512 MiB (defaults)", "passes": 2,
+            "verified": {"frames_checked": len(picks), "slot_edge_frames": len(edges), "mismatches": bad,
+                         "ok": bad == 0},
             "note": "BASELINE config 5: pinned ring -> H2D -> mask -> D2H -> pinned output ring "
                     "(in_place: back into the ring); PCIe-bound"}
 

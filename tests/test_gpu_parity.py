@@ -261,8 +261,9 @@ def test_misaligned_large_batch_exact(torch_cuda, dst_shift, src_shift):
 
 
 @pytest.mark.slow
-def test_c3_full_properties(torch_cuda):
-    """1 GiB: involution over the whole buffer, keystream linearity, oracle on sampled frames."""
+def test_c3_full_exact(torch_cuda):
+    """1 GiB (BASELINE config 3): out of place, every byte against the oracle's in-place pass over
+    a host copy (as C4 is checked); then involution and keystream linearity on the device."""
     torch = torch_cuda
     off, keys, total = synth.config("c3")
     off_t, keys_t = _dev(torch, off, None), _dev(torch, keys, None)
@@ -270,18 +271,16 @@ def test_c3_full_properties(torch_cuda):
     x = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda", generator=g)
     y = torch.empty_like(x)
     nm.mask_batch(y, x, off_t, keys_t)
+    torch.cuda.synchronize()
+    host = x.cpu().numpy()
+    orc.mask_batch_inplace(host, off, keys)         # the reference's expression, every frame
+    assert np.array_equal(y.cpu().numpy(), host)
+    del host
     z = torch.zeros_like(x)
     nm.mask_batch(z, z, off_t, keys_t)              # keystream = mask(0)
     assert torch.equal(torch.bitwise_xor(x, y), z)  # mask(x) ^ x == mask(0)
     nm.mask_batch(y, y, off_t, keys_t)              # involution
     assert torch.equal(y, x)
-    del y
-    picks = synth.rng(33).choice(keys.size, size=16, replace=False)
-    zs = z.cpu().numpy()
-    for k in picks:
-        a, b = int(off[k]), int(off[k + 1])
-        exp = orc.mask_batch(np.zeros(b - a, dtype=np.uint8), np.array([0, b - a], dtype=np.uint64), keys[k:k + 1])
-        assert np.array_equal(zs[a:b], exp)
 
 
 # ------------------------------------------------------- other entry points --
