@@ -112,6 +112,7 @@ int netc_gpu_init(int device);
 #define NETC_GPU_TUNE_PERSISTENT  4   /* round 1's persistent grid-stride walk             */
 #define NETC_GPU_TUNE_TWO_STEPS   8   /* a wavefront's window is two steps of unroll KiB   */
 #define NETC_GPU_TUNE_XCD_ORDER  16   /* each XCD takes a contiguous share of the windows  */
+#define NETC_GPU_TUNE_XCD_GROUPS 32   /* each XCD takes 8 consecutive blocks of every 64    */
 int netc_gpu_tune(int unroll, int max_blocks, int flags);
 
 /**

@@ -232,7 +232,7 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags) {
     if (max_blocks < 0 || max_blocks > (1 << 24)) return fail(NETC_GPU_EINVAL, "max_blocks out of range");
     if (flags != NETC_GPU_TUNE_AUTO &&
         (flags & ~(NETC_GPU_TUNE_NT_LOADS | NETC_GPU_TUNE_NT_STORES | NETC_GPU_TUNE_PERSISTENT |
-                   NETC_GPU_TUNE_TWO_STEPS | NETC_GPU_TUNE_XCD_ORDER)))
+                   NETC_GPU_TUNE_TWO_STEPS | NETC_GPU_TUNE_XCD_ORDER | NETC_GPU_TUNE_XCD_GROUPS)))
         return fail(NETC_GPU_EINVAL, "unknown tune flags");
     g_cfg_word.store(pack_cfg(unroll, max_blocks, flags), std::memory_order_release);
     return 0;

@@ -25,12 +25,14 @@ struct Args {
     uint8_t* verr;             // TEXT validation (VAL kernels): per-frame "local UTF-8 rule broken" flags
     uint8_t vtag;              // ... written as this call's tag (verr[f] == vtag: flagged by this call)
     uint8_t xcd_remap;         // one-window-per-wave walk: give each XCD a contiguous share of the windows
+    int32_t probe_e;           // one-window-per-wave walk: entries of a window's first table probe (<= 64)
+    int32_t probe_bias;        // ... and the frames its base sits before the density's guess
 };
 
 // LaunchCfg::flags (NETC_GPU_TUNE_*): bits 0-1 non-temporal payload stream, 2 the
 // persistent grid-stride walk (round-1 kernel), 3 two steps per wavefront window,
-// 4 XCD-contiguous window order
-enum : int { kNtLoads = 1, kNtStores = 2, kPersistent = 4, kTwoSteps = 8, kXcdRemap = 16 };
+// 4 XCD-contiguous window order, 5 XCD-grouped window order (8 consecutive blocks per XCD)
+enum : int { kNtLoads = 1, kNtStores = 2, kPersistent = 4, kTwoSteps = 8, kXcdRemap = 16, kXcdGroups = 32 };
 
 struct LaunchCfg {
     int unroll = 1;            // KiB loaded per wavefront at once (1, 2, 4, 8)

@@ -49,10 +49,11 @@ extern "C" int netc_gpu_debug_stamps(void* d_buf) {
 
 struct Table {
     int64_t kb;       // virtual frame index held by lane 0
-    uint64_t start;   // this lane's entry: start of frame kb + lane (P coords)
+    uint64_t start;   // this lane's entry: start of frame kb + lane (P coords); kInf past entry e - 1
     uint32_t key;     // this lane's entry: packed key of frame kb + lane
-    uint64_t last;    // start of frame kb + 63 (uniform)
+    uint64_t last;    // start of frame kb + e - 1, the last entry held (uniform)
     bool tail;        // frame n (the open-ended pass-through frame) is in the table
+    int e;            // entries held: 64, or fewer for a window's first probe (uniform)
 };
 
 // Frame k's offset / key.  Args: the caller's arrays.  ArgsScan (frames a
@@ -116,15 +117,25 @@ __device__ __forceinline__ void frame_entry(const A& a, int64_t v, uint64_t& s, 
     k = (v >= 0 && v < n) ? key : 0u;
 }
 
-// issue the table loads (frames kb .. kb+63, one per lane) without waiting for them
+// issue the table loads (frames kb .. kb+e-1, one per lane) without waiting for them.
+// e < 64 (a window's first probe, sized to the frames the window can reach): lanes past
+// e - 1 load entry e - 1 again -- the same cache lines, so the probe touches only the
+// lines of its e entries, and no lane branches around a load (which would draw a
+// vmcnt(0) wait behind the window's payload loads) -- and then hold kInf.
 template <class A>
-__device__ __forceinline__ void table_issue(const A& a, Table& t, int64_t kb, int lane) {
+__device__ __forceinline__ void table_issue(const A& a, Table& t, int64_t kb, int lane, int e = kWave) {
     t.kb = kb;
-    frame_entry(a, kb + lane, t.start, t.key);
-    t.tail = kb + (kWave - 1) >= (int64_t)a.n;
+    t.e = e;
+    frame_entry(a, kb + (lane < e ? lane : e - 1), t.start, t.key);
+    t.tail = kb + (e - 1) >= (int64_t)a.n;
 }
 
-__device__ __forceinline__ void table_finish(Table& t) { t.last = readlane64(t.start, kWave - 1); }
+// the table's loads have landed: entries past e - 1 become kInf (here, at the first use,
+// not at the issue -- a select on a loaded value there would wait for the load)
+__device__ __forceinline__ void table_finish(Table& t) {
+    if (t.e < kWave && (int)__lane_id() >= t.e) t.start = kInf;
+    t.last = readlane64(t.start, t.e - 1);
+}
 
 template <class A>
 __device__ __forceinline__ void table_load(const A& a, Table& t, int64_t kb, int lane) {
@@ -137,7 +148,7 @@ __device__ __forceinline__ void table_load(const A& a, Table& t, int64_t kb, int
 __device__ __forceinline__ bool table_brackets(const Table& t, uint64_t P) {
     const uint64_t m = __ballot(t.start <= P);
     if (m == 0) return false;
-    return t.tail || m != ~0ull;
+    return t.tail || __popcll(m) < t.e;
 }
 
 // Table base for the chunk at P guessed from a frame known to start at s_known
@@ -145,10 +156,11 @@ __device__ __forceinline__ bool table_brackets(const Table& t, uint64_t P) {
 // draws, so the guess error grows only with the square root of the frames in
 // between; the window is biased forward so the chunk's later frames fit too.
 template <class A>
-__device__ __forceinline__ int64_t guess_base(const A& a, int64_t f_known, uint64_t s_known, uint64_t P) {
+__device__ __forceinline__ int64_t guess_base(const A& a, int64_t f_known, uint64_t s_known, uint64_t P,
+                                              int64_t bias = 24) {
     if (P < a.mis) return -1;
     const double ahead = (double)(P - s_known) * a.density;
-    int64_t g = f_known + (int64_t)ahead - 24;
+    int64_t g = f_known + (int64_t)ahead - bias;
     g = g < -1 ? -1 : g;
     return g > (int64_t)a.n ? (int64_t)a.n : g;
 }
@@ -209,10 +221,10 @@ template <class A>
 __device__ __forceinline__ u32x4 span_mask(const A& a, Table& t, uint64_t A0, int lane) {
     const uint64_t Aend = A0 + kSpan;
     // invariant: entry 0 starts at or before A0.  Make the table cover the span.
-    if (!t.tail && t.last < Aend) {
+    if (!t.tail && t.last < Aend) {   // a full table from the span's first frame on
         const uint64_t m = __ballot(t.start <= A0);
         const int j0 = __popcll(m) - 1;
-        if (j0 > 0) table_load(a, t, t.kb + j0, lane);
+        if (j0 > 0 || t.e < kWave) table_load(a, t, t.kb + j0, lane);
     }
     const uint64_t m0 = __ballot(t.start <= A0);
     const int j0 = __popcll(m0) - 1;
@@ -241,7 +253,7 @@ __device__ __forceinline__ u32x4 span_mask(const A& a, Table& t, uint64_t A0, in
         for (;;) {
             const bool more = !(t.tail || t.last >= Aend);   // wave-uniform
             Table tn;
-            if (more) table_issue(a, tn, t.kb + (kWave - 1), lane);
+            if (more) table_issue(a, tn, t.kb + (t.e - 1), lane);
             int l = 0;
 #pragma unroll
             for (int step = 32; step > 0; step >>= 1)
@@ -282,7 +294,7 @@ __device__ __forceinline__ u32x4 span_mask(const A& a, Table& t, uint64_t A0, in
         if (t.tail || t.last >= Aend) break;
         // more than 63 boundaries in one span: advance the table past the last
         // applied entry (re-applying entry 0 again is idempotent) and continue
-        table_load(a, t, t.kb + (kWave - 1), lane);
+        table_load(a, t, t.kb + (t.e - 1), lane);
         b = __ballot(t.start > A0 && t.start < Aend);
     }
     return mask;
@@ -606,13 +618,13 @@ __device__ __forceinline__ void np_resolve(const AT& a, Table& t, uint64_t A, in
 #pragma unroll 1
     for (int step = 0; step < 2; ++step) {
         const uint64_t m = __ballot(t.start <= A);
-        if (m != 0 && (t.tail || m != ~0ull)) return;   // brackets A
+        if (m != 0 && (t.tail || __popcll(m) < t.e)) return;   // brackets A
         int64_t g;
         if (m == 0) {   // every entry starts after A: step back by the distance from entry 0
             const uint64_t s0 = readlane64(t.start, 0);
             g = t.kb - (int64_t)((double)(s0 - A) * a.density) - 40;
         } else {        // every entry starts at or before A: step on from entry 63
-            g = t.kb + (kWave - 1) + (int64_t)((double)(A - t.last) * a.density) - 24;
+            g = t.kb + (t.e - 1) + (int64_t)((double)(A - t.last) * a.density) - 24;
         }
         table_load(a, t, clamp_base(a, g), lane);
     }
@@ -806,6 +818,16 @@ __device__ __forceinline__ void init_frames(ArgsScan& a) {
     a.density = a.total ? (double)a.n / (double)a.total : 0.0;
 }
 
+// A window's first table probe: its base from the batch's mean density, biased back by
+// a.probe_bias frames, holding a.probe_e entries.  Both come from the host (make_args),
+// so the probe is straight-line code with kernel-argument (scalar) parameters -- a
+// branch here on the density made the compiler wait (vmcnt(0)) for the window's payload
+// loads before issuing the table's: +7 % at config 2, +2.5 % at config 4.
+template <class AT>
+__device__ __forceinline__ void first_probe(const AT& a, Table& t, uint64_t A, int lane) {
+    table_issue(a, t, guess_base(a, 0, a.mis, A, a.probe_bias), lane, a.probe_e);
+}
+
 template <int U, int K, bool SRC_ALIGNED, bool NT, bool VAL = false, class AT = Args>
 __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
     constexpr uint64_t kStep = kSpan * U;
@@ -813,11 +835,17 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wpb = blockDim.x / kWave;
     uint64_t block = blockIdx.x;
-    if (a.xcd_remap) {
+    if (a.xcd_remap == 1) {
         // blocks b and b + 8 share an XCD (round-robin dispatch): give each XCD one
         // contiguous share of the batch, so its L2 fetches only that share's descriptors
         const uint64_t nb = gridDim.x, per = nb / 8;
         if (block < per * 8) block = (block % 8) * per + block / 8;
+    } else if (a.xcd_remap == 2) {
+        // groups of 64 blocks: the 8 blocks of a group that share an XCD take 8 consecutive
+        // blocks' windows (64 KiB), so a descriptor line (16 frame offsets) is fetched by one
+        // XCD, while the grid as a whole still streams one compact front
+        const uint64_t nb = gridDim.x;
+        if (block < nb / 64 * 64) block = (block / 64) * 64 + (block % 8) * 8 + (block / 8) % 8;
     }
     const uint64_t wave = block * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // uniform: scalar branches
     if (wave >= a.nwin) return;
@@ -858,7 +886,7 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
         // by vmcnt(0), which held the table's trip behind the payload's
         const uint32_t lm = min((uint32_t)lane, o >> 4);
         c[M] = load_line_block<NT>(S - o + 16 * lm + (uint64_t)M * kSpan);
-        table_issue(a, t, guess_base(a, 0, a.mis, A), lane);
+        first_probe(a, t, A, lane);
         np_resolve(a, t, A, lane);
         switch ((o >> 2) & 3) {   // uniform: constant register indices in each case
             case 0: shift_window<M, 0>(c, v, o, lane); break;
@@ -876,7 +904,7 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
         for (int u = 0; u < U; ++u) d[u] = load_vec<true, NT>(a, base + (uint64_t)u * kSpan + 16ull * lane);
     };
     load_step(A);
-    table_issue(a, t, guess_base(a, 0, a.mis, A), lane);
+    first_probe(a, t, A, lane);
     np_resolve(a, t, A, lane);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -981,7 +1009,25 @@ static Args make_args(uint8_t* dst, const uint8_t* src, uint64_t total, const ui
     a.n = n;
     a.density = total ? (double)n / (double)total : 0.0;
     a.nwin = 0;
+    a.probe_e = kWave;
+    a.probe_bias = 24;
     return a;
+}
+
+// The default walk's first table probe (first_probe), from the window size: windows that
+// hold a frame start or more on average (frames up to ~2 KiB: config 2, small frames) take
+// the base the mean density predicts minus one frame and only the entries the window can
+// reach, ceil(window x density) + 3 -- exact for evenly sized frames.  A full 64-entry
+// probe read 768 B of descriptors per 2 KiB window at config 2 for the 3 entries used,
+// and every XCD's L2 fetched every descriptor line (PMC: 1.048x the algorithmic bytes).
+// Sparser windows (config 4's 256 B - 64 KiB frames) keep 64 entries biased 24 frames
+// back, whose reach absorbs the guess error of random sizes.
+static void set_probe(Args& a, uint64_t win) {
+    const double reach = (double)win * a.density;
+    if (reach >= 1.0 && reach < (double)(kWave - 4)) {
+        a.probe_e = (int)reach + 4;
+        a.probe_bias = 1;
+    }
 }
 
 // In-place unmask of the frames a scan found (ws_scan_gpu.hip): the default walk,
@@ -1031,13 +1077,14 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
     // auto: two steps of `unroll` KiB per wavefront (1 KiB x 2: the fastest walk measured,
     // frame-free and with frames, at 64 MiB and at 1 GiB)
     const bool two = flags < 0 || (flags & kTwoSteps);
-    a.xcd_remap = (flags >= 0 && (flags & kXcdRemap)) ? 1 : 0;
+    a.xcd_remap = (flags >= 0 && (flags & kXcdRemap)) ? 1 : ((flags >= 0 && (flags & kXcdGroups)) ? 2 : 0);
     // src misaligned against dst, auto, >= 256 MiB: windows of 4 x 1 KiB (33 source lines per
     // 4 spans, not 17 per 2): 1 GiB mixed frames 0.88 -> 0.97 of the aligned rate; at 64 MiB
     // 2 x 1 KiB stays ahead (profiles/r02j_misaligned_sweep.jsonl)
     const int U = (!aligned && flags < 0 && total >= (256ull << 20)) ? 2 : cfg.unroll;
     const uint64_t win_vec = 64ull * (uint64_t)U * (two ? 2 : 1);
     a.nwin = (nvec + win_vec - 1) / win_vec;
+    set_probe(a, 16 * win_vec);
     return aligned ? launch_np_u<true>(a, U, nt, two, stream) : launch_np_u<false>(a, U, nt, two, stream);
 }
 
@@ -1153,6 +1200,7 @@ hipError_t launch_mask_validate(uint8_t* dst, const uint8_t* src, uint64_t total
     a.vtag = tag;
     const uint64_t nvec = (a.mis + total + 15) / 16;
     a.nwin = (nvec + 255) / 256;   // windows of 4 KiB (64 vectors x 4)
+    set_probe(a, 4096);
     const bool persistent = cfg.flags >= 0 && (cfg.flags & kPersistent);
     hipError_t e;
     if (a.nwin) {

@@ -97,6 +97,7 @@ NETC_GPU_TUNE_NT_STORES = 2
 NETC_GPU_TUNE_PERSISTENT = 4
 NETC_GPU_TUNE_TWO_STEPS = 8
 NETC_GPU_TUNE_XCD_ORDER = 16
+NETC_GPU_TUNE_XCD_GROUPS = 32
 
 
 NETC_GPU_TUNE_AUTO = -1

@@ -188,7 +188,7 @@ def test_one_huge_frame(torch_cuda):
 
 
 @pytest.mark.parametrize("unroll,max_blocks", [(1, 2048), (2, 64), (8, 0), (4, 1), (4, 100000), (2, 0)])
-@pytest.mark.parametrize("flags", [-1, 0, 3, 7, 4, 11, 27])
+@pytest.mark.parametrize("flags", [-1, 0, 3, 7, 4, 11, 27, 43])
 def test_launch_shapes(torch_cuda, unroll, max_blocks, flags):
     """Every kernel instantiation is bit-exact: U x cache-hint flags x walk (one window per
     wavefront, one or two steps, XCD order; or the persistent walk, flags & 4, with its grid cap)."""
@@ -202,7 +202,7 @@ def test_launch_shapes(torch_cuda, unroll, max_blocks, flags):
         nm.tune()
 
 
-@pytest.mark.parametrize("flags", [-1, 0, 7, 11])
+@pytest.mark.parametrize("flags", [-1, 0, 7, 11, 43])
 def test_near_uniform_frames(torch_cuda, flags):
     """Evenly sized frames with sparse irregular ones: the table-base guesses are exact
     until an irregular frame shifts every later frame start, then must recover

@@ -35,6 +35,7 @@ def test_stream_release_frees_scan_encode_validate_scratch(torch_cuda):
     plain = rng.integers(0, 128, int(off[-1]), dtype=np.uint8)          # ASCII: valid TEXT
     keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     wire, _ = orc.encode_batch(plain, off, keys, None, True)
+    masked = orc.mask_batch(plain, off, keys)                            # what a receiver holds
     exp_hdr, *_ = orc.scan_frames(wire, strict=True)
 
     dev = torch.device("cuda", 0)
@@ -44,6 +45,7 @@ def test_stream_release_frees_scan_encode_validate_scratch(torch_cuda):
     sb = torch.zeros(n + 1, dtype=torch.uint8, device=dev)
     res = torch.zeros(3, dtype=torch.int64, device=dev)
     d_plain = torch.from_numpy(plain).to(dev)
+    d_masked = torch.from_numpy(masked).to(dev)
     d_off = torch.from_numpy(off.view(np.int64)).to(dev)
     d_keys = torch.from_numpy(keys.view(np.int32)).to(dev)
     out_wire = torch.zeros(nm.wire_bound(plain.size, n, True), dtype=torch.uint8, device=dev)
@@ -59,12 +61,12 @@ def test_stream_release_frees_scan_encode_validate_scratch(torch_cuda):
         h = s.value
         nm.scan_frames(d_wire, hdr, sk, sb, res, stream=h)
         nm.encode_frames(out_wire, wo, d_plain, d_off, d_keys, masked=True, stream=h)
-        nm.unmask_validate(dst, d_plain, d_off, d_keys, h0, valid, stream=h)
+        nm.unmask_validate(dst, d_masked, d_off, d_keys, h0, valid, stream=h)
         nm.stream_release(stream=h)          # synchronises h, frees the three scratch sets
         assert hip.hipStreamDestroy(h) == 0
         assert int(res[0]) == n and np.array_equal(hdr[:n].cpu().numpy().view(np.uint64), exp_hdr)
         assert np.array_equal(out_wire[:wire.size].cpu().numpy(), wire)
-        assert bool((valid == 1).all())
+        assert bool((valid == 1).all()) and torch.equal(dst, d_plain)
 
     one_round()
     torch.cuda.synchronize()
