@@ -126,11 +126,14 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *   SCAN_FAST_RANK     0 sends the frame scan's list ranking through the generic
  *                      loop [1]                                     (NETC_SCAN_FAST_RANK)
  *   SCAN_ANCHOR_SLOTS  cap on the frame scan's anchor slots [all]  (NETC_SCAN_ANCHOR_SLOTS)
+ *   VAL_STEPS          netc_gpu_unmask_validate's 4 KiB window as 1, 2 or 4 steps [1]
+ *                                                                  (NETC_VAL_STEPS)
  */
 #define NETC_GPU_KNOB_ENC_DENSE_BYTES   1
 #define NETC_GPU_KNOB_ENC_SCAN_PER      2
 #define NETC_GPU_KNOB_SCAN_FAST_RANK    3
 #define NETC_GPU_KNOB_SCAN_ANCHOR_SLOTS 4
+#define NETC_GPU_KNOB_VAL_STEPS         5
 int netc_gpu_knob(int knob, int64_t value);
 
 /**

@@ -451,59 +451,72 @@ __device__ __forceinline__ void edge_vec(const A& a, uint64_t P, u32x4 mask) {
 // unaligned buffer (at most three chunks per batch): per-vector range checks,
 // a fresh frame search, no prefetch.
 // ------------------------------------------------------ UTF-8 validation --
-// RFC 3629 checked byte by byte from the byte and the 3 before it (the local
-// rules of the "lookup" validators): a byte must be a continuation exactly when a
-// lead 1-3 bytes back asks for one; C0, C1 and F5..FF never occur; the byte after
-// E0 / ED / F0 / F4 is limited (shortest form, surrogates, U+10FFFF).  Four bytes
-// at a time in a dword (SWAR; bit 7 of each byte of the result flags an error),
-// about 45 VALU operations per dword: the lead flags of a dword are computed once
-// and carried to the next, and the four second-byte rules are two nibble lookups
-// (v_perm_b32 over a 16-byte table) ANDed with a lookup on the byte's own high
-// nibble.  tools/ and DESIGN.md §10.3: checked exhaustively against the scalar rule
-// (utf8_rule below) over every 4-byte context of 31 boundary byte values.
-struct Utf8Carry {
-    uint32_t x, l2, l3, l4;   // the previous dword and its lead flags (bytes >= C0 / E0 / F0, bit 7)
+// RFC 3629 by the three-lookup rule (Keiser & Lemire, "Validating UTF-8 in less than one
+// instruction per byte", 2021): for each byte, the AND of three 16-entry lookups -- the
+// previous byte's high nibble, its low nibble, the byte's own high nibble -- flags every
+// error a two-byte window shows (too short, too long, overlong, surrogate, > U+10FFFF, two
+// continuations); that bit (TWO_CONTS, bit 7) is XORed with "a lead two or three bytes back
+// asks for a continuation here".  A message is valid exactly when no byte is flagged and it
+// does not end inside a sequence.  Four bytes at a time in a dword (SWAR): a lookup is one
+// v_perm_b32 over an 8-entry byte table (the high-nibble tables are constant below 0x80, so
+// 8 entries and a select on bit 7 do; the low-nibble table takes two), the previous bytes
+// come by v_alignbyte_b32 from the previous dword, whose own lookups are carried: about 25
+// VALU operations per dword (the round-2 rule took about 45).  tools/utf8_swar_check.py:
+// this formula == the scalar rule (utf8_rule, phase B) at every position over every 4-byte
+// context of 31 boundary bytes, and rule + end check == CPython's strict decoder over every
+// string of up to 4 bytes from 27 of them.
+constexpr uint32_t kB1H_HI = 0x49150121u, kB1H_LO = 0x80808080u;   // prev byte, high nibble 8..F
+constexpr uint32_t kB2H_HI = 0x01010101u, kB2H_LO = 0xBABAAEE6u;   // this byte, high nibble 8..F
+constexpr uint32_t kCLS_HI = 0xC0800000u;                          // high nibble E: 0x80, F: 0xC0
+constexpr uint32_t kB1L_0H = 0xCBCBCB8Bu, kB1L_0L = 0x8383A3E7u;   // prev byte, low nibble 0..7
+constexpr uint32_t kB1L_1H = 0xCBCBDBCBu, kB1L_1L = 0xCBCBCBCBu;   // prev byte, low nibble 8..F
+constexpr uint32_t kSignSel = 0x090B080Au;   // v_perm_b32: byte i <- bit 7 of byte i of S1 (S0 = S1 << 8)
+
+// 0xFF in each byte of v whose bit 7 is set (v_perm_b32's sign selectors: bits 15 / 31 of
+// its two sources, here v << 8 and v)
+__device__ __forceinline__ uint32_t sign_bytes(uint32_t v) { return __builtin_amdgcn_perm(v << 8, v, kSignSel); }
+
+// The lookups of one dword x that the NEXT bytes need (and x's own byte_2_high): b1 =
+// byte_1_high & byte_1_low of each byte (the AND of the two previous-byte lookups depends
+// on the byte alone, so it is computed once, on x, and shifted in for the next bytes);
+// cls = lead class (bit 7: >= E0, bit 6: >= F0).
+struct Utf8Word {
+    uint32_t b1, cls, b2h;
 };
 
-__device__ __forceinline__ Utf8Carry utf8_carry(uint32_t prev) {
-    const uint32_t l2 = prev & (prev << 1) & 0x80808080u;
-    const uint32_t l3 = l2 & (prev << 2);
-    return {prev, l2, l3, l3 & (prev << 3)};
+__device__ __forceinline__ Utf8Word utf8_word(uint32_t x) {
+    const uint32_t mx = sign_bytes(x);                    // x >= 0x80
+    const uint32_t hx = (x >> 4) & 0x07070707u;           // high nibble & 7 (a perm index)
+    const uint32_t lx = x & 0x07070707u;                  // low nibble & 7
+    const uint32_t m3 = __builtin_amdgcn_perm(x << 12, x << 4, kSignSel);   // bit 3 of each byte
+    const uint32_t b1h = (mx & __builtin_amdgcn_perm(kB1H_HI, kB1H_LO, hx)) | (~mx & 0x02020202u);
+    const uint32_t b1l = (m3 & __builtin_amdgcn_perm(kB1L_1H, kB1L_1L, lx)) |
+                         (~m3 & __builtin_amdgcn_perm(kB1L_0H, kB1L_0L, lx));
+    Utf8Word w;
+    w.b1 = b1h & b1l;
+    w.b2h = (mx & __builtin_amdgcn_perm(kB2H_HI, kB2H_LO, hx)) | (~mx & 0x01010101u);
+    w.cls = mx & __builtin_amdgcn_perm(kCLS_HI, 0u, hx);
+    return w;
 }
 
-// t[idx] for each byte's nibble idx (0..15) of a 16-entry byte table held in 4 dwords
-__device__ __forceinline__ uint32_t nibble_lookup(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3, uint32_t idx) {
-    const uint32_t i7 = idx & 0x07070707u;
-    const uint32_t lo = __builtin_amdgcn_perm(t1, t0, i7);   // entries 0..7
-    const uint32_t hi = __builtin_amdgcn_perm(t3, t2, i7);   // entries 8..15
-    const uint32_t m = ((idx & 0x08080808u) >> 3) * 0xFFu;
-    return (m & hi) | (~m & lo);
+// nonzero in each byte of dword w the rule flags; p = the dword before it (its b1, cls)
+__device__ __forceinline__ uint32_t utf8_err(const Utf8Word& w, uint32_t pb1, uint32_t pcls) {
+    const uint32_t b1 = __builtin_amdgcn_alignbyte(w.b1, pb1, 3);   // the previous byte's two lookups
+    // a lead >= E0 two bytes back, or >= F0 three bytes back: this byte must continue it
+    const uint32_t must =
+        (__builtin_amdgcn_alignbyte(w.cls, pcls, 2) | (__builtin_amdgcn_alignbyte(w.cls, pcls, 1) << 1)) & 0x80808080u;
+    return (b1 & w.b2h) ^ must;
 }
 
-__device__ __forceinline__ uint32_t utf8_err_word(uint32_t x, Utf8Carry& c) {
-    const uint32_t H = 0x80808080u;
-    const uint32_t s1 = x << 1;
-    const uint32_t l2 = x & s1 & H;          // byte >= C0: a lead of 2+ bytes
-    const uint32_t l3 = l2 & (x << 2);       // byte >= E0
-    const uint32_t l4 = l3 & (x << 3);       // byte >= F0
-    const uint32_t cont = x & ~s1 & H;       // 80..BF
-    const uint32_t need = __builtin_amdgcn_alignbyte(l2, c.l2, 3) | __builtin_amdgcn_alignbyte(l3, c.l3, 2) |
-                          __builtin_amdgcn_alignbyte(l4, c.l4, 1);
-    uint32_t err = need ^ cont;
-    const uint32_t z = (x & 0xFEFEFEFEu) ^ 0xC0C0C0C0u;            // C0 / C1
-    err |= ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & H;
-    err |= ((x & 0x7F7F7F7Fu) + 0x0B0B0B0Bu) & x & H;               // F5..FF
-    // the byte after E0 / ED / F0 / F4: bits 0-3 = rule broken after E0 / F0 / ED / F4
-    const uint32_t p1 = __builtin_amdgcn_alignbyte(x, c.x, 3);      // the byte before each byte of x
-    const uint32_t lead3 = __builtin_amdgcn_alignbyte(l3, c.l3, 3);  // ... is >= E0
-    // by p1's low nibble: 0 -> E0 or F0, 4 -> F4, D -> ED
-    const uint32_t t1 = nibble_lookup(0x00000003u, 0x00000008u, 0x00000000u, 0x00000400u, p1 & 0x0F0F0F0Fu);
-    const uint32_t sel = ((p1 & 0x10101010u) >> 4) * 5u + 0x05050505u;   // E lead: E0 | ED bits, F lead: F0 | F4
-    // by x's high nibble 8..B (others are not continuations, flagged above)
-    const uint32_t t2 = __builtin_amdgcn_perm(0u, 0x0C0C0903u, (x >> 4) & 0x07070707u);
-    err |= ((t1 & sel & t2) + 0x7F7F7F7Fu) & lead3;
-    c = {x, l2, l3, l4};
-    return err & H;
+// what validation carries from one span to the next: lane 63's last dword and its lookups
+struct Utf8Carry {
+    uint32_t x, b1, cls;
+};
+__device__ __forceinline__ Utf8Carry utf8_start() { return {0u, 0x02020202u, 0u}; }   // as after ASCII
+
+// bit 7 of each byte of e set where the byte is nonzero (the rare error path)
+__device__ __forceinline__ uint32_t nonzero_bytes(uint32_t e) {
+    return (((e & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | e) & 0x80808080u;
 }
 
 // The frame holding position P (P coordinates), or -1: a binary search over the
@@ -531,24 +544,36 @@ __device__ int64_t frame_of(const Args& a, uint64_t P) {
 // another wavefront's chunk, which in place may already hold unmasked or still
 // masked bytes -- utf8_messages() checks them once the whole batch is unmasked.
 // Errors are rare: their frame lookup is a slow path.
-__device__ __forceinline__ void validate_span(const Args& a, const Table& t, uint64_t A0, u32x4 out, uint32_t prevd,
+__device__ __forceinline__ void validate_span(const Args& a, const Table& t, uint64_t A0, u32x4 out, Utf8Carry& sc,
                                               bool seam, int lane) {
     const uint64_t W = A0 + 16ull * (uint64_t)lane;
+    const uint32_t prevd = lane ? (uint32_t)__shfl_up((int)out[3], 1, kWave) : sc.x;
+    // all ASCII across the wave, the 4 bytes before each lane's included (the common case
+    // for text): nothing to check
+    if (!__ballot(((out[0] | out[1] | out[2] | out[3] | prevd) & 0x80808080u) != 0)) {
+        sc = {(uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1), 0x02020202u, 0u};
+        return;
+    }
+    Utf8Word w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = utf8_word(out[k]);
+    // the previous lane's last dword's lookups (lane 0: the previous span's lane 63)
+    const uint32_t ub1 = (uint32_t)__shfl_up((int)w[3].b1, 1, kWave), ucls = (uint32_t)__shfl_up((int)w[3].cls, 1, kWave);
     u32x4 e;
-    // all ASCII across the wave (the common case for text): nothing to check
-    if (!__ballot(((out[0] | out[1] | out[2] | out[3] | prevd) & 0x80808080u) != 0)) return;
-    Utf8Carry c = utf8_carry(prevd);
-    e[0] = utf8_err_word(out[0], c);
-    e[1] = utf8_err_word(out[1], c);
-    e[2] = utf8_err_word(out[2], c);
-    e[3] = utf8_err_word(out[3], c);
+    e[0] = utf8_err(w[0], lane ? ub1 : sc.b1, lane ? ucls : sc.cls);
+    e[1] = utf8_err(w[1], w[0].b1, w[0].cls);
+    e[2] = utf8_err(w[2], w[1].b1, w[1].cls);
+    e[3] = utf8_err(w[3], w[2].b1, w[2].cls);
+    sc = {(uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1),
+          (uint32_t)__builtin_amdgcn_readlane((int)w[3].b1, kWave - 1),
+          (uint32_t)__builtin_amdgcn_readlane((int)w[3].cls, kWave - 1)};
     if (seam && lane == 0) e[0] &= ~0x00FFFFFFu;
     if (!__ballot((e[0] | e[1] | e[2] | e[3]) != 0)) return;
     // one bit per broken byte of the lane's vector
     uint32_t bits = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-        const uint32_t m = (e[w] >> 7) & 0x01010101u;
+        const uint32_t m = (nonzero_bytes(e[w]) >> 7) & 0x01010101u;
         bits |= ((m | m >> 7 | m >> 14 | m >> 21) & 0xFu) << (4 * w);
     }
     if (readlane64(t.start, 0) > A0) {
@@ -644,7 +669,7 @@ __device__ __forceinline__ void edge_chunk(const AT& a, uint64_t A, int lane) {
     }
     Table t;
     table_load(a, t, locate(a, A, lane), lane);
-    uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
+    Utf8Carry carry = utf8_start();   // the previous span's last dword and its lookups (VAL)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t A0 = A + (uint64_t)u * kSpan;
@@ -668,9 +693,7 @@ __device__ __forceinline__ void edge_chunk(const AT& a, uint64_t A, int lane) {
         if (P >= full_lo && P < full_hi) store_vec<NT>(a, P, d[u] ^ m);
         else if (P < vec_end) edge_vec(a, P, m);
         if constexpr (VAL) {
-            const uint32_t up = (uint32_t)__shfl_up((int)out[3], 1, kWave);
-            validate_span(a, t, A0, out, lane ? up : carry, u == 0, lane);
-            carry = (uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1);
+            validate_span(a, t, A0, out, carry, u == 0, lane);
         }
     }
 }
@@ -733,7 +756,7 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
         for (int u = 0; u < U; ++u) dst[u] = load_vec<SRC_ALIGNED, NT>(a, base + (uint64_t)u * kSpan + 16ull * lane);
     };
     auto process = [&](const u32x4 (&src)[U], Table& t, uint64_t base) {
-        uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
+        Utf8Carry carry = utf8_start();   // the previous span's last dword and its lookups (VAL)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t A0 = base + (uint64_t)u * kSpan;
@@ -741,9 +764,7 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
             const u32x4 out = src[u] ^ m;
             store_vec<NT>(a, A0 + 16ull * lane, out);
             if constexpr (VAL) {
-                const uint32_t up = (uint32_t)__shfl_up((int)out[3], 1, kWave);
-                validate_span(a, t, A0, out, lane ? up : carry, u == 0, lane);
-                carry = (uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1);
+                validate_span(a, t, A0, out, carry, u == 0, lane);
             }
         }
     };
@@ -829,7 +850,7 @@ __device__ __forceinline__ void first_probe(const AT& a, Table& t, uint64_t A, i
 }
 
 template <int U, int K, bool SRC_ALIGNED, bool NT, bool VAL = false, class AT = Args>
-__global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
+__global__ __launch_bounds__(256, (VAL && U == 4) ? 8 : 1) void mask_np_kernel(AT a) {
     constexpr uint64_t kStep = kSpan * U;
     constexpr uint64_t kWin = kStep * K;
     const int lane = threadIdx.x & (kWave - 1);
@@ -860,16 +881,14 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
         for (int k = 0; k < K; ++k) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, A + (uint64_t)k * kStep, lane);
         return;
     }
-    uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
+    Utf8Carry carry = utf8_start();   // the previous span's last dword and its lookups (VAL)
     Table t;
     auto emit = [&](uint64_t A0, u32x4 src, bool first) {
         const u32x4 m = span_mask(a, t, A0, lane);
         const u32x4 out = src ^ m;
         store_vec<NT>(a, A0 + 16ull * lane, out);
         if constexpr (VAL) {
-            const uint32_t up = (uint32_t)__shfl_up((int)out[3], 1, kWave);
-            validate_span(a, t, A0, out, lane ? up : carry, first, lane);
-            carry = (uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1);
+            validate_span(a, t, A0, out, carry, first, lane);
         }
     };
     if constexpr (!SRC_ALIGNED) {
@@ -1095,14 +1114,13 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
 // phase A fails it; the first 3 bytes of every frame are checked here with the 3
 // bytes before them in the message; the message must not end inside a sequence.
 __device__ __forceinline__ bool utf8_rule(uint32_t b3, uint32_t b2, uint32_t b1, uint32_t b0) {
-    const bool need = b1 >= 0xC0 || b2 >= 0xE0 || b3 >= 0xF0;
-    const bool cont = (b0 & 0xC0) == 0x80;
-    if (need != cont) return true;
-    if (b0 >= 0xF5 || b0 == 0xC0 || b0 == 0xC1) return true;
-    if ((b1 == 0xE0 && b0 < 0xA0) || (b1 == 0xED && b0 >= 0xA0) || (b1 == 0xF0 && b0 < 0x90) ||
-        (b1 == 0xF4 && b0 >= 0x90))
-        return true;
-    return false;
+    // utf8_err_word's rule for one byte b0 and the 3 before it (0 before a message's start)
+    auto lut8 = [](uint32_t hi, uint32_t lo, uint32_t i) { return ((i < 4 ? lo >> (8 * i) : hi >> (8 * (i - 4)))) & 0xFFu; };
+    const uint32_t b1h = b1 < 0x80 ? 0x02u : lut8(kB1H_HI, kB1H_LO, (b1 >> 4) & 7);
+    const uint32_t b1l = (b1 & 8) ? lut8(kB1L_1H, kB1L_1L, b1 & 7) : lut8(kB1L_0H, kB1L_0L, b1 & 7);
+    const uint32_t b2h = b0 < 0x80 ? 0x01u : lut8(kB2H_HI, kB2H_LO, (b0 >> 4) & 7);
+    const uint32_t must = (b2 >= 0xE0 || b3 >= 0xF0) ? 0x80u : 0u;
+    return ((b1h & b1l & b2h) ^ must) != 0;
 }
 
 __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uint8_t* h0, uint64_t n,
@@ -1183,7 +1201,14 @@ __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uin
 // the VAL kernels: 4 KiB windows (the seams utf8_messages re-checks are at multiples of it)
 template <bool AL>
 static hipError_t launch_val(const Args& a, bool persistent, hipStream_t s) {
-    if (!persistent) return launch_np<4, 1, AL, true, true>(a, s);
+    if (!persistent) {
+        // a 4 KiB window per wavefront as U KiB x K steps (NETC_GPU_KNOB_VAL_STEPS = K: 1, 2 or 4)
+        switch (knob(NETC_GPU_KNOB_VAL_STEPS)) {
+            case 2: return launch_np<2, 2, AL, true, true>(a, s);
+            case 4: return launch_np<1, 4, AL, true, true>(a, s);
+            default: return launch_np<4, 1, AL, true, true>(a, s);
+        }
+    }
     const uint64_t cap = (uint64_t)resident_blocks<4, AL, true>();
     const uint64_t want = (a.nwin + 3) / 4;
     const int blocks = (int)(want < cap ? want : cap);
