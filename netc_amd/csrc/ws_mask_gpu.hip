@@ -476,43 +476,35 @@ constexpr uint32_t kSignSel = 0x090B080Au;   // v_perm_b32: byte i <- bit 7 of b
 // its two sources, here v << 8 and v)
 __device__ __forceinline__ uint32_t sign_bytes(uint32_t v) { return __builtin_amdgcn_perm(v << 8, v, kSignSel); }
 
-// The lookups of one dword x that the NEXT bytes need (and x's own byte_2_high): b1 =
-// byte_1_high & byte_1_low of each byte (the AND of the two previous-byte lookups depends
-// on the byte alone, so it is computed once, on x, and shifted in for the next bytes);
-// cls = lead class (bit 7: >= E0, bit 6: >= F0).
-struct Utf8Word {
-    uint32_t b1, cls, b2h;
+struct Utf8Carry {
+    uint32_t x, b1h, cls;   // the previous dword, its byte_1_high lookup, its lead class (>= E0 / >= F0)
 };
 
-__device__ __forceinline__ Utf8Word utf8_word(uint32_t x) {
+__device__ __forceinline__ Utf8Carry utf8_carry(uint32_t prev) {
+    const uint32_t m = sign_bytes(prev), h = (prev >> 4) & 0x07070707u;
+    return {prev, (m & __builtin_amdgcn_perm(kB1H_HI, kB1H_LO, h)) | (~m & 0x02020202u),
+            m & __builtin_amdgcn_perm(kCLS_HI, 0u, h)};
+}
+
+// nonzero in each byte of x the rule flags; c: the dword before x (updated to x)
+__device__ __forceinline__ uint32_t utf8_err_word(uint32_t x, Utf8Carry& c) {
     const uint32_t mx = sign_bytes(x);                    // x >= 0x80
     const uint32_t hx = (x >> 4) & 0x07070707u;           // high nibble & 7 (a perm index)
-    const uint32_t lx = x & 0x07070707u;                  // low nibble & 7
-    const uint32_t m3 = __builtin_amdgcn_perm(x << 12, x << 4, kSignSel);   // bit 3 of each byte
-    const uint32_t b1h = (mx & __builtin_amdgcn_perm(kB1H_HI, kB1H_LO, hx)) | (~mx & 0x02020202u);
-    const uint32_t b1l = (m3 & __builtin_amdgcn_perm(kB1L_1H, kB1L_1L, lx)) |
-                         (~m3 & __builtin_amdgcn_perm(kB1L_0H, kB1L_0L, lx));
-    Utf8Word w;
-    w.b1 = b1h & b1l;
-    w.b2h = (mx & __builtin_amdgcn_perm(kB2H_HI, kB2H_LO, hx)) | (~mx & 0x01010101u);
-    w.cls = mx & __builtin_amdgcn_perm(kCLS_HI, 0u, hx);
-    return w;
-}
-
-// nonzero in each byte of dword w the rule flags; p = the dword before it (its b1, cls)
-__device__ __forceinline__ uint32_t utf8_err(const Utf8Word& w, uint32_t pb1, uint32_t pcls) {
-    const uint32_t b1 = __builtin_amdgcn_alignbyte(w.b1, pb1, 3);   // the previous byte's two lookups
+    const uint32_t b1hx = (mx & __builtin_amdgcn_perm(kB1H_HI, kB1H_LO, hx)) | (~mx & 0x02020202u);
+    const uint32_t b2h = (mx & __builtin_amdgcn_perm(kB2H_HI, kB2H_LO, hx)) | (~mx & 0x01010101u);
+    const uint32_t cls = mx & __builtin_amdgcn_perm(kCLS_HI, 0u, hx);
+    const uint32_t p1 = __builtin_amdgcn_alignbyte(x, c.x, 3);          // the byte before each byte
+    const uint32_t b1h = __builtin_amdgcn_alignbyte(b1hx, c.b1h, 3);
+    const uint32_t l1 = p1 & 0x07070707u;
+    const uint32_t m3 = __builtin_amdgcn_perm(p1 << 12, p1 << 4, kSignSel);   // bit 3 of each p1 byte
+    const uint32_t b1l = (m3 & __builtin_amdgcn_perm(kB1L_1H, kB1L_1L, l1)) |
+                         (~m3 & __builtin_amdgcn_perm(kB1L_0H, kB1L_0L, l1));
     // a lead >= E0 two bytes back, or >= F0 three bytes back: this byte must continue it
     const uint32_t must =
-        (__builtin_amdgcn_alignbyte(w.cls, pcls, 2) | (__builtin_amdgcn_alignbyte(w.cls, pcls, 1) << 1)) & 0x80808080u;
-    return (b1 & w.b2h) ^ must;
+        (__builtin_amdgcn_alignbyte(cls, c.cls, 2) | (__builtin_amdgcn_alignbyte(cls, c.cls, 1) << 1)) & 0x80808080u;
+    c = {x, b1hx, cls};
+    return (b1h & b1l & b2h) ^ must;
 }
-
-// what validation carries from one span to the next: lane 63's last dword and its lookups
-struct Utf8Carry {
-    uint32_t x, b1, cls;
-};
-__device__ __forceinline__ Utf8Carry utf8_start() { return {0u, 0x02020202u, 0u}; }   // as after ASCII
 
 // bit 7 of each byte of e set where the byte is nonzero (the rare error path)
 __device__ __forceinline__ uint32_t nonzero_bytes(uint32_t e) {
@@ -544,29 +536,22 @@ __device__ int64_t frame_of(const Args& a, uint64_t P) {
 // another wavefront's chunk, which in place may already hold unmasked or still
 // masked bytes -- utf8_messages() checks them once the whole batch is unmasked.
 // Errors are rare: their frame lookup is a slow path.
-__device__ __forceinline__ void validate_span(const Args& a, const Table& t, uint64_t A0, u32x4 out, Utf8Carry& sc,
+__device__ __forceinline__ void validate_span(const Args& a, const Table& t, uint64_t A0, u32x4 out, uint32_t& sc,
                                               bool seam, int lane) {
     const uint64_t W = A0 + 16ull * (uint64_t)lane;
-    const uint32_t prevd = lane ? (uint32_t)__shfl_up((int)out[3], 1, kWave) : sc.x;
+    // the 4 bytes before the lane's (lane 0: the previous span's last 4, or 0 at a window start)
+    const uint32_t up = (uint32_t)__shfl_up((int)out[3], 1, kWave);
+    const uint32_t prevd = lane ? up : sc;
+    sc = (uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1);
+    u32x4 e;
     // all ASCII across the wave, the 4 bytes before each lane's included (the common case
     // for text): nothing to check
-    if (!__ballot(((out[0] | out[1] | out[2] | out[3] | prevd) & 0x80808080u) != 0)) {
-        sc = {(uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1), 0x02020202u, 0u};
-        return;
-    }
-    Utf8Word w[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) w[k] = utf8_word(out[k]);
-    // the previous lane's last dword's lookups (lane 0: the previous span's lane 63)
-    const uint32_t ub1 = (uint32_t)__shfl_up((int)w[3].b1, 1, kWave), ucls = (uint32_t)__shfl_up((int)w[3].cls, 1, kWave);
-    u32x4 e;
-    e[0] = utf8_err(w[0], lane ? ub1 : sc.b1, lane ? ucls : sc.cls);
-    e[1] = utf8_err(w[1], w[0].b1, w[0].cls);
-    e[2] = utf8_err(w[2], w[1].b1, w[1].cls);
-    e[3] = utf8_err(w[3], w[2].b1, w[2].cls);
-    sc = {(uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1),
-          (uint32_t)__builtin_amdgcn_readlane((int)w[3].b1, kWave - 1),
-          (uint32_t)__builtin_amdgcn_readlane((int)w[3].cls, kWave - 1)};
+    if (!__ballot(((out[0] | out[1] | out[2] | out[3] | prevd) & 0x80808080u) != 0)) return;
+    Utf8Carry c = utf8_carry(prevd);
+    e[0] = utf8_err_word(out[0], c);
+    e[1] = utf8_err_word(out[1], c);
+    e[2] = utf8_err_word(out[2], c);
+    e[3] = utf8_err_word(out[3], c);
     if (seam && lane == 0) e[0] &= ~0x00FFFFFFu;
     if (!__ballot((e[0] | e[1] | e[2] | e[3]) != 0)) return;
     // one bit per broken byte of the lane's vector
@@ -669,7 +654,7 @@ __device__ __forceinline__ void edge_chunk(const AT& a, uint64_t A, int lane) {
     }
     Table t;
     table_load(a, t, locate(a, A, lane), lane);
-    Utf8Carry carry = utf8_start();   // the previous span's last dword and its lookups (VAL)
+    uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t A0 = A + (uint64_t)u * kSpan;
@@ -756,7 +741,7 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
         for (int u = 0; u < U; ++u) dst[u] = load_vec<SRC_ALIGNED, NT>(a, base + (uint64_t)u * kSpan + 16ull * lane);
     };
     auto process = [&](const u32x4 (&src)[U], Table& t, uint64_t base) {
-        Utf8Carry carry = utf8_start();   // the previous span's last dword and its lookups (VAL)
+        uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t A0 = base + (uint64_t)u * kSpan;
@@ -850,7 +835,7 @@ __device__ __forceinline__ void first_probe(const AT& a, Table& t, uint64_t A, i
 }
 
 template <int U, int K, bool SRC_ALIGNED, bool NT, bool VAL = false, class AT = Args>
-__global__ __launch_bounds__(256, (VAL && U == 4) ? 8 : 1) void mask_np_kernel(AT a) {
+__global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
     constexpr uint64_t kStep = kSpan * U;
     constexpr uint64_t kWin = kStep * K;
     const int lane = threadIdx.x & (kWave - 1);
@@ -881,7 +866,7 @@ __global__ __launch_bounds__(256, (VAL && U == 4) ? 8 : 1) void mask_np_kernel(A
         for (int k = 0; k < K; ++k) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, A + (uint64_t)k * kStep, lane);
         return;
     }
-    Utf8Carry carry = utf8_start();   // the previous span's last dword and its lookups (VAL)
+    uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
     Table t;
     auto emit = [&](uint64_t A0, u32x4 src, bool first) {
         const u32x4 m = span_mask(a, t, A0, lane);

@@ -401,6 +401,10 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     __shared__ uint32_t stage[4][kWords];      // per wave: its chunk's bytes (+ 32 after)
     __shared__ unsigned long long set[4][kSet];
     __shared__ uint16_t queue[4][kQCap];
+#ifdef NETC_SCAN_K1_EXP
+    __shared__ uint32_t qn[4];
+    if ((threadIdx.x & 63) == 0) qn[threadIdx.x / 64] = 0;
+#endif
     SCAN_SCOPE(0);
     // wv through readfirstlane: the chunk index, its bounds and the edge test below are
     // then scalar (SGPR arithmetic, scalar branches) instead of per-lane VALU
@@ -536,8 +540,17 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         // strict mode prunes exits that cannot start a frame: payload bytes parsed as a
         // chain land on random positions, which pass with ~2 % odds, while the true chain
         // always lands on a real header
+#ifdef NETC_SCAN_K1_EXP
+        // diagnostic build only (tools/, timing of K1's tail): the exit written to a
+        // per-source-chunk list with a plain store -- no target check, no atomic
+        if (!(v & kTerm) && v >= Bend && set_insert(set[wv], v, &ovf)) {
+            const uint32_t k = atomicAdd(&qn[wv], 1u);
+            if (k < (uint32_t)kCand) a.cand[c * kCand + k] = v;
+        }
+#else
         if (!(v & kTerm) && v >= Bend && set_insert(set[wv], v, &ovf) && !quick_reject(a, v))
             append_cand(a, v, v / kChunk / kTileChunks != c / kTileChunks);
+#endif
     }
     SCAN_STAMP(0, 3);   // parsed, exits checked and appended
     if (ovf) atomicOr(a.ovf, kOvfSet);
@@ -1637,6 +1650,9 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.pf_lim = len >= 16 ? len - 16 : 0;
     const unsigned blk = (unsigned)((chunks + kBlkChunks - 1) / kBlkChunks);
     hipLaunchKernelGGL(scan_exits, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, stream, a);
+#if defined(NETC_SCAN_K1_ONLY) || defined(NETC_SCAN_K1_EXP)
+    return hipGetLastError();   // diagnostic builds only (tools/): K1 timed alone
+#endif
     hipLaunchKernelGGL(scan_links, dim3(blk), dim3(kScanT), 0, stream, a);
     hipLaunchKernelGGL(scan_tiles, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a);
     hipLaunchKernelGGL(scan_resolve, dim3(1), dim3(kResolveT), 0, stream, a, tiles);

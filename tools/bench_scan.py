@@ -25,6 +25,10 @@ def main():
     ap.add_argument("--workloads", default="c2,c4")
     ap.add_argument("--non-strict", action="store_true", help="flags 0: the reference's semantics (speculative pass)")
     ap.add_argument("--unmasked", action="store_true", help="unmasked frames (server-to-client direction)")
+    ap.add_argument("--rsv1", action="store_true",
+                    help="every frame with RSV1 set (as permessage-deflate sends them): strict rejects the stream; "
+                         "non-strict runs the speculative pass, which stops at the first such header and walks on "
+                         "serially (ADVICE r2: the cliff, measured)")
     args = ap.parse_args()
     flags = 0 if args.non_strict else 1
 
@@ -45,7 +49,8 @@ def main():
             off, keys = off[: cut + 1], keys[:cut]
         rng = np.random.default_rng(5)
         payload = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
-        wire, wo = orc.encode_batch(payload, off, keys, None, not args.unmasked)
+        b0 = np.full(keys.size, 0xC2, dtype=np.uint8) if args.rsv1 else None
+        wire, wo = orc.encode_batch(payload, off, keys, b0, not args.unmasked)
         if args.unmasked:
             keys = np.zeros_like(keys)
         n = keys.size
@@ -98,7 +103,7 @@ def main():
                hres.ctypes.data)
             reps += 1
         host_s = (time.perf_counter() - t0) / reps
-        print(json.dumps({"workload": wl, "strict": bool(flags), "masked": not args.unmasked, "frames": int(n), "wire_bytes": int(wire.size), "us_per_scan": round(us, 2),
+        print(json.dumps({"workload": wl, "strict": bool(flags), "masked": not args.unmasked, "rsv1": args.rsv1, "frames": int(n), "wire_bytes": int(wire.size), "us_per_scan": round(us, 2),
                           "wire_GBps": round(wire.size / (us * 1e-6) / 1e9, 1),
                           "frames_per_s": round(n / (us * 1e-6), 1), "matches_oracle": bool(ok),
                           "serial_fallback": hex(nm.scan_diag(s)),

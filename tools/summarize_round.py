@@ -41,8 +41,9 @@ def main():
     ap.add_argument("--workload", default="c2")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--src", default=None, help="gpurun_out/ subdirectory (default: the tag)")
     args = ap.parse_args()
-    src = os.path.join(ROOT, "gpurun_out", args.tag)
+    src = os.path.join(ROOT, "gpurun_out", args.src or args.tag)
     prof = os.path.join(ROOT, "profiles")
     wl = args.workload
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
