@@ -73,6 +73,10 @@ def parse_args():
     p.add_argument("--pipelined-probe", action="store_true",
                    help="also time two independent batches in flight on two streams (secondary figure; its "
                         "overlapping launches would inflate a rocprof average of the kernel, so it is off by default)")
+    p.add_argument("--sync", choices=("auto", "spin"), default="auto",
+                   help="how the host waits for the GPU (hipSetDeviceFlags before the context exists): the "
+                        "runtime's heuristic, or spin-wait (the synchronize that closes the timed region returns "
+                        "without a wake-up delay)")
     p.add_argument("--no-shard-leg", dest="shard_leg", action="store_false",
                    help="at N > 1, skip the BASELINE config 4 leg (8 x 1 GiB mixed-frame shards, c4_shards)")
     return p.parse_args()
@@ -401,6 +405,17 @@ def launch_ranks(args) -> int:
     return subprocess.run(cmd).returncode
 
 
+def set_spin_sync(device: int) -> None:
+    """hipSetDeviceFlags(hipDeviceScheduleSpin) on `device` before its context exists: a
+    synchronize then spin-waits on the GPU instead of yielding the thread (the runtime the
+    flag goes to is torch's: same SONAME, already loaded by `import torch`)."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    if hip.hipSetDevice(device) != 0 or hip.hipSetDeviceFlags(1) != 0:   # hipDeviceScheduleSpin = 1
+        print("bench.py: hipSetDeviceFlags(spin) failed; the runtime's default wait is used", file=sys.stderr)
+
+
 def timed_steps(torch, step, steps: int, warmup: int, stream, device, world: int):
     """W untimed steps, then exactly K steps bracketed by barrier + synchronize on both sides.
     Returns (this rank's elapsed seconds, mean launch duration in ms from two HIP events on the
@@ -495,6 +510,8 @@ def main():
     if not rehearsal and torch.cuda.device_count() < world:
         print(f"bench.py: {world} ranks but {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr, flush=True)
         sys.exit(2)
+    if args.sync == "spin":
+        set_spin_sync(local)
     if world > 1:
         import torch.distributed as dist
 
@@ -612,6 +629,7 @@ def main():
                 "parallelism": f"shard{world} (independent frames, one process per GPU, no collective)",
                 "entry": "netc_gpu_mask_batch (include/ws/mask.h)",
                 "devices": "rehearsal: every rank on one GPU" if rehearsal else "one GPU per rank",
+                "host_sync": args.sync,
             },
             "roofline": {
                 "bound": "hbm",
