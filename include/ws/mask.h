@@ -128,12 +128,16 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *   SCAN_ANCHOR_SLOTS  cap on the frame scan's anchor slots [all]  (NETC_SCAN_ANCHOR_SLOTS)
  *   VAL_STEPS          netc_gpu_unmask_validate's 4 KiB window as 1, 2 or 4 steps [1]
  *                                                                  (NETC_VAL_STEPS)
+ *   SCAN_FUSE          0 runs the frame scan's links / tiles / resolve phases as three
+ *                      launches at every size [1: one launch up to 512 MiB]
+ *                                                                  (NETC_SCAN_FUSE)
  */
 #define NETC_GPU_KNOB_ENC_DENSE_BYTES   1
 #define NETC_GPU_KNOB_ENC_SCAN_PER      2
 #define NETC_GPU_KNOB_SCAN_FAST_RANK    3
 #define NETC_GPU_KNOB_SCAN_ANCHOR_SLOTS 4
 #define NETC_GPU_KNOB_VAL_STEPS         5
+#define NETC_GPU_KNOB_SCAN_FUSE         6
 int netc_gpu_knob(int knob, int64_t value);
 
 /**

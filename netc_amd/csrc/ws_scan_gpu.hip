@@ -149,6 +149,7 @@ struct ScanArgs {
     uint32_t* ovf_prev;    // ... reader is every K4 block, so K4 zeroes the previous call's word instead)
     uint32_t* ccount;      // nc + 1 candidate counters (zero when a call starts; K4 re-zeroes)
     uint8_t* ext;          // (nc + 1) * kCand: slot entered from another tile (or the root); K4 re-zeroes
+    uint32_t* tarr;        // K2+ (fused): per-tile arrival counters (the last arrival re-zeroes)
     uint64_t* cand;        // (nc + 1) * kCand candidate positions
     int32_t* link;         // node -> next node, -1 = chain ends, kDupLink
     uint64_t* nterm;       // the terminal where the node's walk leaves its chunk
@@ -373,8 +374,27 @@ __device__ __forceinline__ void append_cand(const ScanArgs& a, uint64_t x, bool 
 // 7-bit length: p + 2 + 4 + 125 >= chunk end  <=>  offset >= 3965 (lane 55 holds 3952-3967)
 static constexpr int kNearLane = 55;
 static constexpr int kQCap = 256;   // K1: exit-capable candidates queued per chunk (more: serial walk)
+static constexpr int kCheapMax = 64;   // K1: more from the cheap selection: the full quick check instead
 
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+
+// Inclusive sum over the wavefront's lanes, in DPP moves (no LDS trip): row_shr 1/2/4/8
+// within each row of 16, then row_bcast 15 / 31 carry the row totals up.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+// Bit 7 of each byte: the byte is x7E/x7F, or with hi = kH xFE/xFF -- a second header byte
+// with a 16/64-bit length (and MASK set, for hi = the byte itself).  3 VALU operations.
+__device__ __forceinline__ uint32_t long_len4(uint32_t r, uint32_t hi) {
+    return ((r & 0x7E7E7E7Eu) + 0x02020202u) & hi & kH;
+}
 
 // The 4 stream bytes at p for the chunk at the end (clamped load; bytes at or past len
 // undefined)
@@ -415,16 +435,27 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     if (lane == 0 && a.start / kChunk == c) append_cand(a, a.start, true);   // the root node
     if (B >= a.len) return;   // the virtual chunk: no bytes
     uint32_t d[4][4], nx[4];
+    if (Bend <= a.pf_lim) {   // wave-uniform: every load in place, no clamps (scalar base + lane offset)
+        const uint8_t* base = a.pf_base + B;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        uint64_t p = B + 1024 * i + 16 * (uint64_t)lane;
-        p = p < a.pf_lim ? p : a.pf_lim;
-        const u32x4 v = __builtin_nontemporal_load((const NETC_GLOBAL u32x4u*)(a.pf_base + p));
+        for (int i = 0; i < 4; ++i) {
+            const u32x4 v = __builtin_nontemporal_load((const NETC_GLOBAL u32x4u*)(base + 1024 * i + 16 * lane));
 #pragma unroll
-        for (int k = 0; k < 4; ++k) d[i][k] = v[k];
-    }
-    {
-        uint64_t q = Bend < a.pf_lim ? Bend : a.pf_lim;
+            for (int k = 0; k < 4; ++k) d[i][k] = v[k];
+        }
+        const u32x4 v = *(const NETC_GLOBAL u32x4u*)(base + kChunk);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nx[k] = v[k];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint64_t p = B + 1024 * i + 16 * (uint64_t)lane;
+            p = p < a.pf_lim ? p : a.pf_lim;
+            const u32x4 v = __builtin_nontemporal_load((const NETC_GLOBAL u32x4u*)(a.pf_base + p));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[i][k] = v[k];
+        }
+        const uint64_t q = Bend < a.pf_lim ? Bend : a.pf_lim;
         const u32x4 v = *(const NETC_GLOBAL u32x4u*)(a.pf_base + q);
 #pragma unroll
         for (int k = 0; k < 4; ++k) nx[k] = v[k];
@@ -472,7 +503,8 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     // for the whole pass, not one per dword.
     uint32_t half[2] = {0, 0};
     const uint32_t specH = a.spec ? kH : 0u;
-    auto pass = [&](auto strict_c) {
+    // the quick check of every position (the first header byte's checks too), vectors 0-3
+    auto full_pass = [&](auto strict_c) {
         constexpr bool kStrict = decltype(strict_c)::value;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -490,9 +522,55 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
             half[i >> 1] |= ci << (4 * (i & 1));
         }
     };
-    if (a.strict) pass(std::integral_constant<bool, true>{});
-    else pass(std::integral_constant<bool, false>{});
-    if (!fast) {   // wave-uniform: an edge chunk; positions before the start or at / past the end are not candidates
+    // Vectors 0-2 lie wholly more than 131 bytes before the chunk's end, so only a 16/64-bit
+    // length can exit from them: the second header byte is x7E/x7F (strict: xFE/xFF, MASK set).
+    // The cheap pass selects them by that test alone (3 VALU per dword, on the raw dwords) and
+    // leaves the first byte's checks to the parse (parse_at's `dead` holds every one of them):
+    // a few more queued positions (about 2 in 256 payload bytes) for the quick check's 7 VALU
+    // per dword.  The bit found at byte q is position q - 1's: byte j of dword k moves to byte
+    // j - 1 (bit 8 j + k -> 8 (j - 1) + k), byte 0 to byte 3 of dword k - 1 (bit k -> 24 + k -
+    // 1), and the lane's byte 0 to the previous lane's position 15 (bit 27).  Vector 3 (lanes
+    // near the end exit with a 7-bit length) takes the full check.
+    auto cheap_pass = [&](auto strict_c) {
+        constexpr bool kStrict = decltype(strict_c)::value;
+        const uint32_t hiR = kStrict ? specH : 0xFFFFFFFFu;   // OR'd into the byte itself: MASK test off
+        uint32_t raw[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            uint32_t ri = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t r = d[i][k];
+                ri |= long_len4(r, r | hiR) >> (7 - k);
+            }
+            raw[i] = ri;
+        }
+        // bit 0 of each (byte 0 of the lane's 16) belongs to the previous lane; vector 3's byte 0
+        // is vector 2's last position (lane 63)
+        const uint32_t r3 = long_len4(d[3][0], d[3][0] | hiR) >> 7;
+        const uint32_t b0s = (raw[0] & 1u) | (raw[1] & 1u) << 1 | (raw[2] & 1u) << 2 | (r3 & 1u) << 3;
+        const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)b0s);
+        uint32_t from_next = (uint32_t)__shfl_down((int)b0s, 1, kWave);
+        from_next = lane == kWave - 1 ? first >> 1 : from_next;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const uint32_t ri = raw[i];
+            const uint32_t ci = (ri >> 8) | ((ri & 0x0Eu) << 23) | (((from_next >> i) & 1u) << 27);
+            half[i >> 1] |= ci << (4 * (i & 1));
+        }
+        uint32_t ci = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t x = d[3][k];
+            const uint32_t y = __builtin_amdgcn_alignbyte(k < 3 ? d[3][k + 1] : nb[3], x, 1);
+            const uint32_t ok = kStrict ? quick_ok4(x, y | specH) : kH;
+            const uint32_t sel = lane >= kNearLane ? kH : ((y & 0x7E7E7E7Eu) + 0x02020202u);
+            ci |= (ok & sel & kH) >> (7 - k);
+        }
+        half[1] |= ci << 4;
+    };
+    // wave-uniform: an edge chunk; positions before the start or at / past the end are not candidates
+    auto edge_mask = [&]() {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint64_t q0 = B + 1024 * i + 16 * (uint64_t)lane;
@@ -507,17 +585,27 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
             }
             half[i >> 1] &= ~(0x0F0F0F0Fu << (4 * (i & 1))) | (vm << (4 * (i & 1)));
         }
-    }
+    };
+    // (non-strict: the two passes select the same positions)
+    if (a.strict) cheap_pass(std::integral_constant<bool, true>{});
+    else cheap_pass(std::integral_constant<bool, false>{});
+    if (!fast) edge_mask();
     uint64_t rel = (uint64_t)half[1] << 32 | half[0];
     // queue them (chunk offsets), then parse round-robin
-    const uint32_t mine = (uint32_t)__popcll(rel);
-    uint32_t incl = mine;
-#pragma unroll
-    for (int dd = 1; dd < kWave; dd <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)incl, dd, kWave);
-        if (lane >= dd) incl += o;
+    uint32_t mine = (uint32_t)__popcll(rel);
+    uint32_t incl = wave_incl_sum(mine);
+    uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+    if (a.strict && total > (uint32_t)kCheapMax) {
+        // wave-uniform: payload bytes that repeat xFE/xFF (a run of one byte under a 4-byte key)
+        // -- the full check keeps those chunks off the queue cap, as before the cheap pass
+        half[0] = half[1] = 0;
+        full_pass(std::integral_constant<bool, true>{});
+        if (!fast) edge_mask();
+        rel = (uint64_t)half[1] << 32 | half[0];
+        mine = (uint32_t)__popcll(rel);
+        incl = wave_incl_sum(mine);
+        total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
     }
-    const uint32_t total = (uint32_t)__shfl((int)incl, kWave - 1, kWave);
     if (total > (uint32_t)kQCap) {   // wave-uniform (adversarial payloads, non-strict mode)
         if (lane == 0) atomicOr(a.ovf, kOvfQueue);
         return;
@@ -642,14 +730,22 @@ __device__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const ui
 // links built in LDS, one thread walks them from the entry -- count / 8 + at most 7
 // hops, leaving an anchor every 8 frames -- and re-parses the last header for the exact
 // terminal.
-__global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
-    __shared__ uint32_t words[kWords];
-    __shared__ uint16_t l1[kChunk];
-    __shared__ uint16_t lj[kChunk];
-    __shared__ uint16_t lk16[kChunk];
-    __shared__ uint32_t queue[kBlkChunks * kCand];
-    __shared__ int nq;
-    SCAN_SCOPE(1);
+struct LinksLds {
+    uint32_t words[kWords];
+    uint16_t l1[kChunk];
+    uint16_t lj[kChunk];
+    uint16_t lk16[kChunk];
+    uint32_t queue[kBlkChunks * kCand];
+    int nq;
+};
+
+__device__ void links_body(const ScanArgs& a, LinksLds& sl) {
+    uint32_t* words = sl.words;
+    uint16_t* l1 = sl.l1;
+    uint16_t* lj = sl.lj;
+    uint16_t* lk16 = sl.lk16;
+    uint32_t* queue = sl.queue;
+    int& nq = sl.nq;
     const int tid = threadIdx.x;
     if (tid == 0) nq = 0;
     __syncthreads();
@@ -734,6 +830,12 @@ __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
         }
         __syncthreads();
     }
+}
+
+__global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
+    __shared__ LinksLds sl;
+    SCAN_SCOPE(1);
+    links_body(a, sl);
 }
 
 // exclusive prefix sum over a block of NT threads; the block total in *total
@@ -831,24 +933,38 @@ __device__ void rank_tile_fast(uint16_t* P, uint16_t* L, uint32_t* W, uint32_t* 
     }
 }
 
-__global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
-    __shared__ uint16_t cid[kTileSlots];   // tile slot -> compact node
-    __shared__ uint16_t gsl[kTileSlots];   // compact node -> tile slot
-    __shared__ uint16_t P[kTileSlots];     // current jump (compact), kNone: at the last node
-    __shared__ uint16_t L[kTileSlots];     // last node reached
-    __shared__ uint32_t W[kTileSlots];     // frames from the node to L's exit
-    __shared__ uint32_t bits[kTileSlots];
-    __shared__ uint16_t P2[kFastNodes], L2[kFastNodes];   // rank_tile_fast: the ping-pong halves
-    __shared__ uint32_t W2[kFastNodes];
-    __shared__ uint16_t elist[kExt];
-    __shared__ uint8_t eroot[kExt];
-    __shared__ int skip;
-    SCAN_SCOPE(2);
+struct TilesLds {
+    uint16_t cid[kTileSlots];   // tile slot -> compact node
+    uint16_t gsl[kTileSlots];   // compact node -> tile slot
+    uint16_t P[kTileSlots];     // current jump (compact), kNone: at the last node
+    uint16_t L[kTileSlots];     // last node reached
+    uint32_t W[kTileSlots];     // frames from the node to L's exit
+    uint32_t bits[kTileSlots];
+    uint16_t P2[kFastNodes], L2[kFastNodes];   // rank_tile_fast: the ping-pong halves
+    uint32_t W2[kFastNodes];
+    uint16_t elist[kExt];
+    uint8_t eroot[kExt];
+    int skip;
+};
+
+__device__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
+    uint16_t* cid = st.cid;
+    uint16_t* gsl = st.gsl;
+    uint16_t* P = st.P;
+    uint16_t* L = st.L;
+    uint32_t* W = st.W;
+    uint32_t* bits = st.bits;
+    uint16_t* P2 = st.P2;
+    uint16_t* L2 = st.L2;
+    uint32_t* W2 = st.W2;
+    uint16_t* elist = st.elist;
+    uint8_t* eroot = st.eroot;
+    int& skip = st.skip;
     const int t = threadIdx.x;
     // overflow: K4 walks serially.  Read once for the block (another tile may set it
     // meanwhile), in the same trip as the chunk data below; checked after the scans
     const uint32_t ovf0 = t == 0 ? __hip_atomic_load(a.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    const uint64_t tile = blockIdx.x, c = tile * kTileChunks + t, s0 = tile * kTileSlots;
+    const uint64_t c = tile * kTileChunks + t, s0 = tile * kTileSlots;
     // the chunk's counter, external flags, links and counts in one trip
     const bool live = c <= a.nc;
     const uint32_t cnt = live ? min(a.ccount[c], (uint32_t)kCand) : 0;
@@ -961,6 +1077,12 @@ __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
     if (t == 0) a.tcount[tile] = (uint32_t)E;
 }
 
+__global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
+    __shared__ TilesLds st;
+    SCAN_SCOPE(2);
+    tiles_body(a, blockIdx.x, st);
+}
+
 // Tile resolution (K3b): the external nodes of all tiles into LDS (tile by tile, in
 // bit order); each one's successor is the external node its path exits to; Wyllie
 // pointer jumping gives R = frames from the node to the end of its chain and marks
@@ -1003,32 +1125,45 @@ __device__ __forceinline__ void put_ext(uint32_t* eslot, uint32_t* ew, int32_t* 
 // thread i holds node i in registers, one barrier per round over ping-pong halves, a
 // fixed round count -- as rank_tile_fast.  The results end in succ / R; mark
 // (monotone) is one array.
-template <int NT>
+template <int NT, int PER>
 __device__ void resolve_fast(uint16_t* succ, uint64_t* R, uint16_t* succ2, uint64_t* R2, uint8_t* mark, int m) {
-    const int i = threadIdx.x;
-    uint16_t ms = i < m ? succ[i] : kNone;
-    uint64_t mr = i < m ? R[i] : 0;
+    uint16_t ms[PER];
+    uint64_t mr[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int i = threadIdx.x + NT * q;
+        ms[q] = i < m ? succ[i] : kNone;
+        mr[q] = i < m ? R[i] : 0;
+    }
     const int rounds = jump_rounds(m);
     for (int r = 0; r < rounds; ++r) {
         const uint16_t* ss = (r & 1) ? succ2 : succ;
         const uint64_t* sr = (r & 1) ? R2 : R;
         uint16_t* ds = (r & 1) ? succ : succ2;
         uint64_t* dr = (r & 1) ? R : R2;
-        if (i < m) {
-            if (ms != kNone) {
-                if (mark[i]) mark[ms] = 1;
-                mr += sr[ms];
-                ms = ss[ms];
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int i = threadIdx.x + NT * q;
+            if (i < m) {
+                if (ms[q] != kNone) {
+                    if (mark[i]) mark[ms[q]] = 1;
+                    mr[q] += sr[ms[q]];
+                    ms[q] = ss[ms[q]];
+                }
+                ds[i] = ms[q];
+                dr[i] = mr[q];
             }
-            ds[i] = ms;
-            dr[i] = mr;
         }
         __syncthreads();
     }
     if (rounds & 1) {
-        if (i < m) {
-            succ[i] = ms;
-            R[i] = mr;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int i = threadIdx.x + NT * q;
+            if (i < m) {
+                succ[i] = ms[q];
+                R[i] = mr[q];
+            }
         }
         __syncthreads();
     }
@@ -1036,7 +1171,7 @@ __device__ void resolve_fast(uint16_t* succ, uint64_t* R, uint16_t* succ2, uint6
 
 // every thread of the block; on return (after a barrier) sm.bad / sm.why say whether the
 // parallel path holds, and R / mark / islast / toff answer per-tile queries
-template <int NT, int MAXT, int CAP>
+template <int NT, int PER, int MAXT, int CAP>
 __device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT, CAP>& sm) {
     const int t = threadIdx.x;
     if (tiles > (uint64_t)MAXT) {   // kernel-uniform
@@ -1143,8 +1278,8 @@ __device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT
         __syncthreads();
         return;
     }
-    if (a.fast_rank && m <= NT) {   // block-uniform: the usual stream (a few external nodes per tile)
-        resolve_fast<NT>(sm.succ, sm.R, sm.succ2, sm.R2, sm.mark, m);
+    if (a.fast_rank && m <= NT * PER) {   // block-uniform: the usual stream (a few external nodes per tile)
+        resolve_fast<NT, PER>(sm.succ, sm.R, sm.succ2, sm.R2, sm.mark, m);
         SCAN_VALUE(3, 6, jump_rounds(m));
         SCAN_STAMP(3, 4);
         return;
@@ -1210,17 +1345,68 @@ __device__ TileInfo tile_info(const ScanArgs& a, const ResolveLds<MAXT, CAP>& sm
     return ti;
 }
 
-// K3b for streams of more than kK4Tiles tiles: one block resolves every tile
-__global__ __launch_bounds__(kResolveT) void scan_resolve(ScanArgs a, uint64_t tiles) {
-    __shared__ ResolveLds<kMaxTiles, kExtCap> sm;
-    SCAN_SCOPE(3);
-    resolve_tiles<kResolveT>(a, tiles, sm);
+// K3b: one block resolves every tile, writes each tile's entry (tinfo) and whether K4
+// walks serially (flags[8], the reason in flags[9])
+template <int NT, int PER, int MAXT, int CAP>
+__device__ void resolve_body(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT, CAP>& sm) {
+    resolve_tiles<NT, PER>(a, tiles, sm);
     if (!sm.bad)
-        for (uint64_t tl = threadIdx.x; tl < tiles; tl += kResolveT) a.tinfo[tl] = tile_info(a, sm, tl, true);
+        for (uint64_t tl = threadIdx.x; tl < tiles; tl += NT) a.tinfo[tl] = tile_info(a, sm, tl, true);
     if (threadIdx.x == 0) {
         a.flags[8] = sm.bad ? 1u : 0u;
         a.flags[9] = sm.bad ? sm.why : 0u;
     }
+}
+
+__global__ __launch_bounds__(kResolveT) void scan_resolve(ScanArgs a, uint64_t tiles) {
+    __shared__ ResolveLds<kMaxTiles, kExtCap> sm;
+    SCAN_SCOPE(3);
+    resolve_body<kResolveT, 1>(a, tiles, sm);
+}
+
+// K2 + K3a + K3b in one launch, for streams of up to kFuseTiles tiles: every block runs
+// K2 on its 16 chunks; the last of a tile's blocks to finish (an arrival counter per
+// tile) runs K3a for that tile, while other tiles' blocks are still in K2; the last tile
+// to finish K3a (one more counter) runs K3b over all of them.  Two launch boundaries
+// and their cold trips fewer, and K3a overlapped with K2.  Each arrival is a release
+// fence by every thread, then one atomic; the block that arrives last resets the
+// counter for the next call and acquires before reading the other blocks' results.
+// The phases' LDS share one union (36 KB: 4 blocks per CU).
+static constexpr int kFuseTiles = 512;   // 512 MiB of stream
+static constexpr int kFuseCap = 1024;    // external nodes
+union FusedLds {
+    LinksLds k2;
+    TilesLds k3a;
+    ResolveLds<kFuseTiles, kFuseCap> k3b;
+};
+
+// true in every thread of the block that arrives last at *counter (of `expect`)
+__device__ __forceinline__ bool arrive_last(uint32_t* counter, uint32_t expect, int* flag) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this thread's results (release only: no L2 invalidate)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t old = atomicAdd(counter, 1u);
+        *flag = old == expect - 1;
+        if (*flag) atomicExch(counter, 0u);   // every block has arrived: reset for the next call
+    }
+    __syncthreads();
+    const bool last = *flag != 0;
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other blocks' results
+    return last;
+}
+
+__global__ __launch_bounds__(kScanT) void scan_links_fused(ScanArgs a, uint64_t tiles, uint32_t blocks) {
+    __shared__ FusedLds sm;
+    __shared__ int flag;
+    SCAN_SCOPE(1);
+    links_body(a, sm.k2);
+    constexpr uint32_t kPerTile = (uint32_t)(kTileChunks / kBlkChunks);
+    const uint32_t tile = blockIdx.x / kPerTile;
+    const uint32_t in_tile = min(blocks - tile * kPerTile, kPerTile);
+    if (!arrive_last(a.tarr + tile, in_tile, &flag)) return;   // block-uniform
+    tiles_body(a, tile, sm.k3a);
+    if (!arrive_last(a.flags + 12, (uint32_t)tiles, &flag)) return;
+    resolve_body<kScanT, kFuseCap / kScanT>(a, tiles, sm.k3b);
 }
 
 // K4, serial fallback (capacities overflowed): one thread walks the whole stream.
@@ -1491,7 +1677,7 @@ std::mutex& stream_scratch_mu() {
 // The scratch layout for `cap` chunks (cap a multiple of kTileChunks): offsets of the
 // regions; flags, ccount and ext first -- the region every call leaves zeroed.
 struct Layout {
-    uint64_t flags, ccount, ext, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, flist, text, tcount, tinfo,
+    uint64_t flags, ccount, ext, tarr, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, flist, text, tcount, tinfo,
         total;
 };
 Layout layout_for(uint64_t cap) {
@@ -1502,6 +1688,7 @@ Layout layout_for(uint64_t cap) {
     l.flags = o;   o = 64;
     l.ccount = o;  o = align(o + cap * 4);
     l.ext = o;     o = align(o + slots);
+    l.tarr = o;    o = align(o + tiles * 4);
     l.cleared = o;
     l.cand = o;    o = align(o + slots * 8);
     l.link = o;    o = align(o + slots * 4);
@@ -1627,6 +1814,7 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     ++s.calls;
     a.ccount = (uint32_t*)(m + l.ccount);
     a.ext = m + l.ext;
+    a.tarr = (uint32_t*)(m + l.tarr);
     a.cand = (uint64_t*)(m + l.cand);
     a.link = (int32_t*)(m + l.link);
     a.nterm = (uint64_t*)(m + l.nterm);
@@ -1653,9 +1841,15 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
 #if defined(NETC_SCAN_K1_ONLY) || defined(NETC_SCAN_K1_EXP)
     return hipGetLastError();   // diagnostic builds only (tools/): K1 timed alone
 #endif
-    hipLaunchKernelGGL(scan_links, dim3(blk), dim3(kScanT), 0, stream, a);
-    hipLaunchKernelGGL(scan_tiles, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a);
-    hipLaunchKernelGGL(scan_resolve, dim3(1), dim3(kResolveT), 0, stream, a, tiles);
+    // K2 + K3a + K3b as one launch up to kFuseTiles tiles (NETC_GPU_KNOB_SCAN_FUSE = 0: three,
+    // as for bigger streams -- tests and A/B)
+    if (tiles <= (uint64_t)kFuseTiles && knob(NETC_GPU_KNOB_SCAN_FUSE) != 0) {
+        hipLaunchKernelGGL(scan_links_fused, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
+    } else {
+        hipLaunchKernelGGL(scan_links, dim3(blk), dim3(kScanT), 0, stream, a);
+        hipLaunchKernelGGL(scan_tiles, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a);
+        hipLaunchKernelGGL(scan_resolve, dim3(1), dim3(kResolveT), 0, stream, a, tiles);
+    }
     hipLaunchKernelGGL(scan_emit, dim3(blk), dim3(kScanT), 0, stream, a, tiles);
     e = hipGetLastError();
     if (e != hipSuccess) s.dirty = true;   // a launch failed: the flags may be left set (lock still held)

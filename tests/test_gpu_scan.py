@@ -185,6 +185,28 @@ def test_adversarial_payload_falls_back(torch_cuda):
     assert run_scan(torch_cuda, wire) == 2
 
 
+@pytest.mark.parametrize("strict", [True, False])
+def test_periodic_payload_takes_full_check(torch_cuda, strict):
+    # zero payloads under the key bytes 70 FE 11 22: every 4th wire byte is xFE, so K1's cheap
+    # selection (second header byte xFE/xFF alone) finds ~1,000 positions per chunk; the chunk
+    # takes the full quick check instead (the byte before each xFE has RSV bits set) and stays
+    # on the parallel path.  Random frames between, so some chunks take each pass.
+    rng = np.random.default_rng(31)
+    sizes = np.concatenate([np.full(3000, 1024), rng.integers(0, 5000, 300)])
+    off = frames_from_sizes(sizes)
+    payload = np.zeros(int(off[-1]), dtype=np.uint8)
+    rand = np.arange(sizes.size) >= 3000
+    for k in np.flatnonzero(rand):
+        payload[int(off[k]):int(off[k + 1])] = rng.integers(0, 256, int(sizes[k]), dtype=np.uint8)
+    keys = np.where(rand, rng.integers(0, 2**32, sizes.size, dtype=np.uint64), 0x2211FE70).astype(np.uint32)
+    order = rng.permutation(sizes.size)
+    sizes, keys = sizes[order], keys[order]
+    off2 = frames_from_sizes(sizes)
+    payload2 = np.concatenate([payload[int(off[k]):int(off[k + 1])] for k in order])
+    wire, _ = orc.encode_batch(payload2, off2, keys, None, True)
+    assert run_scan(torch_cuda, wire, strict=strict, parallel=True) == sizes.size
+
+
 def test_empty(torch_cuda):
     run_scan(torch_cuda, np.zeros(0, dtype=np.uint8))
     run_scan(torch_cuda, np.zeros(1, dtype=np.uint8))
@@ -268,3 +290,32 @@ def test_ranking_paths(torch_cuda, gpu_knob, fast):
     wire, _ = _stream(rng, sizes)
     assert run_scan(torch_cuda, wire, parallel=True) == sizes.size
     assert run_scan(torch_cuda, wire, strict=False, parallel=True) == sizes.size
+
+
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_fused_and_separate_launches(torch_cuda, gpu_knob, fuse):
+    # K2 + K3a + K3b as one launch (arrival counters per tile and per stream, the last
+    # arrival runs the next phase and re-zeroes its counter) or as three (knob SCAN_FUSE =
+    # 0, as for streams over 512 MiB): the same results over alternating stream sizes, the
+    # serial fallback, non-strict streams and truncations, one call after another on one
+    # stream (a counter left non-zero would break the next call)
+    gpu_knob("SCAN_FUSE", fuse)
+    rng = np.random.default_rng(51)
+    big, _ = _stream(rng, np.full(16384, 1024))                      # 16 tiles
+    mixed_sizes = np.concatenate([rng.integers(0, 5000, 2000), rng.integers(0, 130, 2000), [65535, 300000]])
+    rng.shuffle(mixed_sizes)
+    mixed, wo = _stream(rng, mixed_sizes)
+    tiny, _ = _stream(rng, rng.integers(0, 4, 5000))
+    rec = b"".join(bytes.fromhex("82fe") + (5000 + i % 997).to_bytes(2, "big") + bytes(4) for i in range(997))
+    inner = np.tile(np.frombuffer(rec, dtype=np.uint8), 20)
+    adv, _ = orc.encode_batch(inner, np.array([0, inner.size], dtype=np.uint64), np.array([0], dtype=np.uint32),
+                              None, True)
+    for _ in range(2):
+        assert run_scan(torch_cuda, big, parallel=True) == 16384
+        assert run_scan(torch_cuda, mixed, parallel=True) == mixed_sizes.size
+        assert run_scan(torch_cuda, mixed, strict=False, parallel=True) == mixed_sizes.size
+        run_scan(torch_cuda, adv)   # capacity overflow: the serial walk, same results
+        assert run_scan(torch_cuda, tiny, parallel=True) == 5000
+        run_scan(torch_cuda, mixed[:int(wo[1500]) + 5], parallel=True)
+        run_scan(torch_cuda, mixed, start=int(wo[2222]), parallel=True)
+        run_scan(torch_cuda, big[:4096 * 300 + 7], parallel=True)     # a partial last tile
