@@ -438,9 +438,8 @@ __device__ u32x4 compose_vec(const EncArgs& a, EncTable& t, uint64_t A0, uint64_
 // payload start) XOR frame l's key rotated to W gives every byte of the vector that
 // is payload of frame l.  The others -- frame l's header bytes when W is inside it,
 // and everything from the next header start on -- are at most a header plus 15
-// bytes per frame: patch_headers rewrites them in the lanes that hold them when the
-// span has at most one frame start inside it, fix_frame (one thread per frame, in the
-// queued launch) otherwise.  So the vector path has no per-lane header work: the
+// bytes per frame, and fix_frame (one thread per frame, in the queued launch)
+// rewrites exactly those.  So the vector path has no per-lane header work: the
 // previous form inserted the header and shifted the tail in the lane a header
 // touched, with a wave-wide branch costing about 200 vector instructions per span at
 // 1 KiB frames.  A span takes this path when the 64-entry table covers it and every
@@ -569,55 +568,6 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
     });
 }
 
-// The header bytes the vector path maps wrongly (through the frame holding the lane's
-// first byte), patched in the lanes that hold them -- every quantity but the lane's data is
-// wave-uniform, and at most three lanes change:
-//   * frame l0's header, when it ends inside this span (lane 0: a header is <= 14 bytes);
-//   * with one frame start S1 inside the span (nb == 1): frame g = l0 + 1's header, in the
-//     lane holding S1 and the next (a header crossing a 16-byte edge; past lane 63 the next
-//     span's l0 case takes it), and g's first payload bytes in the lane holding S1 when S1
-//     is not its first byte: that lane's load mapped through frame l0, whose payload ends
-//     at g's header, so it holds g's payload hl(g) bytes early -- d shifted up by hl(g).
-// Spans with two or more frame starts leave those frames to fix_frame (queued launch).
-__device__ __forceinline__ u32x4 patch_headers(const EncArgs& a, const EncTable& t, int l0, int nb, uint64_t A0,
-                                               int lane, u32x4 d, u32x4 v) {
-    const bool masked = a.masked != 0;
-    const uint64_t S0 = readlane64(t.start, l0), P0 = readlane64(t.poff, l0), P1 = readlane64(t.poff, l0 + 1);
-    const uint64_t pw0 = S0 + header_len(P1 - P0, masked);
-    if (pw0 > A0 && lane == 0) {   // pw0 > A0 is wave-uniform; one lane patches (a lane branch,
-        // not a select over all lanes: fewer vectors live at once, no scratch)
-        uint64_t lo, hi;
-        build_header(readlane32(t.b0, l0), P1 - P0, masked, readlane32(t.key, l0), lo, hi);
-        const u32x4 sel = select_range(0, (int64_t)(pw0 - A0));
-        v = (v & ~sel) | (shift_bytes(lo, hi, (int)((int64_t)S0 - (int64_t)A0)) & sel);
-    }
-    if (nb == 1) {   // wave-uniform
-        const uint64_t S1 = readlane64(t.start, l0 + 1), P2 = readlane64(t.poff, l0 + 2);
-        const uint64_t len1 = P2 - P1;
-        const int hl1 = (int)header_len(len1, masked);
-        const int L = (int)((S1 - A0) >> 4), o = (int)((S1 - A0) & 15);
-        const uint32_t b01 = readlane32(t.b0, l0 + 1), key1 = readlane32(t.key, l0 + 1);
-        if (lane == L) {
-            uint64_t lo, hi;
-            build_header(b01, len1, masked, key1, lo, hi);
-            const u32x4 h = shift_bytes(lo, hi, o) & select_range(o, o + hl1);
-            if (o > 0) {   // lane L took frame l0
-                const uint64_t dlo = (uint64_t)d[0] | (uint64_t)d[1] << 32, dhi = (uint64_t)d[2] | (uint64_t)d[3] << 32;
-                const uint32_t rk1 = rotr8(key1, A0 + 16ull * (uint64_t)L - (S1 + (uint64_t)hl1));
-                const u32x4 k1 = {rk1, rk1, rk1, rk1};
-                v = (v & select_range(0, o)) | h | ((shift_bytes(dlo, dhi, hl1) ^ k1) & select_from(o + hl1));
-            } else {       // lane L took frame g: only its header bytes are wrong
-                v = (v & select_from(hl1)) | h;
-            }
-        } else if (lane == L + 1 && o + hl1 > 16) {
-            uint64_t lo, hi;
-            build_header(b01, len1, masked, key1, lo, hi);
-            v = (v & select_from(o + hl1 - 16)) | (shift_bytes(lo, hi, o - 16) & select_range(0, o + hl1 - 16));
-        }
-    }
-    return v;
-}
-
 template <int U, bool NT>
 __device__ __forceinline__ void finish_chunk(const EncArgs& a, const EncTable& t, uint64_t A, uint64_t wlo,
                                              uint64_t whi, int lane, const Plan<U>& P) {
@@ -635,7 +585,7 @@ __device__ __forceinline__ void finish_chunk(const EncArgs& a, const EncTable& t
             return;
         }
         const u32x4 kv = {sp.rk, sp.rk, sp.rk, sp.rk};
-        const u32x4 v = patch_headers(a, t, sp.l0, sp.nb, A0, lane, sp.d, sp.d ^ kv);
+        const u32x4 v = sp.d ^ kv;
         store_wire<NT>(a, W, v, wlo, whi);
     });
 }
@@ -705,13 +655,6 @@ __global__ __launch_bounds__(256, W) void encode_frames_kernel(EncArgs a) {
 __device__ __forceinline__ void fix_frame(const EncArgs& a, uint64_t k) {
     const bool masked = a.masked != 0;
     const uint64_t w0 = gptr(a.wo)[k], p0 = gptr(a.off)[k];
-    {   // the assembly kernel patched this header itself (patch_headers) unless another frame
-        // starts in the same 1 KiB span (or its span was composed whole): skip it then
-        const uint64_t S = w0 + a.wmis, A0 = S & ~(kSpan - 1);
-        const uint64_t wp = k > 0 ? gptr(a.wo)[k - 1] + a.wmis : 0, wn = gptr(a.wo)[k + 1] + a.wmis;
-        const bool crowded = (k > 0 && wp > A0) || (k + 1 < a.n && wn < A0 + kSpan);
-        if (S == A0 || !crowded) return;
-    }
     const uint64_t len = gptr(a.off)[k + 1] - p0, hl = header_len(len, masked);
     const uint32_t key = masked ? gptr(a.keys)[k] : 0u;
     uint64_t lo, hi;
