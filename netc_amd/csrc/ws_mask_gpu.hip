@@ -45,6 +45,20 @@ __device__ uint64_t* g_stamps;   // diagnostic build only: 2 x u64 per wavefront
 extern "C" int netc_gpu_debug_stamps(void* d_buf) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &d_buf, sizeof(d_buf));
 }
+// per-wave start / end wall clock (100 MHz), written by lane 0 when the wave leaves
+// (tools/mask_timeline.py sizes the buffer for every window of the launch)
+struct StampOnExit {
+    uint64_t w, s0;
+    __device__ ~StampOnExit() {
+        if ((threadIdx.x & 63) == 0 && g_stamps) {
+            g_stamps[2 * w] = s0;
+            g_stamps[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+};
+#define MASK_STAMP_SCOPE(w) StampOnExit stamp_guard{(w), __builtin_amdgcn_s_memrealtime()}
+#else
+#define MASK_STAMP_SCOPE(w) ((void)0)
 #endif
 
 struct Table {
@@ -709,19 +723,7 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
         a.n = *gptr(a.n_dev);
         a.density = a.total ? (double)a.n / (double)a.total : 0.0;
     }
-#ifdef NETC_MASK_STAMPS
-    // diagnostic build only (tools/): per-wave start / end wall clock (100 MHz)
-    const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
-    struct StampOnExit {
-        uint64_t w, s0;
-        __device__ ~StampOnExit() {
-            if ((threadIdx.x & 63) == 0 && g_stamps) {
-                g_stamps[2 * w] = s0;
-                g_stamps[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
-            }
-        }
-    } stamp_guard{wave, stamp0};
-#endif
+    MASK_STAMP_SCOPE(wave);   // diagnostic build only (tools/)
 
     // interior chunks [ci_lo, ci_hi): every 16-B vector inside the buffer
     const uint64_t full_hi = (a.mis + a.total) & ~15ull;
@@ -855,6 +857,7 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
     }
     const uint64_t wave = block * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // uniform: scalar branches
     if (wave >= a.nwin) return;
+    MASK_STAMP_SCOPE(wave);   // diagnostic build only (tools/mask_timeline.py)
     extern __shared__ uint32_t lds_occupancy_pad[];   // dynamic LDS only limits workgroups per CU
     (void)lds_occupancy_pad;
     init_frames(a);

@@ -1841,9 +1841,11 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
 #if defined(NETC_SCAN_K1_ONLY) || defined(NETC_SCAN_K1_EXP)
     return hipGetLastError();   // diagnostic builds only (tools/): K1 timed alone
 #endif
-    // K2 + K3a + K3b as one launch up to kFuseTiles tiles (NETC_GPU_KNOB_SCAN_FUSE = 0: three,
-    // as for bigger streams -- tests and A/B)
-    if (tiles <= (uint64_t)kFuseTiles && knob(NETC_GPU_KNOB_SCAN_FUSE) != 0) {
+    // K2 + K3a + K3b as one launch up to kFuseTiles tiles only with NETC_GPU_KNOB_SCAN_FUSE = 1
+    // (tests and A/B): every block's agent-scope release is a buffer_wbl2 sc1 (a write-back of
+    // its XCD's L2), and at config 2 a thousand blocks arrive -- 261 us against 25 us for the
+    // three launches (profiles/r03b_scan_fuse_ab.json)
+    if (tiles <= (uint64_t)kFuseTiles && knob(NETC_GPU_KNOB_SCAN_FUSE) > 0) {
         hipLaunchKernelGGL(scan_links_fused, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
     } else {
         hipLaunchKernelGGL(scan_links, dim3(blk), dim3(kScanT), 0, stream, a);

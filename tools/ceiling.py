@@ -89,10 +89,11 @@ def main():
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         lib.netc_gpu_debug_stamps.argtypes = [ctypes.c_void_p]
         lib.netc_gpu_tune.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
-        stamps = torch.zeros(2 * 65536, dtype=torch.int64, device=dev)
-        assert lib.netc_gpu_debug_stamps(stamps.data_ptr()) == 0
         for wl in ("c2", "c4"):
             off, keys, total = synth.config(wl)
+            # two words for every window the launch can have (a window is >= 1 KiB)
+            stamps = torch.zeros(2 * (total // 1024 + 1024), dtype=torch.int64, device=dev)
+            assert lib.netc_gpu_debug_stamps(stamps.data_ptr()) == 0
             nb = max(2, (2 << 30) // total)
             bufs = [torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev) for _ in range(nb)]
             off_t = torch.from_numpy(off.view(np.int64)).to(dev)
