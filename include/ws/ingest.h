@@ -54,9 +54,10 @@ struct netc_ws_ingest;
  *  per slot, from the previous slot -- the host header walk over the pinned slot
  *  (netc_ws_scan_frames_host, O(frames)), whose descriptors go to the GPU with the bytes for
  *  the unmask only, when its frames averaged >= 16 KiB or (without NETC_WS_INGEST_STRICT) it
- *  held headers with RSV bits, reserved opcodes or fragmented control frames (the GPU scan's
- *  parallel pass stops at those); otherwise the GPU frame scan (netc_gpu_scan_frames,
- *  O(bytes), no host work).  The results are the same either way. */
+ *  held headers with RSV2 / RSV3 bits, reserved opcodes or fragmented control frames (the
+ *  GPU scan's parallel pass stops at those; RSV1, which permessage-deflate sets, it accepts);
+ *  otherwise the GPU frame scan (netc_gpu_scan_frames, O(bytes), no host work).  The results
+ *  are the same either way. */
 #define NETC_WS_INGEST_SCAN_GPU  2   /* always the GPU frame scan */
 #define NETC_WS_INGEST_SCAN_HOST 4   /* always the host header walk */
 

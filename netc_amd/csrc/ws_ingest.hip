@@ -208,10 +208,10 @@ int resolve(netc_ws_ingest* g, IngestSlot& s) {
     return 0;
 }
 
-// A non-strict stream whose previous slot held headers a client must not send (RSV set:
-// an extension such as permessage-deflate; a reserved opcode; a fragmented control frame):
-// the GPU scan's parallel pass filters like strict mode except for MASK and would stop at
-// the first of them and walk on serially, so such streams go to the host walk.
+// A non-strict stream whose previous slot held headers a client must not send (RSV2 / RSV3
+// set; a reserved opcode; a fragmented control frame): the GPU scan's parallel pass filters
+// like strict mode except for MASK and RSV1 (permessage-deflate) and would stop at the
+// first of them and walk on serially, so such streams go to the host walk.
 //   * GPU-scanned slot: the scan says so itself -- its diag word (nonzero when any part
 //     of the slot was walked serially) is copied to h_res[3] before "scanned", so
 //     resolve() reads it with the result.  The slot's descriptors (h_b0) are NOT read
@@ -222,7 +222,7 @@ bool unchecked_headers(const IngestSlot& p) {
     uint32_t bad = 0;
     for (uint64_t k = 0; k < p.frames; ++k) {
         const uint32_t b = p.h_b0[k], op = b & 0x0F;
-        bad |= (b & 0x70) | (op - 3 <= 4) | (op >= 11) | ((op >= 8) & !(b & 0x80));
+        bad |= (b & 0x30) | (op - 3 <= 4) | (op >= 11) | ((op >= 8) & !(b & 0x80));
     }
     return bad != 0;
 }

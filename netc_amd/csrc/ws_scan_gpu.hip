@@ -142,7 +142,7 @@ struct ScanArgs {
     uint64_t nc;           // chunks (the last one, index nc, is virtual: positions >= len)
     int strict;            // the header filter is on (always, see spec)
     int spec;              // the caller asked for no checks: the parallel pass runs with the strict
-                           // filter minus the MASK check, and K4 walks on serially, unchecked, from
+                           // filter minus the MASK and RSV1 checks, and K4 walks on serially, unchecked, from
                            // a header that filter rejects (speculative: RFC-clean streams never stop)
     uint32_t* flags;       // [8] K3b -> K4: serial fallback (big streams), [9] why the last call walked serially
     uint32_t* ovf;         // this call's overflow bits (flags[0] / flags[2] on alternate calls: the
@@ -175,6 +175,15 @@ struct ScanArgs {
                            // loop always; NETC_SCAN_FAST_RANK=0, tests)
 };
 
+// RSV bits the header filter rejects: all three in strict mode; in the speculative pass
+// (non-strict: the caller accepts every header) RSV2 / RSV3 only -- RSV1 is what
+// permessage-deflate sets on every data frame's first fragment (RFC 7692 §6), so such
+// streams stay on the parallel path (a stop there walked the rest serially).
+// Garbage positions then pass the filter twice as often, no more.
+__device__ __forceinline__ uint32_t rsv_reject(const ScanArgs& a) { return a.spec ? 0x30u : 0x70u; }
+// the same on 4 first-header bytes at once (quick_ok4's x): RSV1 cleared in the speculative pass
+__device__ __forceinline__ uint32_t rsv_keep4(const ScanArgs& a) { return a.spec ? 0xBFBFBFBFu : 0xFFFFFFFFu; }
+
 // One header at stream position p (bytes b[0..13] from p; bytes past len unused).
 // Returns the link: the next header position, or a terminal.  (The serial fallback.)
 template <typename Bytes>
@@ -195,7 +204,7 @@ __device__ __forceinline__ uint64_t parse_at(const ScanArgs& a, uint64_t p, cons
     if (a.strict) {
         const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
         const bool control = opcode >= 8;
-        if ((!mask && !a.spec) || (first & 0x70) || reserved || (control && (!(first & 0x80) || plen > 125)) ||
+        if ((!mask && !a.spec) || (first & rsv_reject(a)) || reserved || (control && (!(first & 0x80) || plen > 125)) ||
             (plen >> 63))
             return term(kDead, p);
     }
@@ -218,7 +227,7 @@ __device__ __forceinline__ bool quick_reject(const ScanArgs& a, uint64_t x) {
     const uint32_t first = gptr(a.wire)[x], second = gptr(a.wire)[x + 1];
     const uint32_t opcode = first & 0x0F;
     const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
-    return (!(second & 0x80) && !a.spec) || (first & 0x70) || reserved || (opcode >= 8 && !(first & 0x80));
+    return (!(second & 0x80) && !a.spec) || (first & rsv_reject(a)) || reserved || (opcode >= 8 && !(first & 0x80));
 }
 
 // 16 stream bytes from LDS position i as 4 dwords (5 dword reads + v_alignbyte),
@@ -257,7 +266,7 @@ __device__ __forceinline__ uint64_t parse_at(const ScanArgs& a, uint64_t p, cons
     const bool hdr_short = p + 2 + ext > a.len;
     const bool reserved = (opcode >= 3) & ((opcode <= 7) | (opcode >= 11));
     const bool control = opcode >= 8;
-    const bool dead = (a.strict != 0) & (((mask == 0) & (a.spec == 0)) | ((first & 0x70) != 0) | reserved |
+    const bool dead = (a.strict != 0) & (((mask == 0) & (a.spec == 0)) | ((first & rsv_reject(a)) != 0) | reserved |
                                          (control & (((first & 0x80) == 0) | (plen > 125))) | ((plen >> 63) != 0));
     const bool pay_short = (p + hl > a.len) | (plen > a.len - (p + hl));
     if (key_out) {
@@ -503,6 +512,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     // for the whole pass, not one per dword.
     uint32_t half[2] = {0, 0};
     const uint32_t specH = a.spec ? kH : 0u;
+    const uint32_t specX = rsv_keep4(a);   // RSV1 cleared from the first bytes in the speculative pass
     // the quick check of every position (the first header byte's checks too), vectors 0-3
     auto full_pass = [&](auto strict_c) {
         constexpr bool kStrict = decltype(strict_c)::value;
@@ -513,7 +523,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
             for (int k = 0; k < 4; ++k) {
                 const uint32_t x = d[i][k];
                 const uint32_t y = __builtin_amdgcn_alignbyte(k < 3 ? d[i][k + 1] : nb[i], x, 1);
-                const uint32_t ok = kStrict ? quick_ok4(x, y | specH) : kH;
+                const uint32_t ok = kStrict ? quick_ok4(x & specX, y | specH) : kH;
                 // a 7-bit length cannot leave the chunk unless the position is near its end
                 // (a per-byte threshold test for those lanes cost more VALU than it saved)
                 const uint32_t sel = ((i == 3 && lane >= kNearLane) ? kH : ((y & 0x7E7E7E7Eu) + 0x02020202u));
@@ -563,7 +573,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         for (int k = 0; k < 4; ++k) {
             const uint32_t x = d[3][k];
             const uint32_t y = __builtin_amdgcn_alignbyte(k < 3 ? d[3][k + 1] : nb[3], x, 1);
-            const uint32_t ok = kStrict ? quick_ok4(x, y | specH) : kH;
+            const uint32_t ok = kStrict ? quick_ok4(x & specX, y | specH) : kH;
             const uint32_t sel = lane >= kNearLane ? kH : ((y & 0x7E7E7E7Eu) + 0x02020202u);
             ci |= (ok & sel & kH) >> (7 - k);
         }
@@ -689,7 +699,8 @@ __device__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const ui
 #pragma unroll
     for (int k = 0; k < kPer / 4; ++k) {
         const uint32_t ok =
-            a.strict ? quick_ok4(w[k], __builtin_amdgcn_alignbyte(w[k + 1], w[k], 1) | (a.spec ? kH : 0u)) : kH;
+            a.strict ? quick_ok4(w[k] & rsv_keep4(a), __builtin_amdgcn_alignbyte(w[k + 1], w[k], 1) | (a.spec ? kH : 0u))
+                     : kH;
 #pragma unroll
         for (int j = 0; j < 4; ++j) cand |= ((ok >> (8 * j + 7)) & 1u) << (4 * k + j);
     }
@@ -1437,7 +1448,7 @@ __device__ void serial_walk(const ScanArgs& args) {
 }
 
 // K4, speculative pass (spec): the parallel pass stopped at a header the strict filter
-// (minus the MASK check) rejects, which the caller accepts: one thread walks on from
+// (minus the MASK and RSV1 checks) rejects, which the caller accepts: one thread walks on from
 // there, unchecked, appending frames after the ones found in parallel.
 __device__ void spec_continue(const ScanArgs& args) {
     const uint64_t stop = args.result[2];

@@ -168,11 +168,12 @@ def test_scan_choice_follows_frame_size(torch_cuda, scan_mode):
 
 
 def test_non_strict_scan_choice(torch_cuda, scan_mode):
-    # non-strict: 1 KiB frames stay on the GPU by default until a slot holds RSV1 frames (as
-    # permessage-deflate sends them), after which the host walk takes the slots
+    # non-strict: 1 KiB frames stay on the GPU by default until a slot holds RSV2 frames (the
+    # GPU scan's parallel pass stops at them), after which the host walk takes the slots.  RSV1
+    # frames (permessage-deflate) stay on the GPU (test_non_strict_rsv1_stays_on_gpu).
     rng = np.random.default_rng(78)
     b0 = np.full(6000, 0x82, dtype=np.uint8)
-    b0[3000:] = 0xC2
+    b0[3000:] = 0xA2
     wire, *_ = make_stream(rng, np.full(6000, 1024), b0=b0)
     with ni.Ingest(0, slot_bytes=1 << 20, nslots=3, strict=False) as ing:
         col = Collector()
@@ -190,11 +191,11 @@ def test_non_strict_choice_several_slots_one_write(torch_cuda, scan_mode):
     # one write() that fills several slots submits each slot right after the
     # previous one, while the previous slot's descriptor copy back is still queued.  The choice
     # must come from the scan's own diag word (copied with its result), not from those
-    # descriptors: slot 0 (no history) is GPU-scanned and meets RSV1 headers, so with the
+    # descriptors: slot 0 (no history) is GPU-scanned and meets RSV2 headers, so with the
     # per-slot choice every later slot takes the host walk -- exactly, whatever the timing.
     rng = np.random.default_rng(79)
     n = 800
-    wire, *_ = make_stream(rng, np.full(n, 1024), b0=np.full(n, 0xC2, dtype=np.uint8))
+    wire, *_ = make_stream(rng, np.full(n, 1024), b0=np.full(n, 0xA2, dtype=np.uint8))
     with ni.Ingest(0, slot_bytes=256 << 10, nslots=4, strict=False) as ing:
         assert ing.write(wire) == wire.size   # ~806 KiB: four slots, all in one call
         ing.submit()
@@ -208,6 +209,21 @@ def test_non_strict_choice_several_slots_one_write(torch_cuda, scan_mode):
             assert (gpu, host) == (1, nb - 1)
         else:
             assert (gpu, host) == ((nb, 0) if scan_mode == "gpu" else (0, nb))
+
+
+def test_non_strict_rsv1_stays_on_gpu(torch_cuda, scan_mode):
+    # permessage-deflate streams (RSV1 on every frame) are scanned by the GPU's parallel pass
+    # in non-strict mode: in "auto" every slot stays on the GPU scan
+    rng = np.random.default_rng(81)
+    n = 3000
+    wire, *_ = make_stream(rng, np.full(n, 1024), b0=np.full(n, 0xC2, dtype=np.uint8))
+    with ni.Ingest(0, slot_bytes=1 << 20, nslots=3, strict=False) as ing:
+        col = Collector()
+        feed(ing, col, wire, [1 << 20] * (wire.size // (1 << 20) + 1))
+        assert col.check(wire, strict=False) == n
+        gpu, host = ing.scan_counts()
+        nb = len(col.batches)
+        assert (gpu, host) == ((0, nb) if scan_mode == "host" else (nb, 0))
 
 
 def test_python_default_is_non_strict(torch_cuda):

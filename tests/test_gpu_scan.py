@@ -130,11 +130,26 @@ def test_strict_errors_mid_stream(torch_cuda):
         wire = np.concatenate([good, np.frombuffer(bad, dtype=np.uint8), good])
         run_scan(torch_cuda, wire, strict=True)
         run_scan(torch_cuda, wire, strict=False)
-        # the headers a client must not send but the reference accepts (RSV set, a fragmented
-        # control frame): the non-strict pass stops there and walks on serially
+        # the headers a client must not send but the reference accepts (RSV2/RSV3 set, a reserved
+        # opcode, a fragmented control frame): the non-strict pass stops there and walks on
+        # serially.  RSV1 (permessage-deflate) does not stop it.
         op = bad[0] & 0x0F
-        stops = bool(bad[0] & 0x70) or 3 <= op <= 7 or op >= 11 or (op >= 8 and not bad[0] & 0x80)
+        stops = bool(bad[0] & 0x30) or 3 <= op <= 7 or op >= 11 or (op >= 8 and not bad[0] & 0x80)
         assert nm.scan_diag() == (0x10000 if stops else 0)
+
+
+@pytest.mark.parametrize("b0, stops", [(0xC2, False), (0xC1, False), (0xA2, True), (0x92, True)])
+def test_non_strict_rsv_headers(torch_cuda, b0, stops):
+    # every frame with RSV1 set, as permessage-deflate sends them, stays on the
+    # speculative parallel pass (diag 0); RSV2 / RSV3 still stop it at the first header and the
+    # rest is walked serially (diag bit 16).  Results equal the oracle's either way; strict mode
+    # rejects the first header.
+    rng = np.random.default_rng(41)
+    sizes = rng.integers(0, 5000, 3000)
+    wire, _ = _stream(rng, sizes, b0=np.full(sizes.size, b0, dtype=np.uint8))
+    assert run_scan(torch_cuda, wire, strict=False, parallel=not stops) == sizes.size
+    assert nm.scan_diag() == (0x10000 if stops else 0)
+    assert run_scan(torch_cuda, wire, strict=True) == 0
 
 
 def test_header_byte_variants(torch_cuda):

@@ -27,8 +27,8 @@ def main():
     ap.add_argument("--unmasked", action="store_true", help="unmasked frames (server-to-client direction)")
     ap.add_argument("--rsv1", action="store_true",
                     help="every frame with RSV1 set (as permessage-deflate sends them): strict rejects the stream; "
-                         "non-strict runs the speculative pass, which stops at the first such header and walks on "
-                         "serially (ADVICE r2: the cliff, measured)")
+                         "non-strict keeps the speculative parallel pass (it filters RSV2 / RSV3 only since round 3; "
+                         "ADVICE r2 measured the serial-walk cliff it replaced)")
     args = ap.parse_args()
     flags = 0 if args.non_strict else 1
 
