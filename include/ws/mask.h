@@ -128,9 +128,10 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *   SCAN_ANCHOR_SLOTS  cap on the frame scan's anchor slots [all]  (NETC_SCAN_ANCHOR_SLOTS)
  *   VAL_STEPS          netc_gpu_unmask_validate's 4 KiB window as 1, 2 or 4 steps [1]
  *                                                                  (NETC_VAL_STEPS)
- *   SCAN_FUSE          1 runs the frame scan's links / tiles / resolve phases as one
- *                      launch up to 512 MiB (arrival counters; slower on MI355X: each
- *                      block's release writes back its XCD's L2) [0: three launches]
+ *   SCAN_FUSE          the frame scan's links / tiles / resolve phases: 0 three launches;
+ *                      1 one launch up to 512 MiB (arrival counters; slower on MI355X:
+ *                      each block's release writes back its XCD's L2) [links, then
+ *                      tiles + resolve as one launch up to 256 MiB]
  *                                                                  (NETC_SCAN_FUSE)
  */
 #define NETC_GPU_KNOB_ENC_DENSE_BYTES   1

@@ -553,9 +553,10 @@ __device__ int64_t frame_of(const Args& a, uint64_t P) {
 __device__ __forceinline__ void validate_span(const Args& a, const Table& t, uint64_t A0, u32x4 out, uint32_t& sc,
                                               bool seam, int lane) {
     const uint64_t W = A0 + 16ull * (uint64_t)lane;
-    // the 4 bytes before the lane's (lane 0: the previous span's last 4, or 0 at a window start)
-    const uint32_t up = (uint32_t)__shfl_up((int)out[3], 1, kWave);
-    const uint32_t prevd = lane ? up : sc;
+    // the 4 bytes before the lane's (lane 0: the previous span's last 4, or 0 at a window start):
+    // one DPP move, wave_shr:1 -- lane 0 keeps sc (an LDS permute here put a ds_bpermute round
+    // trip on every span's dependency chain)
+    const uint32_t prevd = (uint32_t)__builtin_amdgcn_update_dpp((int)sc, (int)out[3], 0x138, 0xF, 0xF, false);
     sc = (uint32_t)__builtin_amdgcn_readlane((int)out[3], kWave - 1);
     u32x4 e;
     // all ASCII across the wave, the 4 bytes before each lane's included (the common case

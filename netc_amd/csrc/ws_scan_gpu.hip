@@ -70,7 +70,11 @@ static constexpr int kExt = 32;                               // external nodes 
 static constexpr int kResolveT = 1024;                        // K3b threads
 static constexpr int kExtCap = 4096;                          // K3b: external nodes of the whole stream
 static constexpr int kMaxTiles = 8192;                        // K3b: tiles (8 GiB of stream)
-static constexpr int kBlkChunks = 16;                         // K2 / K4: chunks per block
+#ifndef NETC_SCAN_BLK
+#define NETC_SCAN_BLK 16   // A/B builds
+#endif
+static constexpr int kBlkChunks = NETC_SCAN_BLK;              // K2 / K4: chunks per block
+static_assert(kBlkChunks * kCand <= 256 && kTileChunks % kBlkChunks == 0, "K2: one thread per node slot");
 static constexpr int32_t kDupLink = -2;                       // K2: slot repeats an earlier slot's position
 static constexpr int kWalkHops = 64;                          // K2 / K4: frames walked one by one
 static constexpr int kList = 8;                               // K2 -> K4: frames recorded per node
@@ -126,6 +130,31 @@ struct TileExt {
     uint32_t root;   // it is the stream start
     uint64_t term;   // K2's terminal of the path's last node in the tile
 };
+// K3a -> K3b records travel by relaxed agent-scope stores and loads (global_store / load
+// ... sc1: through to the memory-side caches, past the XCD's own L2), so the K3b phase can
+// run in the last block of the K3a launch (scan_tiles_resolve) with no L2 write-back or
+// invalidate: every storing wave waits for its stores, the block then adds to an arrival
+// counter, and the last block to arrive reads with sc1 loads only (MI355X_MICROARCH.md,
+// cross-workgroup hand-offs, first row).
+__device__ __forceinline__ void put_text(TileExt* p, const TileExt& e) {
+    uint64_t w[3];
+    __builtin_memcpy(w, &e, sizeof(w));
+#pragma unroll
+    for (int i = 0; i < 3; ++i) __hip_atomic_store((uint64_t*)p + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ TileExt get_text(const TileExt* p) {
+    uint64_t w[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) w[i] = __hip_atomic_load((const uint64_t*)p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    TileExt e;
+    __builtin_memcpy(&e, w, sizeof(w));
+    return e;
+}
+__device__ __forceinline__ uint32_t get_sc1(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+static_assert(sizeof(TileExt) == 24, "TileExt: three 8-byte words");
+
 // K3b -> K4: a tile's true entry
 struct TileInfo {
     int32_t j;       // its bit (index in the tile's external list), or -1: the chain does not enter the tile
@@ -1083,9 +1112,9 @@ __device__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
         e.xl = a.link[last];
         e.root = eroot[t];
         e.term = a.nterm[last];
-        a.text[tile * kExt + t] = e;
+        put_text(&a.text[tile * kExt + t], e);
     }
-    if (t == 0) a.tcount[tile] = (uint32_t)E;
+    if (t == 0) __hip_atomic_store(&a.tcount[tile], (uint32_t)E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
@@ -1107,7 +1136,7 @@ __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
 // per workgroup round, and K4 has several.)
 static constexpr int kExtFirst = 2;
 
-template <int MAXT, int CAP>
+template <int MAXT, int CAP, int PP = kResolveT>
 struct ResolveLds {
     uint32_t toff[MAXT + 1];
     uint32_t eslot[CAP];
@@ -1115,8 +1144,8 @@ struct ResolveLds {
     int32_t exl[CAP];
     uint64_t R[CAP];
     uint16_t succ[CAP];
-    uint64_t R2[kResolveT];      // resolve_fast: the ping-pong halves
-    uint16_t succ2[kResolveT];
+    uint64_t R2[PP];      // resolve_fast: the ping-pong halves (its NT x PER nodes)
+    uint16_t succ2[PP];
     uint8_t mark[CAP];
     uint8_t islast[CAP];   // its path ends in its tile (no successor)
     int bad, root_idx;
@@ -1183,7 +1212,7 @@ __device__ void resolve_fast(uint16_t* succ, uint64_t* R, uint16_t* succ2, uint6
 // every thread of the block; on return (after a barrier) sm.bad / sm.why say whether the
 // parallel path holds, and R / mark / islast / toff answer per-tile queries
 template <int NT, int PER, int MAXT, int CAP>
-__device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT, CAP>& sm) {
+__device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT, CAP, NT * PER>& sm) {
     const int t = threadIdx.x;
     if (tiles > (uint64_t)MAXT) {   // kernel-uniform
         if (t == 0) {
@@ -1201,11 +1230,11 @@ __device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT
 #pragma unroll
     for (int r = 0; r < kTR; ++r) {
         const uint64_t tl = (uint64_t)t + (uint64_t)NT * r;
-        tc[r] = tl < tiles ? a.tcount[tl] : 0;
+        tc[r] = tl < tiles ? get_sc1(&a.tcount[tl]) : 0;
     }
     if ((uint64_t)t < tiles) {
-        e0 = a.text[(uint64_t)t * kExt];
-        e1 = a.text[(uint64_t)t * kExt + 1];
+        e0 = get_text(&a.text[(uint64_t)t * kExt]);
+        e1 = get_text(&a.text[(uint64_t)t * kExt + 1]);
     }
     if (t == 0) {   // the overflow word in the same trip
         const uint32_t ovf = __hip_atomic_load(a.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1245,7 +1274,7 @@ __device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT
             if (tc[r] > 1) put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, o + 1, e1);
         } else {
             for (uint32_t j = 0; j < tc[r] && j < (uint32_t)kExtFirst; ++j)
-                put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, o + j, a.text[tl * kExt + j]);
+                put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, o + j, get_text(&a.text[tl * kExt + j]));
         }
         more |= tc[r] > (uint32_t)kExtFirst;
     }
@@ -1255,7 +1284,7 @@ __device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT
             const uint64_t tl = (uint64_t)t + (uint64_t)NT * r;
             if (tl >= tiles) break;
             for (uint32_t j = kExtFirst; j < tc[r]; ++j)
-                put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, sm.toff[tl] + j, a.text[tl * kExt + j]);
+                put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, sm.toff[tl] + j, get_text(&a.text[tl * kExt + j]));
         }
         __syncthreads();
     }
@@ -1330,8 +1359,8 @@ __device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT
 
 // tile tl's true entry (at most one marked node: the chain enters a tile once); if the
 // chain ends in it and `results`, the scan's results too
-template <int MAXT, int CAP>
-__device__ TileInfo tile_info(const ScanArgs& a, const ResolveLds<MAXT, CAP>& sm, uint64_t tl, bool results) {
+template <int MAXT, int CAP, int PP>
+__device__ TileInfo tile_info(const ScanArgs& a, const ResolveLds<MAXT, CAP, PP>& sm, uint64_t tl, bool results) {
     TileInfo ti;
     ti.j = -1;
     ti.we = 0;
@@ -1343,7 +1372,8 @@ __device__ TileInfo tile_info(const ScanArgs& a, const ResolveLds<MAXT, CAP>& sm
             ti.we = sm.ew[i];
             ti.base = total - sm.R[i];
             if (results && sm.islast[i]) {   // the chain ends in this tile
-                const uint64_t term_v = a.text[tl * kExt + ti.j].term;
+                const uint64_t term_v = __hip_atomic_load(&a.text[tl * kExt + ti.j].term, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
                 const uint64_t ty = term_type(term_v), pos = term_pos(term_v);
                 // an exit onto a position K1 pruned: the chain dies there
                 const bool dead = ty == kDead || ty == kExit;
@@ -1359,7 +1389,7 @@ __device__ TileInfo tile_info(const ScanArgs& a, const ResolveLds<MAXT, CAP>& sm
 // K3b: one block resolves every tile, writes each tile's entry (tinfo) and whether K4
 // walks serially (flags[8], the reason in flags[9])
 template <int NT, int PER, int MAXT, int CAP>
-__device__ void resolve_body(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT, CAP>& sm) {
+__device__ void resolve_body(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT, CAP, NT * PER>& sm) {
     resolve_tiles<NT, PER>(a, tiles, sm);
     if (!sm.bad)
         for (uint64_t tl = threadIdx.x; tl < tiles; tl += NT) a.tinfo[tl] = tile_info(a, sm, tl, true);
@@ -1418,6 +1448,44 @@ __global__ __launch_bounds__(kScanT) void scan_links_fused(ScanArgs a, uint64_t 
     tiles_body(a, tile, sm.k3a);
     if (!arrive_last(a.flags + 12, (uint32_t)tiles, &flag)) return;
     resolve_body<kScanT, kFuseCap / kScanT>(a, tiles, sm.k3b);
+}
+
+// K3a + K3b as one launch, for streams of up to kMergeTiles tiles (the default there): every
+// block ranks its tile (K3a); the last block to arrive resolves all tiles (K3b) -- one launch
+// boundary and K3b's cold first trip fewer.  Unlike scan_links_fused this needs no release
+// fence: the only bytes K3b reads from this launch are the tiles' external-node records and
+// counts, written and read with sc1 stores and loads (put_text / get_text), and the overflow
+// word, set by atomics.  Each wave waits for its stores, the block's barrier follows, then
+// one lane adds to the arrival counter (flags[13]); the block whose add returns tiles - 1
+// resets it for the next call.  The phases' LDS share one union (62 KB: two blocks per CU):
+// K3b with 256 threads, the one-barrier ranking up to 1,024 external nodes, the generic loop
+// up to kMergeCap (more: the serial walk, as past kExtCap in the separate launch).  Up to 256
+// tiles only: there every tile's count and first records come in the first trip (thread t,
+// tile t); past that the K3b phase takes a second dependent trip, and at config 4 (257 tiles)
+// the merged launch measured 90.6 us against 87.5 for the separate ones (r03g), while at
+// config 2 (65 tiles) it saves 0.9 us (42.8 against 43.7).
+static constexpr int kMergeTiles = kScanT;   // 256 MiB of stream
+static constexpr int kMergeCap = 2048;    // external nodes
+union MergedLds {
+    TilesLds k3a;
+    ResolveLds<kMergeTiles, kMergeCap, 1024> k3b;
+};
+
+__global__ __launch_bounds__(kScanT) void scan_tiles_resolve(ScanArgs a, uint64_t tiles) {
+    __shared__ MergedLds sm;
+    __shared__ int last;
+    SCAN_SCOPE(2);
+    tiles_body(a, blockIdx.x, sm.k3a);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 stores have completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(a.flags + 13, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = old == (uint32_t)tiles - 1;
+        if (last) __hip_atomic_store(a.flags + 13, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;   // block-uniform
+    resolve_body<kScanT, 1024 / kScanT>(a, tiles, sm.k3b);
 }
 
 // K4, serial fallback (capacities overflowed): one thread walks the whole stream.
@@ -1852,12 +1920,18 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
 #if defined(NETC_SCAN_K1_ONLY) || defined(NETC_SCAN_K1_EXP)
     return hipGetLastError();   // diagnostic builds only (tools/): K1 timed alone
 #endif
-    // K2 + K3a + K3b as one launch up to kFuseTiles tiles only with NETC_GPU_KNOB_SCAN_FUSE = 1
-    // (tests and A/B): every block's agent-scope release is a buffer_wbl2 sc1 (a write-back of
-    // its XCD's L2), and at config 2 a thousand blocks arrive -- 261 us against 25 us for the
-    // three launches (profiles/r03b_scan_fuse_ab.json)
-    if (tiles <= (uint64_t)kFuseTiles && knob(NETC_GPU_KNOB_SCAN_FUSE) > 0) {
+    // K2, K3a, K3b: by default K2 and then K3a + K3b as one launch up to kMergeTiles (256) tiles
+    // (scan_tiles_resolve), three launches above.  NETC_GPU_KNOB_SCAN_FUSE (tests and A/B):
+    // 0 three launches at every size; 1 K2 + K3a + K3b as one launch up to kFuseTiles tiles
+    // (scan_links_fused: every block's agent-scope release is a buffer_wbl2 sc1 -- a write-back
+    // of its XCD's L2 -- and at config 2 a thousand blocks arrive: 128 us against 43 us for the
+    // three launches, profiles/r03b_scan_fuse_ab.json).
+    const int64_t fuse = knob(NETC_GPU_KNOB_SCAN_FUSE);
+    if (fuse == 1 && tiles <= (uint64_t)kFuseTiles) {
         hipLaunchKernelGGL(scan_links_fused, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
+    } else if (fuse != 0 && tiles <= (uint64_t)kMergeTiles) {
+        hipLaunchKernelGGL(scan_links, dim3(blk), dim3(kScanT), 0, stream, a);
+        hipLaunchKernelGGL(scan_tiles_resolve, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a, tiles);
     } else {
         hipLaunchKernelGGL(scan_links, dim3(blk), dim3(kScanT), 0, stream, a);
         hipLaunchKernelGGL(scan_tiles, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a);

@@ -307,13 +307,14 @@ def test_ranking_paths(torch_cuda, gpu_knob, fast):
     assert run_scan(torch_cuda, wire, strict=False, parallel=True) == sizes.size
 
 
-@pytest.mark.parametrize("fuse", ["1", "0"])
+@pytest.mark.parametrize("fuse", ["1", "0", "-1"])
 def test_fused_and_separate_launches(torch_cuda, gpu_knob, fuse):
-    # K2 + K3a + K3b as one launch (arrival counters per tile and per stream, the last
-    # arrival runs the next phase and re-zeroes its counter) or as three (knob SCAN_FUSE =
-    # 0, as for streams over 512 MiB): the same results over alternating stream sizes, the
-    # serial fallback, non-strict streams and truncations, one call after another on one
-    # stream (a counter left non-zero would break the next call)
+    # K2 + K3a + K3b as one launch (knob SCAN_FUSE = 1: arrival counters per tile and per
+    # stream, the last arrival runs the next phase and re-zeroes its counter), as three
+    # (SCAN_FUSE = 0, as for streams over 512 MiB), or the default, K3a + K3b as one launch
+    # (the last tile block to arrive resolves; sc1 hand-off): the same results over
+    # alternating stream sizes, the serial fallback, non-strict streams and truncations, one
+    # call after another on one stream (a counter left non-zero would break the next call)
     gpu_knob("SCAN_FUSE", fuse)
     rng = np.random.default_rng(51)
     big, _ = _stream(rng, np.full(16384, 1024))                      # 16 tiles
