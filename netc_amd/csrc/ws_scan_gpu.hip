@@ -70,11 +70,21 @@ static constexpr int kExt = 32;                               // external nodes 
 static constexpr int kResolveT = 1024;                        // K3b threads
 static constexpr int kExtCap = 4096;                          // K3b: external nodes of the whole stream
 static constexpr int kMaxTiles = 8192;                        // K3b: tiles (8 GiB of stream)
+// K2 / K4 chunks per block.  Round 2 had 16 for both; at config 4 (65,537 chunks, most of them
+// without a node) the blocks were the cost: 32 per K2 block (a thread per node slot, all 256
+// busy) and 32 per K4 block took K2 13.5 -> 9.7 us and K4 9.4 -> 6.2 us at config 4 (r03h2),
+// the scan 87.6 -> 81.3 us, config 2 unchanged (42.8); 64 per K4 block: config 4 80.1, config 2
+// 43.2 (r03i2).
 #ifndef NETC_SCAN_BLK
-#define NETC_SCAN_BLK 16   // A/B builds
+#define NETC_SCAN_BLK 32   // A/B builds
 #endif
-static constexpr int kBlkChunks = NETC_SCAN_BLK;              // K2 / K4: chunks per block
+#ifndef NETC_SCAN_EMIT
+#define NETC_SCAN_EMIT 32
+#endif
+static constexpr int kBlkChunks = NETC_SCAN_BLK;              // K2: chunks per block
+static constexpr int kEmitChunks = NETC_SCAN_EMIT;            // K4: chunks per block
 static_assert(kBlkChunks * kCand <= 256 && kTileChunks % kBlkChunks == 0, "K2: one thread per node slot");
+static_assert(kEmitChunks <= 256 && kTileChunks % kEmitChunks == 0, "K4: one thread per chunk, blocks inside a tile");
 static constexpr int32_t kDupLink = -2;                       // K2: slot repeats an earlier slot's position
 static constexpr int kWalkHops = 64;                          // K2 / K4: frames walked one by one
 static constexpr int kList = 8;                               // K2 -> K4: frames recorded per node
@@ -1226,15 +1236,22 @@ __device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT
     // trip 1: every tile's count, and the first records of the first NT tiles
     // (issued together, used after the scan)
     uint32_t tc[kTR];
-    TileExt e0, e1;
+    // the first two records of the tiles of the first kPre rounds (all of them when a thread
+    // has at most two tiles: the merged launch up to 512 tiles) come in this trip too
+    constexpr int kPre = kTR <= 2 ? kTR : 1;
+    TileExt e0[kPre], e1[kPre];
 #pragma unroll
     for (int r = 0; r < kTR; ++r) {
         const uint64_t tl = (uint64_t)t + (uint64_t)NT * r;
         tc[r] = tl < tiles ? get_sc1(&a.tcount[tl]) : 0;
     }
-    if ((uint64_t)t < tiles) {
-        e0 = get_text(&a.text[(uint64_t)t * kExt]);
-        e1 = get_text(&a.text[(uint64_t)t * kExt + 1]);
+#pragma unroll
+    for (int r = 0; r < kPre; ++r) {
+        const uint64_t tl = (uint64_t)t + (uint64_t)NT * r;
+        if (tl < tiles) {
+            e0[r] = get_text(&a.text[tl * kExt]);
+            e1[r] = get_text(&a.text[tl * kExt + 1]);
+        }
     }
     if (t == 0) {   // the overflow word in the same trip
         const uint32_t ovf = __hip_atomic_load(a.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1269,9 +1286,10 @@ __device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT
         const uint64_t tl = (uint64_t)t + (uint64_t)NT * r;
         if (tl >= tiles) break;
         const uint32_t o = sm.toff[tl];
-        if (r == 0) {
-            if (tc[r] > 0) put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, o, e0);
-            if (tc[r] > 1) put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, o + 1, e1);
+        if (r < kPre) {
+            const int rp = r < kPre ? r : 0;   // (a constant once unrolled)
+            if (tc[r] > 0) put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, o, e0[rp]);
+            if (tc[r] > 1) put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, o + 1, e1[rp]);
         } else {
             for (uint32_t j = 0; j < tc[r] && j < (uint32_t)kExtFirst; ++j)
                 put_ext(sm.eslot, sm.ew, sm.exl, sm.R, sm.mark, o + j, get_text(&a.text[tl * kExt + j]));
@@ -1459,12 +1477,12 @@ __global__ __launch_bounds__(kScanT) void scan_links_fused(ScanArgs a, uint64_t 
 // one lane adds to the arrival counter (flags[13]); the block whose add returns tiles - 1
 // resets it for the next call.  The phases' LDS share one union (62 KB: two blocks per CU):
 // K3b with 256 threads, the one-barrier ranking up to 1,024 external nodes, the generic loop
-// up to kMergeCap (more: the serial walk, as past kExtCap in the separate launch).  Up to 256
-// tiles only: there every tile's count and first records come in the first trip (thread t,
-// tile t); past that the K3b phase takes a second dependent trip, and at config 4 (257 tiles)
-// the merged launch measured 90.6 us against 87.5 for the separate ones (r03g), while at
-// config 2 (65 tiles) it saves 0.9 us (42.8 against 43.7).
-static constexpr int kMergeTiles = kScanT;   // 256 MiB of stream
+// up to kMergeCap (more: the serial walk, as past kExtCap in the separate launch).  Every
+// tile's count and first two records come in the K3b phase's first trip (thread t: tiles t
+// and t + 256); with tiles past 256 read in a second dependent trip, config 4 (257 tiles)
+// measured 90.6 us merged against 87.5 separate (r03g), while config 2 (65 tiles) saves
+// 0.9 us (42.8 against 43.7).
+static constexpr int kMergeTiles = 2 * kScanT;   // 512 MiB of stream
 static constexpr int kMergeCap = 2048;    // external nodes
 union MergedLds {
     TilesLds k3a;
@@ -1553,7 +1571,7 @@ __device__ __forceinline__ void put_frame(const ScanArgs& a, uint64_t k, uint64_
     }
 }
 
-// K4: the chunks' descriptors, kBlkChunks chunks per block.  Thread t < kBlkChunks
+// K4: the chunks' descriptors, kEmitChunks chunks per block.  Thread t < kEmitChunks
 // takes chunk t: its true entry is the node whose path bits hold the tile entry's bit;
 // a chunk of at most kWalkHops frames is walked by that thread (header bytes from
 // global memory).  Longer ones: with K2' anchors one wavefront per chunk, lane u
@@ -1568,14 +1586,14 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
     __shared__ uint16_t lk16[kChunk];  // 2^k hops (pong); 16 hops after the last pass
     __shared__ uint16_t anchor[kChunk / kStride + 1];
     __shared__ int nanchor, nqa, nqb;
-    __shared__ uint32_t qa_node[kBlkChunks], qb_node[kBlkChunks];
-    __shared__ uint64_t qa_base[kBlkChunks], qb_base[kBlkChunks];
+    __shared__ uint32_t qa_node[kEmitChunks], qb_node[kEmitChunks];
+    __shared__ uint64_t qa_base[kEmitChunks], qb_base[kEmitChunks];
     __shared__ TileInfo bti;
     __shared__ int fbs;
     SCAN_SCOPE(4);
     (void)tiles;
     const int tid = threadIdx.x;
-    const uint64_t tile = (uint64_t)blockIdx.x * kBlkChunks / kTileChunks;   // kBlkChunks divides kTileChunks
+    const uint64_t tile = (uint64_t)blockIdx.x * kEmitChunks / kTileChunks;   // kEmitChunks divides kTileChunks
     if (tid == 0) {
         fbs = __hip_atomic_load(&a.flags[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
         bti = a.tinfo[tile];
@@ -1585,8 +1603,8 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
     }
     __syncthreads();
     const bool fb = fbs != 0;
-    if (tid < kBlkChunks) {
-        const uint64_t c = (uint64_t)blockIdx.x * kBlkChunks + tid;
+    if (tid < kEmitChunks) {
+        const uint64_t c = (uint64_t)blockIdx.x * kEmitChunks + tid;
         if (c <= a.nc) {
             // the chunk's counter, path bits, W, counts and positions, and its tile's entry, in one trip
             const uint32_t cnt = min(a.ccount[c], (uint32_t)kCand);
@@ -1920,7 +1938,7 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
 #if defined(NETC_SCAN_K1_ONLY) || defined(NETC_SCAN_K1_EXP)
     return hipGetLastError();   // diagnostic builds only (tools/): K1 timed alone
 #endif
-    // K2, K3a, K3b: by default K2 and then K3a + K3b as one launch up to kMergeTiles (256) tiles
+    // K2, K3a, K3b: by default K2 and then K3a + K3b as one launch up to kMergeTiles (512) tiles
     // (scan_tiles_resolve), three launches above.  NETC_GPU_KNOB_SCAN_FUSE (tests and A/B):
     // 0 three launches at every size; 1 K2 + K3a + K3b as one launch up to kFuseTiles tiles
     // (scan_links_fused: every block's agent-scope release is a buffer_wbl2 sc1 -- a write-back
@@ -1937,7 +1955,8 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         hipLaunchKernelGGL(scan_tiles, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a);
         hipLaunchKernelGGL(scan_resolve, dim3(1), dim3(kResolveT), 0, stream, a, tiles);
     }
-    hipLaunchKernelGGL(scan_emit, dim3(blk), dim3(kScanT), 0, stream, a, tiles);
+    hipLaunchKernelGGL(scan_emit, dim3((unsigned)((chunks + kEmitChunks - 1) / kEmitChunks)), dim3(kScanT), 0, stream, a,
+                       tiles);
     e = hipGetLastError();
     if (e != hipSuccess) s.dirty = true;   // a launch failed: the flags may be left set (lock still held)
     return e;
