@@ -1477,12 +1477,11 @@ __global__ __launch_bounds__(kScanT) void scan_links_fused(ScanArgs a, uint64_t 
 // one lane adds to the arrival counter (flags[13]); the block whose add returns tiles - 1
 // resets it for the next call.  The phases' LDS share one union (62 KB: two blocks per CU):
 // K3b with 256 threads, the one-barrier ranking up to 1,024 external nodes, the generic loop
-// up to kMergeCap (more: the serial walk, as past kExtCap in the separate launch).  Every
-// tile's count and first two records come in the K3b phase's first trip (thread t: tiles t
-// and t + 256); with tiles past 256 read in a second dependent trip, config 4 (257 tiles)
-// measured 90.6 us merged against 87.5 separate (r03g), while config 2 (65 tiles) saves
-// 0.9 us (42.8 against 43.7).
-static constexpr int kMergeTiles = 2 * kScanT;   // 512 MiB of stream
+// up to kMergeCap (more: the serial walk, as past kExtCap in the separate launch).  Up to 256
+// tiles: at config 2 (65 tiles) the merge saves 0.9 us (42.8 against 43.7, r03g); at config 4
+// (257 tiles) the merged launch measured 17.6 us against 7.2 + 7.6 for the separate ones, also
+// with both rounds of tile records read in the first trip (r03j), so bigger streams keep them.
+static constexpr int kMergeTiles = kScanT;   // 256 MiB of stream
 static constexpr int kMergeCap = 2048;    // external nodes
 union MergedLds {
     TilesLds k3a;
@@ -1938,7 +1937,7 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
 #if defined(NETC_SCAN_K1_ONLY) || defined(NETC_SCAN_K1_EXP)
     return hipGetLastError();   // diagnostic builds only (tools/): K1 timed alone
 #endif
-    // K2, K3a, K3b: by default K2 and then K3a + K3b as one launch up to kMergeTiles (512) tiles
+    // K2, K3a, K3b: by default K2 and then K3a + K3b as one launch up to kMergeTiles (256) tiles
     // (scan_tiles_resolve), three launches above.  NETC_GPU_KNOB_SCAN_FUSE (tests and A/B):
     // 0 three launches at every size; 1 K2 + K3a + K3b as one launch up to kFuseTiles tiles
     // (scan_links_fused: every block's agent-scope release is a buffer_wbl2 sc1 -- a write-back
