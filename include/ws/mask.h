@@ -126,8 +126,8 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *   SCAN_FAST_RANK     0 sends the frame scan's list ranking through the generic
  *                      loop [1]                                     (NETC_SCAN_FAST_RANK)
  *   SCAN_ANCHOR_SLOTS  cap on the frame scan's anchor slots [all]  (NETC_SCAN_ANCHOR_SLOTS)
- *   VAL_STEPS          netc_gpu_unmask_validate's 4 KiB window as 1, 2 or 4 steps [1]
- *                                                                  (NETC_VAL_STEPS)
+ *   VAL_STEPS          netc_gpu_unmask_validate's 4 KiB window as 1, 2 or 4 steps
+ *                      [2 up to 256 MiB, 1 above]                  (NETC_VAL_STEPS)
  *   SCAN_FUSE          the frame scan's links / tiles / resolve phases: 0 three launches;
  *                      1 one launch up to 512 MiB (arrival counters; slower on MI355X:
  *                      each block's release writes back its XCD's L2) [links, then

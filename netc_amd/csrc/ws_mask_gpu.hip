@@ -1191,8 +1191,12 @@ __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uin
 template <bool AL>
 static hipError_t launch_val(const Args& a, bool persistent, hipStream_t s) {
     if (!persistent) {
-        // a 4 KiB window per wavefront as U KiB x K steps (NETC_GPU_KNOB_VAL_STEPS = K: 1, 2 or 4)
-        switch (knob(NETC_GPU_KNOB_VAL_STEPS)) {
+        // a 4 KiB window per wavefront as U KiB x K steps (NETC_GPU_KNOB_VAL_STEPS = K: 1, 2 or
+        // 4).  Default by batch size: two 2 KiB steps up to 256 MiB (config 2: 32.3 against 33.2
+        // us), one 4 KiB step above (config 4: 454-461 against 468-475 us; r03l)
+        int64_t k = knob(NETC_GPU_KNOB_VAL_STEPS);
+        if (k < 0) k = a.total <= (256ull << 20) ? 2 : 1;
+        switch (k) {
             case 2: return launch_np<2, 2, AL, true, true>(a, s);
             case 4: return launch_np<1, 4, AL, true, true>(a, s);
             default: return launch_np<4, 1, AL, true, true>(a, s);

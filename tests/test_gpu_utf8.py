@@ -107,10 +107,10 @@ def run_validate(torch, frames, shift=0, inplace=True):
     return exp
 
 
-@pytest.mark.parametrize("steps", [None, 2, 4])
+@pytest.mark.parametrize("steps", [None, 1, 2, 4])
 @pytest.mark.parametrize("seed", range(4))
 def test_mixed_messages(torch_cuda, gpu_knob, seed, steps):
-    gpu_knob("VAL_STEPS", steps)   # the 4 KiB window as 1 (default), 2 or 4 steps
+    gpu_knob("VAL_STEPS", steps)   # the 4 KiB window as 1, 2 or 4 steps (None: by batch size)
     rng = np.random.default_rng(seed)
     exp = run_validate(torch_cuda, build_batch(rng, 300, 3000))
     assert 0 < (exp == 0).sum()   # some messages are invalid
@@ -142,7 +142,7 @@ def test_tiny_fragments(torch_cuda):
     run_validate(torch_cuda, frames)
 
 
-@pytest.mark.parametrize("steps", [None, 2, 4])
+@pytest.mark.parametrize("steps", [None, 1, 2, 4])
 def test_errors_at_every_boundary(torch_cuda, gpu_knob, steps):
     # one long valid TEXT frame per case with an error at a vector / span / chunk edge
     gpu_knob("VAL_STEPS", steps)
@@ -163,7 +163,7 @@ def test_errors_at_every_boundary(torch_cuda, gpu_knob, steps):
     assert (exp[:-1] == 0).all() and exp[-1] == 1
 
 
-@pytest.mark.parametrize("steps", [None, 2, 4])
+@pytest.mark.parametrize("steps", [None, 1, 2, 4])
 @pytest.mark.parametrize("shift", [0, 5])
 def test_errors_at_chunk_seams(torch_cuda, gpu_knob, shift, steps):
     gpu_knob("VAL_STEPS", steps)
