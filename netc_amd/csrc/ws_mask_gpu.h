@@ -27,6 +27,8 @@ struct Args {
     uint8_t xcd_remap;         // one-window-per-wave walk: give each XCD a contiguous share of the windows
     int32_t probe_e;           // one-window-per-wave walk: entries of a window's first table probe (<= 64)
     int32_t probe_bias;        // ... and the frames its base sits before the density's guess
+    uint8_t seam_src;          // VAL, out of place: a window checks the first bytes after its start itself
+                               // (the 4 bytes before it unmasked from src); utf8_messages skips the seams
 };
 
 // LaunchCfg::flags (NETC_GPU_TUNE_*): bits 0-1 non-temporal payload stream, 2 the

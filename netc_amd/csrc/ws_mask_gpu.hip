@@ -630,6 +630,32 @@ __device__ __forceinline__ void validate_span(const Args& a, const Table& t, uin
     }
 }
 
+// VAL, out of place (seam_src): the 4 bytes before window start A (P coordinates, A a multiple
+// of 4 KiB, so the dword is aligned when src is) unmasked from src, which no wavefront writes,
+// with the key of the frame holding A at its phase there.  When that frame starts less than 4
+// bytes before A, the bytes before its start come out wrong -- they only feed the rule for the
+// frame's first 3 bytes, which validate_span drops (utf8_messages checks them).  The caller's
+// table holds the frame containing A (entry 0 starts at or before A).
+template <bool SRC_ALIGNED>
+__device__ __forceinline__ uint32_t seam_raw(const Args& a, uint64_t A) {   // issued with the window's loads
+    if constexpr (SRC_ALIGNED) {
+        return *(const NETC_GLOBAL uint32_t*)(a.src_base + A - 4);
+    } else {
+        typedef uint32_t u32u __attribute__((aligned(1)));
+        return *(const NETC_GLOBAL u32u*)(a.src_base + A - 4);
+    }
+}
+__device__ __forceinline__ uint32_t seam_unmask(const Table& t, uint64_t A, uint32_t raw) {   // once t is resolved
+    const int j0 = __popcll(__ballot(t.start <= A)) - 1;
+    const uint64_t s0 = readlane64(t.start, j0);
+    return raw ^ rotr8(readlane32(t.key, j0), A - 4 - s0);
+}
+template <bool SRC_ALIGNED>
+__device__ __forceinline__ uint32_t seam_carry(const Args& a, const Table& t, uint64_t A) {
+    return seam_unmask(t, A, seam_raw<SRC_ALIGNED>(a, A));
+}
+__device__ __forceinline__ bool own_seam(const Args& a, uint64_t A) { return a.seam_src && A >= a.mis + 4; }
+
 template <class A>
 __device__ __forceinline__ int64_t clamp_base(const A& a, int64_t g) {
     g = g < -1 ? -1 : g;
@@ -657,7 +683,7 @@ __device__ __forceinline__ void np_resolve(const AT& a, Table& t, uint64_t A, in
 }
 
 template <int U, bool SRC_ALIGNED, bool NT, bool VAL, class AT>
-__device__ __forceinline__ void edge_chunk(const AT& a, uint64_t A, int lane) {
+__device__ __forceinline__ void edge_chunk(const AT& a, uint64_t A, int lane, uint32_t& carry, bool first) {
     const uint64_t full_lo = a.mis ? 16 : 0;
     const uint64_t full_hi = (a.mis + a.total) & ~15ull;
     const uint64_t vec_end = (a.mis + a.total + 15) & ~15ull;
@@ -669,7 +695,18 @@ __device__ __forceinline__ void edge_chunk(const AT& a, uint64_t A, int lane) {
     }
     Table t;
     table_load(a, t, locate(a, A, lane), lane);
-    uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
+    // VAL: carry = the previous span's last 4 unmasked bytes, across the steps of a window
+    // (first: this is the window's first step; its first 3 bytes are left to utf8_messages
+    // unless the window checks its own seam)
+    bool seam = first;
+    if constexpr (VAL) {
+        if constexpr (std::is_same<AT, Args>::value) {
+            if (first && own_seam(a, A)) {   // wave-uniform
+                carry = seam_carry<SRC_ALIGNED>(a, t, A);
+                seam = false;
+            }
+        }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t A0 = A + (uint64_t)u * kSpan;
@@ -693,7 +730,7 @@ __device__ __forceinline__ void edge_chunk(const AT& a, uint64_t A, int lane) {
         if (P >= full_lo && P < full_hi) store_vec<NT>(a, P, d[u] ^ m);
         else if (P < vec_end) edge_vec(a, P, m);
         if constexpr (VAL) {
-            validate_span(a, t, A0, out, carry, u == 0, lane);
+            validate_span(a, t, A0, out, carry, seam && u == 0, lane);
         }
     }
 }
@@ -732,9 +769,10 @@ __global__ __launch_bounds__(256, kMinWaves[U]) void mask_frames_kernel(Args a) 
     uint64_t ci_hi = full_hi / kWin;
     if (ci_hi < ci_lo) ci_hi = ci_lo;
     // edge chunks: chunk 0 when the buffer start is unaligned, and [ci_hi, nwin)
-    if (a.mis && wave == 0) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, 0, lane);
+    uint32_t ec = 0;
+    if (a.mis && wave == 0) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, 0, lane, ec, true);
     for (uint64_t e = ci_hi; e < a.nwin; ++e)
-        if (e % nwaves == (wave + 1) % nwaves) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, e * kWin, lane);
+        if (e % nwaves == (wave + 1) % nwaves) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, e * kWin, lane, ec, true);
 
     uint64_t c = ci_lo + wave;
     if (c >= ci_hi) return;
@@ -838,7 +876,7 @@ __device__ __forceinline__ void first_probe(const AT& a, Table& t, uint64_t A, i
 }
 
 template <int U, int K, bool SRC_ALIGNED, bool NT, bool VAL = false, class AT = Args>
-__global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
+__global__ __launch_bounds__(256, (VAL && K == 1) ? 8 : 1) void mask_np_kernel(AT a) {
     constexpr uint64_t kStep = kSpan * U;
     constexpr uint64_t kWin = kStep * K;
     const int lane = threadIdx.x & (kWave - 1);
@@ -866,11 +904,16 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
     const uint64_t full_lo = a.mis ? 16 : 0;
     const uint64_t full_hi = (a.mis + a.total) & ~15ull;
     if (A < full_lo || A + kWin > full_hi) {   // a window holding a partial vector (<= 2 per batch)
+        uint32_t ec = 0;   // VAL: the carry runs across the window's steps (a step start is no seam)
 #pragma unroll 1
-        for (int k = 0; k < K; ++k) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, A + (uint64_t)k * kStep, lane);
+        for (int k = 0; k < K; ++k) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, A + (uint64_t)k * kStep, lane, ec, k == 0);
         return;
     }
     uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
+    // VAL, out of place: the window checks its own first bytes (seam_raw / seam_unmask); the
+    // src dword before it is loaded with the window's payload, unmasked once the table is in
+    const bool own = VAL && own_seam(a, A);   // wave-uniform
+    uint32_t seam_w = 0;
     Table t;
     auto emit = [&](uint64_t A0, u32x4 src, bool first) {
         const u32x4 m = span_mask(a, t, A0, lane);
@@ -894,8 +937,12 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
         // by vmcnt(0), which held the table's trip behind the payload's
         const uint32_t lm = min((uint32_t)lane, o >> 4);
         c[M] = load_line_block<NT>(S - o + 16 * lm + (uint64_t)M * kSpan);
+        if constexpr (VAL) seam_w = seam_raw<SRC_ALIGNED>(a, own ? A : A + 4);   // (not own: a dword of the window, unused)
         first_probe(a, t, A, lane);
         np_resolve(a, t, A, lane);
+        if constexpr (VAL) {
+            if (own) carry = seam_unmask(t, A, seam_w);
+        }
         switch ((o >> 2) & 3) {   // uniform: constant register indices in each case
             case 0: shift_window<M, 0>(c, v, o, lane); break;
             case 1: shift_window<M, 1>(c, v, o, lane); break;
@@ -903,7 +950,7 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
             default: shift_window<M, 3>(c, v, o, lane); break;
         }
 #pragma unroll
-        for (int m = 0; m < M; ++m) emit(A + (uint64_t)m * kSpan, v[m], m == 0);
+        for (int m = 0; m < M; ++m) emit(A + (uint64_t)m * kSpan, v[m], m == 0 && !own);
         return;
     }
     u32x4 d[U];
@@ -912,14 +959,18 @@ __global__ __launch_bounds__(256) void mask_np_kernel(AT a) {
         for (int u = 0; u < U; ++u) d[u] = load_vec<true, NT>(a, base + (uint64_t)u * kSpan + 16ull * lane);
     };
     load_step(A);
+    if constexpr (VAL) seam_w = seam_raw<true>(a, own ? A : A + 4);   // (not own: a dword of the window, unused)
     first_probe(a, t, A, lane);
     np_resolve(a, t, A, lane);
+    if constexpr (VAL) {
+        if (own) carry = seam_unmask(t, A, seam_w);
+    }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint64_t base = A + (uint64_t)k * kStep;
         if (k > 0) load_step(base);
 #pragma unroll
-        for (int u = 0; u < U; ++u) emit(base + (uint64_t)u * kSpan, d[u], k == 0 && u == 0);
+        for (int u = 0; u < U; ++u) emit(base + (uint64_t)u * kSpan, d[u], k == 0 && u == 0 && !own);
     }
 }
 
@@ -1008,6 +1059,7 @@ static Args make_args(uint8_t* dst, const uint8_t* src, uint64_t total, const ui
     a.verr = nullptr;
     a.vtag = 0;
     a.xcd_remap = 0;
+    a.seam_src = 0;
     a.mis = (uint64_t)(uintptr_t)dst & 15u;
     a.dst_base = dst - a.mis;
     a.src_base = src - a.mis;
@@ -1137,31 +1189,45 @@ __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uin
                 if ((h0[j] & 0x0F) >= 8) continue;
                 if (verr[j] == tag) bad = true;
                 const uint64_t lo = off[j], hi = off[j + 1];
-                for (uint64_t p = lo; p < hi && p < lo + 3; ++p) {
-                    const uint32_t b = dst[p];
-                    bad |= utf8_rule(h3, h2, h1, b);
-                    h3 = h2;
-                    h2 = h1;
-                    h1 = b;
+                // the frame's first and last 3 bytes in one trip (clamped into the frame; a
+                // load in a loop of data-dependent length was a trip per byte)
+                uint32_t fb[3] = {0, 0, 0}, lb[3] = {0, 0, 0};
+                if (hi > lo) {
+                    const uint64_t last = hi - 1;
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) {
+                        fb[d] = dst[lo + d < last ? lo + d : last];
+                        lb[d] = dst[hi - lo > 3 ? hi - 3 + d : lo];   // (used only when hi - lo > 3)
+                    }
+                }
+#pragma unroll
+                for (int d = 0; d < 3; ++d) {
+                    if (lo + d < hi) {
+                        bad |= utf8_rule(h3, h2, h1, fb[d]);
+                        h3 = h2;
+                        h2 = h1;
+                        h1 = fb[d];
+                    }
                 }
                 // the first 3 bytes of every chunk inside the frame, which phase A skips
                 // (in place, another wavefront's chunk held the bytes before them).  The
                 // 4 bytes before and after each chunk start (aligned dwords: dst - mis is
                 // 16-aligned, chunk starts are multiples of win >= 4096) are read for 8
                 // chunks at a time -- one at a time, a 64 KiB frame's 16 seams were 16
-                // round trips to memory in a row.
-                for (uint64_t cb = (lo + 3 + mis + win - 1) / win * win; cb < hi + mis && !bad; cb += 8 * win) {
+                // round trips to memory in a row.  The 16 loads are unconditional (a chunk
+                // start past the frame re-reads the first one; bytes at or past hi are read
+                // but never used -- an aligned dword holding a byte of the buffer lies in
+                // that byte's page): a load under a per-lane branch made the compiler wait
+                // for each one in turn (29.7 us at config 4, r03k).
+                const uint64_t cb0 = win ? (lo + 3 + mis + win - 1) / win * win : ~0ull;   // win 0: no seams to check
+                for (uint64_t cb = cb0; win && cb < hi + mis && !bad; cb += 8 * win) {
                     uint32_t wb[8], wa[8];
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
-                        const uint64_t c = cb + (uint64_t)i * win, q = c - mis;   // q: the chunk's first byte
-                        wb[i] = wa[i] = 0;
-                        if (c < hi + mis) {
-                            wb[i] = *(const NETC_GLOBAL uint32_t*)(dst + q - 4);
-                            if (q + 4 <= hi) wa[i] = *(const NETC_GLOBAL uint32_t*)(dst + q);
-                            else
-                                for (uint64_t t = q; t < hi; ++t) wa[i] |= (uint32_t)dst[t] << (8 * (t - q));
-                        }
+                        const uint64_t c = cb + (uint64_t)i * win;
+                        const uint64_t q = (c < hi + mis ? c : cb) - mis;   // q: the chunk's first byte
+                        wb[i] = *(const NETC_GLOBAL uint32_t*)(dst + q - 4);
+                        wa[i] = *(const NETC_GLOBAL uint32_t*)(dst + q);
                     }
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
@@ -1175,9 +1241,9 @@ __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uin
                     }
                 }
                 if (hi - lo > 3) {   // the frame's own last 3 bytes become the history
-                    h3 = dst[hi - 3];
-                    h2 = dst[hi - 2];
-                    h1 = dst[hi - 1];
+                    h3 = lb[0];
+                    h2 = lb[1];
+                    h1 = lb[2];
                 }
             }
             if (h1 >= 0xC0 || h2 >= 0xE0 || h3 >= 0xF0) bad = true;   // ends inside a sequence
@@ -1220,6 +1286,10 @@ hipError_t launch_mask_validate(uint8_t* dst, const uint8_t* src, uint64_t total
     a.nwin = (nvec + 255) / 256;   // windows of 4 KiB (64 vectors x 4)
     set_probe(a, 4096);
     const bool persistent = cfg.flags >= 0 && (cfg.flags & kPersistent);
+    // out of place, one-window walk: each window checks the bytes after its own start (the 4
+    // before it unmasked from src, which nobody writes), so utf8_messages skips the seams (win
+    // 0).  In place the bytes before a window may or may not be unmasked yet when it reads them.
+    a.seam_src = dst != src && !persistent;
     hipError_t e;
     if (a.nwin) {
         const bool aligned = (((uintptr_t)src ^ (uintptr_t)dst) & 15u) == 0;
@@ -1227,7 +1297,7 @@ hipError_t launch_mask_validate(uint8_t* dst, const uint8_t* src, uint64_t total
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(utf8_messages, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dst, off, header0, n,
-                       verr, tag, a.mis, kSpan * 4, valid);
+                       verr, tag, a.mis, a.seam_src ? 0 : kSpan * 4, valid);
     return hipGetLastError();
 }
 

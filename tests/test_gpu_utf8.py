@@ -163,12 +163,14 @@ def test_errors_at_every_boundary(torch_cuda, gpu_knob, steps):
     assert (exp[:-1] == 0).all() and exp[-1] == 1
 
 
+@pytest.mark.parametrize("inplace", [True, False])
 @pytest.mark.parametrize("steps", [None, 1, 2, 4])
 @pytest.mark.parametrize("shift", [0, 5])
-def test_errors_at_chunk_seams(torch_cuda, gpu_knob, shift, steps):
+def test_errors_at_chunk_seams(torch_cuda, gpu_knob, shift, steps, inplace):
     gpu_knob("VAL_STEPS", steps)
     # long frames (many 4 KiB chunks each) with one broken byte among the first 3 bytes
-    # of a chunk -- the bytes only phase B checks -- or just before / after them
+    # of a chunk -- the bytes phase B checks in place; out of place each window checks its
+    # own first bytes (the 4 before it unmasked from src) -- or just before / after them
     rng = np.random.default_rng(70 + shift)
     flen, win, mis = 70000, 4096, shift & 15   # torch allocations are 256-B aligned
     frames, o = [], 0
@@ -181,7 +183,36 @@ def test_errors_at_chunk_seams(torch_cuda, gpu_knob, shift, steps):
                 body[p] = (0xFF, 0x80, 0xC0)[i % 3]
         frames.append((0x81, bytes(body)))
         o += flen
-    run_validate(torch_cuda, frames, shift=shift)
+    run_validate(torch_cuda, frames, shift=shift, inplace=inplace)
+
+
+@pytest.mark.parametrize("inplace", [True, False])
+@pytest.mark.parametrize("steps", [2, 4])
+@pytest.mark.parametrize("shift", [0, 7])
+def test_errors_at_step_starts_of_the_last_window(torch_cuda, gpu_knob, steps, shift, inplace):
+    # a window of several steps that holds a partial vector (the batch's last) runs its steps
+    # one by one; the first 3 bytes of each later step are checked with the carry from the
+    # step before (they are no 4 KiB seam that phase B would check)
+    gpu_knob("VAL_STEPS", steps)
+    rng = np.random.default_rng(90 + steps + shift)
+    win, mis = 4096, shift & 15
+    total = 5 * win + 3000 - mis                     # the last window is partial
+    last = (mis + total) // win * win                # its first byte (P coordinates)
+    step = win // steps
+    for k in range(1, steps):
+        for d in range(3):
+            # an overlong 2-byte sequence C0 80 whose second byte is byte d of the step: the
+            # rule flags that byte and no other (ASCII around it)
+            q = last + k * step + d - mis            # payload offset of the flagged byte
+            if q + 6 >= total:
+                continue
+            body = bytearray(b"a" * 1000) + bytearray(text_bytes(rng, total)[:total - 1000])
+            body[q - 5:q + 6] = b"a" * 11
+            body[-4:] = b"tail"                      # no code point cut at the end
+            body[q - 1], body[q] = 0xC0, 0x80
+            frames = [(0x81, bytes(body[:1000])), (0x81, bytes(body[1000:]))]
+            exp = run_validate(torch_cuda, frames, shift=shift, inplace=inplace)
+            assert exp.tolist() == [1, 0]
 
 
 def test_large_text_batch(torch_cuda):
