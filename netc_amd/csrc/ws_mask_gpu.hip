@@ -912,7 +912,8 @@ __global__ __launch_bounds__(256, (VAL && K == 1) ? 8 : 1) void mask_np_kernel(A
     uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
     // VAL, out of place: the window checks its own first bytes (seam_raw / seam_unmask); the
     // src dword before it is loaded with the window's payload, unmasked once the table is in
-    const bool own = VAL && own_seam(a, A);   // wave-uniform
+    constexpr bool kOwn = VAL && K == 1;      // (launch_mask_validate sets seam_src for one-step windows only)
+    const bool own = kOwn && own_seam(a, A);  // wave-uniform
     uint32_t seam_w = 0;
     Table t;
     auto emit = [&](uint64_t A0, u32x4 src, bool first) {
@@ -937,10 +938,10 @@ __global__ __launch_bounds__(256, (VAL && K == 1) ? 8 : 1) void mask_np_kernel(A
         // by vmcnt(0), which held the table's trip behind the payload's
         const uint32_t lm = min((uint32_t)lane, o >> 4);
         c[M] = load_line_block<NT>(S - o + 16 * lm + (uint64_t)M * kSpan);
-        if constexpr (VAL) seam_w = seam_raw<SRC_ALIGNED>(a, own ? A : A + 4);   // (not own: a dword of the window, unused)
+        if constexpr (kOwn) seam_w = seam_raw<SRC_ALIGNED>(a, own ? A : A + 4);   // (not own: a dword of the window, unused)
         first_probe(a, t, A, lane);
         np_resolve(a, t, A, lane);
-        if constexpr (VAL) {
+        if constexpr (kOwn) {
             if (own) carry = seam_unmask(t, A, seam_w);
         }
         switch ((o >> 2) & 3) {   // uniform: constant register indices in each case
@@ -959,10 +960,10 @@ __global__ __launch_bounds__(256, (VAL && K == 1) ? 8 : 1) void mask_np_kernel(A
         for (int u = 0; u < U; ++u) d[u] = load_vec<true, NT>(a, base + (uint64_t)u * kSpan + 16ull * lane);
     };
     load_step(A);
-    if constexpr (VAL) seam_w = seam_raw<true>(a, own ? A : A + 4);   // (not own: a dword of the window, unused)
+    if constexpr (kOwn) seam_w = seam_raw<true>(a, own ? A : A + 4);   // (not own: a dword of the window, unused)
     first_probe(a, t, A, lane);
     np_resolve(a, t, A, lane);
-    if constexpr (VAL) {
+    if constexpr (kOwn) {
         if (own) carry = seam_unmask(t, A, seam_w);
     }
 #pragma unroll
@@ -1254,14 +1255,17 @@ __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uin
 }
 
 // the VAL kernels: 4 KiB windows (the seams utf8_messages re-checks are at multiples of it)
+// a 4 KiB window per wavefront as U KiB x K steps (NETC_GPU_KNOB_VAL_STEPS = K: 1, 2 or 4).
+// Default by batch size: two 2 KiB steps up to 256 MiB (config 2: 32.3 against 33.2 us), one
+// 4 KiB step above (config 4: 454-461 against 468-475 us; r03l)
+static int val_steps(uint64_t total) {
+    const int64_t k = knob(NETC_GPU_KNOB_VAL_STEPS);
+    return k == 2 || k == 4 ? (int)k : (k == 1 ? 1 : (total <= (256ull << 20) ? 2 : 1));
+}
+
 template <bool AL>
-static hipError_t launch_val(const Args& a, bool persistent, hipStream_t s) {
+static hipError_t launch_val(const Args& a, bool persistent, int k, hipStream_t s) {
     if (!persistent) {
-        // a 4 KiB window per wavefront as U KiB x K steps (NETC_GPU_KNOB_VAL_STEPS = K: 1, 2 or
-        // 4).  Default by batch size: two 2 KiB steps up to 256 MiB (config 2: 32.3 against 33.2
-        // us), one 4 KiB step above (config 4: 454-461 against 468-475 us; r03l)
-        int64_t k = knob(NETC_GPU_KNOB_VAL_STEPS);
-        if (k < 0) k = a.total <= (256ull << 20) ? 2 : 1;
         switch (k) {
             case 2: return launch_np<2, 2, AL, true, true>(a, s);
             case 4: return launch_np<1, 4, AL, true, true>(a, s);
@@ -1289,11 +1293,15 @@ hipError_t launch_mask_validate(uint8_t* dst, const uint8_t* src, uint64_t total
     // out of place, one-window walk: each window checks the bytes after its own start (the 4
     // before it unmasked from src, which nobody writes), so utf8_messages skips the seams (win
     // 0).  In place the bytes before a window may or may not be unmasked yet when it reads them.
-    a.seam_src = dst != src && !persistent;
+    // Only with one-step windows: with two steps the kernel measured 2 us slower at config 2
+    // (27.9 against 26.0 us) than the seams cost phase B there; at config 4 (one step) it saves
+    // 3 us (442.5 against 445.5; phase B 27.7 -> 8.1 us) (r03n)
+    const int k = val_steps(total);
+    a.seam_src = dst != src && !persistent && k == 1;
     hipError_t e;
     if (a.nwin) {
         const bool aligned = (((uintptr_t)src ^ (uintptr_t)dst) & 15u) == 0;
-        e = aligned ? launch_val<true>(a, persistent, stream) : launch_val<false>(a, persistent, stream);
+        e = aligned ? launch_val<true>(a, persistent, k, stream) : launch_val<false>(a, persistent, k, stream);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(utf8_messages, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dst, off, header0, n,
