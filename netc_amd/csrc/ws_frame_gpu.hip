@@ -946,12 +946,14 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     // (the vector path would queue most spans and leave a header fixup per frame)
     a.all_spans = src_total < dense_bytes() * n ? 1u : 0u;
     const bool nt = cfg.flags < 0 || (cfg.flags & (kNtLoads | kNtStores));
-    // U = 2 KiB chunks (measured faster than 4 KiB at configs 2 and 4) unless netc_gpu_tune's
-    // unroll is 8, which selects 4 KiB.  Wire up to 256 MiB: 7 wavefronts per SIMD (72 VGPRs;
-    // C2 40.1 -> 39.3 us); larger: 6 (76 VGPRs; C4 418 vs 425 us at 7, 424 at 8 with spills;
-    // profiles/r02k_ab_enc_occupancy.json)
-    if (cfg.unroll >= 8) return launch_enc_u<4, 5>(a, wire_bound, nt, cfg.max_blocks, stream);
-    if (wire_bound <= (256ull << 20)) return launch_enc_u<2, 7>(a, wire_bound, nt, cfg.max_blocks, stream);
+    // Chunk size: netc_gpu_tune's unroll 8 selects 4 KiB, 2 or 4 select 2 KiB; the default
+    // (unroll 1) takes 4 KiB up to 256 MiB of wire (C2 39.0-39.3 against 39.8-39.9 us, three
+    // rounds, profiles/r03r_enc_chunk.json) and 2 KiB above (C4 416-417 against 422-423 us).
+    // 2 KiB: 7 wavefronts per SIMD up to 256 MiB (72 VGPRs), 6 above (76 VGPRs; C4 418 vs 425
+    // us at 7, 424 at 8 with spills; profiles/r02k_ab_enc_occupancy.json)
+    const bool small = wire_bound <= (256ull << 20);
+    if (cfg.unroll >= 8 || (cfg.unroll <= 1 && small)) return launch_enc_u<4, 5>(a, wire_bound, nt, cfg.max_blocks, stream);
+    if (small) return launch_enc_u<2, 7>(a, wire_bound, nt, cfg.max_blocks, stream);
     return launch_enc_u<2, 6>(a, wire_bound, nt, cfg.max_blocks, stream);
 }
 
