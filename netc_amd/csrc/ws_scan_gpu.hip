@@ -465,6 +465,17 @@ __device__ __forceinline__ uint32_t dword_clamped(const ScanArgs& a, uint64_t p)
 // from the LDS copy -- one pass, a few lanes busy -- and their distinct exits become
 // candidate entries of the chunks they land in.  (Parsing them vector by vector, a
 // window cut from registers each time, cost 13 us of K1's 27 at config 2.)
+// NT: non-temporal loads of the chunk.  Up to 128 MiB of stream K1 reads with plain loads, so
+// the header bytes K2 and K4 read again soon after are still cached: config 2 41.2-41.4 against
+// 42.3-42.6 us; above, the non-temporal stream is faster (config 4 80.8-82.9 against 82.7-84.3
+// us with plain loads; r03t, profiles/r03t_scan_k1_loads.json).
+template <bool NT>
+__device__ __forceinline__ u32x4 k1_load(const uint8_t* p) {
+    if constexpr (NT) return __builtin_nontemporal_load((const NETC_GLOBAL u32x4u*)p);
+    return *(const NETC_GLOBAL u32x4u*)p;
+}
+
+template <bool NT>
 __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     __shared__ uint32_t stage[4][kWords];      // per wave: its chunk's bytes (+ 32 after)
     __shared__ unsigned long long set[4][kSet];
@@ -487,7 +498,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         const uint8_t* base = a.pf_base + B;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const u32x4 v = __builtin_nontemporal_load((const NETC_GLOBAL u32x4u*)(base + 1024 * i + 16 * lane));
+            const u32x4 v = k1_load<NT>(base + 1024 * i + 16 * lane);
 #pragma unroll
             for (int k = 0; k < 4; ++k) d[i][k] = v[k];
         }
@@ -499,7 +510,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         for (int i = 0; i < 4; ++i) {
             uint64_t p = B + 1024 * i + 16 * (uint64_t)lane;
             p = p < a.pf_lim ? p : a.pf_lim;
-            const u32x4 v = __builtin_nontemporal_load((const NETC_GLOBAL u32x4u*)(a.pf_base + p));
+            const u32x4 v = k1_load<NT>(a.pf_base + p);
 #pragma unroll
             for (int k = 0; k < 4; ++k) d[i][k] = v[k];
         }
@@ -1933,7 +1944,8 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.pf_base = len >= 16 ? wire : m + l.flags;
     a.pf_lim = len >= 16 ? len - 16 : 0;
     const unsigned blk = (unsigned)((chunks + kBlkChunks - 1) / kBlkChunks);
-    hipLaunchKernelGGL(scan_exits, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, stream, a);
+    if (len <= (128ull << 20)) hipLaunchKernelGGL(scan_exits<false>, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL(scan_exits<true>, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, stream, a);
 #if defined(NETC_SCAN_K1_ONLY) || defined(NETC_SCAN_K1_EXP)
     return hipGetLastError();   // diagnostic builds only (tools/): K1 timed alone
 #endif
