@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--unroll", default="4,8", help="netc_gpu_tune unroll values to time (4: 2 KiB chunks, the default; 8: 4 KiB)")
     ap.add_argument("--max-blocks", default="0", help="netc_gpu_tune max_blocks values (0: the library's choice; "
                                                        "a huge value: one chunk per wavefront over a covering grid)")
+    ap.add_argument("--flags", default="-1", help="netc_gpu_tune flags values (-1: auto, non-temporal payload "
+                                                  "loads and stores; 8: plain loads and stores)")
     args = ap.parse_args()
 
     import torch
@@ -58,8 +60,9 @@ def main():
             if rc:
                 raise RuntimeError(nm._lib.gpu().netc_gpu_strerror())
 
-        for unroll, mb in [(int(u), int(m)) for u in args.unroll.split(",") for m in args.max_blocks.split(",")]:
-            nm.tune(unroll, mb)
+        for unroll, mb, fl in [(int(u), int(m), int(f)) for u in args.unroll.split(",") for m in args.max_blocks.split(",")
+                               for f in args.flags.split(",")]:
+            nm.tune(unroll, mb, fl)
             K = args.steps if wl == "c2" else max(10, args.steps // 5)
             with torch.cuda.stream(s):
                 for i in range(args.warmup):
@@ -83,7 +86,7 @@ def main():
                 exp = orc.encode_frame(src_h[lo:hi].tobytes(), 2, int(keys[k]).to_bytes(4, "little"))
                 bad += wire[int(wo_h[k]): int(wo_h[k + 1])].tobytes() != exp
             alg = total + wire_len
-            print(json.dumps({"workload": wl, "unroll": unroll, "max_blocks": mb, "frames": int(n), "payload_bytes": int(total), "wire_bytes": int(wire_len),
+            print(json.dumps({"workload": wl, "unroll": unroll, "max_blocks": mb, "flags": fl, "frames": int(n), "payload_bytes": int(total), "wire_bytes": int(wire_len),
                               "us_per_step": round(us, 2), "achieved_GBps": round(alg / (us * 1e-6) / 1e9, 1),
                               "frac_of_8TBps": round(alg / (us * 1e-6) / 8e12, 4),
                               "payload_GiBps": round(total / (us * 1e-6) / 2**30, 1),
