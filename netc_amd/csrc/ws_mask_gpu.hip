@@ -1267,7 +1267,10 @@ template <bool AL>
 static hipError_t launch_val(const Args& a, bool persistent, int k, hipStream_t s) {
     if (!persistent) {
         switch (k) {
-            case 2: return launch_np<2, 2, AL, true, true>(a, s);
+            // two steps (up to 256 MiB by default): plain payload loads and stores, so phase B
+            // reads the unmasked bytes from cache (config 2 31.7 against 32.4 us); one step
+            // (above 256 MiB): non-temporal (config 4 458-463 against 474-480 with plain; r03w)
+            case 2: return launch_np<2, 2, AL, false, true>(a, s);
             case 4: return launch_np<1, 4, AL, true, true>(a, s);
             default: return launch_np<4, 1, AL, true, true>(a, s);
         }
