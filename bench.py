@@ -70,9 +70,10 @@ def parse_args():
     p.add_argument("--c5-gib", type=float, default=16.0,
                    help="BASELINE config 5 leg: GiB of 4 KiB frames streamed host->device->host from a pinned "
                         "ring (rank 0, N = 1; 0 disables)")
-    p.add_argument("--pipelined-probe", action="store_true",
-                   help="also time two independent batches in flight on two streams (secondary figure; its "
-                        "overlapping launches would inflate a rocprof average of the kernel, so it is off by default)")
+    p.add_argument("--no-pipelined-probe", dest="pipelined_probe", action="store_false",
+                   help="skip the secondary figure timed after the headline: the same steps with two independent "
+                        "batches in flight on two streams (pipelined_2stream).  Profiling runs pass this: the "
+                        "overlapping launches would mix into a rocprof average of the kernel")
     p.add_argument("--sync", choices=("auto", "spin"), default="auto",
                    help="how the host waits for the GPU (hipSetDeviceFlags before the context exists): the "
                         "runtime's heuristic, or spin-wait (the synchronize that closes the timed region returns "
@@ -111,13 +112,33 @@ def make_batches(torch, workload: str, rank: int, rotation_bytes: int, device):
     return batches, total, keys.size
 
 
+# the sources the headline kernel is compiled from: a PMC traffic entry is valid only for the
+# kernel it was measured on
+KERNEL_SOURCES = ("netc_amd/csrc/ws_mask_gpu.hip", "netc_amd/csrc/ws_mask_gpu.h", "netc_amd/csrc/gpu_util.h")
+
+
+def kernel_source_hash() -> str:
+    """sha256 (first 16 hex digits) over the headline kernel's sources, in KERNEL_SOURCES order."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def traffic_per_launch(workload: str):
     """HBM bytes per launch of the masking kernel from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic.json, written by tools/summarize_prof.py from separate --pmc
-    FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950 corrections applied), or None."""
+    (profiles/pmc_traffic.json, written by tools/summarize_round.py from separate --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950 corrections applied), or None when
+    there is no entry or the entry was measured on other kernel sources (its
+    kernel_source_sha256 differs from this tree's): a stale figure is never published."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         rec = json.load(open(path))[workload]
+        if rec.get("kernel_source_sha256") != kernel_source_hash():
+            return None
         return rec["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
         return None
@@ -638,6 +659,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic_per_launch(args.workload),
+                "traffic_source": "profiles/pmc_traffic.json entry for this workload whose kernel_source_sha256 "
+                                  f"equals this tree's ({kernel_source_hash()}); null when none does",
                 "kernel_ms_mean": round(kern_mean, 5),
                 "kernel_timing": "HIP events on the launch stream around the K timed launches, / K "
                                  "(slowest rank)",

@@ -55,9 +55,11 @@ struct netc_ws_ingest;
  *  (netc_ws_scan_frames_host, O(frames)), whose descriptors go to the GPU with the bytes for
  *  the unmask only, when its frames averaged >= 16 KiB or (without NETC_WS_INGEST_STRICT) it
  *  held headers with RSV2 / RSV3 bits, reserved opcodes or fragmented control frames (the
- *  GPU scan's parallel pass stops at those; RSV1, which permessage-deflate sets, it accepts);
- *  otherwise the GPU frame scan (netc_gpu_scan_frames, O(bytes), no host work).  The results
- *  are the same either way. */
+ *  GPU scan's parallel pass stops at those; RSV1, which permessage-deflate sets, it accepts),
+ *  or, when it was GPU-scanned, any part of it was walked serially for another reason (a
+ *  capacity of the parallel pass overflowed: netc_gpu_scan_diag's nonzero reasons, which the
+ *  host walk handles at its O(frames) cost); otherwise the GPU frame scan
+ *  (netc_gpu_scan_frames, O(bytes), no host work).  The results are the same either way. */
 #define NETC_WS_INGEST_SCAN_GPU  2   /* always the GPU frame scan */
 #define NETC_WS_INGEST_SCAN_HOST 4   /* always the host header walk */
 

@@ -134,6 +134,9 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *                      each block's release writes back its XCD's L2) [links, then
  *                      tiles + resolve as one launch up to 256 MiB]
  *                                                                  (NETC_SCAN_FUSE)
+ *   MASK_TAPER         bytes at the end of a netc_gpu_mask_batch batch walked in one-step
+ *                      windows instead of two-step ones, so the launch's last waves are
+ *                      short and finish together [0]               (NETC_MASK_TAPER)
  */
 #define NETC_GPU_KNOB_ENC_DENSE_BYTES   1
 #define NETC_GPU_KNOB_ENC_SCAN_PER      2
@@ -141,6 +144,7 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
 #define NETC_GPU_KNOB_SCAN_ANCHOR_SLOTS 4
 #define NETC_GPU_KNOB_VAL_STEPS         5
 #define NETC_GPU_KNOB_SCAN_FUSE         6
+#define NETC_GPU_KNOB_MASK_TAPER        7
 int netc_gpu_knob(int knob, int64_t value);
 
 /**
@@ -195,7 +199,10 @@ int netc_gpu_unmask_validate(int device, void *d_dst, const void *d_src, size_t 
  * own payload start).  All shards are launched before any is waited for; with
  * `synchronize` != 0 the call returns after every shard has completed.
  * streams may be NULL (each device's default stream).  No collective is used:
- * frames are independent.
+ * frames are independent.  On failure no work of the call is left in flight: the
+ * shards before the failing one have completed (they are synchronised before the
+ * call returns), the failing shard and the ones after it were not launched, and
+ * netc_gpu_strerror() names the failing shard ("shard i ...").
  */
 int netc_gpu_mask_batch_multi(int nshards, const int *devices, void *const *d_dst, const void *const *d_src,
                               const size_t *total_bytes, const uint64_t *const *d_frame_offsets,

@@ -213,8 +213,10 @@ int resolve(netc_ws_ingest* g, IngestSlot& s) {
 // like strict mode except for MASK and RSV1 (permessage-deflate) and would stop at the
 // first of them and walk on serially, so such streams go to the host walk.
 //   * GPU-scanned slot: the scan says so itself -- its diag word (nonzero when any part
-//     of the slot was walked serially) is copied to h_res[3] before "scanned", so
-//     resolve() reads it with the result.  The slot's descriptors (h_b0) are NOT read
+//     of the slot was walked serially: a speculative stop at such a header, or a capacity
+//     of the parallel pass overflowed -- adversarial payloads, for which the host walk is
+//     the cheaper route too) is copied to h_res[3] before "scanned", so resolve() reads it
+//     with the result.  The slot's descriptors (h_b0) are NOT read
 //     here: their copy back is queued behind the unmask and may still be running.
 //   * host-walked slot: h_b0 was written by the walk itself, before the submission.
 bool unchecked_headers(const IngestSlot& p) {

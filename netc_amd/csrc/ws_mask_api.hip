@@ -47,12 +47,12 @@ netc_gpu::LaunchCfg cfg_now() {
 // Measurement / test knobs (netc_gpu_knob).  Seeded once per process from the environment
 // (tools/ sweeps set NETC_ENC_SCAN_PER=...), then changed only through netc_gpu_knob; the
 // launch paths read one atomic word, never getenv.
-constexpr int kKnobs = 8;
+constexpr int kKnobs = 8;   // knobs 1 .. 7 (include/ws/mask.h NETC_GPU_KNOB_*)
 std::atomic<int64_t> g_knob[kKnobs];
 std::once_flag g_knob_once;
 void knobs_init() {
     static const char* const env[kKnobs] = {nullptr, "NETC_ENC_DENSE_BYTES", "NETC_ENC_SCAN_PER", "NETC_SCAN_FAST_RANK",
-                                            "NETC_SCAN_ANCHOR_SLOTS", "NETC_VAL_STEPS", "NETC_SCAN_FUSE", nullptr};
+                                            "NETC_SCAN_ANCHOR_SLOTS", "NETC_VAL_STEPS", "NETC_SCAN_FUSE", "NETC_MASK_TAPER"};
     for (int k = 0; k < kKnobs; ++k) {
         const char* e = env[k] ? getenv(env[k]) : nullptr;
         g_knob[k].store(e && *e ? (int64_t)strtoll(e, nullptr, 10) : -1, std::memory_order_relaxed);
@@ -239,7 +239,7 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags) {
 }
 
 int netc_gpu_knob(int knob, int64_t value) {
-    if (knob < NETC_GPU_KNOB_ENC_DENSE_BYTES || knob > NETC_GPU_KNOB_SCAN_FUSE)
+    if (knob < NETC_GPU_KNOB_ENC_DENSE_BYTES || knob > NETC_GPU_KNOB_MASK_TAPER)
         return fail(NETC_GPU_EINVAL, "unknown knob %d", knob);
     std::call_once(g_knob_once, knobs_init);
     g_knob[knob].store(value < 0 ? -1 : value, std::memory_order_relaxed);
@@ -283,25 +283,49 @@ int netc_gpu_mask_batch_multi(int nshards, const int* devices, void* const* d_ds
     if (nshards == 0) return 0;
     if (!devices || !d_dst || !d_src || !total_bytes || !d_frame_offsets || !d_keys || !nframes)
         return fail(NETC_GPU_EINVAL, "null shard array");
-    for (int i = 0; i < nshards; ++i)
-        if (int r = check_device(devices[i])) return r;
-    // launch every shard before waiting on any: the shards run concurrently
+    // Launch every shard before waiting on any: the shards run concurrently.  A shard that
+    // fails (bad arguments, an unknown device, a launch error) ends the call only after the
+    // shards launched before it have completed, so on any return no work of this call is in
+    // flight: shards 0 .. i-1 are then complete, shard i (named in netc_gpu_strerror) and the
+    // ones after it untouched.
+    auto drain = [&](int upto) {
+        for (int j = 0; j < upto; ++j) {
+            DeviceGuard g(devices[j]);
+            if (g.err == hipSuccess) (void)hipStreamSynchronize(streams ? (hipStream_t)streams[j] : nullptr);
+        }
+    };
     for (int i = 0; i < nshards; ++i) {
-        DeviceGuard g(devices[i]);
-        if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
-        hipStream_t s = streams ? (hipStream_t)streams[i] : nullptr;
-        if (int r = mask_batch_on_current(d_dst[i], d_src[i], total_bytes[i], d_frame_offsets[i], d_keys[i],
-                                          nframes[i], s))
-            return r;
+        int r = check_device(devices[i]);
+        if (!r) {
+            DeviceGuard g(devices[i]);
+            if (g.err != hipSuccess) {
+                r = fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+            } else {
+                hipStream_t s = streams ? (hipStream_t)streams[i] : nullptr;
+                r = mask_batch_on_current(d_dst[i], d_src[i], total_bytes[i], d_frame_offsets[i], d_keys[i],
+                                          nframes[i], s);
+            }
+        }
+        if (r) {
+            char why[sizeof(g_err)];
+            snprintf(why, sizeof(why), "%s", g_err);
+            drain(i);
+            return fail(r, "shard %d (shards before it completed, none after it launched): %s", i, why);
+        }
     }
     if (synchronize) {
-        for (int i = 0; i < nshards; ++i) {
+        int rc = 0;
+        for (int i = 0; i < nshards; ++i) {   // every shard is waited for, even after a failure
             DeviceGuard g(devices[i]);
-            if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
-            hipStream_t s = streams ? (hipStream_t)streams[i] : nullptr;
-            hipError_t e = hipStreamSynchronize(s);
-            if (e != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipStreamSynchronize", e);
+            if (g.err != hipSuccess) {
+                if (!rc) rc = fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
+                continue;
+            }
+            hipError_t e = hipStreamSynchronize(streams ? (hipStream_t)streams[i] : nullptr);
+            if (e != hipSuccess && !rc) rc = fail(NETC_GPU_ERUNTIME, "shard %d: hipStreamSynchronize: %s", i,
+                                                  hipGetErrorString(e));
         }
+        return rc;
     }
     return 0;
 }

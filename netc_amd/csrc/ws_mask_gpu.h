@@ -29,6 +29,8 @@ struct Args {
     int32_t probe_bias;        // ... and the frames its base sits before the density's guess
     uint8_t seam_src;          // VAL, out of place: a window checks the first bytes after its start itself
                                // (the 4 bytes before it unmasked from src); utf8_messages skips the seams
+    uint64_t full_win;         // one-window-per-wave walk, K > 1 steps: windows from this one on are ONE step
+                               // (the batch's tapered end, NETC_GPU_KNOB_MASK_TAPER); ~0: none
 };
 
 // LaunchCfg::flags (NETC_GPU_TUNE_*): bits 0-1 non-temporal payload stream, 2 the

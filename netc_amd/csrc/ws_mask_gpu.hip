@@ -900,13 +900,19 @@ __global__ __launch_bounds__(256, (VAL && K == 1) ? 8 : 1) void mask_np_kernel(A
     extern __shared__ uint32_t lds_occupancy_pad[];   // dynamic LDS only limits workgroups per CU
     (void)lds_occupancy_pad;
     init_frames(a);
-    const uint64_t A = wave * kWin;
+    // tapered end (aligned mask walk only): the windows from a.full_win on are one step each, so
+    // the last waves of the launch are short (wave-uniform, scalar)
+    constexpr bool kTaper = SRC_ALIGNED && !VAL && K > 1;
+    const bool short_win = kTaper && wave >= a.full_win;
+    const uint64_t A = short_win ? a.full_win * kWin + (wave - a.full_win) * kStep : wave * kWin;
+    const int ksteps = short_win ? 1 : K;
     const uint64_t full_lo = a.mis ? 16 : 0;
     const uint64_t full_hi = (a.mis + a.total) & ~15ull;
-    if (A < full_lo || A + kWin > full_hi) {   // a window holding a partial vector (<= 2 per batch)
+    if (A < full_lo || A + (uint64_t)ksteps * kStep > full_hi) {   // a window holding a partial vector (<= 2 per batch)
         uint32_t ec = 0;   // VAL: the carry runs across the window's steps (a step start is no seam)
 #pragma unroll 1
-        for (int k = 0; k < K; ++k) edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, A + (uint64_t)k * kStep, lane, ec, k == 0);
+        for (int k = 0; k < ksteps; ++k)
+            edge_chunk<U, SRC_ALIGNED, NT, VAL>(a, A + (uint64_t)k * kStep, lane, ec, k == 0);
         return;
     }
     uint32_t carry = 0;   // the previous span's last 4 unmasked bytes (VAL)
@@ -969,6 +975,7 @@ __global__ __launch_bounds__(256, (VAL && K == 1) ? 8 : 1) void mask_np_kernel(A
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint64_t base = A + (uint64_t)k * kStep;
+        if (kTaper && k >= ksteps) break;   // wave-uniform: a tapered window's single step is done
         if (k > 0) load_step(base);
 #pragma unroll
         for (int u = 0; u < U; ++u) emit(base + (uint64_t)u * kSpan, d[u], k == 0 && u == 0 && !own);
@@ -1072,6 +1079,7 @@ static Args make_args(uint8_t* dst, const uint8_t* src, uint64_t total, const ui
     a.nwin = 0;
     a.probe_e = kWave;
     a.probe_bias = 24;
+    a.full_win = ~0ull;
     return a;
 }
 
@@ -1146,6 +1154,15 @@ hipError_t launch_mask_frames(uint8_t* dst, const uint8_t* src, uint64_t total, 
     const uint64_t win_vec = 64ull * (uint64_t)U * (two ? 2 : 1);
     a.nwin = (nvec + win_vec - 1) / win_vec;
     set_probe(a, 16 * win_vec);
+    // NETC_GPU_KNOB_MASK_TAPER (A/B, tools/): the batch's last `taper` bytes in one-step windows
+    const int64_t taper = knob(NETC_GPU_KNOB_MASK_TAPER);
+    if (two && aligned && taper > 0) {
+        const uint64_t step = 1024ull * (uint64_t)U, span = nvec * 16;
+        uint64_t t = ((uint64_t)taper + step - 1) / step * step;
+        t = t < span ? t : span;
+        a.full_win = (span - t) / (2 * step);
+        a.nwin = a.full_win + (span - a.full_win * 2 * step + step - 1) / step;
+    }
     return aligned ? launch_np_u<true>(a, U, nt, two, stream) : launch_np_u<false>(a, U, nt, two, stream);
 }
 

@@ -45,6 +45,7 @@
 #include <stdlib.h>
 
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -1772,8 +1773,10 @@ void scan_scratch_free(ScanScratch* s) {
 
 namespace {
 // the per-(device, stream) scratch of the public netc_gpu_scan_frames entry
-std::map<std::pair<int, hipStream_t>, ScanScratch*>& stream_scratch() {
-    static std::map<std::pair<int, hipStream_t>, ScanScratch*> m;
+// shared_ptr: scan_diag keeps the scratch alive through its device read without holding the
+// global lock (a concurrent release drops only the map's reference)
+std::map<std::pair<int, hipStream_t>, std::shared_ptr<ScanScratch>>& stream_scratch() {
+    static std::map<std::pair<int, hipStream_t>, std::shared_ptr<ScanScratch>> m;
     return m;
 }
 std::mutex& stream_scratch_mu() {
@@ -1848,32 +1851,39 @@ const uint32_t* scan_scratch_diag_word(const ScanScratch* s) {
 }
 
 // Why the last scan on (device, stream) took the serial walk (0: it did not); the
-// caller has synchronised the stream.  -1: no scratch for that stream.
+// caller has synchronised the stream.  -1: no scratch for that stream.  The global lock is
+// held only to find the scratch and read its address (a growing scan replaces s->mem under
+// that lock and retires, never frees, the old allocation); the scratch itself stays alive
+// through the shared_ptr while the word is copied on the caller's stream, so no other
+// thread's scan, launch or release waits behind this device copy.
 int64_t scan_diag(int device, hipStream_t stream) {
-    // the lock is held across the read: a concurrent release (or a growing scan) of the same
-    // (device, stream) must not free or replace s->mem under it
-    std::lock_guard<std::mutex> g(stream_scratch_mu());
-    auto it = stream_scratch().find({device, stream});
-    if (it == stream_scratch().end()) return -1;
-    ScanScratch* s = it->second;
+    std::shared_ptr<ScanScratch> keep;
+    const uint8_t* word = nullptr;
+    {
+        std::lock_guard<std::mutex> g(stream_scratch_mu());
+        auto it = stream_scratch().find({device, stream});
+        if (it == stream_scratch().end()) return -1;
+        keep = it->second;
+        if (!keep->mem) return -1;
+        word = (const uint8_t*)keep->mem + 9 * sizeof(uint32_t);
+    }
     uint32_t why = 0;
-    if (!s->mem || hipMemcpy(&why, (uint8_t*)s->mem + 9 * sizeof(uint32_t), sizeof(why), hipMemcpyDeviceToHost) !=
-                       hipSuccess)
+    if (hipMemcpyAsync(&why, word, sizeof(why), hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
         return -1;
     return why;
 }
 
 int release_stream_scratch(int device, hipStream_t stream) {
-    ScanScratch* s = nullptr;
+    std::shared_ptr<ScanScratch> s;
     {
         std::lock_guard<std::mutex> g(stream_scratch_mu());
         auto it = stream_scratch().find({device, stream});
         if (it == stream_scratch().end()) return 0;
-        s = it->second;
+        s = std::move(it->second);
         stream_scratch().erase(it);
     }
-    scan_scratch_free(s);
-    return 1;
+    return 1;   // freed (scan_scratch_free) when the last reference -- this one, or a scan_diag's -- drops
 }
 
 hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start, bool strict, uint64_t* hdr,
@@ -1903,9 +1913,13 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         int dev = 0;
         if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
         lk = std::unique_lock<std::mutex>(stream_scratch_mu());
-        ScanScratch*& slot = stream_scratch()[{dev, stream}];
-        if (!slot && !(slot = scan_scratch_new())) return hipErrorOutOfMemory;
-        sp = slot;
+        std::shared_ptr<ScanScratch>& slot = stream_scratch()[{dev, stream}];
+        if (!slot) {
+            ScanScratch* fresh = scan_scratch_new();
+            if (!fresh) return hipErrorOutOfMemory;
+            slot = std::shared_ptr<ScanScratch>(fresh, scan_scratch_free);
+        }
+        sp = slot.get();
     }
     ScanScratch& s = *sp;
     if ((e = scratch_grow(s, chunks, stream)) != hipSuccess) return e;

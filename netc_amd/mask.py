@@ -109,7 +109,8 @@ def tune(unroll: int = 1, max_blocks: int = 0, flags: int = NETC_GPU_TUNE_AUTO) 
     _check(_lib.gpu().netc_gpu_tune(unroll, max_blocks, flags))
 
 
-KNOBS = {"ENC_DENSE_BYTES": 1, "ENC_SCAN_PER": 2, "SCAN_FAST_RANK": 3, "SCAN_ANCHOR_SLOTS": 4, "VAL_STEPS": 5, "SCAN_FUSE": 6}
+KNOBS = {"ENC_DENSE_BYTES": 1, "ENC_SCAN_PER": 2, "SCAN_FAST_RANK": 3, "SCAN_ANCHOR_SLOTS": 4, "VAL_STEPS": 5, "SCAN_FUSE": 6,
+         "MASK_TAPER": 7}
 
 
 def set_knob(name: str, value: int) -> None:

@@ -106,6 +106,22 @@ def test_ragged_frames_and_alignment(torch_cuda, dst_shift, src_shift):
     run_case(torch_cuda, payload, off, keys, dst_shift, src_shift)
 
 
+@pytest.mark.parametrize("taper", [1, 4096, 5000, 3 << 20, 1 << 40])
+@pytest.mark.parametrize("shift,inplace", [(0, True), (5, True), (3, False)])
+def test_tapered_end(torch_cuda, gpu_knob, taper, shift, inplace):
+    # NETC_GPU_KNOB_MASK_TAPER: the batch's last bytes in one-step windows (the end of the launch);
+    # 1 << 40 tapers the whole batch, 1 a single step; the batch ends in a partial vector
+    gpu_knob("MASK_TAPER", taper)
+    off = synth.mixed_offsets((6 << 20) + 11, 1, 70000, seed=13)
+    keys = synth.random_keys(off.size - 1, 13)
+    payload = synth.host_payload(int(off[-1]), 13)
+    run_case(torch_cuda, payload, off, keys, shift, shift, inplace=inplace)
+    sizes = [1024] * 4096                                       # config 2's shape, smaller
+    off = frames_from_sizes(sizes)
+    run_case(torch_cuda, synth.host_payload(4 << 20, 14), off, synth.random_keys(4096, 14), shift, shift,
+             inplace=inplace)
+
+
 @pytest.mark.parametrize("inplace", [False, True])
 def test_in_place_and_out_of_place(torch_cuda, inplace):
     off = synth.mixed_offsets(3 << 20, 256, 65536, seed=5)
@@ -298,6 +314,42 @@ def test_multi_shard_entry(torch_cuda):
     nm.mask_batch_multi(shards, synchronize=True)
     for (dst, _, _, _), e in zip(shards, expect):
         assert np.array_equal(dst.cpu().numpy(), e)
+
+
+def test_multi_shard_failing_shard(torch_cuda):
+    # a failing shard must not leave earlier shards in flight.  Shard 1 is invalid
+    # (null destination): shard 0 has completed and is exact when the call returns, shard 2
+    # was never launched, and the error names shard 1.
+    import ctypes
+
+    from netc_amd import _lib
+
+    torch = torch_cuda
+    lib = _lib.gpu()
+    off = synth.mixed_offsets(16 << 20, 1, 70000, seed=41)
+    keys = synth.random_keys(off.size - 1, 41)
+    payload = synth.host_payload(int(off[-1]), 41)
+    src = torch.from_numpy(payload).cuda()
+    dsts = [torch.zeros_like(src) for _ in range(3)]
+    off_t, keys_t = _dev(torch, off, None), _dev(torch, keys, None)
+    k = 3
+    VP = ctypes.c_void_p * k
+    devs = (ctypes.c_int * k)(0, 0, 0)
+    dst_p = VP(dsts[0].data_ptr(), None, dsts[2].data_ptr())
+    src_p = VP(*([src.data_ptr()] * k))
+    totals = (ctypes.c_size_t * k)(*([int(off[-1])] * k))
+    offs = VP(*([off_t.data_ptr()] * k))
+    kp = VP(*([keys_t.data_ptr()] * k))
+    ns = (ctypes.c_size_t * k)(*([keys.size] * k))
+    s = torch.cuda.Stream()
+    strs = VP(*([s.cuda_stream] * k))
+    rc = lib.netc_gpu_mask_batch_multi(k, devs, dst_p, src_p, totals, offs, kp, ns, strs, 0)
+    assert rc == nm.NETC_GPU_EINVAL
+    assert b"shard 1" in lib.netc_gpu_strerror()
+    # no synchronize here: the call itself waited for shard 0
+    assert s.query(), "shard 0 still in flight after the failing call returned"
+    assert np.array_equal(dsts[0].cpu().numpy(), orc.mask_batch(payload, off, keys))
+    assert int(dsts[2].count_nonzero()) == 0
 
 
 def test_multi_shard_distinct_devices(torch_cuda):

@@ -78,7 +78,13 @@ def build_batch(rng, n_msgs, max_len, bad_frac=0.3, control_frac=0.1, binary_fra
     return frames
 
 
-def run_validate(torch, frames, shift=0, inplace=True):
+# where dst lies: in place; out of place 3 bytes off src's alignment (the SRC_ALIGNED = false
+# kernels); out of place 16 bytes on, co-aligned with src (SRC_ALIGNED = true: with one-step
+# windows each window checks its own first bytes from src -- seam_raw<true> -- ADVICE r3)
+PLACES = {"inplace": None, "oop_misaligned": 3, "oop_coaligned": 16}
+
+
+def run_validate(torch, frames, shift=0, inplace=True, dshift=3):
     payload = np.frombuffer(b"".join(p for _, p in frames), dtype=np.uint8)
     n = len(frames)
     off = np.zeros(n + 1, dtype=np.uint64)
@@ -95,7 +101,7 @@ def run_validate(torch, frames, shift=0, inplace=True):
         dst = src
     else:
         dbuf = torch.zeros(total + 2 * GUARD, dtype=torch.uint8, device="cuda")
-        dst = dbuf[GUARD + shift + 3: GUARD + shift + 3 + total]
+        dst = dbuf[GUARD + shift + dshift: GUARD + shift + dshift + total]
     valid = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
     nm.unmask_validate(dst, src, _dev(torch, off), _dev(torch, keys), torch.from_numpy(h0).cuda(), valid)
     torch.cuda.synchronize()
@@ -142,8 +148,9 @@ def test_tiny_fragments(torch_cuda):
     run_validate(torch_cuda, frames)
 
 
+@pytest.mark.parametrize("place", sorted(PLACES))
 @pytest.mark.parametrize("steps", [None, 1, 2, 4])
-def test_errors_at_every_boundary(torch_cuda, gpu_knob, steps):
+def test_errors_at_every_boundary(torch_cuda, gpu_knob, steps, place):
     # one long valid TEXT frame per case with an error at a vector / span / chunk edge
     gpu_knob("VAL_STEPS", steps)
     rng = np.random.default_rng(60)
@@ -159,14 +166,14 @@ def test_errors_at_every_boundary(torch_cuda, gpu_knob, steps):
                 cut = cut[:-1]
             frames.append((0x81, cut + bad + b"tail"))
     frames.append((0x81, base))   # and a valid one
-    exp = run_validate(torch_cuda, frames)
+    exp = run_validate(torch_cuda, frames, inplace=PLACES[place] is None, dshift=PLACES[place] or 0)
     assert (exp[:-1] == 0).all() and exp[-1] == 1
 
 
-@pytest.mark.parametrize("inplace", [True, False])
+@pytest.mark.parametrize("place", sorted(PLACES))
 @pytest.mark.parametrize("steps", [None, 1, 2, 4])
 @pytest.mark.parametrize("shift", [0, 5])
-def test_errors_at_chunk_seams(torch_cuda, gpu_knob, shift, steps, inplace):
+def test_errors_at_chunk_seams(torch_cuda, gpu_knob, shift, steps, place):
     gpu_knob("VAL_STEPS", steps)
     # long frames (many 4 KiB chunks each) with one broken byte among the first 3 bytes
     # of a chunk -- the bytes phase B checks in place; out of place each window checks its
@@ -183,7 +190,7 @@ def test_errors_at_chunk_seams(torch_cuda, gpu_knob, shift, steps, inplace):
                 body[p] = (0xFF, 0x80, 0xC0)[i % 3]
         frames.append((0x81, bytes(body)))
         o += flen
-    run_validate(torch_cuda, frames, shift=shift, inplace=inplace)
+    run_validate(torch_cuda, frames, shift=shift, inplace=PLACES[place] is None, dshift=PLACES[place] or 0)
 
 
 @pytest.mark.parametrize("inplace", [True, False])

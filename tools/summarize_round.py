@@ -19,6 +19,7 @@ import json
 import os
 import shutil
 import statistics
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = "mask_np_kernel<1, 2, true, true, false, netc_gpu::Args>"   # the headline instantiation
@@ -89,7 +90,11 @@ def main():
     json.dump(out, open(os.path.join(prof, f"{args.tag}_{wl}_summary.json"), "w"), indent=1)
     tp = os.path.join(prof, "pmc_traffic.json")
     traffic = json.load(open(tp)) if os.path.exists(tp) else {}
-    traffic[wl] = {"hbm_bytes_per_launch": int(hbm), "source": f"profiles/{args.tag}_{wl}_summary.json"}
+    sys.path.insert(0, ROOT)
+    from bench import kernel_source_hash   # the sources this pass measured (the tree it ran from)
+
+    traffic[wl] = {"hbm_bytes_per_launch": int(hbm), "source": f"profiles/{args.tag}_{wl}_summary.json",
+                   "kernel_source_sha256": kernel_source_hash()}
     json.dump(traffic, open(tp, "w"), indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "bench_line"}, indent=1))
 
