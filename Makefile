@@ -20,7 +20,8 @@ HOST_SRCS  := $(wildcard netc_amd/csrc/host/*.c)
 HOST_HDRS  := $(wildcard include/*.h include/*/*.h)
 GPU_SRCS   := netc_amd/csrc/ws_mask_gpu.hip netc_amd/csrc/ws_frame_gpu.hip netc_amd/csrc/ws_scan_gpu.hip netc_amd/csrc/ws_ingest.hip \
               netc_amd/csrc/ws_mask_api.hip
-GPU_HDRS   := netc_amd/csrc/ws_mask_gpu.h netc_amd/csrc/gpu_util.h include/ws/mask.h include/ws/frame.h include/ws/ingest.h
+GPU_HDRS   := netc_amd/csrc/ws_mask_gpu.h netc_amd/csrc/gpu_util.h include/ws/mask.h include/ws/frame.h include/ws/ingest.h \
+              include/ws/route.h include/ws/common.h
 
 .PHONY: all host gpu oracle diag clean asan
 all: host gpu oracle

@@ -150,6 +150,22 @@ struct ws_message;   /* include/ws/common.h */
 int netc_ws_ingest_next_message(struct netc_ws_ingest *ing, struct ws_message *message, size_t max_payload_length,
                                 int wait);
 
+/**
+ * Serve netc's own ws_parse_frame (libnetc.so) on `sockfd` from `ring` (include/ws/route.h):
+ * while attached, ws_parse_frame(client, &state, limit) on that socket takes the next message
+ * from the ring -- receiving with large recv() calls into the pinned slots, frames found and
+ * unmasked on the GPU -- with the reference's contract (src/ws/common.c:134-348): 0 and
+ * state->message filled (the caller frees message.buffer, src/web/server.c:139), 1 when the
+ * socket has nothing more now, or WS_FRAME_PARSE_ERROR_* (PAYLOAD_TOO_BIG against `limit`,
+ * RECV once the peer closed and every message was returned).  Other sockets keep the CPU
+ * parser.  The ring reads ahead of the message it returns, so a caller driven by readiness
+ * events calls ws_parse_frame again after a 0 until it returns 1 (the level-triggered event
+ * does not fire for bytes already in the ring).  One thread per connection, as netc runs it;
+ * detach before destroying the ring.  0 or NETC_GPU_EINVAL.
+ */
+int netc_ws_gpu_attach(int sockfd, struct netc_ws_ingest *ring);
+int netc_ws_gpu_detach(int sockfd);
+
 /** Slots submitted so far whose frames the GPU scan found (*gpu) / the host walk found (*host).  0 or EINVAL. */
 int netc_ws_ingest_scan_counts(const struct netc_ws_ingest *ing, uint64_t *gpu, uint64_t *host);
 

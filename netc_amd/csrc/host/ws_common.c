@@ -19,6 +19,7 @@
  */
 #include "../../../include/ws/common.h"
 #include "../../../include/ws/mask.h"
+#include "../../../include/ws/route.h"
 #include "../../../include/tcp/server.h"
 #include "../../../include/utils/error.h"
 
@@ -204,6 +205,12 @@ int ws_parse_frame(struct web_client *client, struct ws_frame_parsing_state *st,
     const socket_t fd = client_socket(client);
     size_t got = 0;
     int r;
+
+    /* a connection with a receive route attached (include/ws/route.h: e.g. the GPU ingest ring,
+       netc_ws_gpu_attach) is served by it, with this function's contract */
+    void *route_ctx = NULL;
+    const netc_ws_route_fn route = netc_ws_route_get((int)fd, &route_ctx);
+    if (route) return route(route_ctx, (int)fd, st, MAX_PAYLOAD_LENGTH);
 
     for (;;)
     {

@@ -41,6 +41,7 @@ extern "C" {
 #include "../../include/ws/frame.h"
 #include "../../include/ws/ingest.h"
 #include "../../include/ws/common.h"
+#include "../../include/ws/route.h"
 extern __thread int netc_errno_reason;   // include/utils/error.h
 }
 
@@ -601,6 +602,49 @@ int netc_ws_ingest_next_message(struct netc_ws_ingest* g, struct ws_message* mes
         (void)netc_ws_ingest_release(g, &b);
         m.have = false;
     }
+}
+
+// ws_parse_frame on a socket attached to a ring (include/ws/route.h): the reference's receive
+// contract (src/ws/common.c:134-348; caller src/web/server.c:86-140) served from the ring.
+// Buffered messages first; when none is complete, one recv() into the ring and again, until
+// a message is ready (0), the socket has nothing more now (1: wait for the next readiness
+// event), or the stream ended (< 0).  state->message gets the message as ws_parse_frame
+// would fill it (opcode, caller-owned malloc'd buffer, payload_length with a TEXT message's
+// NUL); the rest of the parser state is not used.
+static int gpu_route(void* ctx, int sockfd, struct ws_frame_parsing_state* state, size_t max_payload_length) {
+    netc_ws_ingest* g = (netc_ws_ingest*)ctx;
+    int full = 0;
+    for (;;) {
+        struct ws_message m;
+        const int r = netc_ws_ingest_next_message(g, &m, max_payload_length, 1);
+        if (r == 0) {
+            state->message = m;
+            return 0;
+        }
+        if (r < 0) return r;
+        const long n = netc_ws_ingest_recv(g, sockfd);
+        if (n == 0) return 1;                              // drained: wait for readiness
+        if (n > 0 || n == NETC_WS_INGEST_CLOSED) {         // (closed: what it sent is delivered first)
+            full = 0;
+            continue;
+        }
+        // no free slot: next_message releases slots as it consumes them; a ring that stays full
+        // with no message completing cannot progress
+        if (n == NETC_WS_INGEST_FULL && ++full < 3) continue;
+        return message_code((int)n);
+    }
+}
+
+int netc_ws_gpu_attach(int sockfd, struct netc_ws_ingest* ring) {
+    if (!ring) return api_fail(NETC_GPU_EINVAL, "attach: null ring");
+    if (netc_ws_route_attach(sockfd, gpu_route, ring) != 0)
+        return api_fail(NETC_GPU_EINVAL, "attach: socket %d out of range", sockfd);
+    return 0;
+}
+
+int netc_ws_gpu_detach(int sockfd) {
+    if (netc_ws_route_detach(sockfd) != 0) return api_fail(NETC_GPU_EINVAL, "detach: socket %d out of range", sockfd);
+    return 0;
 }
 
 int netc_ws_ingest_scan_counts(const struct netc_ws_ingest* g, uint64_t* gpu, uint64_t* host) {

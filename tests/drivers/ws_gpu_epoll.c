@@ -25,7 +25,14 @@
  *   client log: per sent message       u8 opcode, u8 masked, u8 key[4], u64 frames, u64 length, payload
  * Exit status 0 when every reply the client checks was right; stdout: one summary line.
  *
- * usage: ws_gpu_epoll SERVER_LOG CLIENT_LOG [auto|gpu|host] [slot_bytes]
+ * Route "parse" (5th argument): the server calls ONLY netc's own ws_parse_frame (libnetc.so),
+ * exactly as src/web/server.c:86 does, with the ring attached to the socket by
+ * netc_ws_gpu_attach (include/ws/ingest.h): ws_parse_frame then receives into
+ * the ring and returns the GPU-unmasked messages; the server memsets its parser state after
+ * each message (server.c:139-140) and calls again until it returns 1.  Route "ingest" (the
+ * default): netc_ws_ingest_recv + netc_ws_ingest_next_message directly.
+ *
+ * usage: ws_gpu_epoll SERVER_LOG CLIENT_LOG [auto|gpu|host] [slot_bytes] [ingest|parse]
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -87,6 +94,7 @@ struct server {
     int port;
     const char *log_path;
     int scan_flags;
+    int parse_route;           /* serve through ws_parse_frame on the attached socket */
     size_t slot_bytes;
     int rc;                    /* 0 ok */
     uint64_t delivered, gpu_slots, host_slots;
@@ -132,8 +140,14 @@ static void *server_main(void *arg) {
     struct epoll_event ev = {.events = EPOLLIN, .data.fd = fd};
     if (ep < 0 || epoll_ctl(ep, EPOLL_CTL_ADD, fd, &ev) != 0) goto out;
 
+    if (S->parse_route && netc_ws_gpu_attach(fd, ing) != 0) {
+        fprintf(stderr, "server: attach: %s\n", netc_gpu_strerror());
+        goto out;
+    }
     int burst_count = 0, open = 1;
     uint64_t burst_hash = FNV0;
+    struct ws_frame_parsing_state st;   /* parse route: the connection's parser state (web_client's) */
+    memset(&st, 0, sizeof st);
     while (open) {
         struct epoll_event got;
         int n = epoll_wait(ep, &got, 1, 20000);
@@ -142,15 +156,25 @@ static void *server_main(void *arg) {
             fprintf(stderr, "server: epoll_wait %s\n", n == 0 ? "timed out" : strerror(errno));
             goto out;
         }
-        long r = netc_ws_ingest_recv(ing, fd);
-        if (r == NETC_WS_INGEST_CLOSED) open = 0;   /* what it sent is still delivered below */
-        else if (r < 0 && r != NETC_WS_INGEST_FULL) {
-            fprintf(stderr, "server: recv: %ld %s\n", r, netc_gpu_strerror());
-            goto out;
+        if (!S->parse_route) {
+            long r = netc_ws_ingest_recv(ing, fd);
+            if (r == NETC_WS_INGEST_CLOSED) open = 0;   /* what it sent is still delivered below */
+            else if (r < 0 && r != NETC_WS_INGEST_FULL) {
+                fprintf(stderr, "server: recv: %ld %s\n", r, netc_gpu_strerror());
+                goto out;
+            }
         }
         struct ws_message m;
         int res;
-        while ((res = netc_ws_ingest_next_message(ing, &m, SERVER_LIMIT, 1)) == 0) {
+        for (;;) {
+            if (S->parse_route) {
+                /* src/web/server.c:86, unchanged: the attached socket is served from the ring */
+                res = ws_parse_frame(pr.wc, &st, SERVER_LIMIT);
+                if (res == 0) m = st.message;
+            } else {
+                res = netc_ws_ingest_next_message(ing, &m, SERVER_LIMIT, 1);
+            }
+            if (res != 0) break;
             const uint8_t op = m.opcode;
             const uint8_t kind = op == WS_OPCODE_PING ? 'P' : op == WS_OPCODE_PONG ? 'Q' : op == WS_OPCODE_CLOSE ? 'C' : 'M';
             const uint64_t len = m.payload_length;
@@ -195,10 +219,13 @@ static void *server_main(void *arg) {
                 }
             }
             free(m.buffer);   /* the caller owns the message (src/web/server.c:139) */
+            if (S->parse_route) memset(&st, 0, sizeof st);   /* src/web/server.c:140 */
             if (!open) break;
         }
         if (res < 0) {   /* malformed: on_ws_malformed_frame + close 1002 (src/web/server.c:88-95) */
-            if (open) {
+            if (S->parse_route && res == WS_FRAME_PARSE_ERROR_RECV) {
+                open = 0;   /* the peer closed and every message before that was returned */
+            } else if (open) {
                 fprintf(stderr, "server: malformed frame (%d): %s\n", res, netc_gpu_strerror());
                 send_close(pr.wc, 1002, (const uint8_t *)"Malformed frame.", 16);
                 goto out;
@@ -208,6 +235,7 @@ static void *server_main(void *arg) {
     netc_ws_ingest_scan_counts(ing, &S->gpu_slots, &S->host_slots);
     S->rc = 0;
 out:
+    if (S->parse_route && fd >= 0) netc_ws_gpu_detach(fd);
     if (ep >= 0) close(ep);
     if (fd >= 0) close(fd);
     if (ing) netc_ws_ingest_destroy(ing);
@@ -281,6 +309,7 @@ int main(int argc, char **argv) {
     S.scan_flags = argc > 3 && !strcmp(argv[3], "gpu") ? NETC_WS_INGEST_SCAN_GPU
                    : argc > 3 && !strcmp(argv[3], "host") ? NETC_WS_INGEST_SCAN_HOST : 0;
     S.slot_bytes = argc > 4 ? (size_t)strtoull(argv[4], NULL, 10) : (size_t)1 << 20;
+    S.parse_route = argc > 5 && !strcmp(argv[5], "parse");
     if (netc_gpu_init(0) != 0) {   /* keep runtime initialisation off the event loop */
         fprintf(stderr, "netc_gpu_init: %s\n", netc_gpu_strerror());
         return 2;
@@ -376,8 +405,9 @@ int main(int argc, char **argv) {
     close(cfd);
     fclose(g_clog);
     pthread_join(th, NULL);
-    printf("{\"server_rc\": %d, \"client_ok\": %d, \"delivered\": %llu, \"gpu_slots\": %llu, \"host_slots\": %llu}\n",
+    printf("{\"server_rc\": %d, \"client_ok\": %d, \"delivered\": %llu, \"gpu_slots\": %llu, \"host_slots\": %llu, "
+           "\"route\": \"%s\"}\n",
            S.rc, !g_fail, (unsigned long long)S.delivered, (unsigned long long)S.gpu_slots,
-           (unsigned long long)S.host_slots);
+           (unsigned long long)S.host_slots, S.parse_route ? "parse" : "ingest");
     return S.rc || g_fail;
 }

@@ -10,7 +10,11 @@ callback, free); and a client that sends through libnetc.so's ws_send_message --
 script (reference tests/ws/test001.c:192-273), a ping, one 16 MiB message in 256 frames, a
 burst of 2,000 fragmented messages -- checking every reply with ws_parse_frame.
 
-Checked here, per scan mode of the ring:
+Route "parse" runs the same server with ONLY netc's ws_parse_frame on its side: the socket is
+attached to the ring (netc_ws_gpu_attach), so libnetc.so's ws_parse_frame receives into the ring
+and returns the GPU-unmasked messages with the reference's 0 / 1 / < 0 contract.
+
+Checked here, per scan mode of the ring and route:
   * the program's own checks (replies, pong payload, close echo, 16 MiB and burst hashes);
   * every message the GPU route delivered equals, in order, what libnetc's ws_parse_frame
     delivers from the same bytes -- rebuilt from the client's log of (opcode, key, frames,
@@ -65,14 +69,18 @@ def read_client_log(path):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("mode", ["auto", "gpu", "host"])
-def test_epoll_server_on_gpu_ingest(tmp_path, mode):
+@pytest.mark.parametrize("mode,route", [("auto", "ingest"), ("gpu", "ingest"), ("host", "ingest"),
+                                        ("auto", "parse"), ("gpu", "parse")])
+def test_epoll_server_on_gpu_ingest(tmp_path, mode, route):
+    # route "parse": the server calls only netc's ws_parse_frame on a socket attached to the ring
+    # (netc_ws_gpu_attach) -- the kept C API reaching the GPU
     assert os.path.exists(EXE), "tests/bin/ws_gpu_epoll missing: run make"
     slog, clog = str(tmp_path / "server.log"), str(tmp_path / "client.log")
-    r = subprocess.run([EXE, slog, clog, mode, str(1 << 20)], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([EXE, slog, clog, mode, str(1 << 20), route], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, f"rc {r.returncode}\nstdout: {r.stdout}\nstderr: {r.stderr[-3000:]}"
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     assert summary["server_rc"] == 0 and summary["client_ok"] == 1
+    assert summary["route"] == route
     gpu_slots, host_slots = summary["gpu_slots"], summary["host_slots"]
     if mode == "gpu":
         assert host_slots == 0 and gpu_slots > 0

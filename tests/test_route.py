@@ -1,0 +1,102 @@
+"""Per-connection receive routes of ws_parse_frame (include/ws/route.h, libnetc.so; CPU).
+
+While a route is attached to a socket, libnetc's ws_parse_frame on that socket returns the
+route's result (this is how netc_ws_gpu_attach puts the GPU ingest ring behind netc's own
+call, reference src/web/server.c:86); other sockets, and the socket again after detach, keep
+the CPU parser.  The GPU route itself is exercised end to end by tests/test_gpu_epoll.py
+(route "parse")."""
+
+import ctypes
+import socket
+
+from netc_amd import _lib
+from tests.wsutil import Endpoint, ParseState, libc, pair, send_wire
+
+ROUTE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t)
+
+
+def host():
+    lib = _lib.host()
+    lib.netc_ws_route_attach.argtypes = [ctypes.c_int, ROUTE_FN, ctypes.c_void_p]
+    lib.netc_ws_route_attach.restype = ctypes.c_int
+    lib.netc_ws_route_detach.argtypes = [ctypes.c_int]
+    lib.netc_ws_route_detach.restype = ctypes.c_int
+    lib.netc_ws_route_get.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    lib.netc_ws_route_get.restype = ctypes.c_void_p
+    return lib
+
+
+def test_route_serves_attached_socket_only():
+    lib = host()
+    a, b = pair()
+    c, d = pair()
+    calls = []
+    payload = b"routed message"
+    keep = ctypes.create_string_buffer(payload)
+
+    def route(ctx, fd, state, limit):
+        calls.append((ctx, fd, limit))
+        st = ctypes.cast(state, ctypes.POINTER(ParseState)).contents
+        buf = libc.malloc(len(payload))
+        ctypes.memmove(buf, keep, len(payload))
+        st.message.opcode = 2
+        st.message.buffer = buf
+        st.message.payload_length = len(payload)
+        return 0
+
+    libc.malloc.restype = ctypes.c_void_p
+    libc.malloc.argtypes = [ctypes.c_size_t]
+    fn = ROUTE_FN(route)
+    eb, ed = Endpoint(b), Endpoint(d)
+    try:
+        assert lib.netc_ws_route_attach(b.fileno(), fn, 1234) == 0
+        ctx = ctypes.c_void_p()
+        assert lib.netc_ws_route_get(b.fileno(), ctypes.byref(ctx)) and ctx.value == 1234
+        assert not lib.netc_ws_route_get(d.fileno(), ctypes.byref(ctx))
+        # attached socket: the route's message, with ws_parse_frame's 0 / caller-owned buffer contract
+        st = ParseState()
+        assert lib.ws_parse_frame(ctypes.byref(eb.client), ctypes.byref(st), 77) == 0
+        assert calls == [(1234, b.fileno(), 77)]
+        assert st.message.opcode == 2 and ctypes.string_at(st.message.buffer, st.message.payload_length) == payload
+        libc.free(st.message.buffer)
+        # another socket: the CPU parser on real bytes
+        rc, w = send_wire(b"cpu path", 1, b"\x01\x02\x03\x04", 1)
+        assert rc == 1
+        c.sendall(w)
+        st2 = ParseState()
+        while (r := lib.ws_parse_frame(ctypes.byref(ed.client), ctypes.byref(st2), 1 << 20)) == 1:
+            pass
+        assert r == 0 and ctypes.string_at(st2.message.buffer, st2.message.payload_length) == b"cpu path\0"
+        libc.free(st2.message.buffer)
+        assert len(calls) == 1
+        # detached: the CPU parser again on the first socket
+        assert lib.netc_ws_route_detach(b.fileno()) == 0
+        assert not lib.netc_ws_route_get(b.fileno(), ctypes.byref(ctx))
+        a.sendall(w)
+        st3 = ParseState()
+        while (r := lib.ws_parse_frame(ctypes.byref(eb.client), ctypes.byref(st3), 1 << 20)) == 1:
+            pass
+        assert r == 0 and ctypes.string_at(st3.message.buffer, st3.message.payload_length) == b"cpu path\0"
+        libc.free(st3.message.buffer)
+        assert len(calls) == 1
+    finally:
+        lib.netc_ws_route_detach(b.fileno())
+        for s in (a, b, c, d):
+            s.close()
+
+
+def test_route_rejects_bad_arguments():
+    lib = host()
+    fn = ROUTE_FN(lambda *args: 1)
+    assert lib.netc_ws_route_attach(-1, fn, None) == -1
+    assert lib.netc_ws_route_attach(1 << 30, fn, None) == -1
+    assert lib.netc_ws_route_detach(-5) == -1
+    assert lib.netc_ws_route_detach(1000) == 0            # nothing attached: fine
+    s = socket.socket()
+    try:
+        assert lib.netc_ws_route_attach(s.fileno(), fn, None) == 0
+        assert lib.netc_ws_route_attach(s.fileno(), fn, None) == 0   # re-attach replaces
+        assert lib.netc_ws_route_detach(s.fileno()) == 0
+        assert lib.netc_ws_route_detach(s.fileno()) == 0
+    finally:
+        s.close()
