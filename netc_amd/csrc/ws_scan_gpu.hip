@@ -86,28 +86,15 @@ static constexpr int kBlkChunks = NETC_SCAN_BLK;              // K2: chunks per 
 static constexpr int kEmitChunks = NETC_SCAN_EMIT;            // K4: chunks per block
 static_assert(kBlkChunks * kCand <= 256 && kTileChunks % kBlkChunks == 0, "K2: one thread per node slot");
 static_assert(kEmitChunks <= 256 && kTileChunks % kEmitChunks == 0, "K4: one thread per chunk, blocks inside a tile");
+static constexpr int32_t kDupLink = -2;                       // K2: slot repeats an earlier slot's position
 static constexpr int kWalkHops = 64;                          // K2 / K4: frames walked one by one
 static constexpr int kList = 8;                               // K2 -> K4: frames recorded per node
 static constexpr int kListSlots = 4;                          // ... for node slots 0..3 of a chunk
 static constexpr uint32_t kH = 0x80808080u;
-// K1 -> K2 candidate routing.  A chunk's exits that land at most kNear chunks ahead (every 7- and
-// 16-bit length: p + 2 + 2 + 4 + 65535 < the chunk end + 17 chunks) go to the chunk's own exit
-// list with plain stores -- word 0 the count, words 1..kXL-1 the positions -- and K2 gathers the
-// lists of the kNear chunks before each of its chunks.  Farther exits (64-bit lengths) and the
-// stream start are appended to the target chunk's far list by atomics (bit 63: entered from
-// another tile).  K1 thus neither reads an exit's target bytes nor waits for a returning atomic
-// on the common path; K2 prunes the candidates with its first header read (round 4).
-static constexpr int kXL = 32;                                // words per chunk exit list
-static constexpr uint64_t kNear = 17;
-static constexpr int kFar = 8;                                // far candidates per chunk
-static constexpr int kRaw = 32;                               // K2: candidates gathered per chunk
-static constexpr int kSrc = kBlkChunks + (int)kNear;          // K2: exit lists a block reads
-static constexpr int kSrcFirst = 8;                           // ... 16-B pieces of each in the first trip
-static constexpr uint64_t kExtBit = 1ull << 63;
 // why a scan fell back to the serial walk (flags[9], read by netc_gpu_scan_diag): bits
 // 0-7 flags[0] (K1 bucket full, K1 exit set full, K2 exit onto no candidate, K3a tile
 // external list full, K1 candidate queue full), 8+ K3b's own reason
-enum : uint32_t { kOvfBucket = 1, kOvfSet = 2, kOvfLink = 4, kOvfExt = 8, kOvfQueue = 16, kOvfList = 32 };
+enum : uint32_t { kOvfBucket = 1, kOvfSet = 2, kOvfLink = 4, kOvfExt = 8, kOvfQueue = 16 };
 enum : uint32_t { kWhyRoot = 1u << 8, kWhyTiles = 2u << 8, kWhyExtCap = 3u << 8, kWhySucc = 4u << 8 };
 // bit 16: a speculative (non-strict) pass stopped at a header the filter rejects; the rest was walked serially
 enum : uint32_t { kWhySpec = 1u << 16 };
@@ -200,12 +187,11 @@ struct ScanArgs {
     uint32_t* flags;       // [8] K3b -> K4: serial fallback (big streams), [9] why the last call walked serially
     uint32_t* ovf;         // this call's overflow bits (flags[0] / flags[2] on alternate calls: the
     uint32_t* ovf_prev;    // ... reader is every K4 block, so K4 zeroes the previous call's word instead)
-    uint64_t* xl;          // K1 -> K2: per real chunk kXL words, its near exits (word 0: count)
-    uint32_t* fcount;      // K1 -> K2: nc + 1 far-list counters (zero when a call starts; K2 re-zeroes)
-    uint64_t* fcand;       // ... (nc + 1) * kFar far candidates, bit 63: entered from another tile
-    uint32_t* ccount;      // K2: nc + 1 node counts
-    uint8_t* ext;          // K2: (nc + 1) * kCand: node entered from another tile (or the root)
-    uint64_t* cand;        // K2: (nc + 1) * kCand node positions
+    uint32_t* ccount;      // nc + 1 candidate counters (zero when a call starts; K4 re-zeroes)
+    uint8_t* ext;          // (nc + 1) * kCand: slot entered from another tile (or the root); K4 re-zeroes
+    uint32_t* tarr;        // K2+ (fused): per-tile arrival counters (the last arrival re-zeroes)
+    uint64_t* cand;        // (nc + 1) * kCand candidate positions
+    int32_t* link;         // node -> next node, -1 = chain ends, kDupLink
     uint64_t* nterm;       // the terminal where the node's walk leaves its chunk
     uint32_t* ncnt;        // frames on that walk
     uint32_t* wsum;        // K3a: frames from the node to its tile's exit
@@ -333,11 +319,6 @@ __device__ __forceinline__ uint64_t parse_at(const ScanArgs& a, uint64_t p, cons
 
 // LDS copy of the chunk: stream bytes [B, B + kChunk + 32), zero past len.
 static constexpr int kWords = (int)((kChunk + 32) / 4);
-// K1's LDS copy reaches kAhead bytes into the next chunk: an exit of a 7-bit length from the
-// chunk's last 131 bytes lands there, and its first two bytes are checked in LDS (garbage exits
-// pruned without a trip; round 4)
-static constexpr int kAhead = 144;
-static constexpr int kK1Words = (int)((kChunk + kAhead + 16) / 4);
 
 __device__ void load_chunk(const ScanArgs& a, uint64_t B, uint32_t* words) {
     typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
@@ -425,14 +406,17 @@ __device__ __forceinline__ bool set_insert(unsigned long long* set, uint64_t x, 
     return false;
 }
 
-// x as a far candidate of the chunk it lies in (an exit more than kNear chunks ahead, or the
-// stream start); ext: appended from a chunk of another tile, or the stream start (K3a's
-// external nodes)
-__device__ __forceinline__ void far_append(const ScanArgs& a, uint64_t x, bool ext) {
+// x as a candidate entry (node slot) of the chunk it lies in; ext: appended from a
+// chunk of another tile, or the stream start (K3a's external nodes)
+__device__ __forceinline__ void append_cand(const ScanArgs& a, uint64_t x, bool ext) {
     const uint64_t t = x / kChunk;   // x <= len: t <= nc
-    const uint32_t slot = atomicAdd(&a.fcount[t], 1u);
-    if (slot < (uint32_t)kFar) a.fcand[t * kFar + slot] = x | (ext ? kExtBit : 0ull);
-    else atomicOr(a.ovf, kOvfBucket);
+    const uint32_t slot = atomicAdd(&a.ccount[t], 1u);
+    if (slot < (uint32_t)kCand) {
+        a.cand[t * kCand + slot] = x;
+        if (ext) a.ext[t * kCand + slot] = 1;
+    } else {
+        atomicOr(a.ovf, kOvfBucket);
+    }
 }
 
 // a lane of the last vector of a chunk whose 16 positions can exit the chunk with a
@@ -442,7 +426,6 @@ static constexpr int kQCap = 256;   // K1: exit-capable candidates queued per ch
 static constexpr int kCheapMax = 64;   // K1: more from the cheap selection: the full quick check instead
 
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
-typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 // Inclusive sum over the wavefront's lanes, in DPP moves (no LDS trip): row_shr 1/2/4/8
 // within each row of 16, then row_bcast 15 / 31 carry the row totals up.
@@ -495,12 +478,13 @@ __device__ __forceinline__ u32x4 k1_load(const uint8_t* p) {
 
 template <bool NT>
 __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
-    __shared__ uint32_t stage[4][kK1Words];    // per wave: its chunk's bytes (+ kAhead after)
+    __shared__ uint32_t stage[4][kWords];      // per wave: its chunk's bytes (+ 32 after)
     __shared__ unsigned long long set[4][kSet];
     __shared__ uint16_t queue[4][kQCap];
-    __shared__ uint64_t xq[4][kXL];            // per wave: its chunk's near exits (word 0: the count)
-    __shared__ uint32_t xn[4];
-    if ((threadIdx.x & 63) == 0) xn[threadIdx.x / 64] = 0;
+#ifdef NETC_SCAN_K1_EXP
+    __shared__ uint32_t qn[4];
+    if ((threadIdx.x & 63) == 0) qn[threadIdx.x / 64] = 0;
+#endif
     SCAN_SCOPE(0);
     // wv through readfirstlane: the chunk index, its bounds and the edge test below are
     // then scalar (SGPR arithmetic, scalar branches) instead of per-lane VALU
@@ -508,7 +492,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     if (c > a.nc) return;
     const uint64_t B = c * kChunk, Bend = B + kChunk;
-    if (lane == 0 && a.start / kChunk == c) far_append(a, a.start, true);   // the root node
+    if (lane == 0 && a.start / kChunk == c) append_cand(a, a.start, true);   // the root node
     if (B >= a.len) return;   // the virtual chunk: no bytes
     uint32_t d[4][4], nx[4];
     if (Bend <= a.pf_lim) {   // wave-uniform: every load in place, no clamps (scalar base + lane offset)
@@ -558,14 +542,6 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     for (int i = 0; i < 4; ++i)
         *(u32x4*)&st[(1024 * i + 16 * lane) / 4] = u32x4{d[i][0], d[i][1], d[i][2], d[i][3]};
     if (lane < 4) st[kChunk / 4 + lane] = nx[lane];
-    // the next chunk's first kAhead bytes (lanes 1 .. 8; lane 0's are nx), when the whole reach
-    // lies inside the stream (wave-uniform); else exits there are left to K2's prune
-    const bool ahead = Bend + kAhead + 16 <= a.len;
-    if (ahead) {
-        const int la = lane >= 1 && lane < kAhead / 16 ? lane : 1;
-        const u32x4 v = *(const NETC_GLOBAL u32x4u*)(a.wire + Bend + 16 * (uint64_t)la);
-        if (lane >= 1 && lane < kAhead / 16) *(u32x4*)&st[kChunk / 4 + 4 * lane] = v;
-    }
     SCAN_STAMP(0, 1);   // the chunk's bytes have arrived
     set[wv][lane] = ~0ull;   // the wave's exit set
     // the dword after each lane's 16 bytes (readfirstlane outside the lane-63 branch:
@@ -691,12 +667,8 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         incl = wave_incl_sum(mine);
         total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
     }
-    uint64_t* const xlist = a.xl + c * kXL;
     if (total > (uint32_t)kQCap) {   // wave-uniform (adversarial payloads, non-strict mode)
-        if (lane == 0) {
-            atomicOr(a.ovf, kOvfQueue);
-            xlist[0] = 0;   // (the serial walk takes over; K2 reads an empty list)
-        }
+        if (lane == 0) atomicOr(a.ovf, kOvfQueue);
         return;
     }
     uint32_t at = incl - mine;
@@ -717,43 +689,42 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         // strict mode prunes exits that cannot start a frame: payload bytes parsed as a
         // chain land on random positions, which pass with ~2 % odds, while the true chain
         // always lands on a real header
-        // distinct exits: near ones into the chunk's list (K2 prunes them), far ones onto their
-        // target's far list, pruned here by the quick check of the target (rare: 64-bit lengths)
-        const uint64_t vo = v - B;   // (an exit's offset from the chunk start, >= kChunk)
-        const bool local = ahead && vo + 2 <= (uint64_t)(kChunk + kAhead);
-        bool pruned = false;
-        if (local && a.strict) {   // the target's first two bytes in LDS: can a header start there?
-            const uint32_t first = ((const uint8_t*)st)[vo], second = ((const uint8_t*)st)[vo + 1];
-            const uint32_t opcode = first & 0x0F;
-            const bool reserved = (opcode >= 3 && opcode <= 7) || opcode >= 11;
-            pruned = (!(second & 0x80) && !a.spec) || (first & rsv_reject(a)) || reserved || (opcode >= 8 && !(first & 0x80));
+#ifdef NETC_SCAN_K1_EXP
+        // diagnostic build only (tools/, timing of K1's tail): the exit written to a
+        // per-source-chunk list with a plain store -- no target check, no atomic
+        if (!(v & kTerm) && v >= Bend && set_insert(set[wv], v, &ovf)) {
+            const uint32_t k = atomicAdd(&qn[wv], 1u);
+            if (k < (uint32_t)kCand) a.cand[c * kCand + k] = v;
         }
-        if (!(v & kTerm) && v >= Bend && !pruned && set_insert(set[wv], v, &ovf)) {
-            if (v / kChunk - c <= kNear) {
-                const uint32_t k = atomicAdd(&xn[wv], 1u);   // LDS
-                if (k < (uint32_t)(kXL - 1)) xq[wv][k + 1] = v;
-            } else if (!quick_reject(a, v)) {
-                far_append(a, v, v / kChunk / kTileChunks != c / kTileChunks);
-            }
-        }
+#else
+        if (!(v & kTerm) && v >= Bend && set_insert(set[wv], v, &ovf) && !quick_reject(a, v))
+            append_cand(a, v, v / kChunk / kTileChunks != c / kTileChunks);
+#endif
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // the list: word 0 the count, then the exits; only the words in use are written (16-B stores)
-    const uint32_t nxl = xn[wv];
-    const uint32_t nw = nxl < (uint32_t)(kXL - 1) ? nxl : (uint32_t)(kXL - 1);
-    if (lane == 0) xq[wv][0] = nw;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if ((uint32_t)lane * 2 < nw + 1) {
-        const uint64_t w0 = xq[wv][2 * lane], w1 = xq[wv][2 * lane + 1];
-        *(NETC_GLOBAL u64x2*)(xlist + 2 * lane) = u64x2{w0, w1};
-    }
-    SCAN_STAMP(0, 3);   // parsed, exits listed
+    SCAN_STAMP(0, 3);   // parsed, exits checked and appended
     if (ovf) atomicOr(a.ovf, kOvfSet);
-    if (lane == 0 && nxl > (uint32_t)(kXL - 1)) atomicOr(a.ovf, kOvfList);
+}
+
+// node -> the candidate its chain exits to (the first slot holding that position, or
+// -1) and the terminal where it ends
+__device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint64_t x, uint64_t v, uint32_t cnt) {
+    int32_t next = -1;
+    if (term_type(v) == kExit) {
+        const uint64_t y = term_pos(v), t = y / kChunk;
+        // the counter and the bucket's 8 positions (one line) in one trip
+        const uint32_t n = min(a.ccount[t], (uint32_t)kCand);
+        uint64_t ts[kCand];
+#pragma unroll
+        for (int j = 0; j < kCand; ++j) ts[j] = a.cand[t * kCand + j];
+#pragma unroll
+        for (int j = kCand - 1; j >= 0; --j)
+            if ((uint32_t)j < n && ts[j] == y) next = (int32_t)(t * kCand + j);   // the first match
+        // not a candidate: pruned by K1 (the chain dies at y), or its bucket overflowed
+        if (next < 0 && !quick_reject(a, y)) atomicOr(a.ovf, kOvfLink);
+    }
+    a.link[node] = next;
+    a.nterm[node] = v;
+    a.ncnt[node] = cnt;
 }
 
 // Every position of the chunk that can start a header (strict: passes the quick
@@ -814,229 +785,85 @@ __device__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const ui
     return src;
 }
 
-// K2: the nodes of kBlkChunks chunks per block.
-//   1. Gather: the exit lists of the kNear chunks before the block's first chunk and of its own
-//      chunks (K1, plain stores; first kSrcFirst 16-B pieces of each in one trip, the rest in a
-//      second trip only for lists that long) and the block's far lists; every exit landing in
-//      one of the block's chunks is a raw candidate of that chunk (LDS), external when it comes
-//      from another tile.  Repeated positions merge (their external flags OR'd).
-//   2. Prune + walk, one thread per distinct candidate: the header at the candidate is read and
-//      parsed -- a candidate whose first header the filter rejects cannot be an entry and is
-//      dropped (what K1 did with a dependent read of every exit's target before round 4) --
-//      and the others become the chunk's nodes (slots in LDS order): their chain walked to the
-//      terminal where it leaves the chunk, counting frames.  Chains of more than kWalkHops
-//      frames are finished by the whole block afterwards: the chunk's 16-hop links built in
-//      LDS, one thread walks them from the entry -- count / 8 + at most 7 hops, leaving an
-//      anchor every 8 frames -- and re-parses the last header for the exact terminal.
-//   Links between nodes are resolved by position in K3a (the target chunk's nodes are known
-//   only once its block has pruned them).
+// K2: nodes of kBlkChunks chunks per block, one thread per slot: a repeated position
+// defers to its first slot (passing on its external flag); a node's chain is walked
+// from global memory to the candidate it exits to.  Chains of more than kWalkHops
+// frames in the chunk are finished by the whole block afterwards: the chunk's 16-hop
+// links built in LDS, one thread walks them from the entry -- count / 8 + at most 7
+// hops, leaving an anchor every 8 frames -- and re-parses the last header for the exact
+// terminal.
 struct LinksLds {
-    union {
-        struct {   // the long-chain phase (after the walks)
-            uint32_t words[kWords];
-            uint16_t l1[kChunk];
-            uint16_t lj[kChunk];
-            uint16_t lk16[kChunk];
-        } w;
-        struct {   // gathering and pruning (before)
-            uint64_t raw[kBlkChunks][kRaw];     // gathered candidates (bit 63: external)
-            uint8_t dupext[kBlkChunks][kRaw];   // an external duplicate merged into this first copy
-            uint16_t work[kBlkChunks * kRaw];   // distinct candidates (index into raw)
-        } g;
-    };
+    uint32_t words[kWords];
+    uint16_t l1[kChunk];
+    uint16_t lj[kChunk];
+    uint16_t lk16[kChunk];
     uint32_t queue[kBlkChunks * kCand];
-    uint16_t qpos[kBlkChunks * kCand];   // the queued node's position in its chunk
     int nq;
-    uint32_t nraw[kBlkChunks];
-    uint32_t nnode[kBlkChunks];
-    uint8_t extf[kBlkChunks][kCand];     // the nodes' external flags (one 8-byte word per chunk)
-    uint32_t nwork;
-    uint32_t srcn[kSrc];                 // exit-list counts
 };
 
-__device__ __forceinline__ void raw_append(const ScanArgs& a, LinksLds& sl, uint64_t c0, uint64_t x, bool ext) {
-    const uint64_t t = x / kChunk;
-    if (t < c0 || t >= c0 + kBlkChunks || t > a.nc) return;   // another block's chunk
-    const uint32_t u = (uint32_t)(t - c0);
-    const uint32_t i = atomicAdd(&sl.nraw[u], 1u);
-    if (i < (uint32_t)kRaw) sl.g.raw[u][i] = x | (ext ? kExtBit : 0ull);
-    else atomicOr(a.ovf, kOvfBucket);
-}
-
 __device__ void links_body(const ScanArgs& a, LinksLds& sl) {
-    uint32_t* words = sl.w.words;
-    uint16_t* l1 = sl.w.l1;
-    uint16_t* lj = sl.w.lj;
-    uint16_t* lk16 = sl.w.lk16;
+    uint32_t* words = sl.words;
+    uint16_t* l1 = sl.l1;
+    uint16_t* lj = sl.lj;
+    uint16_t* lk16 = sl.lk16;
+    uint32_t* queue = sl.queue;
     int& nq = sl.nq;
     const int tid = threadIdx.x;
-    const uint64_t c0 = (uint64_t)blockIdx.x * kBlkChunks;
-    const int64_t s_lo = (int64_t)c0 - (int64_t)kNear;   // the first source chunk
-    // ---- trip 1: exit lists (pieces 0 .. kSrcFirst-1 of each) and the block's far lists
-    constexpr int kP1 = kSrc * kSrcFirst;
-    constexpr int kPR = (kP1 + kScanT - 1) / kScanT;
-    u64x2 pc[kPR];
-#pragma unroll
-    for (int r = 0; r < kPR; ++r) {
-        const int p = tid + kScanT * r;
-        const int64_t sc = s_lo + p / kSrcFirst;
-        const bool ok = p < kP1 && sc >= 0 && sc < (int64_t)a.nc;
-        pc[r] = ok ? *(const NETC_GLOBAL u64x2*)(a.xl + (uint64_t)sc * kXL + 2 * (p % kSrcFirst)) : u64x2{0, 0};
-    }
-    uint32_t fc = 0;
-    u64x2 fw[kFar / 2];
-    const uint64_t cf = c0 + (uint64_t)tid;
-    const bool fown = tid < kBlkChunks && cf <= a.nc;
-    if (fown) {
-        fc = a.fcount[cf];
-#pragma unroll
-        for (int q = 0; q < kFar / 2; ++q) fw[q] = *(const NETC_GLOBAL u64x2*)(a.fcand + cf * kFar + 2 * q);
-    }
-    if (tid < kBlkChunks) {
-        sl.nraw[tid] = 0;
-        sl.nnode[tid] = 0;
-        *(uint64_t*)sl.extf[tid] = 0;
-    }
-    for (int i = tid; i < kBlkChunks * kRaw; i += kScanT) sl.g.dupext[i / kRaw][i % kRaw] = 0;
-    if (tid == 0) {
-        nq = 0;
-        sl.nwork = 0;
-    }
-#pragma unroll
-    for (int r = 0; r < kPR; ++r) {   // the counts
-        const int p = tid + kScanT * r;
-        if (p < kP1 && p % kSrcFirst == 0) {
-            const int64_t sc = s_lo + p / kSrcFirst;
-            sl.srcn[p / kSrcFirst] = (sc >= 0 && sc < (int64_t)a.nc) ? (uint32_t)min(pc[r][0], (uint64_t)(kXL - 1)) : 0u;
-        }
-    }
+    if (tid == 0) nq = 0;
     __syncthreads();
-    // ---- raw candidates
+    if (tid < kBlkChunks * kCand) {
+        const uint64_t s = (uint64_t)blockIdx.x * (kBlkChunks * kCand) + tid, c = s / kCand;
+        const uint32_t i = (uint32_t)(s % kCand);
+        // the counter, the bucket (one line) and the external flags in one trip
+        const uint32_t cc = c <= a.nc ? a.ccount[c] : 0;
+        uint64_t cs[kCand];
 #pragma unroll
-    for (int r = 0; r < kPR; ++r) {
-        const int p = tid + kScanT * r;
-        if (p >= kP1) continue;
-        const int si = p / kSrcFirst, q = p % kSrcFirst;
-        const uint32_t n = sl.srcn[si];
-        const uint64_t sc = (uint64_t)(s_lo + si);
+        for (int j = 0; j < kCand; ++j) cs[j] = c <= a.nc ? a.cand[c * kCand + j] : 0;
+        const uint64_t x = c <= a.nc ? a.cand[s] : 0;
+        if (c <= a.nc && i < min(cc, (uint32_t)kCand)) {
+            int dup = -1;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t w = (uint32_t)(2 * q + h);
-            if (w >= 1 && w <= n) {
-                const uint64_t x = pc[r][h];
-                raw_append(a, sl, c0, x, x / kChunk / kTileChunks != sc / kTileChunks);
+            for (int j = kCand - 1; j >= 0; --j)
+                if ((uint32_t)j < i && cs[j] == x) dup = j;   // the first earlier slot with x
+            if (dup >= 0) {
+                a.link[s] = kDupLink;
+                a.ncnt[s] = 0;
+                if (a.ext[s]) a.ext[c * kCand + dup] = 1;
+            } else {
+                const uint64_t B = c * kChunk;
+                uint32_t cnt = 0;
+                // the walk's first kList frames, for K4 (read only if this node is the
+                // chunk's true entry and its walk has at most kList frames)
+                uint64_t* fl = a.flist + (c * kListSlots + (i < (uint32_t)kListSlots ? i : 0)) * kList;
+                const bool rec = i < (uint32_t)kListSlots;
+                const uint64_t v = x - B < kChunk
+                                       ? walk_frames<false>(a, B, nullptr, x, kWalkHops,
+                                                            [&](uint64_t p, uint32_t key, uint8_t b0) {
+                                                                if (rec && cnt < (uint32_t)kList)
+                                                                    fl[cnt] = (p - B) | (uint64_t)b0 << 16 |
+                                                                              (uint64_t)key << 32;
+                                                                ++cnt;
+                                                            })
+                                       : term(kEnd, x);   // x == len on a chunk edge
+                if (v == 0) {
+                    queue[atomicAdd(&nq, 1)] = (uint32_t)s;
+                } else {
+                    a.anq[s] = ~0u;
+                    link_node(a, s, x, v, cnt);
+                }
             }
-        }
-    }
-    if (fown && fc) {
-        const uint32_t m = fc < (uint32_t)kFar ? fc : (uint32_t)kFar;
-#pragma unroll
-        for (int j = 0; j < kFar; ++j)
-            if ((uint32_t)j < m) {
-                const uint64_t x = fw[j / 2][j & 1];
-                raw_append(a, sl, c0, x & ~kExtBit, (x & kExtBit) != 0);
-            }
-        a.fcount[cf] = 0;   // the next call's K1 appends from zero (K2 is the only reader)
-    }
-    // lists longer than the first trip took (non-strict streams now and then): the rest of them
-    const bool longer = tid < kSrc && sl.srcn[tid] >= (uint32_t)(2 * kSrcFirst);
-    if (__syncthreads_or(longer)) {
-        constexpr int kRest = kXL / 2 - kSrcFirst;
-        for (int p = tid; p < kSrc * kRest; p += kScanT) {
-            const int si = p / kRest, q = kSrcFirst + p % kRest;
-            const uint32_t n = sl.srcn[si];
-            if ((uint32_t)(2 * q) > n) continue;
-            const uint64_t sc = (uint64_t)(s_lo + si);
-            const u64x2 v = *(const NETC_GLOBAL u64x2*)(a.xl + sc * kXL + 2 * q);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const uint32_t w = (uint32_t)(2 * q + h);
-                if (w <= n) raw_append(a, sl, c0, v[h], v[h] / kChunk / kTileChunks != sc / kTileChunks);
-            }
-        }
-    }
-    __syncthreads();
-    // ---- distinct candidates: a repeated position merges into its first copy
-    for (int e = tid; e < kBlkChunks * kRaw; e += kScanT) {
-        const int u = e / kRaw, j = e % kRaw;
-        const uint32_t n = min(sl.nraw[u], (uint32_t)kRaw);
-        if ((uint32_t)j >= n) continue;
-        const uint64_t xe = sl.g.raw[u][j], x = xe & ~kExtBit;
-        int f = j;
-        for (int i = 0; i < j; ++i)
-            if ((sl.g.raw[u][i] & ~kExtBit) == x) {
-                f = i;
-                break;
-            }
-        if (f < j) {
-            if (xe & kExtBit) sl.g.dupext[u][f] = 1;
-        } else {
-            sl.g.work[atomicAdd(&sl.nwork, 1u)] = (uint16_t)e;
         }
     }
     __syncthreads();
     SCAN_STAMP(1, 1);
-    // ---- prune + walk: one thread per distinct candidate
-    const uint32_t nwork = sl.nwork;
-    for (uint32_t wi = (uint32_t)tid; wi < nwork; wi += kScanT) {
-        const uint32_t e = sl.g.work[wi];
-        const int u = (int)(e / kRaw), j = (int)(e % kRaw);
-        const uint64_t xe = sl.g.raw[u][j], x = xe & ~kExtBit;
-        const bool ext = (xe & kExtBit) != 0 || sl.g.dupext[u][j] != 0;
-        const uint64_t c = c0 + (uint64_t)u, B = c * kChunk;
-        uint32_t key0;
-        uint8_t b00;
-        const uint64_t v0 = parse_at(a, x, window_global(a, x), &key0, &b00);
-        // pruned: no chain enters here -- except at the stream start, where a rejected first
-        // header is the chain's (dead) end and the scan's result
-        if ((v0 & kTerm) && term_type(v0) == kDead && term_pos(v0) == x && x != a.start) continue;
-        const uint32_t k = atomicAdd(&sl.nnode[u], 1u);
-        if (k >= (uint32_t)kCand) {
-            atomicOr(a.ovf, kOvfBucket);
-            continue;
-        }
-        const uint64_t s = c * kCand + k;
-        a.cand[s] = x;
-        if (ext) sl.extf[u][k] = 1;
-        uint32_t cnt = 0;
-        // the walk's first kList frames, for K4 (read only if this node is the chunk's true
-        // entry and its walk has at most kList of them)
-        uint64_t* fl = a.flist + (c * kListSlots + (k < (uint32_t)kListSlots ? k : 0)) * kList;
-        const bool rec = k < (uint32_t)kListSlots;
-        auto emit = [&](uint64_t p, uint32_t key, uint8_t b0) {
-            if (rec && cnt < (uint32_t)kList) fl[cnt] = (p - B) | (uint64_t)b0 << 16 | (uint64_t)key << 32;
-            ++cnt;
-        };
-        uint64_t v = v0;
-        if (!(v0 & kTerm)) {   // the header at x is a frame: on from its successor
-            emit(x, key0, b00);
-            v = walk_frames<false>(a, B, nullptr, v0, kWalkHops - 1, emit);
-        }
-        if (v == 0) {   // more than kWalkHops frames in the chunk: the block finishes it below
-            const int q = atomicAdd(&nq, 1);
-            sl.queue[q] = (uint32_t)s;
-            sl.qpos[q] = (uint16_t)(x - B);
-        } else {
-            a.anq[s] = ~0u;
-            a.nterm[s] = v;
-            a.ncnt[s] = cnt;
-        }
-    }
-    __syncthreads();
-    if (tid < kBlkChunks && c0 + (uint64_t)tid <= a.nc) {
-        const uint64_t c = c0 + (uint64_t)tid;
-        a.ccount[c] = min(sl.nnode[tid], (uint32_t)kCand);
-        *(uint64_t*)(a.ext + c * kCand) = *(const uint64_t*)sl.extf[tid];   // kCand == 8 flag bytes
-    }
-    SCAN_STAMP(1, 2);
     const int n = nq;
     for (int qi = 0; qi < n; ++qi) {
-        const uint64_t node = sl.queue[qi], chunk = node / kCand, B = chunk * kChunk;
+        const uint64_t node = queue[qi], chunk = node / kCand, B = chunk * kChunk;
         load_chunk(a, B, words);
         chunk_links16(a, B, words, l1, lj, lk16);
         const uint16_t* l8 = lj;   // the 8-hop links (the pass before the last)
         if (tid == 0) {
-            const uint64_t x = B + sl.qpos[qi];   // in [B, B + kChunk): the walk above started there
+            const uint64_t x = a.cand[node];   // in [B, B + kChunk): the walk above started there
             uint32_t p = (uint32_t)(x - B), hops = 0;
             // the walk's positions every 8 frames are K4's anchors if this node turns out
             // to be its chunk's true entry: kept in the block's slots while they last
@@ -1061,8 +888,7 @@ __device__ void links_body(const ScanArgs& a, LinksLds& sl) {
                 v = term(kExit, v);
                 ++hops;
             }
-            a.nterm[node] = v;
-            a.ncnt[node] = hops;
+            link_node(a, node, x, v, hops);
         }
         __syncthreads();
     }
@@ -1170,15 +996,12 @@ __device__ void rank_tile_fast(uint16_t* P, uint16_t* L, uint32_t* W, uint32_t* 
 }
 
 struct TilesLds {
+    uint16_t cid[kTileSlots];   // tile slot -> compact node
     uint16_t gsl[kTileSlots];   // compact node -> tile slot
     uint16_t P[kTileSlots];     // current jump (compact), kNone: at the last node
     uint16_t L[kTileSlots];     // last node reached
     uint32_t W[kTileSlots];     // frames from the node to L's exit
     uint32_t bits[kTileSlots];
-    uint32_t cpos[kTileSlots];  // the node's position - the tile's first byte
-    uint64_t cterm[kTileSlots]; // the node's terminal (K2)
-    uint16_t cfirst[kTileChunks];   // the chunk's first compact node
-    uint8_t ccn[kTileChunks];       // ... and its node count
     uint16_t P2[kFastNodes], L2[kFastNodes];   // rank_tile_fast: the ping-pong halves
     uint32_t W2[kFastNodes];
     uint16_t elist[kExt];
@@ -1186,12 +1009,8 @@ struct TilesLds {
     int skip;
 };
 
-// K3a.  Links are resolved by position (round 4): a node's terminal is an exit to a position
-// y; inside the tile the node at y is found among the nodes of y's chunk in LDS, outside it
-// (an external link, K3b's business) in the target chunk's node list in global memory, for
-// the tile's path ends only.  No node at y: the chain dies there (K2 pruned y because its
-// header fails the filter; a candidate dropped for capacity sets an overflow bit instead).
 __device__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
+    uint16_t* cid = st.cid;
     uint16_t* gsl = st.gsl;
     uint16_t* P = st.P;
     uint16_t* L = st.L;
@@ -1207,25 +1026,27 @@ __device__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
     // overflow: K4 walks serially.  Read once for the block (another tile may set it
     // meanwhile), in the same trip as the chunk data below; checked after the scans
     const uint32_t ovf0 = t == 0 ? __hip_atomic_load(a.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    const uint64_t c = tile * kTileChunks + t, s0 = tile * kTileSlots, tB = tile * kTileChunks * kChunk;
-    // the chunk's node count, external flags, positions, terminals and counts in one trip
+    const uint64_t c = tile * kTileChunks + t, s0 = tile * kTileSlots;
+    // the chunk's counter, external flags, links and counts in one trip
     const bool live = c <= a.nc;
     const uint32_t cnt = live ? min(a.ccount[c], (uint32_t)kCand) : 0;
     const uint64_t exf = live ? *(const uint64_t*)(a.ext + c * kCand) : 0;   // kCand == 8 flag bytes
-    uint64_t cds[kCand], nts[kCand];
+    int32_t lks[kCand];
     uint32_t nws[kCand];
+    uint32_t rootm = 0;   // the slot holding the stream start
 #pragma unroll
     for (int j = 0; j < kCand; ++j) {
-        cds[j] = live ? a.cand[c * kCand + j] : 0;
-        nts[j] = live ? a.nterm[c * kCand + j] : 0;
+        lks[j] = live ? a.link[c * kCand + j] : kDupLink;
         nws[j] = live ? a.ncnt[c * kCand + j] : 0;
     }
-    uint32_t rootm = 0, extm = 0;   // the slot holding the stream start; the external slots
+    if (live && c == a.start / kChunk) {   // only the stream start's chunk holds the root
 #pragma unroll
-    for (int j = 0; j < kCand; ++j) {
-        if ((uint32_t)j < cnt && cds[j] == a.start) rootm |= 1u << j;
-        if ((uint32_t)j < cnt && ((exf >> (8 * j)) & 0xFF)) extm |= 1u << j;
+        for (int j = 0; j < kCand; ++j) rootm |= (a.cand[c * kCand + j] == a.start ? 1u : 0u) << j;
     }
+    uint32_t extm = 0;
+#pragma unroll
+    for (int j = 0; j < kCand; ++j)
+        if ((uint32_t)j < cnt && ((exf >> (8 * j)) & 0xFF) && lks[j] != kDupLink) extm |= 1u << j;
     uint64_t V64, E64;
     const uint32_t base = (uint32_t)block_scan<kScanT>(cnt, &V64);
     if (t == 0) skip = ovf0 != 0;
@@ -1238,16 +1059,18 @@ __device__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
     }
     const int V = (int)V64, E = (int)E64;
     SCAN_VALUE(2, 5, V);
-    st.cfirst[t] = (uint16_t)base;
-    st.ccn[t] = (uint8_t)cnt;
+    for (uint32_t i = 0; i < cnt; ++i) {
+        cid[t * kCand + i] = (uint16_t)(base + i);
+        gsl[base + i] = (uint16_t)(t * kCand + i);
+    }
+    __syncthreads();
 #pragma unroll
     for (int i = 0; i < kCand; ++i) {
         if ((uint32_t)i >= cnt) break;
         const uint32_t k = base + i;
-        gsl[k] = (uint16_t)(t * kCand + i);
-        st.cpos[k] = (uint32_t)(cds[i] - tB);
-        st.cterm[k] = nts[i];
-        W[k] = nws[i];
+        const int32_t lk = lks[i];
+        P[k] = (lk >= 0 && (uint64_t)lk - s0 < kTileSlots) ? cid[(uint64_t)lk - s0] : kNone;
+        W[k] = lk == kDupLink ? 0u : nws[i];
         L[k] = (uint16_t)k;
         if ((extm >> i) & 1) {
             bits[k] = 1u << eidx;
@@ -1257,24 +1080,6 @@ __device__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
         } else {
             bits[k] = 0;
         }
-    }
-    __syncthreads();
-    // local links: the node at the exit position, among the nodes of its chunk
-#pragma unroll
-    for (int i = 0; i < kCand; ++i) {
-        if ((uint32_t)i >= cnt) break;
-        const uint64_t v = nts[i];
-        uint16_t pk = kNone;
-        if ((v & kTerm) && term_type(v) == kExit) {
-            const uint64_t y = term_pos(v);
-            if (y >= tB && y - tB < kTileChunks * kChunk) {
-                const uint32_t yo = (uint32_t)(y - tB), u2 = yo / (uint32_t)kChunk;
-                const uint32_t f = st.cfirst[u2], n2 = st.ccn[u2];
-                for (uint32_t m = f; m < f + n2; ++m)
-                    if (st.cpos[m] == yo) pk = (uint16_t)m;
-            }
-        }
-        P[base + i] = pk;
     }
     __syncthreads();
     SCAN_STAMP(2, 3);
@@ -1322,28 +1127,13 @@ __device__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
     }
     if (t < E) {
         const uint32_t k = elist[t];
-        const uint32_t last = L[k];
-        const uint64_t v = st.cterm[last];
-        // the path's end: an exit to another tile links to the node at that position there
-        int32_t xl = -1;
-        if ((v & kTerm) && term_type(v) == kExit) {
-            const uint64_t y = term_pos(v), t2 = y / kChunk;
-            if (t2 / kTileChunks != tile && t2 <= a.nc) {
-                const uint32_t n2 = min(a.ccount[t2], (uint32_t)kCand);
-                uint64_t cd2[kCand];
-#pragma unroll
-                for (int j = 0; j < kCand; ++j) cd2[j] = a.cand[t2 * kCand + j];
-#pragma unroll
-                for (int j = kCand - 1; j >= 0; --j)
-                    if ((uint32_t)j < n2 && cd2[j] == y) xl = (int32_t)(t2 * kCand + j);
-            }
-        }
+        const uint64_t last = s0 + gsl[L[k]];
         TileExt e;
         e.slot = (uint32_t)(s0 + gsl[k]);
         e.w = W[k];
-        e.xl = xl;
+        e.xl = a.link[last];
         e.root = eroot[t];
-        e.term = v;
+        e.term = a.nterm[last];
         put_text(&a.text[tile * kExt + t], e);
     }
     if (t == 0) __hip_atomic_store(&a.tcount[tile], (uint32_t)E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1645,6 +1435,51 @@ __global__ __launch_bounds__(kResolveT) void scan_resolve(ScanArgs a, uint64_t t
     resolve_body<kResolveT, 1>(a, tiles, sm);
 }
 
+// K2 + K3a + K3b in one launch, for streams of up to kFuseTiles tiles: every block runs
+// K2 on its 16 chunks; the last of a tile's blocks to finish (an arrival counter per
+// tile) runs K3a for that tile, while other tiles' blocks are still in K2; the last tile
+// to finish K3a (one more counter) runs K3b over all of them.  Two launch boundaries
+// and their cold trips fewer, and K3a overlapped with K2.  Each arrival is a release
+// fence by every thread, then one atomic; the block that arrives last resets the
+// counter for the next call and acquires before reading the other blocks' results.
+// The phases' LDS share one union (36 KB: 4 blocks per CU).
+static constexpr int kFuseTiles = 512;   // 512 MiB of stream
+static constexpr int kFuseCap = 1024;    // external nodes
+union FusedLds {
+    LinksLds k2;
+    TilesLds k3a;
+    ResolveLds<kFuseTiles, kFuseCap> k3b;
+};
+
+// true in every thread of the block that arrives last at *counter (of `expect`)
+__device__ __forceinline__ bool arrive_last(uint32_t* counter, uint32_t expect, int* flag) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this thread's results (release only: no L2 invalidate)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t old = atomicAdd(counter, 1u);
+        *flag = old == expect - 1;
+        if (*flag) atomicExch(counter, 0u);   // every block has arrived: reset for the next call
+    }
+    __syncthreads();
+    const bool last = *flag != 0;
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other blocks' results
+    return last;
+}
+
+__global__ __launch_bounds__(kScanT) void scan_links_fused(ScanArgs a, uint64_t tiles, uint32_t blocks) {
+    __shared__ FusedLds sm;
+    __shared__ int flag;
+    SCAN_SCOPE(1);
+    links_body(a, sm.k2);
+    constexpr uint32_t kPerTile = (uint32_t)(kTileChunks / kBlkChunks);
+    const uint32_t tile = blockIdx.x / kPerTile;
+    const uint32_t in_tile = min(blocks - tile * kPerTile, kPerTile);
+    if (!arrive_last(a.tarr + tile, in_tile, &flag)) return;   // block-uniform
+    tiles_body(a, tile, sm.k3a);
+    if (!arrive_last(a.flags + 12, (uint32_t)tiles, &flag)) return;
+    resolve_body<kScanT, kFuseCap / kScanT>(a, tiles, sm.k3b);
+}
+
 // K3a + K3b as one launch, for streams of up to kMergeTiles tiles (the default there): every
 // block ranks its tile (K3a); the last block to arrive resolves all tiles (K3b) -- one launch
 // boundary and K3b's cold first trip fewer.  Unlike scan_links_fused this needs no release
@@ -1752,7 +1587,9 @@ __device__ __forceinline__ void put_frame(const ScanArgs& a, uint64_t k, uint64_
 // a chunk of at most kWalkHops frames is walked by that thread (header bytes from
 // global memory).  Longer ones: with K2' anchors one wavefront per chunk, lane u
 // parsing the 8 frames from anchor u; without, the whole block from LDS (16-hop links,
-// an anchor every 16 frames, thread u the 16 frames from anchor u).
+// an anchor every 16 frames, thread u the 16 frames from anchor u).  Every chunk's
+// candidate counter and external flags are zeroed here, after their last reader:
+// the next call needs no clearing launch.
 __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) {
     __shared__ uint32_t words[kWords];
     __shared__ uint16_t l1[kChunk];    // next header (local index) or kNoLink
@@ -1837,6 +1674,8 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
                                        [&](uint64_t p, uint32_t key, uint8_t b0) { put_frame(a, k++, p, key, b0); });
                 }
             }
+            a.ccount[c] = 0;
+            *(uint64_t*)(a.ext + c * kCand) = 0;   // kCand == 8 flag bytes, 8-aligned
         }
     }
     if (fb) {   // block-uniform
@@ -1946,10 +1785,10 @@ std::mutex& stream_scratch_mu() {
 }
 
 // The scratch layout for `cap` chunks (cap a multiple of kTileChunks): offsets of the
-// regions; flags and the far-list counters first -- the region every call leaves zeroed.
+// regions; flags, ccount and ext first -- the region every call leaves zeroed.
 struct Layout {
-    uint64_t flags, fcount, cleared, ccount, ext, fcand, xl, cand, nterm, ncnt, wsum, pbits, anq, anc, anc_n, flist, text,
-        tcount, tinfo, total;
+    uint64_t flags, ccount, ext, tarr, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, flist, text, tcount, tinfo,
+        total;
 };
 Layout layout_for(uint64_t cap) {
     auto align = [](uint64_t x) { return (x + 63) & ~63ull; };
@@ -1957,13 +1796,12 @@ Layout layout_for(uint64_t cap) {
     Layout l;
     uint64_t o = 0;
     l.flags = o;   o = 64;
-    l.fcount = o;  o = align(o + cap * 4);
-    l.cleared = o;
     l.ccount = o;  o = align(o + cap * 4);
     l.ext = o;     o = align(o + slots);
-    l.fcand = o;   o = align(o + cap * kFar * 8);
-    l.xl = o;      o = align(o + cap * kXL * 8);
+    l.tarr = o;    o = align(o + tiles * 4);
+    l.cleared = o;
     l.cand = o;    o = align(o + slots * 8);
+    l.link = o;    o = align(o + slots * 4);
     l.nterm = o;   o = align(o + slots * 8);
     l.ncnt = o;    o = align(o + slots * 4);
     l.wsum = o;    o = align(o + slots * 4);
@@ -2095,12 +1933,11 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.ovf = a.flags + ((s.calls & 1) ? 2 : 0);
     a.ovf_prev = a.flags + ((s.calls & 1) ? 0 : 2);
     ++s.calls;
-    a.fcount = (uint32_t*)(m + l.fcount);
-    a.fcand = (uint64_t*)(m + l.fcand);
-    a.xl = (uint64_t*)(m + l.xl);
     a.ccount = (uint32_t*)(m + l.ccount);
     a.ext = m + l.ext;
+    a.tarr = (uint32_t*)(m + l.tarr);
     a.cand = (uint64_t*)(m + l.cand);
+    a.link = (int32_t*)(m + l.link);
     a.nterm = (uint64_t*)(m + l.nterm);
     a.ncnt = (uint32_t*)(m + l.ncnt);
     a.wsum = (uint32_t*)(m + l.wsum);
@@ -2123,16 +1960,19 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     const unsigned blk = (unsigned)((chunks + kBlkChunks - 1) / kBlkChunks);
     if (len <= (128ull << 20)) hipLaunchKernelGGL(scan_exits<false>, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, stream, a);
     else hipLaunchKernelGGL(scan_exits<true>, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, stream, a);
-#if defined(NETC_SCAN_K1_ONLY)
+#if defined(NETC_SCAN_K1_ONLY) || defined(NETC_SCAN_K1_EXP)
     return hipGetLastError();   // diagnostic builds only (tools/): K1 timed alone
 #endif
     // K2, K3a, K3b: by default K2 and then K3a + K3b as one launch up to kMergeTiles (256) tiles
-    // (scan_tiles_resolve), three launches above.  NETC_GPU_KNOB_SCAN_FUSE = 0 (tests and A/B):
-    // three launches at every size.  (Round 3's K2 + K3a + K3b launch with agent-scope release
-    // arrivals -- a buffer_wbl2 sc1 per block -- measured 128 against 43 us at config 2 and is
-    // gone, profiles/r03b_scan_fuse_ab.json.)
+    // (scan_tiles_resolve), three launches above.  NETC_GPU_KNOB_SCAN_FUSE (tests and A/B):
+    // 0 three launches at every size; 1 K2 + K3a + K3b as one launch up to kFuseTiles tiles
+    // (scan_links_fused: every block's agent-scope release is a buffer_wbl2 sc1 -- a write-back
+    // of its XCD's L2 -- and at config 2 a thousand blocks arrive: 128 us against 43 us for the
+    // three launches, profiles/r03b_scan_fuse_ab.json).
     const int64_t fuse = knob(NETC_GPU_KNOB_SCAN_FUSE);
-    if (fuse != 0 && tiles <= (uint64_t)kMergeTiles) {
+    if (fuse == 1 && tiles <= (uint64_t)kFuseTiles) {
+        hipLaunchKernelGGL(scan_links_fused, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
+    } else if (fuse != 0 && tiles <= (uint64_t)kMergeTiles) {
         hipLaunchKernelGGL(scan_links, dim3(blk), dim3(kScanT), 0, stream, a);
         hipLaunchKernelGGL(scan_tiles_resolve, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a, tiles);
     } else {

@@ -309,9 +309,8 @@ def test_ranking_paths(torch_cuda, gpu_knob, fast):
 
 @pytest.mark.parametrize("strict", [True, False])
 def test_far_exits(torch_cuda, strict):
-    # frames of 64-bit lengths (> 17 chunks ahead): their exits reach K2 through the target's
-    # far list (atomics), the others through the source chunks' exit lists; both kinds mixed,
-    # and several big frames in a row (tiles entered only by far exits)
+    # frames of 64-bit lengths (exits more than a tile ahead) mixed with 7- and 16-bit ones, and
+    # several big frames in a row (tiles entered only from far away)
     rng = np.random.default_rng(61 + strict)
     sizes = np.concatenate([rng.integers(70000, 1 << 21, 60), rng.integers(0, 5000, 600), [65535, 65536, 65537]])
     rng.shuffle(sizes)
@@ -324,9 +323,10 @@ def test_far_exits(torch_cuda, strict):
 
 @pytest.mark.parametrize("fuse", ["1", "0", "-1"])
 def test_fused_and_separate_launches(torch_cuda, gpu_knob, fuse):
-    # K3a + K3b as three launches with K2 (knob SCAN_FUSE = 0, as for streams over 256 MiB) or
-    # the default, K3a + K3b as one launch (the last tile block to arrive resolves; sc1
-    # hand-off; SCAN_FUSE = 1 is the default since round 4 retired the K2 + K3 launch): the same results over
+    # K2 + K3a + K3b as one launch (knob SCAN_FUSE = 1: arrival counters per tile and per
+    # stream, the last arrival runs the next phase and re-zeroes its counter), as three
+    # (SCAN_FUSE = 0, as for streams over 512 MiB), or the default, K3a + K3b as one launch
+    # (the last tile block to arrive resolves; sc1 hand-off): the same results over
     # alternating stream sizes, the serial fallback, non-strict streams and truncations, one
     # call after another on one stream (a counter left non-zero would break the next call)
     gpu_knob("SCAN_FUSE", fuse)
