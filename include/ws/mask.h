@@ -134,6 +134,9 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *                      each block's release writes back its XCD's L2) [links, then
  *                      tiles + resolve as one launch up to 256 MiB]
  *                                                                  (NETC_SCAN_FUSE)
+ *   ENC_SRC            1 selects the source-driven frame assembly (one pass over the payload
+ *                      buffer, headers written in it; measured slower than the default
+ *                      wire-driven kernels + header fixups) [0]      (NETC_ENC_SRC)
  *   MASK_TAPER         bytes at the end of a netc_gpu_mask_batch batch walked in one-step
  *                      windows instead of two-step ones, so the launch's last waves are
  *                      short and finish together [0]               (NETC_MASK_TAPER)
@@ -145,6 +148,7 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
 #define NETC_GPU_KNOB_VAL_STEPS         5
 #define NETC_GPU_KNOB_SCAN_FUSE         6
 #define NETC_GPU_KNOB_MASK_TAPER        7
+#define NETC_GPU_KNOB_ENC_SRC           8
 int netc_gpu_knob(int knob, int64_t value);
 
 /**

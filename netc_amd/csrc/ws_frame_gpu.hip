@@ -154,6 +154,14 @@ struct EncArgs {
     uint32_t* defer_count;
     uint64_t defer_cap;
     uint32_t all_spans;        // dense batch: the compose launch takes every span (no assembly launch)
+    // source-driven assembly (encode_src_kernel)
+    const uint8_t* src_base;   // src rounded down to 16 (P coordinates: byte q of src is at P = q + smis)
+    uint64_t smis;             // src & 15
+    uint64_t nwin;             // windows of the source walk
+    double density;            // frames per payload byte (table-base guesses)
+    int32_t probe_e;           // entries of a window's first table probe (<= 64)
+    const uint32_t* keys_ld;   // keys, or any readable array when unmasked (loads are never branched around)
+    const uint8_t* b0_ld;      // b0, or any readable array when null
 };
 
 // spans per wave trip of the dense compose launch
@@ -647,6 +655,24 @@ __global__ __launch_bounds__(256, W) void encode_frames_kernel(EncArgs a) {
     }
 }
 
+typedef unsigned __int128 u128;
+
+// the low `left` (<= 16) bytes of v at w, with the widest naturally aligned stores
+__device__ __forceinline__ void put_bytes(NETC_GLOBAL uint8_t* w, u128 v, uint64_t left) {
+    uint64_t addr = (uint64_t)(uintptr_t)w;
+    while (left) {
+        const uint64_t sz = (addr & 1) || left < 2 ? 1 : (addr & 2) || left < 4 ? 2 : (addr & 4) || left < 8 ? 4 : 8;
+        NETC_GLOBAL uint8_t* q = (NETC_GLOBAL uint8_t*)addr;
+        if (sz == 8) *(NETC_GLOBAL uint64_t*)q = (uint64_t)v;
+        else if (sz == 4) *(NETC_GLOBAL uint32_t*)q = (uint32_t)v;
+        else if (sz == 2) *(NETC_GLOBAL uint16_t*)q = (uint16_t)v;
+        else *q = (uint8_t)v;
+        v >>= 8 * sz;
+        addr += sz;
+        left -= sz;
+    }
+}
+
 // Frame k's header, and its payload bytes from the header's end to the end of the
 // 16-byte wire vector the header starts in (clipped to the frame): the bytes the
 // assembly kernel leaves wrong, since it maps a whole vector through the frame that
@@ -684,22 +710,9 @@ __device__ __forceinline__ void fix_frame(const EncArgs& a, uint64_t k) {
     }
     // header then payload bytes, hl + m <= 16 of them inside one 16-byte wire vector, written
     // with the widest naturally aligned stores (at most 5, was one store per byte)
-    typedef unsigned __int128 u128;
     const u128 hmask = hl >= 16 ? ~(u128)0 : (((u128)1 << (8 * hl)) - 1);
     const u128 pay = (u128)dhi << 64 | dlo;
-    u128 v = (((u128)hi << 64 | lo) & hmask) | (hl < 16 ? pay << (8 * hl) : (u128)0);
-    uint64_t addr = (uint64_t)(uintptr_t)w, left = hl + m;
-    while (left) {
-        const uint64_t sz = (addr & 1) || left < 2 ? 1 : (addr & 2) || left < 4 ? 2 : (addr & 4) || left < 8 ? 4 : 8;
-        NETC_GLOBAL uint8_t* q = (NETC_GLOBAL uint8_t*)addr;
-        if (sz == 8) *(NETC_GLOBAL uint64_t*)q = (uint64_t)v;
-        else if (sz == 4) *(NETC_GLOBAL uint32_t*)q = (uint32_t)v;
-        else if (sz == 2) *(NETC_GLOBAL uint16_t*)q = (uint16_t)v;
-        else *q = (uint8_t)v;
-        v >>= 8 * sz;
-        addr += sz;
-        left -= sz;
-    }
+    put_bytes(w, (((u128)hi << 64 | lo) & hmask) | (hl < 16 ? pay << (8 * hl) : (u128)0), hl + m);
 }
 
 // The queued spans: each wavefront takes queue entries in turn and composes them;
@@ -745,6 +758,327 @@ __global__ __launch_bounds__(256) void encode_queued_kernel(EncArgs a) {
         const uint64_t W = A0 + 16ull * (uint64_t)lane;
         const u32x4 v = compose_vec(a, t, A0, W, lane);
         if (W < whi) store_wire<false>(a, W, v, wlo, whi);
+    }
+}
+
+// ------------------------------------------------------------ source-driven --
+// Round 4 (an A/B path, NETC_GPU_KNOB_ENC_SRC = 1 -- measured slower than the
+// wire-driven default, see launch_encode_frames): the assembly walks the SOURCE.  The wire is the payload buffer with
+// a header inserted before each frame's payload, so a wavefront takes a window of the payload
+// buffer and issues its 16-B loads at once -- their addresses need no frame table, where the
+// wire-driven kernel above could not issue a window's loads before its table resolved -- and
+// looks up the window's frames while they are in flight.  Each lane's 16 bytes then go to
+// their wire position:
+//   * inside one frame's payload (all lanes but about one per frame): one unaligned 16-B store
+//     of the bytes XOR the frame's key at its phase;
+//   * holding one frame start, at byte j (that frame's first payload byte): the lane's wire
+//     region is its 16 bytes with the frame's header (hl bytes) inserted at j -- 16 + hl
+//     contiguous bytes -- written as two overlapping 16-B stores (the bytes before j, the
+//     bytes from j on shifted by hl) and then the header's narrow stores; one lane's stores to
+//     one address land in program order, so the header overwrites what the 16-B stores left
+//     in its place;
+//   * anything else (frame starts closer than 16 bytes, empty frames, the batch's ends, a
+//     partial vector): byte-exact per lane from the frame table (src_general).
+// The lanes' regions tile the wire, so no byte is written by two lanes and the headers need
+// no launch of their own (encode_queued_kernel, one thread per frame: 8 us at config 2).
+static constexpr int64_t kPastEnd = INT64_MAX;
+
+struct SrcTable {
+    int64_t kb;        // frame index of lane 0's entry (-1: the virtual head)
+    int64_t start;     // P coordinates of the entry's payload start; -1 for the head, kPastEnd past frame n
+    uint64_t wo;       // its wire offset (header start)
+    uint32_t key, b0;
+    int64_t last;      // start of entry e - 1 (uniform)
+    bool tail;         // the entry for frame n is in the table
+    int e;             // entries held: 64, or fewer for a window's first probe (uniform)
+};
+
+// issue the table loads of frames kb .. kb + e - 1 (lanes past e - 1 re-load entry e - 1: the
+// same lines, no lane branches around a load); the values are selected in src_finish
+__device__ __forceinline__ void src_issue(const EncArgs& a, SrcTable& t, int64_t kb, int lane, int e = kWave) {
+    const int64_t n = (int64_t)a.n, v = kb + (lane < e ? lane : e - 1);
+    const int64_t vo = v < 0 ? 0 : (v > n ? n : v);
+    const int64_t vk = v < 0 ? 0 : (v >= n ? (n > 0 ? n - 1 : 0) : v);
+    const uint64_t off = gptr(a.off)[vo];
+    t.wo = gptr(a.wo)[vo];
+    t.key = gptr(a.keys_ld)[vk];   // (selected in src_finish: a branch here would drain the payload loads)
+    t.b0 = (uint32_t)gptr(a.b0_ld)[vk];
+    t.kb = kb;
+    t.e = e;
+    t.start = v < 0 ? -1 : (v <= n ? (int64_t)(off + a.smis) : kPastEnd);
+    t.tail = kb + (e - 1) >= n;
+}
+
+__device__ __forceinline__ void src_finish(const EncArgs& a, SrcTable& t) {
+    t.key = a.masked ? t.key : 0u;
+    t.b0 = a.b0 ? t.b0 : 0x82u;
+    if (t.e < kWave && (int)__lane_id() >= t.e) t.start = kPastEnd;
+    t.last = (int64_t)readlane64((uint64_t)t.start, t.e - 1);
+}
+
+__device__ __forceinline__ void src_load(const EncArgs& a, SrcTable& t, int64_t kb, int lane) {
+    src_issue(a, t, kb, lane);
+    src_finish(a, t);
+}
+
+// Largest virtual frame L whose payload starts strictly before P (-1: the head), wave-uniform:
+// a comb probe around the density's guess, then 64-ary narrowing over off[] (as ws_mask_gpu's
+// locate, with a strict bound: the frames starting AT P belong to the span from P on)
+__device__ int64_t src_locate(const EncArgs& a, uint64_t P, int lane) {
+    if (P <= a.smis) return -1;
+    const uint64_t q = P - a.smis;
+    int64_t L = -1, H = (int64_t)a.n + 1;
+    if (a.n > (uint64_t)kWave && a.src_total > 0) {
+        constexpr int64_t kStride = 16;
+        int64_t g = (int64_t)((double)q * a.density);
+        g = g > (int64_t)a.n ? (int64_t)a.n : g;
+        const int64_t base = g - 31 * kStride;
+        const int64_t idx = base + (int64_t)lane * kStride;
+        const bool valid = idx >= 0 && idx <= (int64_t)a.n;
+        const uint64_t val = valid ? gptr(a.off)[idx] : 0;
+        const uint64_t lt = __ballot(valid && val < q);
+        const uint64_t ge = __ballot(valid && val >= q);
+        if (lt) L = base + (int64_t)(63 - __builtin_clzll(lt)) * kStride;
+        if (ge) H = base + (int64_t)__builtin_ctzll(ge) * kStride;
+    }
+    while (H - L > kWave) {
+        const int64_t lo = L + 1;
+        const int64_t step = (H - lo + kWave - 1) / kWave;
+        const int64_t idx = lo + (int64_t)lane * step;
+        const bool valid = idx < H;
+        const uint64_t val = valid ? gptr(a.off)[idx] : kInf;
+        const uint64_t lt = __ballot(valid && val < q);
+        const uint64_t ge = __ballot(valid && val >= q);
+        if (lt) L = lo + (int64_t)(63 - __builtin_clzll(lt)) * step;
+        if (ge) H = lo + (int64_t)__builtin_ctzll(ge) * step;
+    }
+    return L;
+}
+
+__device__ __forceinline__ int64_t src_clamp(const EncArgs& a, int64_t g) {
+    g = g < -1 ? -1 : g;
+    return g > (int64_t)a.n ? (int64_t)a.n : g;
+}
+
+// the table base the density predicts for the window at A: the frame holding byte A - 1
+__device__ __forceinline__ int64_t src_guess(const EncArgs& a, uint64_t A) {
+    if (A <= a.smis) return -1;
+    return src_clamp(a, (int64_t)((double)(A - a.smis - 1) * a.density));
+}
+
+// make t (issued at a guessed base) bracket A: entry 0 starts before A, a later entry at or after it
+__device__ __forceinline__ void src_resolve(const EncArgs& a, SrcTable& t, uint64_t A, int lane) {
+    src_finish(a, t);
+#pragma unroll 1
+    for (int step = 0; step < 2; ++step) {
+        const uint64_t m = __ballot(t.start < (int64_t)A);
+        if (m != 0 && (t.tail || __popcll(m) < t.e)) return;
+        int64_t g;
+        if (m == 0) {   // every entry starts at or after A: step back by the distance from entry 0
+            const int64_t s0 = (int64_t)readlane64((uint64_t)t.start, 0);
+            g = t.kb - (int64_t)((double)(s0 - (int64_t)A) * a.density) - 40;
+        } else {        // every entry starts before A: step on from the last
+            g = t.kb + (t.e - 1) + (int64_t)((double)((int64_t)A - t.last) * a.density) - 24;
+        }
+        src_load(a, t, src_clamp(a, g), lane);
+    }
+    const uint64_t m = __ballot(t.start < (int64_t)A);
+    if (!(m != 0 && (t.tail || __popcll(m) < t.e))) src_load(a, t, src_locate(a, A, lane), lane);
+}
+
+__device__ __forceinline__ uint8_t vbyte(const u32x4& d, int64_t i) {
+    const uint32_t w = i < 4 ? d[0] : (i < 8 ? d[1] : (i < 12 ? d[2] : d[3]));
+    return (uint8_t)(w >> (8 * (i & 3)));
+}
+
+// The byte-exact path: every payload byte of the lane's vector [P, P + 16) (d) to its wire
+// position, and the header of every frame whose payload starts in it (empty frames too).
+// Per lane a binary search of the table (ds_bpermute) finds the last frame starting before
+// P, then the lane walks the frames starting in its 16 bytes; spans with more frames than
+// one table holds are walked in 62-entry windows (entry 62 is shared by two windows: its
+// bytes are written twice, with the same values).  act: the lane takes part.
+__device__ void src_general(const EncArgs& a, SrcTable t, uint64_t A0, int64_t P, u32x4 d, bool act, int lane) {
+    constexpr int kLast = kWave - 2;
+    const int64_t Aend = (int64_t)(A0 + kSpan);
+    const bool masked = a.masked != 0;
+    NETC_GLOBAL uint8_t* wire = gptr(a.wire_base) + a.wmis;
+    if (t.e < kWave) src_load(a, t, t.kb, lane);   // a window's first probe: the full table
+    for (;;) {
+        const bool more = !t.tail && t.last < Aend;   // wave-uniform
+        SrcTable tn;
+        if (more) src_issue(a, tn, t.kb + kLast, lane);
+        int l = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const int c = l + step;
+            const int64_t sc = (int64_t)bperm64((uint64_t)t.start, c <= kLast ? c : kLast);   // every lane takes part
+            if (c <= kLast && sc < P) l = c;
+        }
+        for (int c = l;; ++c) {
+            const int cc = c <= kLast ? c : kLast;
+            const int64_t S = (int64_t)bperm64((uint64_t)t.start, cc), Sn = (int64_t)bperm64((uint64_t)t.start, cc + 1);
+            const uint64_t wo = bperm64(t.wo, cc);
+            const uint32_t key = (uint32_t)__builtin_amdgcn_ds_bpermute(cc << 2, (int)t.key);
+            const uint32_t b0 = (uint32_t)__builtin_amdgcn_ds_bpermute(cc << 2, (int)t.b0);
+            const int64_t j = t.kb + cc;
+            const bool cont = act && c <= kLast && j < (int64_t)a.n && S < P + 16;
+            if (cont && j >= 0) {
+                const uint64_t len = (uint64_t)(Sn - S), hl = header_len(len, masked);
+                if (S >= P) {   // the frame's header: this lane holds its first payload byte (or its place)
+                    uint64_t lo, hi;
+                    build_header(b0, len, masked, key, lo, hi);
+                    put_bytes(wire + wo, (u128)hi << 64 | lo, hl);
+                }
+                const int64_t blo = S > P ? S : P, bhi = Sn < P + 16 ? Sn : P + 16;
+                for (int64_t p = blo; p < bhi; ++p)
+                    wire[wo + hl + (uint64_t)(p - S)] = vbyte(d, p - P) ^ (uint8_t)(key >> (8 * ((p - S) & 3)));
+            }
+            if (!__ballot(cont)) break;
+        }
+        if (!more) break;
+        t = tn;
+        src_finish(a, t);
+    }
+}
+
+typedef uint32_t u32x4s __attribute__((ext_vector_type(4), aligned(1)));   // unaligned 16-B store
+
+template <bool NT>
+__device__ __forceinline__ void store_u(NETC_GLOBAL uint8_t* p, u32x4 v) {
+    NETC_GLOBAL u32x4s* q = (NETC_GLOBAL u32x4s*)p;
+    if constexpr (NT) __builtin_nontemporal_store(v, q);
+    else *q = v;
+}
+
+__device__ __forceinline__ u128 as128(u32x4 v) {
+    return (u128)v[0] | (u128)v[1] << 32 | (u128)v[2] << 64 | (u128)v[3] << 96;
+}
+__device__ __forceinline__ u32x4 from128(u128 x) {
+    return u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
+}
+__device__ __forceinline__ u128 low_bytes(int64_t k) {   // bytes [0, k) set, k clamped to [0, 16]
+    return k <= 0 ? (u128)0 : (k >= 16 ? ~(u128)0 : (((u128)1 << (8 * k)) - 1));
+}
+
+// One span of the window (1 KiB of source at A0; d = the lane's 16 bytes at P).  interior:
+// d was loaded whole (every byte inside the buffer).
+template <bool NT>
+__device__ __forceinline__ void src_span(const EncArgs& a, SrcTable& t, uint64_t A0, u32x4 d, bool interior, int lane) {
+    const int64_t Aend = (int64_t)(A0 + kSpan);
+    const int64_t P = (int64_t)(A0 + 16ull * (uint64_t)lane);
+    const bool masked = a.masked != 0;
+    int lbase = __popcll(__ballot(t.start < (int64_t)A0)) - 1;
+    if (!(t.tail || t.last >= Aend) && (lbase > 0 || t.e < kWave)) {   // a full table from the span's first frame on
+        src_load(a, t, t.kb + lbase, lane);
+        lbase = __popcll(__ballot(t.start < (int64_t)A0)) - 1;
+    }
+    const uint64_t bm = __ballot(t.start >= (int64_t)A0 && t.start < Aend);
+    const int nb = __popcll(bm);
+    const bool covered = interior && lbase >= 0 && lbase + nb + 2 <= t.e - 1 && (t.tail || t.last >= Aend);
+    bool fast = false;
+    if (covered) {   // wave-uniform
+        NETC_GLOBAL uint8_t* wire = gptr(a.wire_base) + a.wmis;
+        int lp = lbase, cnt = 0;
+        for (uint64_t b = bm; b; b &= b - 1) {   // the span's frame starts (wave-uniform loop)
+            const int64_t sb = (int64_t)readlane64((uint64_t)t.start, __builtin_ctzll(b));
+            lp += sb < P ? 1 : 0;
+            cnt += (sb >= P && sb < P + 16) ? 1 : 0;
+        }
+        const int64_t f = t.kb + lp;
+        fast = cnt <= 1 && f >= 0 && f + cnt < (int64_t)a.n;
+        // the lane's frames: lp (its first byte's, or the one ending at P) and lp + 1 (the start)
+        int64_t S0, S1, S2;
+        uint64_t w0, w1;
+        uint32_t k0, k1, h1;
+        if (nb == 0) {   // one frame covers the span: read once for the wave
+            S0 = (int64_t)readlane64((uint64_t)t.start, lbase);
+            S1 = (int64_t)readlane64((uint64_t)t.start, lbase + 1);
+            S2 = S1;
+            w0 = readlane64(t.wo, lbase);
+            w1 = w0;
+            k0 = readlane32(t.key, lbase);
+            k1 = k0;
+            h1 = 0;
+        } else {
+            S0 = (int64_t)bperm64((uint64_t)t.start, lp);
+            S1 = (int64_t)bperm64((uint64_t)t.start, lp + 1);
+            S2 = (int64_t)bperm64((uint64_t)t.start, lp + 2);
+            w0 = bperm64(t.wo, lp);
+            w1 = bperm64(t.wo, lp + 1);
+            k0 = (uint32_t)__builtin_amdgcn_ds_bpermute(lp << 2, (int)t.key);
+            k1 = (uint32_t)__builtin_amdgcn_ds_bpermute((lp + 1) << 2, (int)t.key);
+            h1 = (uint32_t)__builtin_amdgcn_ds_bpermute((lp + 1) << 2, (int)t.b0);
+        }
+        if (fast) {
+            const uint64_t len0 = (uint64_t)(S1 - S0);
+            const uint32_t rk0 = rotr8(k0, (uint64_t)(P - S0));
+            u32x4 m = {rk0, rk0, rk0, rk0};
+            if (cnt == 0) {   // inside frame lp's payload
+                store_u<NT>(wire + w0 + header_len(len0, masked) + (uint64_t)(P - S0), d ^ m);
+            } else {          // frame lp + 1 starts at byte j
+                const int64_t j = S1 - P;
+                const uint64_t len1 = (uint64_t)(S2 - S1), hl = header_len(len1, masked);
+                const uint32_t rk1 = rotr8(k1, (uint64_t)(P - S1));
+                const u32x4 sel = select_from(j);
+                m = (m & ~sel) | (u32x4{rk1, rk1, rk1, rk1} & sel);
+                const u32x4 out = d ^ m;
+                NETC_GLOBAL uint8_t* R = wire + w1 - (uint64_t)j;   // the lane's wire region: 16 + hl bytes
+                // (plain stores: the header's narrow stores overwrite part of them, and a lane's
+                // stores to one address are kept in order under one cache policy)
+                if (j > 0) store_u<false>(R, out);                   // bytes before j (the rest overwritten below)
+                const u128 o = as128(out);
+                store_u<false>(R + hl, from128(((o >> (8 * hl)) & low_bytes(j - (int64_t)hl)) | (o & ~low_bytes(j))));
+                uint64_t lo, hi;
+                build_header(h1, len1, masked, k1, lo, hi);
+                put_bytes(wire + w1, (u128)hi << 64 | lo, hl);        // last: over what the stores left there
+            }
+        }
+    }
+    if (__ballot(!fast)) src_general(a, t, A0, P, d, !fast, lane);
+}
+
+// guarded load of the lane's 16 bytes at P (partial vectors at the buffer's ends): bytes
+// outside [smis, smis + src_total) read as 0 and never written
+__device__ __forceinline__ u32x4 src_guarded(const EncArgs& a, int64_t P) {
+    u32x4 v = {0, 0, 0, 0};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        const int64_t p = P + b;
+        if (p >= (int64_t)a.smis && p < (int64_t)(a.smis + a.src_total))
+            v[b >> 2] |= (uint32_t)gptr(a.src_base)[p] << (8 * (b & 3));
+    }
+    return v;
+}
+
+// One window of K KiB of the payload buffer per wavefront, a grid covering the buffer (as the
+// mask kernel's default walk): the window's loads first, the table lookup under them.
+template <int K, bool NT>
+__global__ __launch_bounds__(256) void encode_src_kernel(EncArgs a) {
+    constexpr uint64_t kWin = kSpan * K;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / kWave) +
+                          (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // uniform
+    if (wave >= a.nwin) return;
+    const uint64_t A = wave * kWin;
+    const uint64_t full_lo = a.smis ? 16 : 0, full_hi = (a.smis + a.src_total) & ~15ull;
+    const bool interior = A >= full_lo && A + kWin <= full_hi;   // wave-uniform
+    u32x4 d[K];
+    if (interior) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const NETC_GLOBAL u32x4* p = gptr(reinterpret_cast<const u32x4*>(a.src_base + A + (uint64_t)k * kSpan + 16ull * lane));
+            if constexpr (NT) d[k] = __builtin_nontemporal_load(p);
+            else d[k] = *p;
+        }
+    }
+    SrcTable t;
+    src_issue(a, t, src_guess(a, A), lane, a.probe_e);
+    src_resolve(a, t, A, lane);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t A0 = A + (uint64_t)k * kSpan;
+        const u32x4 v = interior ? d[k] : src_guarded(a, (int64_t)(A0 + 16ull * lane));
+        src_span<NT>(a, t, A0, v, interior, lane);
     }
 }
 
@@ -951,6 +1285,29 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     // rounds, profiles/r03r_enc_chunk.json) and 2 KiB above (C4 416-417 against 422-423 us).
     // 2 KiB: 7 wavefronts per SIMD up to 256 MiB (72 VGPRs), 6 above (76 VGPRs; C4 418 vs 425
     // us at 7, 424 at 8 with spills; profiles/r02k_ab_enc_occupancy.json)
+    // NETC_GPU_KNOB_ENC_SRC = 1: the source-driven walk (round 4 experiment, kept for A/B: parity
+    // green, but slower than the wire-driven kernels at both shapes measured -- config 2 35.3 us
+    // against 26.6 + 7.9 for the wire-driven kernel and the header fixups, config 4 428-438 us
+    // against 404 + 8; its unaligned 16-B stores cost ~5 % at config 4 and the per-span frame
+    // logic more than the fixup launch at config 2; profiles/r04c_encode_src_ab.json)
+    if (!a.all_spans && knob(NETC_GPU_KNOB_ENC_SRC) == 1) {
+        constexpr int K = 2;
+        constexpr uint64_t kWin = kSpan * K;
+        a.smis = (uint64_t)(uintptr_t)src & 15u;
+        a.src_base = src - a.smis;
+        a.density = (double)n / (double)src_total;
+        // + 1: the window holding P = smis + src_total writes the headers of empty frames at the end
+        a.nwin = (a.smis + src_total) / kWin + 1;
+        const double reach = (double)kWin * a.density;
+        a.probe_e = reach < (double)(kWave - 6) ? (int)reach + 6 : kWave;
+        a.keys_ld = masked ? keys : reinterpret_cast<const uint32_t*>(off);   // off[0 .. n] is readable
+        a.b0_ld = b0 ? b0 : reinterpret_cast<const uint8_t*>(off);
+        const uint64_t blocks = (a.nwin + 3) / 4;
+        if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+        if (nt) hipLaunchKernelGGL((encode_src_kernel<K, true>), dim3((unsigned)blocks), dim3(256), 0, stream, a);
+        else hipLaunchKernelGGL((encode_src_kernel<K, false>), dim3((unsigned)blocks), dim3(256), 0, stream, a);
+        return hipGetLastError();
+    }
     const bool small = wire_bound <= (256ull << 20);
     if (cfg.unroll >= 8 || (cfg.unroll <= 1 && small)) return launch_enc_u<4, 5>(a, wire_bound, nt, cfg.max_blocks, stream);
     if (small) return launch_enc_u<2, 7>(a, wire_bound, nt, cfg.max_blocks, stream);

@@ -1182,23 +1182,102 @@ __device__ __forceinline__ bool utf8_rule(uint32_t b3, uint32_t b2, uint32_t b1,
     return ((b1h & b1l & b2h) ^ must) != 0;
 }
 
+// the first 3 and last 3 bytes of [lo, hi) (clamped into it; bytes past a short frame's end are
+// never used) in one trip -- a load in a loop of data-dependent length was a trip per byte
+__device__ __forceinline__ void frame_edges(const uint8_t* dst, uint64_t lo, uint64_t hi, uint32_t (&fb)[3],
+                                            uint32_t (&lb)[3]) {
+    if (hi > lo) {
+        const uint64_t last = hi - 1;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            fb[d] = dst[lo + d < last ? lo + d : last];
+            lb[d] = dst[hi - lo > 3 ? hi - 3 + d : lo];   // (used only when hi - lo > 3)
+        }
+    }
+}
+
+// the first 3 bytes of every window start strictly inside [lo + 3, hi) (the bytes phase A left:
+// in place another wavefront's window held the bytes before them); the 4 bytes before and
+// after each start (aligned dwords: dst - mis is 16-aligned, window starts are multiples of
+// win >= 4096) are read for 8 windows at a time, unconditionally (a start past the frame
+// re-reads the first one; a load under a per-lane branch made the compiler wait for each one
+// in turn: 29.7 us at config 4, r03k).  win 0: no seams to check.
+__device__ __forceinline__ bool seams_bad(const uint8_t* dst, uint64_t lo, uint64_t hi, uint64_t mis, uint64_t win) {
+    bool bad = false;
+    const uint64_t cb0 = win ? (lo + 3 + mis + win - 1) / win * win : ~0ull;
+    for (uint64_t cb = cb0; win && cb < hi + mis && !bad; cb += 8 * win) {
+        uint32_t wb[8], wa[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint64_t c = cb + (uint64_t)i * win;
+            const uint64_t q = (c < hi + mis ? c : cb) - mis;   // q: the window's first byte
+            wb[i] = *(const NETC_GLOBAL uint32_t*)(dst + q - 4);
+            wa[i] = *(const NETC_GLOBAL uint32_t*)(dst + q);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint64_t c = cb + (uint64_t)i * win, q = c - mis;
+            const uint64_t w = (uint64_t)wa[i] << 32 | wb[i];   // bytes q - 4 .. q + 3
+            auto B = [&](int j) { return (uint32_t)(w >> (8 * j)) & 0xFFu; };
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+                if (c < hi + mis && q + d >= lo + 3 && q + d < hi) bad |= utf8_rule(B(1 + d), B(2 + d), B(3 + d), B(4 + d));
+        }
+    }
+    return bad;
+}
+
+// Phase B of the TEXT check: one thread per frame.  Everything a single-frame TEXT message (FIN
+// and opcode 1: config 2's frames) needs -- its header byte, flag, offsets -- comes in one trip,
+// its first and last 3 bytes in a second (round 4: the message walk took four dependent trips
+// for it, 6.6 us at config 2); the thread of a FIN continuation frame walks back to its
+// message's first frame and, for a TEXT message, forward again over its data frames (control
+// frames skipped).  Any frame flagged by phase A fails the message; the first 3 bytes of every
+// frame are checked here with the 3 bytes before them in the message; the message must not end
+// inside a sequence.
 __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uint8_t* h0, uint64_t n,
                               const uint8_t* verr, uint8_t tag, uint64_t mis, uint64_t win, uint8_t* valid) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
+    const uint32_t hk = h0[k];
+    const uint8_t fk = verr[k];
+    const uint64_t lk = off[k], hk_end = off[k + 1];
     uint8_t verdict = 1;
-    const uint32_t opk = h0[k] & 0x0F;
-    if (opk <= 2 && (h0[k] & 0x80)) {
-        // the message's first frame
+    const uint32_t opk = hk & 0x0F;
+    if ((hk & 0x80) && opk == 1) {
+        // a single-frame TEXT message
+        bool bad = fk == tag;
+        uint32_t fb[3] = {0, 0, 0}, lb[3] = {0, 0, 0};
+        frame_edges(dst, lk, hk_end, fb, lb);
+        uint32_t h1 = 0, h2 = 0, h3 = 0;   // the last 3 bytes of the message so far (h1 = last)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            if (lk + d < hk_end) {
+                bad |= utf8_rule(h3, h2, h1, fb[d]);
+                h3 = h2;
+                h2 = h1;
+                h1 = fb[d];
+            }
+        }
+        if (hk_end - lk > 3) {
+            h3 = lb[0];
+            h2 = lb[1];
+            h1 = lb[2];
+        }
+        if (h1 >= 0xC0 || h2 >= 0xE0 || h3 >= 0xF0) bad = true;   // ends inside a sequence
+        if (!bad) bad = seams_bad(dst, lk, hk_end, mis, win);
+        verdict = bad ? 0 : 1;
+    } else if ((hk & 0x80) && opk == 0) {
+        // the last frame of a fragmented message: its first frame
         int64_t first = -1;
-        for (int64_t j = (int64_t)k; j >= 0; --j) {
+        for (int64_t j = (int64_t)k - 1; j >= 0; --j) {
             const uint32_t op = h0[j] & 0x0F;
             if (op >= 8) continue;                              // control frame inside the message
             if (op != 0) {
                 first = j;
                 break;
             }
-            if (j != (int64_t)k && (h0[j] & 0x80)) break;       // a finished message: orphan continuation
+            if (h0[j] & 0x80) break;                            // a finished message: orphan continuation
         }
         if (first >= 0 && (h0[first] & 0x0F) == 1) {
             uint32_t h1 = 0, h2 = 0, h3 = 0;   // the last 3 bytes of the message so far (h1 = last)
@@ -1207,17 +1286,8 @@ __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uin
                 if ((h0[j] & 0x0F) >= 8) continue;
                 if (verr[j] == tag) bad = true;
                 const uint64_t lo = off[j], hi = off[j + 1];
-                // the frame's first and last 3 bytes in one trip (clamped into the frame; a
-                // load in a loop of data-dependent length was a trip per byte)
                 uint32_t fb[3] = {0, 0, 0}, lb[3] = {0, 0, 0};
-                if (hi > lo) {
-                    const uint64_t last = hi - 1;
-#pragma unroll
-                    for (int d = 0; d < 3; ++d) {
-                        fb[d] = dst[lo + d < last ? lo + d : last];
-                        lb[d] = dst[hi - lo > 3 ? hi - 3 + d : lo];   // (used only when hi - lo > 3)
-                    }
-                }
+                frame_edges(dst, lo, hi, fb, lb);
 #pragma unroll
                 for (int d = 0; d < 3; ++d) {
                     if (lo + d < hi) {
@@ -1227,37 +1297,7 @@ __global__ void utf8_messages(const uint8_t* dst, const uint64_t* off, const uin
                         h1 = fb[d];
                     }
                 }
-                // the first 3 bytes of every chunk inside the frame, which phase A skips
-                // (in place, another wavefront's chunk held the bytes before them).  The
-                // 4 bytes before and after each chunk start (aligned dwords: dst - mis is
-                // 16-aligned, chunk starts are multiples of win >= 4096) are read for 8
-                // chunks at a time -- one at a time, a 64 KiB frame's 16 seams were 16
-                // round trips to memory in a row.  The 16 loads are unconditional (a chunk
-                // start past the frame re-reads the first one; bytes at or past hi are read
-                // but never used -- an aligned dword holding a byte of the buffer lies in
-                // that byte's page): a load under a per-lane branch made the compiler wait
-                // for each one in turn (29.7 us at config 4, r03k).
-                const uint64_t cb0 = win ? (lo + 3 + mis + win - 1) / win * win : ~0ull;   // win 0: no seams to check
-                for (uint64_t cb = cb0; win && cb < hi + mis && !bad; cb += 8 * win) {
-                    uint32_t wb[8], wa[8];
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const uint64_t c = cb + (uint64_t)i * win;
-                        const uint64_t q = (c < hi + mis ? c : cb) - mis;   // q: the chunk's first byte
-                        wb[i] = *(const NETC_GLOBAL uint32_t*)(dst + q - 4);
-                        wa[i] = *(const NETC_GLOBAL uint32_t*)(dst + q);
-                    }
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const uint64_t c = cb + (uint64_t)i * win, q = c - mis;
-                        const uint64_t w = (uint64_t)wa[i] << 32 | wb[i];   // bytes q - 4 .. q + 3
-                        auto B = [&](int j) { return (uint32_t)(w >> (8 * j)) & 0xFFu; };
-#pragma unroll
-                        for (int d = 0; d < 3; ++d)
-                            if (c < hi + mis && q + d >= lo + 3 && q + d < hi)
-                                bad |= utf8_rule(B(1 + d), B(2 + d), B(3 + d), B(4 + d));
-                    }
-                }
+                bad |= seams_bad(dst, lo, hi, mis, win);
                 if (hi - lo > 3) {   // the frame's own last 3 bytes become the history
                     h3 = lb[0];
                     h2 = lb[1];

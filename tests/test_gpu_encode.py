@@ -73,8 +73,15 @@ def _payload(rng, n):
     return rng.integers(0, 256, n, dtype=np.uint8)
 
 
+# the assembly path: None = the default (wire-driven kernels + per-frame header fixups), "1" =
+# the source-driven walk writing headers in the same pass (NETC_GPU_KNOB_ENC_SRC, A/B path)
+PATHS = [None, "1"]
+
+
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("masked", [True, False])
-def test_every_length_class(torch_cuda, masked):
+def test_every_length_class(torch_cuda, gpu_knob, masked, path):
+    gpu_knob("ENC_SRC", path)
     rng = np.random.default_rng(11)
     sizes = EDGE_SIZES + EDGE_SIZES[::-1]
     off = frames_from_sizes(sizes)
@@ -84,9 +91,11 @@ def test_every_length_class(torch_cuda, masked):
     run_encode(torch_cuda, payload, off, keys, masked=masked)
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("wire_shift", [0, 1, 3, 7, 8, 13, 15])
 @pytest.mark.parametrize("src_shift", [0, 5, 12])
-def test_alignments(torch_cuda, wire_shift, src_shift):
+def test_alignments(torch_cuda, gpu_knob, wire_shift, src_shift, path):
+    gpu_knob("ENC_SRC", path)
     rng = np.random.default_rng(100 + wire_shift * 16 + src_shift)
     sizes = rng.integers(0, 3000, 300)
     off = frames_from_sizes(sizes)
@@ -120,8 +129,10 @@ def test_tiny_frames_many_per_span(torch_cuda):
         run_encode(torch_cuda, payload, off, keys, masked=masked, wire_shift=3)
 
 
-def test_payload_with_unframed_prefix(torch_cuda):
+@pytest.mark.parametrize("path", PATHS)
+def test_payload_with_unframed_prefix(torch_cuda, gpu_knob, path):
     # frames need not start at payload byte 0: off[0] > 0 (bytes before it are not sent)
+    gpu_knob("ENC_SRC", path)
     rng = np.random.default_rng(12)
     sizes = rng.integers(0, 2000, 50)
     off = frames_from_sizes(sizes, start=777)
@@ -137,6 +148,30 @@ def test_single_frame_sizes(torch_cuda):
         payload = _payload(rng, size)
         keys = np.array([0x3D21FA37], dtype=np.uint32)
         run_encode(torch_cuda, payload, off, keys)
+        run_encode(torch_cuda, payload, off, keys, wire_shift=7, src_shift=3)
+
+
+@pytest.mark.parametrize("path", PATHS)
+@pytest.mark.parametrize("src_shift", [0, 9])
+def test_frame_starts_at_every_lane_byte(torch_cuda, gpu_knob, src_shift, path):
+    # the source-driven lanes: a frame start at each byte j of a lane's 16 (one start per lane:
+    # two overlapping 16-B stores + the header), two starts in one lane (frames of 1..15 B),
+    # empty frames between long ones, and the batch ending on, inside and after a vector edge
+    gpu_knob("ENC_SRC", path)
+    rng = np.random.default_rng(77 + src_shift)
+    sizes = []
+    for j in range(16):
+        sizes += [1024 + j, 1000 - j, 17, 40 + j]
+    sizes += [5, 9, 0, 0, 300, 0, 2048, 3, 15, 16, 1, 4000]
+    for tail in (0, 1, 15, 16, 33):
+        sz = sizes + [tail]
+        off = frames_from_sizes(sz)
+        payload = _payload(rng, int(off[-1]))
+        keys = rng.integers(0, 2**32, len(sz), dtype=np.uint64).astype(np.uint32)
+        h0 = rng.choice(np.array([0x81, 0x82, 0x01, 0x00, 0x80, 0x89], dtype=np.uint8), len(sz))
+        for wire_shift in (0, 11):
+            run_encode(torch_cuda, payload, off, keys, header0=h0, wire_shift=wire_shift, src_shift=src_shift)
+        run_encode(torch_cuda, payload, off, keys, masked=False, src_shift=src_shift)
 
 
 def test_rfc6455_hello(torch_cuda):
@@ -164,8 +199,10 @@ def test_empty_batch(torch_cuda):
     assert int(wo.cpu()[0]) == 0
 
 
-def test_c2_full_size(torch_cuda):
+@pytest.mark.parametrize("path", PATHS)
+def test_c2_full_size(torch_cuda, gpu_knob, path):
     # config 2 shape: 65,536 x 1 KiB frames, independent keys
+    gpu_knob("ENC_SRC", path)
     rng = np.random.default_rng(0x6E657463)
     n = 65536
     off = frames_from_sizes(np.full(n, 1024))
@@ -174,8 +211,10 @@ def test_c2_full_size(torch_cuda):
     run_encode(torch_cuda, payload, off, keys)
 
 
-def test_mixed_64mib(torch_cuda):
+@pytest.mark.parametrize("path", PATHS)
+def test_mixed_64mib(torch_cuda, gpu_knob, path):
     # config 4 shape (sizes uniform in [256, 65536], unaligned), 64 MiB
+    gpu_knob("ENC_SRC", path)
     rng = np.random.default_rng(44)
     sizes = rng.integers(256, 65537, 4096)
     off = frames_from_sizes(sizes)
@@ -218,13 +257,15 @@ def test_launch_shapes(torch_cuda, unroll, max_blocks):
         nm.tune()
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("dense", ["0", "100000"])
 @pytest.mark.parametrize("masked", [True, False])
-def test_both_compose_paths(torch_cuda, gpu_knob, dense, masked):
+def test_both_compose_paths(torch_cuda, gpu_knob, dense, masked, path):
     # the same batches through the vector path + queued compose (knob ENC_DENSE_BYTES = 0)
     # and through the dense per-lane compose of every span (threshold above any mean):
     # uniform 16 / 8 / 1 B frames, empty frames, 0..30 B mixes, and long frames between
     gpu_knob("ENC_DENSE_BYTES", dense)
+    gpu_knob("ENC_SRC", path)
     rng = np.random.default_rng(21)
     parts = [np.full(3000, 16), np.full(2000, 8), rng.integers(0, 31, 4000), np.full(1500, 1),
              np.array([126, 65536, 0, 0, 125, 3000]), np.zeros(700, dtype=np.int64), rng.integers(100, 300, 200)]

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round-4 A/B pass for the rewritten frame scan and frame assembly (through gpurun, from the
+# repo root): their GPU suites on the new build, then tools/bench_scan.py and
+# tools/bench_encode.py alternating abl/libnetc_ws_gpu_prev.so (the round-3 kernels, built
+# before the change) and the new library.   TAG=... bash tools/gpu_r04b.sh
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+T=${TAG:-r04b}
+mkdir -p gpurun_out/$T
+ln -sf ../netc_amd/lib/libnetc.so abl/libnetc.so
+timeout -k 10 800 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu ${SUITES:-tests/test_gpu_scan.py tests/test_gpu_encode.py tests/test_gpu_ingest.py tests/test_gpu_epoll.py} > gpurun_out/$T/tests.log 2>&1 || { echo TESTFAIL; grep -E "FAILED|Error|assert" gpurun_out/$T/tests.log | head -30; tail -40 gpurun_out/$T/tests.log; exit 1; }
+tail -2 gpurun_out/$T/tests.log
+[ "${AB:-1}" = 0 ] && exit 0
+LIBS="abl/libnetc_ws_gpu_prev.so netc_amd/lib/libnetc_ws_gpu.so" TOOL="tools/bench_scan.py --steps 50" ROUNDS=2 bash tools/gpu_ab_libs.sh ${T}_scan || exit 1
+LIBS="abl/libnetc_ws_gpu_prev.so netc_amd/lib/libnetc_ws_gpu.so" TOOL="tools/bench_scan.py --steps 50 --non-strict" ROUNDS=1 bash tools/gpu_ab_libs.sh ${T}_scan_ns || exit 1
+LIBS="abl/libnetc_ws_gpu_prev.so netc_amd/lib/libnetc_ws_gpu.so" TOOL="tools/bench_encode.py --steps 50 --unroll 1" ROUNDS=2 bash tools/gpu_ab_libs.sh ${T}_enc || exit 1
+echo all done
