@@ -18,15 +18,15 @@ HIPFLAGS   ?= -O3 -g -fPIC -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-r
 
 HOST_SRCS  := $(wildcard netc_amd/csrc/host/*.c)
 HOST_HDRS  := $(wildcard include/*.h include/*/*.h)
-GPU_SRCS   := netc_amd/csrc/ws_mask_gpu.hip netc_amd/csrc/ws_frame_gpu.hip netc_amd/csrc/ws_scan_gpu.hip netc_amd/csrc/ws_ingest.hip \
+GPU_SRCS   := netc_amd/csrc/ws_mask_gpu.hip netc_amd/csrc/ws_frame_gpu.hip netc_amd/csrc/ws_scan_gpu.hip netc_amd/csrc/ws_ingest.hip netc_amd/csrc/ws_egress.hip \
               netc_amd/csrc/ws_mask_api.hip
 GPU_HDRS   := netc_amd/csrc/ws_mask_gpu.h netc_amd/csrc/gpu_util.h include/ws/mask.h include/ws/frame.h include/ws/ingest.h \
-              include/ws/route.h include/ws/common.h
+              include/ws/route.h include/ws/common.h include/ws/egress.h
 
 .PHONY: all host gpu oracle diag clean asan
 all: host gpu oracle
 host: $(LIBDIR)/libnetc.so
-gpu: $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc_ceiling.so tests/bin/ws_gpu_epoll
+gpu: $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc_ceiling.so tests/bin/ws_gpu_epoll tests/bin/ws_egress_bench
 
 $(LIBDIR)/libnetc.so: $(HOST_SRCS) $(HOST_HDRS)
 	@mkdir -p $(LIBDIR)
@@ -53,11 +53,17 @@ tests/bin/ws_gpu_epoll: tests/drivers/ws_gpu_epoll.c $(LIBDIR)/libnetc_ws_gpu.so
 	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -L$(LIBDIR) -lnetc_ws_gpu -lnetc -L/opt/rocm/lib -lamdhip64 \
 	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib -lpthread
 
+# send rates of the GPU egress ring beside the CPU ws_send_message (tools/bench_egress.py)
+tests/bin/ws_egress_bench: tests/drivers/ws_egress_bench.c $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc.so $(HOST_HDRS)
+	@mkdir -p tests/bin
+	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -L$(LIBDIR) -lnetc_ws_gpu -lnetc -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib -lpthread
+
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(LIBDIR)/*.so build/*.o tests/bin/ws_gpu_epoll
+	rm -f $(LIBDIR)/*.so build/*.o tests/bin/ws_gpu_epoll tests/bin/ws_egress_bench
 	$(MAKE) -C oracle clean
 
 # diagnostics (tools/, not part of the product)

@@ -2,7 +2,8 @@
 #define NETC_WS_ROUTE_H
 
 /*
- * Per-connection receive routes for ws_parse_frame (libnetc.so).
+ * Per-connection receive routes for ws_parse_frame and send routes for
+ * ws_send_message (libnetc.so).
  *
  * netc's web layer receives a WebSocket message with one call,
  * ws_parse_frame(client, &client->ws_parsing_state, limit) (reference
@@ -17,18 +18,27 @@
  * route keep the CPU parser.  netc_ws_gpu_attach (include/ws/ingest.h) attaches
  * the GPU ingest ring this way.
  *
+ * Send routes work the same way for ws_send_message(client, message, key,
+ * num_frames) (reference src/ws/common.c:36-130): while a send route is attached
+ * to a socket, ws_send_message on it returns send_route(ctx, sockfd, message,
+ * key, num_frames) with ws_send_message's contract (1 once sent, else the failing
+ * send() result).  netc_ws_gpu_attach_send (include/ws/egress.h) attaches the GPU
+ * egress ring this way.  A socket's receive and send routes are independent.
+ *
  * Threading: attach / detach / parse of ONE socket from one thread at a time
  * (as netc drives a connection); different sockets from any threads.  A route
  * must stay valid until it is detached.
  */
 
 #include <stddef.h>
+#include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
 struct ws_frame_parsing_state;
+struct ws_message;
 
 typedef int (*netc_ws_route_fn)(void *ctx, int sockfd, struct ws_frame_parsing_state *state,
                                 size_t max_payload_length);
@@ -41,6 +51,18 @@ int netc_ws_route_detach(int sockfd);
 
 /** The route attached to sockfd, or NULL (*ctx filled when one is). */
 netc_ws_route_fn netc_ws_route_get(int sockfd, void **ctx);
+
+typedef int (*netc_ws_send_route_fn)(void *ctx, int sockfd, struct ws_message *message, uint8_t masking_key[4],
+                                     size_t num_frames);
+
+/** Route ws_send_message on sockfd to fn(ctx, ...).  0, or -1 (bad fd / null fn; errno = EINVAL / ENOMEM). */
+int netc_ws_send_route_attach(int sockfd, netc_ws_send_route_fn fn, void *ctx);
+
+/** Back to the CPU path on sockfd.  0 (also when nothing was attached), -1 on a bad fd. */
+int netc_ws_send_route_detach(int sockfd);
+
+/** The send route attached to sockfd, or NULL (*ctx filled when one is). */
+netc_ws_send_route_fn netc_ws_send_route_get(int sockfd, void **ctx);
 
 #ifdef __cplusplus
 }

@@ -137,6 +137,13 @@ static size_t encode_header(uint8_t *out, int fin, uint8_t opcode, const uint8_t
 int ws_send_message(struct web_client *client, struct ws_message *message, uint8_t masking_key[4], size_t num_frames)
 {
     const socket_t fd = client_socket(client);
+
+    /* a connection with a send route attached (include/ws/route.h: e.g. the GPU egress ring,
+       netc_ws_gpu_attach_send) is served by it, with this function's contract */
+    void *route_ctx = NULL;
+    const netc_ws_send_route_fn route = netc_ws_send_route_get((int)fd, &route_ctx);
+    if (route) return route(route_ctx, (int)fd, message, masking_key, num_frames);
+
     if (num_frames == 0) num_frames = 1;
 
     /* frame sizes as the reference (src/ws/common.c:42-49): equal split, remainder on the last frame */

@@ -1,0 +1,254 @@
+/*
+ * Host-to-socket send rates of the GPU egress ring (include/ws/egress.h) beside libnetc's CPU
+ * ws_send_message, for tools/bench_egress.py (VERDICT r3 "missing" #3).
+ *
+ * Messages of one size, each with its own key (masked, the client side) or none, from a
+ * host-resident source buffer; every leg moves the same messages:
+ *   ring_mem      netc_ws_egress_queue per message; when the ring is full the oldest finished
+ *                 slot is taken and released (a consumer that discards the wire); at the end
+ *                 submit + drain -- the ring alone, host memory to host memory
+ *   ring_socket   the same, but finished slots go out with netc_ws_egress_send on a Unix
+ *                 socketpair (a reader thread discards), flushed at the end
+ *   route_socket  libnetc's ws_send_message on a socket attached to a DEFER ring
+ *                 (netc_ws_gpu_attach_send), flushed at the end
+ *   cpu_socket    libnetc's ws_send_message on the CPU path, same socketpair
+ *   cpu_mem       the CPU path's work without the socket: header + netc_ws_mask of every frame
+ *                 into one host wire buffer
+ * One JSON line per leg on stdout.
+ *
+ * usage: ws_egress_bench MSG_BYTES TOTAL_MIB [masked 0|1] [legs: comma list, default all]
+ */
+#define _GNU_SOURCE
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "tcp/server.h"
+#include "ws/common.h"
+#include "ws/egress.h"
+#include "ws/mask.h"
+
+struct web_client_head {
+    struct tcp_client *tcp_client;
+};
+
+static double now(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+static void *drain_reader(void *arg) {
+    const int fd = *(int *)arg;
+    const size_t cap = 8u << 20;
+    char *buf = malloc(cap);
+    uint64_t *total = calloc(1, sizeof(uint64_t));
+    for (;;) {
+        const ssize_t r = recv(fd, buf, cap, 0);
+        if (r <= 0) break;
+        *total += (uint64_t)r;
+    }
+    free(buf);
+    return total;
+}
+
+struct sockpair {
+    int fd[2];
+    pthread_t th;
+};
+
+static void sp_open(struct sockpair *s) {
+    if (socketpair(AF_UNIX, SOCK_STREAM, 0, s->fd)) {
+        perror("socketpair");
+        exit(2);
+    }
+    const int sz = 8 << 20;
+    for (int i = 0; i < 2; ++i) {
+        setsockopt(s->fd[i], SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
+        setsockopt(s->fd[i], SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+    }
+    pthread_create(&s->th, NULL, drain_reader, &s->fd[1]);
+}
+
+static uint64_t sp_close(struct sockpair *s) {
+    shutdown(s->fd[0], SHUT_WR);
+    void *ret = NULL;
+    pthread_join(s->th, &ret);
+    const uint64_t got = *(uint64_t *)ret;
+    free(ret);
+    close(s->fd[0]);
+    close(s->fd[1]);
+    return got;
+}
+
+static uint64_t hdr_len(uint64_t n, int masked) { return 2 + (n <= 125 ? 0 : n <= 0xFFFF ? 2 : 8) + (masked ? 4 : 0); }
+
+static void report(const char *leg, size_t msg, uint64_t nmsg, int masked, uint64_t wire, double secs,
+                   uint64_t socket_bytes) {
+    const double pay = (double)msg * (double)nmsg;
+    printf("{\"leg\": \"%s\", \"msg_bytes\": %zu, \"messages\": %llu, \"masked\": %d, \"payload_GiBps\": %.3f, "
+           "\"wire_GBps\": %.3f, \"msgs_per_s\": %.0f, \"seconds\": %.4f, \"socket_bytes\": %llu, \"wire_bytes\": %llu}\n",
+           leg, msg, (unsigned long long)nmsg, masked, pay / secs / (1u << 30), (double)wire / secs / 1e9,
+           (double)nmsg / secs, secs, (unsigned long long)socket_bytes, (unsigned long long)wire);
+    fflush(stdout);
+}
+
+static int want(const char *legs, const char *leg) {
+    if (!legs) return 1;
+    const size_t n = strlen(leg);
+    for (const char *p = legs; (p = strstr(p, leg)); p += n)
+        if ((p == legs || p[-1] == ',') && (p[n] == 0 || p[n] == ',')) return 1;
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 3) {
+        fprintf(stderr, "usage: %s MSG_BYTES TOTAL_MIB [masked] [legs]\n", argv[0]);
+        return 2;
+    }
+    const size_t msg = (size_t)strtoull(argv[1], NULL, 0);
+    const uint64_t total = strtoull(argv[2], NULL, 0) << 20;
+    const int masked = argc > 3 ? atoi(argv[3]) : 1;
+    const char *legs = argc > 4 ? argv[4] : NULL;
+    const uint64_t nmsg = total / msg;
+    const size_t src_bytes = (size_t)(total < (64u << 20) ? total : (64u << 20));   /* reused round robin */
+    const uint64_t per_src = src_bytes / msg;
+    uint8_t *src = malloc(src_bytes);
+    uint8_t *keys = malloc(4 * per_src);
+    for (size_t i = 0; i < src_bytes; ++i) src[i] = (uint8_t)(i * 131 + (i >> 9));
+    for (uint64_t i = 0; i < 4 * per_src; ++i) keys[i] = (uint8_t)(i * 89 + 7);
+    uint64_t wire_total = 0;
+    for (uint64_t i = 0; i < nmsg; ++i) wire_total += hdr_len(msg, masked) + msg;
+
+    struct netc_ws_egress *eg = NULL;
+    int rc;
+    if ((rc = netc_ws_egress_create(&eg, 0, 0, 0, 0, 0))) {
+        fprintf(stderr, "egress create: %d %s\n", rc, netc_gpu_strerror());
+        return 1;
+    }
+    /* warm: one full pass of slots (first-touch of pinned pages, kernels loaded) */
+    for (int pass = 0; pass < 2; ++pass) {
+        const int timed = pass == 1;
+        if (!want(legs, "ring_mem") && timed) break;
+        const double t0 = now();
+        const uint64_t n = timed ? nmsg : (nmsg < 20000 ? nmsg : 20000);
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint64_t j = i % per_src;
+            rc = netc_ws_egress_queue(eg, src + j * msg, msg, WS_OPCODE_BINARY, masked ? keys + 4 * j : NULL, 1);
+            if (rc == NETC_WS_EGRESS_FULL) {
+                struct netc_ws_wire w;
+                if (netc_ws_egress_next(eg, &w, 1) != 1 || netc_ws_egress_release(eg, &w)) return 1;
+                rc = netc_ws_egress_queue(eg, src + j * msg, msg, WS_OPCODE_BINARY, masked ? keys + 4 * j : NULL, 1);
+            }
+            if (rc) {
+                fprintf(stderr, "queue: %d %s\n", rc, netc_gpu_strerror());
+                return 1;
+            }
+        }
+        if (netc_ws_egress_submit(eg)) return 1;
+        uint64_t got = 0;
+        struct netc_ws_wire w;
+        while ((rc = netc_ws_egress_next(eg, &w, 1)) == 1) {
+            got += w.len;
+            netc_ws_egress_release(eg, &w);
+        }
+        if (rc < 0) return 1;
+        if (timed) report("ring_mem", msg, nmsg, masked, wire_total, now() - t0, 0);
+    }
+    if (want(legs, "ring_socket")) {
+        struct sockpair sp;
+        sp_open(&sp);
+        const double t0 = now();
+        for (uint64_t i = 0; i < nmsg; ++i) {
+            const uint64_t j = i % per_src;
+            rc = netc_ws_egress_queue(eg, src + j * msg, msg, WS_OPCODE_BINARY, masked ? keys + 4 * j : NULL, 1);
+            if (rc == NETC_WS_EGRESS_FULL) {
+                /* the oldest slot onto the socket (waits for it), the rest when finished */
+                if (netc_ws_egress_send(eg, sp.fd[0], 0) == 0 && netc_ws_egress_send(eg, sp.fd[0], 1) < 0) return 1;
+                rc = netc_ws_egress_queue(eg, src + j * msg, msg, WS_OPCODE_BINARY, masked ? keys + 4 * j : NULL, 1);
+            }
+            if (rc) return 1;
+        }
+        if (netc_ws_egress_flush(eg, sp.fd[0]) < 0) return 1;
+        const double secs = now() - t0;
+        report("ring_socket", msg, nmsg, masked, wire_total, secs, sp_close(&sp));
+    }
+    struct tcp_client tcp;
+    struct web_client_head head = {&tcp};
+    struct ws_message m;
+    if (want(legs, "route_socket")) {
+        struct netc_ws_egress *dg = NULL;
+        if (netc_ws_egress_create(&dg, 0, 0, 0, 0, NETC_WS_EGRESS_DEFER)) return 1;
+        struct sockpair sp;
+        sp_open(&sp);
+        memset(&tcp, 0, sizeof(tcp));
+        tcp.sockfd = sp.fd[0];
+        netc_ws_gpu_attach_send(sp.fd[0], dg);
+        const double t0 = now();
+        for (uint64_t i = 0; i < nmsg; ++i) {
+            const uint64_t j = i % per_src;
+            ws_build_message(&m, WS_OPCODE_BINARY, msg, src + j * msg);
+            if (ws_send_message((struct web_client *)&head, &m, masked ? keys + 4 * j : NULL, 1) != 1) return 1;
+        }
+        if (netc_ws_egress_flush(dg, sp.fd[0]) < 0) return 1;
+        const double secs = now() - t0;
+        netc_ws_gpu_detach_send(sp.fd[0]);
+        report("route_socket", msg, nmsg, masked, wire_total, secs, sp_close(&sp));
+        netc_ws_egress_destroy(dg);
+    }
+    if (want(legs, "cpu_socket")) {
+        struct sockpair sp;
+        sp_open(&sp);
+        memset(&tcp, 0, sizeof(tcp));
+        tcp.sockfd = sp.fd[0];
+        const double t0 = now();
+        for (uint64_t i = 0; i < nmsg; ++i) {
+            const uint64_t j = i % per_src;
+            ws_build_message(&m, WS_OPCODE_BINARY, msg, src + j * msg);
+            if (ws_send_message((struct web_client *)&head, &m, masked ? keys + 4 * j : NULL, 1) != 1) return 1;
+        }
+        const double secs = now() - t0;
+        report("cpu_socket", msg, nmsg, masked, wire_total, secs, sp_close(&sp));
+    }
+    if (want(legs, "cpu_mem")) {
+        uint8_t *wire = malloc((size_t)(per_src * (hdr_len(msg, masked) + msg)));
+        const double t0 = now();
+        uint64_t w = 0;
+        for (uint64_t i = 0; i < nmsg; ++i) {
+            const uint64_t j = i % per_src;
+            if (j == 0) w = 0;
+            uint8_t *o = wire + w;
+            size_t h = 0;
+            o[h++] = 0x82;
+            const uint8_t mb = masked ? 0x80 : 0;
+            if (msg <= 125) o[h++] = (uint8_t)(mb | msg);
+            else if (msg <= 0xFFFF) {
+                o[h++] = mb | 126;
+                o[h++] = (uint8_t)(msg >> 8);
+                o[h++] = (uint8_t)msg;
+            } else {
+                o[h++] = mb | 127;
+                for (int b = 7; b >= 0; --b) o[h++] = (uint8_t)((uint64_t)msg >> (8 * b));
+            }
+            if (masked) {
+                memcpy(o + h, keys + 4 * j, 4);
+                h += 4;
+                netc_ws_mask(o + h, src + j * msg, msg, keys + 4 * j, 0);
+            } else
+                memcpy(o + h, src + j * msg, msg);
+            w += h + msg;
+        }
+        const double secs = now() - t0;
+        report("cpu_mem", msg, nmsg, masked, wire_total, secs, 0);
+        free(wire);
+    }
+    netc_ws_egress_destroy(eg);
+    free(src);
+    free(keys);
+    return 0;
+}

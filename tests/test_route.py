@@ -100,3 +100,58 @@ def test_route_rejects_bad_arguments():
         assert lib.netc_ws_route_detach(s.fileno()) == 0
     finally:
         s.close()
+
+
+SEND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_size_t)
+
+
+def test_send_route_serves_attached_socket_only():
+    """ws_send_message on a socket with a send route returns the route's result; the receive
+    route of the same socket is independent; other sockets and detached ones use the CPU path"""
+    lib = host()
+    lib.netc_ws_send_route_attach.argtypes = [ctypes.c_int, SEND_FN, ctypes.c_void_p]
+    lib.netc_ws_send_route_attach.restype = ctypes.c_int
+    lib.netc_ws_send_route_detach.argtypes = [ctypes.c_int]
+    lib.netc_ws_send_route_detach.restype = ctypes.c_int
+    lib.netc_ws_send_route_get.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    lib.netc_ws_send_route_get.restype = ctypes.c_void_p
+    from tests.wsutil import WsMessage
+    a, b = pair()
+    calls = []
+
+    def route(ctx, fd, message, key, nframes):
+        m = ctypes.cast(message, ctypes.POINTER(WsMessage)).contents
+        calls.append((ctx, fd, m.opcode, m.payload_length, bytes(ctypes.string_at(key, 4)) if key else None, nframes))
+        return 1
+
+    fn = SEND_FN(route)
+    ea = Endpoint(a)
+    payload = ctypes.create_string_buffer(b"hello", 6)
+    msg = WsMessage()
+    lib.ws_build_message(ctypes.byref(msg), 2, 5, payload)
+    key = (ctypes.c_uint8 * 4)(1, 2, 3, 4)
+    try:
+        assert lib.netc_ws_send_route_attach(a.fileno(), fn, 77) == 0
+        ctx = ctypes.c_void_p()
+        assert lib.netc_ws_send_route_get(a.fileno(), ctypes.byref(ctx)) and ctx.value == 77
+        assert not lib.netc_ws_route_get(a.fileno(), ctypes.byref(ctx))   # no receive route
+        assert lib.ws_send_message(ctypes.byref(ea.client), ctypes.byref(msg), key, 3) == 1
+        assert calls == [(77, a.fileno(), 2, 5, b"\x01\x02\x03\x04", 3)]
+        b.setblocking(False)
+        try:
+            assert b.recv(100) == b""   # nothing went out on the CPU path
+        except BlockingIOError:
+            pass
+        assert lib.netc_ws_send_route_detach(a.fileno()) == 0
+        assert not lib.netc_ws_send_route_get(a.fileno(), ctypes.byref(ctx))
+        assert lib.ws_send_message(ctypes.byref(ea.client), ctypes.byref(msg), None, 1) == 1
+        b.setblocking(True)
+        assert b.recv(100) == b"\x82\x05hello"
+        assert len(calls) == 1
+        assert lib.netc_ws_send_route_attach(-1, fn, None) == -1
+        assert lib.netc_ws_send_route_detach(-1) == -1
+    finally:
+        lib.netc_ws_send_route_detach(a.fileno())
+        a.close()
+        b.close()
