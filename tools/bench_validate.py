@@ -20,14 +20,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def valid_text(rng, off, total):
+# share of multi-byte code points per --text kind: "dense" (the default, about one character in
+# 16: every 1 KiB span of a wavefront holds some), "sparse" (one in 4,096: most spans are pure
+# ASCII), "ascii" (none: the per-span ASCII early-out takes every span)
+WIDE_SHARE = {"dense": 0.06, "sparse": 1 / 4096, "ascii": 0.0}
+
+
+def valid_text(rng, off, total, kind="dense"):
     """UTF-8 text, every frame (a one-frame TEXT message) valid on its own: JSON-like ASCII
-    with 2-, 3- and 4-byte code points (about one in 16 characters), tiled from a 1 MiB
+    with 2-, 3- and 4-byte code points (WIDE_SHARE[kind] of the characters), tiled from a 1 MiB
     sample; a code point cut by a frame edge is replaced by ASCII 'x' bytes."""
     ascii_toks = [c.encode() for c in 'abcdefghijklmnopqrstuvwxyz {}[]":,0123456789']
     wide_toks = [c.encode() for c in "éü€中😀"]
     toks = ascii_toks + wide_toks
-    p = [0.94 / len(ascii_toks)] * len(ascii_toks) + [0.06 / len(wide_toks)] * len(wide_toks)
+    w = WIDE_SHARE[kind]
+    p = [(1 - w) / len(ascii_toks)] * len(ascii_toks) + [w / len(wide_toks)] * len(wide_toks)
     pick = rng.choice(len(toks), size=1 << 20, p=p)
     sample = np.frombuffer(b"".join(toks[i] for i in pick), dtype=np.uint8)
     text = np.resize(sample, total).copy()
@@ -54,6 +61,8 @@ def valid_text(rng, off, total):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--text", default="dense", choices=sorted(WIDE_SHARE))
+    ap.add_argument("--workloads", default="c2,c4")
     args = ap.parse_args()
 
     import torch
@@ -65,10 +74,10 @@ def main():
     s = torch.cuda.Stream(dev)
     sh = s.cuda_stream
     rng = np.random.default_rng(9)
-    for wl in ("c2", "c4"):
+    for wl in args.workloads.split(","):
         off, keys, total = synth.config(wl)
         n = keys.size
-        text = valid_text(rng, off, total)
+        text = valid_text(rng, off, total, args.text)
         # 1 % of the frames (messages) broken: one 0xFF byte somewhere in the frame
         bad = rng.choice(n, size=max(1, n // 100), replace=False)
         lens = (off[bad + 1] - off[bad]).astype(np.int64)
@@ -116,7 +125,7 @@ def main():
         from oracle import oracle as orc
 
         exp = orc.validate_batch(text, off, np.full(n, 0x81, dtype=np.uint8))
-        print(json.dumps({"workload": wl, "frames": int(n), "payload_bytes": int(total),
+        print(json.dumps({"workload": wl, "text": args.text, "wide_share": WIDE_SHARE[args.text], "frames": int(n), "payload_bytes": int(total),
                           "validate_us": round(us_v, 2), "mask_only_us": round(us_m, 2),
                           "validate_GBps": round(2 * total / (us_v * 1e-6) / 1e9, 1),
                           "mask_only_GBps": round(2 * total / (us_m * 1e-6) / 1e9, 1),
