@@ -362,12 +362,16 @@ __device__ __forceinline__ Win window_global(const ScanArgs& a, uint64_t p) {
 // 0 if `hops` frames did not get there.  Windows from LDS (words, the chunk) or
 // from global memory.
 template <bool LDS, typename F>
-__device__ uint64_t walk_frames(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t e, int hops, F&& emit) {
+__device__ uint64_t walk_frames(const ScanArgs& a, uint64_t B, const uint32_t* words, uint64_t e, int hops, F&& emit,
+                                uint64_t* stop = nullptr) {
     const uint64_t Bend = B + kChunk;
     uint64_t p = e;
     for (int h = 0;; ++h) {
         if (p >= Bend) return term(kExit, p);
-        if (h == hops) return 0;
+        if (h == hops) {
+            if (stop) *stop = p;   // the next frame's header
+            return 0;
+        }
         uint32_t key;
         uint8_t b0;
         const uint64_t v = LDS ? parse_at(a, p, window_at(words, (int)(p - B)), &key, &b0)
@@ -792,20 +796,160 @@ __device__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const ui
 // links built in LDS, one thread walks them from the entry -- count / 8 + at most 7
 // hops, leaving an anchor every 8 frames -- and re-parses the last header for the exact
 // terminal.
-struct LinksLds {
+// K2's per-wavefront path for dense chunks (round 4): a node whose walk shows more than
+// kWalkHops frames in its chunk -- small frames, e.g. 16-B payloads put ~190 frames in a
+// chunk -- is finished by ONE wavefront from its own LDS instead of the whole block, so the
+// block's four wavefronts take four such chunks at once (the block path ran a block's 32
+// queued chunks one after another: 371 us of K2 at 64 MiB of 16-B frames, r04k).  Only
+// positions that pass the strict quick check can be on a chain, so the wavefront keeps them
+// compact: their sorted chunk offsets (at most kDenseCand; more, or a non-strict scan, leaves
+// the node to the block path), each one's 1-hop successor as an index into that list (a
+// bitmap of the list and a popcount), three doubling passes to 8-hop successors, then one lane walks the entry's chain
+// -- count / 8 + at most 7 hops, an anchor every 8 frames as the block path leaves them.
+static constexpr int kDenseCand = 392;   // 4 x 7.7 KB per block: K2 keeps 5 blocks per CU
+static constexpr int kProbeHops = 16;    // K2: frames walked from global memory before judging density
+struct DenseLds {
     uint32_t words[kWords];
-    uint16_t l1[kChunk];
-    uint16_t lj[kChunk];
-    uint16_t lk16[kChunk];
-    uint32_t queue[kBlkChunks * kCand];
+    uint64_t bm[kWave];         // candidate bitmap: bit u of word L <-> chunk offset 64 L + u
+    uint16_t pre[kWave];        // candidates before word L (the index of its first)
+    uint16_t pos[kDenseCand];   // candidate positions (chunk offsets), ascending
+    uint16_t s1[kDenseCand];    // 1-hop successor (index into pos), kNoLink: none in the list
+    uint16_t sa[kDenseCand];    // doubling halves; sa ends with the 8-hop successors
+    uint16_t sb[kDenseCand];
+};
+
+struct LinksLds {
+    union {
+        struct {
+            uint32_t words[kWords];
+            uint16_t l1[kChunk];
+            uint16_t lj[kChunk];
+            uint16_t lk16[kChunk];
+        } b;
+        DenseLds w[kScanT / kWave];
+    };
+    uint32_t queue[kBlkChunks * kCand];   // queued nodes; ~0u once the wavefront path took one
     int nq;
 };
 
+// the wavefront's LDS ops so far are visible to its other lanes
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// the chunk at B (+ 32 bytes, zero past len) into one wavefront's LDS words; the caller syncs
+__device__ __forceinline__ void wave_load_chunk(const ScanArgs& a, uint64_t B, uint32_t* words, int lane) {
+    typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+    if (B + kChunk + 32 <= a.len) {
+        for (int v = lane; v < kWords / 4; v += kWave) {   // 16-B loads (any alignment of the stream)
+            const u32x4 x = *(const NETC_GLOBAL u32x4u*)(a.wire + B + 16 * (uint64_t)v);
+            words[4 * v] = x[0];
+            words[4 * v + 1] = x[1];
+            words[4 * v + 2] = x[2];
+            words[4 * v + 3] = x[3];
+        }
+    } else {
+        uint8_t* bytes = (uint8_t*)words;
+        for (int i = lane; i < kWords * 4; i += kWave) bytes[i] = B + i < a.len ? gptr(a.wire)[B + i] : 0;
+    }
+}
+
+// index of chunk offset t (< kChunk) in d.pos, or kNoLink: two LDS reads and a popcount
+__device__ __forceinline__ uint16_t dense_find(const DenseLds& d, uint32_t t) {
+    const uint64_t w = d.bm[t >> 6], below = w & ((1ull << (t & 63)) - 1);
+    return (w >> (t & 63)) & 1 ? (uint16_t)(d.pre[t >> 6] + __popcll(below)) : kNoLink;
+}
+
+// One queued node by the calling wavefront (see DenseLds); false (wave-uniform, nothing
+// written) leaves it to the block path.  qi: its queue index (anchor slot as the block path).
+__device__ bool dense_node(const ScanArgs& a, DenseLds& d, uint64_t node, uint32_t qi) {
+    if (!a.strict) return false;   // every position a candidate: the block path
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
+    wave_load_chunk(a, B, d.words, lane);
+    const uint64_t x = a.cand[node];   // in [B, B + kChunk): K2's walk started there
+    wave_lds_sync();
+    // the lane's 64 positions [64 lane, 64 lane + 64) through the quick check
+    uint64_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t w0 = d.words[16 * lane + k], w1 = d.words[16 * lane + k + 1];
+        const uint32_t ok = quick_ok4(w0 & rsv_keep4(a), __builtin_amdgcn_alignbyte(w1, w0, 1) | (a.spec ? kH : 0u));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bits |= (uint64_t)((ok >> (8 * j + 7)) & 1u) << (4 * k + j);
+    }
+    const uint32_t mine = (uint32_t)__popcll(bits);
+    const uint32_t incl = wave_incl_sum(mine);
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+    if (m > (uint32_t)kDenseCand || m == 0) return false;   // wave-uniform
+    uint32_t at = incl - mine;
+    d.bm[lane] = bits;
+    d.pre[lane] = (uint16_t)at;
+    for (; bits; bits &= bits - 1) d.pos[at++] = (uint16_t)(64 * lane + __builtin_ctzll(bits));
+    wave_lds_sync();
+    // 1-hop successors, as indexes into pos
+    for (uint32_t i = lane; i < m; i += kWave) {
+        const uint32_t p = d.pos[i];
+        const uint64_t v = parse_at(a, B + p, window_at(d.words, (int)p), nullptr, nullptr);
+        d.s1[i] = (!(v & kTerm) && v < Bend) ? dense_find(d, (uint32_t)(v - B)) : kNoLink;
+    }
+    wave_lds_sync();
+    // 2, 4, 8 hops
+    const uint16_t* src = d.s1;
+    uint16_t* dst = d.sa;
+#pragma unroll
+    for (int pass = 0; pass < 3; ++pass) {
+        for (uint32_t i = lane; i < m; i += kWave) {
+            const uint16_t y = src[i];
+            dst[i] = y == kNoLink ? kNoLink : src[y];
+        }
+        wave_lds_sync();
+        src = dst;
+        dst = dst == d.sa ? d.sb : d.sa;
+    }
+    const uint16_t* s8 = src;   // (sa after three passes)
+    int ok = 0;
+    if (lane == 0) {
+        const uint16_t e = x - B < kChunk ? dense_find(d, (uint32_t)(x - B)) : kNoLink;
+        if (e != kNoLink) {
+            ok = 1;
+            uint32_t p = e, hops = 0;
+            const uint64_t q = (uint64_t)blockIdx.x * kBlkChunks + qi;
+            const bool keep = qi < (uint32_t)kBlkChunks && q < a.anc_cap;
+            uint16_t* anc = a.anc + (keep ? q : 0) * kAncSlot;
+            int na = 0;
+            if (keep) anc[na++] = d.pos[p];
+            while (s8[p] != kNoLink) {
+                p = s8[p];
+                hops += kAncStride;
+                if (keep && na < kAncMax) anc[na++] = d.pos[p];
+            }
+            if (keep) a.anc_n[q] = (uint32_t)na;
+            a.anq[node] = keep ? (uint32_t)q : ~0u;
+            while (d.s1[p] != kNoLink) {
+                p = d.s1[p];
+                ++hops;
+            }
+            uint64_t v = parse_at(a, B + d.pos[p], window_at(d.words, (int)d.pos[p]), nullptr, nullptr);
+            if (!(v & kTerm)) {
+                ++hops;   // the last listed frame
+                if (v >= Bend) v = term(kExit, v);   // its successor is past the chunk
+                else   // a position off the list (it fails the quick check): the chain dies there
+                    v = parse_at(a, v, window_at(d.words, (int)(v - B)), nullptr, nullptr);
+            }
+            link_node(a, node, x, v, hops);
+        }
+    }
+    return __builtin_amdgcn_readfirstlane(ok) != 0;
+}
+
 __device__ void links_body(const ScanArgs& a, LinksLds& sl) {
-    uint32_t* words = sl.words;
-    uint16_t* l1 = sl.l1;
-    uint16_t* lj = sl.lj;
-    uint16_t* lk16 = sl.lk16;
+    uint32_t* words = sl.b.words;
+    uint16_t* l1 = sl.b.l1;
+    uint16_t* lj = sl.b.lj;
+    uint16_t* lk16 = sl.b.lk16;
     uint32_t* queue = sl.queue;
     int& nq = sl.nq;
     const int tid = threadIdx.x;
@@ -836,15 +980,19 @@ __device__ void links_body(const ScanArgs& a, LinksLds& sl) {
                 // chunk's true entry and its walk has at most kList frames)
                 uint64_t* fl = a.flist + (c * kListSlots + (i < (uint32_t)kListSlots ? i : 0)) * kList;
                 const bool rec = i < (uint32_t)kListSlots;
-                const uint64_t v = x - B < kChunk
-                                       ? walk_frames<false>(a, B, nullptr, x, kWalkHops,
-                                                            [&](uint64_t p, uint32_t key, uint8_t b0) {
-                                                                if (rec && cnt < (uint32_t)kList)
-                                                                    fl[cnt] = (p - B) | (uint64_t)b0 << 16 |
-                                                                              (uint64_t)key << 32;
-                                                                ++cnt;
-                                                            })
-                                       : term(kEnd, x);   // x == len on a chunk edge
+                auto emit = [&](uint64_t p, uint32_t key, uint8_t b0) {
+                    if (rec && cnt < (uint32_t)kList) fl[cnt] = (p - B) | (uint64_t)b0 << 16 | (uint64_t)key << 32;
+                    ++cnt;
+                };
+                uint64_t v = term(kEnd, x);   // x == len on a chunk edge
+                if (x - B < kChunk) {
+                    // kProbeHops frames first: a chain on course for more than kWalkHops frames in
+                    // the chunk goes to the LDS paths now, not after kWalkHops dependent reads
+                    uint64_t at = 0;
+                    v = walk_frames<false>(a, B, nullptr, x, kProbeHops, emit, &at);
+                    if (v == 0 && (at - x) * (kWalkHops / kProbeHops) >= B + kChunk - x)
+                        v = walk_frames<false>(a, B, nullptr, at, kWalkHops - kProbeHops, emit);
+                }
                 if (v == 0) {
                     queue[atomicAdd(&nq, 1)] = (uint32_t)s;
                 } else {
@@ -857,7 +1005,16 @@ __device__ void links_body(const ScanArgs& a, LinksLds& sl) {
     __syncthreads();
     SCAN_STAMP(1, 1);
     const int n = nq;
+    if (n == 0) return;   // block-uniform
+    // dense chunks: one wavefront each (DenseLds), the block's wavefronts side by side
+    {
+        const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+        for (int qi = wv; qi < n; qi += kScanT / kWave)
+            if (dense_node(a, sl.w[wv], queue[qi], (uint32_t)qi) && (threadIdx.x & (kWave - 1)) == 0) queue[qi] = ~0u;
+    }
+    __syncthreads();
     for (int qi = 0; qi < n; ++qi) {
+        if (queue[qi] == ~0u) continue;   // block-uniform: taken by a wavefront
         const uint64_t node = queue[qi], chunk = node / kCand, B = chunk * kChunk;
         load_chunk(a, B, words);
         chunk_links16(a, B, words, l1, lj, lk16);
@@ -1592,9 +1749,17 @@ __device__ __forceinline__ void put_frame(const ScanArgs& a, uint64_t k, uint64_
 // the next call needs no clearing launch.
 __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) {
     __shared__ uint32_t words[kWords];
-    __shared__ uint16_t l1[kChunk];    // next header (local index) or kNoLink
-    __shared__ uint16_t lj[kChunk];    // 2^k hops (ping)
-    __shared__ uint16_t lk16[kChunk];  // 2^k hops (pong); 16 hops after the last pass
+    __shared__ union {
+        struct {
+            uint16_t l1[kChunk];    // next header (local index) or kNoLink
+            uint16_t lj[kChunk];    // 2^k hops (ping)
+            uint16_t lk16[kChunk];  // 2^k hops (pong); 16 hops after the last pass
+        } b;
+        uint32_t ww[kScanT / kWave][kWords];   // anchored chunks: each wavefront's chunk bytes
+    } lu;
+    uint16_t* const l1 = lu.b.l1;
+    uint16_t* const lj = lu.b.lj;
+    uint16_t* const lk16 = lu.b.lk16;
     __shared__ uint16_t anchor[kChunk / kStride + 1];
     __shared__ int nanchor, nqa, nqb;
     __shared__ uint32_t qa_node[kEmitChunks], qb_node[kEmitChunks];
@@ -1684,26 +1849,33 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
     }
     __syncthreads();
     SCAN_STAMP(4, 1);
-    // anchored chunks: one wavefront each
+    // anchored chunks: one wavefront each, the chunk's bytes staged in the wavefront's LDS (one
+    // coalesced 4-KiB read; the 8-frame runs from the anchors then parse from LDS instead of a
+    // dependent global read per frame: K4 117 -> see DESIGN §14 at 64 MiB of 16-B frames)
     const int lane = tid & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(tid / kWave);
     for (int q = wv; q < nqa; q += kScanT / kWave) {
         const uint64_t node = qa_node[q], chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
+        uint32_t* ww = lu.ww[wv];
+        wave_load_chunk(a, B, ww, lane);
         const uint32_t slot = a.anq[node];
         const int na = (int)a.anc_n[slot];
+        wave_lds_sync();
         for (int u = lane; u < na; u += kWave) {
             uint64_t k = qa_base[q] + (uint64_t)u * kAncStride;
             uint64_t pos = B + a.anc[(uint64_t)slot * kAncSlot + u];
             for (int h = 0; h < kAncStride && pos < Bend; ++h) {
                 uint32_t key;
                 uint8_t b0;
-                const uint64_t v = parse_at(a, pos, window_global(a, pos), &key, &b0);
+                const uint64_t v = parse_at(a, pos, window_at(ww, (int)(pos - B)), &key, &b0);
                 if (v & kTerm) break;
                 put_frame(a, k++, pos, key, b0);
                 pos = v;
             }
         }
+        wave_lds_sync();   // (the next chunk overwrites ww)
     }
-    // the rest: the block from LDS
+    // the rest: the block from LDS (its arrays overlay the wavefronts' chunk bytes)
+    if (nqb) __syncthreads();   // block-uniform
     for (int q = 0; q < nqb; ++q) {
         const uint64_t node = qb_node[q], chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
         load_chunk(a, B, words);   // ends with a barrier
