@@ -807,7 +807,7 @@ __device__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const ui
 // bitmap of the list and a popcount), three doubling passes to 8-hop successors, then one lane walks the entry's chain
 // -- count / 8 + at most 7 hops, an anchor every 8 frames as the block path leaves them.
 static constexpr int kDenseCand = 392;   // 4 x 7.7 KB per block: K2 keeps 5 blocks per CU
-static constexpr int kProbeHops = 16;    // K2: frames walked from global memory before judging density
+static constexpr int kProbeHops = 8;     // K2: frames walked from global memory before judging density
 struct DenseLds {
     uint32_t words[kWords];
     uint64_t bm[kWave];         // candidate bitmap: bit u of word L <-> chunk offset 64 L + u
@@ -1013,6 +1013,7 @@ __device__ void links_body(const ScanArgs& a, LinksLds& sl) {
             if (dense_node(a, sl.w[wv], queue[qi], (uint32_t)qi) && (threadIdx.x & (kWave - 1)) == 0) queue[qi] = ~0u;
     }
     __syncthreads();
+    SCAN_STAMP(1, 2);   // dense chunks done
     for (int qi = 0; qi < n; ++qi) {
         if (queue[qi] == ~0u) continue;   // block-uniform: taken by a wavefront
         const uint64_t node = queue[qi], chunk = node / kCand, B = chunk * kChunk;
@@ -1747,6 +1748,10 @@ __device__ __forceinline__ void put_frame(const ScanArgs& a, uint64_t k, uint64_
 // an anchor every 16 frames, thread u the 16 frames from anchor u).  Every chunk's
 // candidate counter and external flags are zeroed here, after their last reader:
 // the next call needs no clearing launch.
+// K4's anchored emit: anchors per round (their runs staged in LDS, then stored frame by frame)
+static constexpr int kEmitGroup = 32;
+static constexpr uint16_t kNoFrame = 0xFFFF;
+
 __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) {
     __shared__ uint32_t words[kWords];
     __shared__ union {
@@ -1755,14 +1760,19 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
             uint16_t lj[kChunk];    // 2^k hops (ping)
             uint16_t lk16[kChunk];  // 2^k hops (pong); 16 hops after the last pass
         } b;
-        uint32_t ww[kScanT / kWave][kWords];   // anchored chunks: each wavefront's chunk bytes
+        struct {
+            uint32_t ww[kScanT / kWave][kWords];   // anchored chunks: each wavefront's chunk bytes
+            uint32_t tkey[kScanT / kWave][kEmitGroup * kAncStride];   // ... and its frames, staged
+            uint16_t tpos[kScanT / kWave][kEmitGroup * kAncStride];   //     for coalesced stores
+            uint8_t tb0[kScanT / kWave][kEmitGroup * kAncStride];
+        } w;
     } lu;
     uint16_t* const l1 = lu.b.l1;
     uint16_t* const lj = lu.b.lj;
     uint16_t* const lk16 = lu.b.lk16;
     __shared__ uint16_t anchor[kChunk / kStride + 1];
     __shared__ int nanchor, nqa, nqb;
-    __shared__ uint32_t qa_node[kEmitChunks], qb_node[kEmitChunks];
+    __shared__ uint32_t qa_node[kEmitChunks], qb_node[kEmitChunks], qa_slot[kEmitChunks];
     __shared__ uint64_t qa_base[kEmitChunks], qb_base[kEmitChunks];
     __shared__ TileInfo bti;
     __shared__ int fbs;
@@ -1810,9 +1820,11 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
                 const uint64_t e = c * kCand + ie;
                 const uint64_t base = ti.base + ti.we - we;
                 if (count > (uint32_t)kWalkHops) {
-                    if (a.anq[e] != ~0u) {
+                    const uint32_t slot = a.anq[e];
+                    if (slot != ~0u) {
                         const int q = atomicAdd(&nqa, 1);
                         qa_node[q] = (uint32_t)e;
+                        qa_slot[q] = slot;
                         qa_base[q] = base;
                     } else {
                         const int q = atomicAdd(&nqb, 1);
@@ -1855,25 +1867,49 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
     const int lane = tid & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(tid / kWave);
     for (int q = wv; q < nqa; q += kScanT / kWave) {
         const uint64_t node = qa_node[q], chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
-        uint32_t* ww = lu.ww[wv];
+        uint32_t* ww = lu.w.ww[wv];
+        // one trip: the chunk, the anchor count and the first 64 anchors (a slot holds kAncSlot)
+        const uint32_t slot = qa_slot[q];
+        const uint16_t* anc = a.anc + (uint64_t)slot * kAncSlot;
+        const uint32_t na_ld = a.anc_n[slot];
+        const uint16_t anc0 = anc[lane];
         wave_load_chunk(a, B, ww, lane);
-        const uint32_t slot = a.anq[node];
-        const int na = (int)a.anc_n[slot];
+        const int na = (int)na_ld;
         wave_lds_sync();
-        for (int u = lane; u < na; u += kWave) {
-            uint64_t k = qa_base[q] + (uint64_t)u * kAncStride;
-            uint64_t pos = B + a.anc[(uint64_t)slot * kAncSlot + u];
-            for (int h = 0; h < kAncStride && pos < Bend; ++h) {
-                uint32_t key;
-                uint8_t b0;
-                const uint64_t v = parse_at(a, pos, window_at(ww, (int)(pos - B)), &key, &b0);
-                if (v & kTerm) break;
-                put_frame(a, k++, pos, key, b0);
-                pos = v;
+        // kEmitGroup anchors per round: lane u < kEmitGroup parses the run of anchor ub + u into
+        // entries 8 u .. 8 u + 7 of the staging arrays (kNoFrame past its end), then the wavefront
+        // stores the round's frames with consecutive lanes on consecutive frames (the runs'
+        // own order put each store instruction on 8-frame strides: 64 MiB of 16-B frames,
+        // 4.2 M frames x 3 scattered stores)
+        uint32_t* tkey = lu.w.tkey[wv];
+        uint16_t* tpos = lu.w.tpos[wv];
+        uint8_t* tb0 = lu.w.tb0[wv];
+        for (int ub = 0; ub < na; ub += kEmitGroup) {
+            const int u = ub + lane;
+            if (lane < kEmitGroup) {
+                uint64_t pos = u < na ? B + (ub == 0 ? anc0 : anc[u]) : Bend;   // (anc0 = anc[lane])
+#pragma unroll 1
+                for (int h = 0; h < kAncStride; ++h) {
+                    const int i = lane * kAncStride + h;
+                    uint64_t v = kTerm;
+                    uint32_t key = 0;
+                    uint8_t b0 = 0;
+                    if (pos < Bend) v = parse_at(a, pos, window_at(ww, (int)(pos - B)), &key, &b0);
+                    tpos[i] = (v & kTerm) ? kNoFrame : (uint16_t)(pos - B);
+                    tkey[i] = key;
+                    tb0[i] = b0;
+                    if (!(v & kTerm)) pos = v;
+                    else pos = Bend;
+                }
             }
+            wave_lds_sync();
+            const uint64_t k0 = qa_base[q] + (uint64_t)ub * kAncStride;
+            for (int i = lane; i < kEmitGroup * kAncStride; i += kWave)
+                if (tpos[i] != kNoFrame) put_frame(a, k0 + i, B + tpos[i], tkey[i], tb0[i]);
+            wave_lds_sync();   // (the next round overwrites the staging arrays)
         }
-        wave_lds_sync();   // (the next chunk overwrites ww)
     }
+    SCAN_STAMP(4, 2);   // (wave 0's) anchored chunks done
     // the rest: the block from LDS (its arrays overlay the wavefronts' chunk bytes)
     if (nqb) __syncthreads();   // block-uniform
     for (int q = 0; q < nqb; ++q) {

@@ -8,7 +8,8 @@ R=$GRAFT_REPO_ROOT
 cd $R
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
-ln -sf ../netc_amd/lib/libnetc.so tools/libnetc.so   # the copies in tools/ find libnetc.so through $ORIGIN
+ln -sf ../netc_amd/lib/libnetc.so tools/libnetc.so   # the copies in tools/ and abl/ find libnetc.so through $ORIGIN
+ln -sf ../netc_amd/lib/libnetc.so abl/libnetc.so
 for i in $(seq 1 ${ROUNDS:-2}); do
   for L in $LIBS; do
     n=$(basename $L .so)

@@ -17,7 +17,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["NETC_GPU_LIB"] = os.path.join(ROOT, "tools", "libnetc_ws_gpu_stamps.so")
+os.environ.setdefault("NETC_GPU_LIB", os.path.join(ROOT, "tools", "libnetc_ws_gpu_stamps.so"))
 
 NAMES = ["K1 scan_exits", "K2 scan_links", "K3a scan_tiles", "K3b scan_resolve", "K4 scan_emit"]
 BLOCKS = 8192
@@ -43,7 +43,13 @@ def main():
     assert lib.netc_gpu_debug_scan_stamps(stamps.data_ptr()) == 0
     s = torch.cuda.Stream(dev)
     for wl in args.workloads.split(","):
-        off, keys, total = synth.config(wl)
+        if wl.startswith("u"):   # uniform frames of int(wl[1:]) payload bytes, 64 MiB of payload
+            fb = int(wl[1:])
+            nf = (64 << 20) // fb
+            off = np.arange(nf + 1, dtype=np.uint64) * np.uint64(fb)
+            keys = np.random.default_rng(3).integers(0, 2**32, nf, dtype=np.uint64).astype(np.uint32)
+        else:
+            off, keys, total = synth.config(wl)
         if wl == "c4":
             cut = int(np.searchsorted(off, 256 << 20))
             off, keys = off[: cut + 1], keys[:cut]
@@ -85,6 +91,11 @@ def main():
                 live = blk[:, 0] > 0
                 starts, ends = blk[live, 0], blk[live, 7]
                 ends = ends[ends > 0]
+                if starts.size == 0 or ends.size == 0:   # not launched (e.g. K3b inside K3a's launch)
+                    row_span.append((None, None, 0))
+                    row_gap.append(None)
+                    row_ph.append([None] * 7)
+                    continue
                 if t0 is None:
                     t0 = starts.min()
                 row_span.append(((starts.min() - t0) / 100.0, (ends.max() - starts.min()) / 100.0, int(live.sum())))
@@ -121,7 +132,7 @@ def main():
                 "gap_before_us": med([r[k] for r in gaps]),
                 "phase_median_us": [med([r[k][i] for r in phases]) for i in range(7)],
             })
-        last = [r[4][0] + r[4][1] for r in spans]
+        last = [r[4][0] + r[4][1] for r in spans if r[4][0] is not None]
         out["first_start_to_last_end_us"] = round(float(np.median(last)), 2)
         print(json.dumps(out), flush=True)
         del w
