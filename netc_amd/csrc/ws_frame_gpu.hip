@@ -88,7 +88,7 @@ __global__ __launch_bounds__(kScanThreads) void wire_offsets_chained(const uint6
     auto pos = [](uint32_t j) { return j + j / kScanPer; };
     const uint64_t tile = blockIdx.x, base = tile * kScanBlock;
     const uint32_t t0 = threadIdx.x * kScanPer;   // this thread's frames: base + t0 ..
-    if (tile == 0 && threadIdx.x == 0) *defer_count = 0;   // the assembly kernel's queue (runs after)
+    if (tile == 0 && threadIdx.x == 0) *defer_count = 0;   // (a spare word of the scratch; no reader since round 4)
 #pragma unroll
     for (int i = 0; i < kScanPer; ++i) {
         const uint32_t j = i * kScanThreads + threadIdx.x;
@@ -154,6 +154,8 @@ struct EncArgs {
     uint32_t* defer_count;
     uint64_t defer_cap;
     uint32_t all_spans;        // dense batch: the compose launch takes every span (no assembly launch)
+    uint32_t main_blocks;      // encode_frames_kernel: blocks 0 .. main_blocks-1 assemble, the rest fix headers
+    uint32_t per_wave;         // ... each assembly wavefront lists its unmapped spans at defer[wave * per_wave ..]
     // source-driven assembly (encode_src_kernel)
     const uint8_t* src_base;   // src rounded down to 16 (P coordinates: byte q of src is at P = q + smis)
     uint64_t smis;             // src & 15
@@ -444,10 +446,9 @@ __device__ u32x4 compose_vec(const EncArgs& a, EncTable& t, uint64_t A0, uint64_
 // lane's wire vector at W, take the frame l holding W (header start S <= W < next
 // header start Sn): one unaligned 16-B load at s = W + (off[l] - pw_l) (pw = wire
 // payload start) XOR frame l's key rotated to W gives every byte of the vector that
-// is payload of frame l.  The others -- frame l's header bytes when W is inside it,
-// and everything from the next header start on -- are at most a header plus 15
-// bytes per frame, and fix_frame (one thread per frame, in the queued launch)
-// rewrites exactly those.  So the vector path has no per-lane header work: the
+// is payload of frame l.  A vector holding any header byte (frame l's when W is inside
+// its header, or the next frame's) is not stored here: fix_vectors (one thread per frame,
+// the launch's trailing blocks) composes each of those whole.  So the vector path has no per-lane header work: the
 // previous form inserted the header and shifted the tail in the lane a header
 // touched, with a wave-wide branch costing about 200 vector instructions per span at
 // 1 KiB frames.  A span takes this path when the 64-entry table covers it and every
@@ -456,7 +457,7 @@ __device__ u32x4 compose_vec(const EncArgs& a, EncTable& t, uint64_t A0, uint64_
 
 // per-lane frame data from the table (ds_bpermute: every lane of the wave executes it)
 struct LaneFrames {
-    uint64_t S;       // wire header start of frame l (W coordinates)
+    uint64_t S, Sn;   // wire header starts of frames l, l + 1 (W coordinates)
     uint64_t P, Pn;   // payload offsets of frames l, l + 1
     uint32_t K;       // key of frame l
 };
@@ -468,6 +469,7 @@ __device__ __forceinline__ uint32_t bperm32(uint32_t x, int src) {
 __device__ __forceinline__ LaneFrames lane_frames(const EncTable& t, int l) {
     LaneFrames f;
     f.S = bperm64(t.start, l);
+    f.Sn = bperm64(t.start, l + 1);
     f.P = bperm64(t.poff, l);
     f.Pn = bperm64(t.poff, l + 1);
     f.K = bperm32(t.key, l);
@@ -478,12 +480,13 @@ __device__ __forceinline__ LaneFrames lane_frames(const EncTable& t, int l) {
 // read once for the wave (readlane), each lane picks frame l0 or l0 + 1.
 __device__ __forceinline__ LaneFrames frames_near(const EncTable& t, int l0, int nb, uint64_t W, int l) {
     if (nb > 1) return lane_frames(t, l);
-    const uint64_t S0 = readlane64(t.start, l0), S1 = readlane64(t.start, l0 + 1);
+    const uint64_t S0 = readlane64(t.start, l0), S1 = readlane64(t.start, l0 + 1), S2 = readlane64(t.start, l0 + 2);
     const uint64_t P0 = readlane64(t.poff, l0), P1 = readlane64(t.poff, l0 + 1), P2 = readlane64(t.poff, l0 + 2);
     const uint32_t K0 = readlane32(t.key, l0), K1 = readlane32(t.key, l0 + 1);
     const bool in1 = nb == 1 && W >= S1;
     LaneFrames f;
     f.S = in1 ? S1 : S0;
+    f.Sn = in1 ? S2 : S1;
     f.P = in1 ? P1 : P0;
     f.Pn = in1 ? P2 : P1;
     f.K = in1 ? K1 : K0;
@@ -505,6 +508,8 @@ struct SpanPlan {
 template <int U>
 struct Plan {
     SpanPlan s[U];
+    uint32_t own;       // bit u: span u's vector of this lane holds no header byte, so this kernel
+                        // stores it (the others: fix_vectors)
 };
 
 // f(integral_constant<int, I>) for I = 0 .. N-1, unrolled at compile time: span
@@ -522,6 +527,7 @@ template <int U, bool NT>
 __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, uint64_t A, uint64_t wlo,
                                            uint64_t whi, int lane, Plan<U>& P) {
     const bool masked = a.masked != 0;
+    P.own = 0;
     static_for<0, U>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
         SpanPlan& sp = P.s[u];
@@ -533,6 +539,7 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
         int kind = kSpanNone, l0 = 0, nb = 0;
         int64_t ad = 0;
         uint32_t rk = 0;
+        bool own = false;
         do {
             if (A0 >= whi) break;
             kind = kSpanQueued;
@@ -550,6 +557,8 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
                 kind = kSpanFast;
                 ad = (int64_t)W + delta;
                 rk = rotr8(readlane32(t.key, l0), A0 - pw);
+                const uint64_t Sn = readlane64(t.start, l0 + 1);
+                own = W >= pw && (W + 16 <= Sn || Sn >= whi);   // (the last frame: store_wire clips at whi)
                 break;
             }
             // this lane's frame: the entries starting at or before W
@@ -562,7 +571,9 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
             kind = kSpanFast;
             ad = s0;
             rk = rotr8(f.K, W - pw);
+            own = W >= pw && (W + 16 <= f.Sn || f.Sn >= whi);
         } while (false);
+        P.own |= own ? 1u << u : 0u;
         sp.l0 = l0;
         sp.nb = nb;
         sp.kind = kind;
@@ -578,41 +589,166 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
 
 template <int U, bool NT>
 __device__ __forceinline__ void finish_chunk(const EncArgs& a, const EncTable& t, uint64_t A, uint64_t wlo,
-                                             uint64_t whi, int lane, const Plan<U>& P) {
+                                             uint64_t whi, int lane, const Plan<U>& P, uint64_t* list, uint32_t& nl) {
     static_for<0, U>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
         const SpanPlan& sp = P.s[u];
         const uint64_t A0 = A + (uint64_t)u * kSpan;
         const uint64_t W = A0 + 16ull * (uint64_t)lane;
         if (sp.kind == kSpanNone) return;
-        if (sp.kind == kSpanQueued) {
-            if (lane == 0) {
-                const uint32_t slot = atomicAdd(a.defer_count, 1u);
-                if (slot < a.defer_cap) a.defer[slot] = A0;   // capacity covers every span
-            }
+        if (sp.kind == kSpanQueued) {   // wave-uniform: listed, composed after the wavefront's windows
+            if (lane == 0) list[nl] = A0;
+            ++nl;
             return;
         }
         const u32x4 kv = {sp.rk, sp.rk, sp.rk, sp.rk};
         const u32x4 v = sp.d ^ kv;
-        store_wire<NT>(a, W, v, wlo, whi);
+        if ((P.own >> u) & 1u) store_wire<NT>(a, W, v, wlo, whi);
     });
+}
+
+// The wire vector at V (W coordinates, 16-aligned), byte-exact, by one thread: every frame from
+// j0 (the frame holding byte V) to the last one starting inside it -- header bytes from
+// build_header, payload bytes from one 16-B source load each -- then one store.
+__device__ void compose_thread(const EncArgs& a, uint64_t V, int64_t j0, uint64_t wlo, uint64_t whi) {
+    const bool masked = a.masked != 0;
+    u32x4 out = {0, 0, 0, 0};
+    uint64_t S = gptr(a.wo)[j0] + a.wmis, o = gptr(a.off)[j0];
+    for (int64_t j = j0; j < (int64_t)a.n && S < V + 16; ++j) {
+        const uint64_t Sn = gptr(a.wo)[j + 1] + a.wmis, on = gptr(a.off)[j + 1];
+        const uint64_t len = on - o, pw = S + header_len(len, masked);
+        const uint32_t key = masked ? gptr(a.keys)[j] : 0u;
+        const int64_t hs = (int64_t)(S - V), he = (int64_t)(pw - V), phi = (int64_t)(Sn - V);
+        if (he > 0 && hs < 16) {
+            uint64_t hl, hh;
+            build_header(a.b0 ? (uint32_t)gptr(a.b0)[j] : 0x82u, len, masked, key, hl, hh);
+            out |= shift_bytes(hl, hh, (int)hs) & select_range(hs, he);
+        }
+        if (phi > 0 && he < 16 && phi > he) {
+            const int64_t s0 = (int64_t)o - he;   // source offset of the vector's byte 0
+            u32x4 v;
+            if (s0 >= 0 && (uint64_t)s0 + 16 <= a.src_total) v = load_u<false>(a.src + s0);
+            else v = load_guarded(a, s0, he < 0 ? 0 : (int)he, phi > 16 ? 16 : (int)phi);
+            const uint32_t rk = rotr8(key, (uint64_t)(-he));   // phase of byte 0: V - pw
+            const u32x4 kv = {rk, rk, rk, rk};
+            out |= (v ^ kv) & select_range(he, phi);
+        }
+        S = Sn;
+        o = on;
+    }
+    store_wire<false>(a, V, out, wlo, whi);
+}
+
+// The vectors holding frame k's header bytes (one, or two when the header crosses a 16-B
+// edge) that frame k owns -- the first is frame k - 1's when k - 1's header reaches into it --
+// composed byte-exactly.  The assembly stores only vectors with no header byte (SpanPlan::own),
+// so the two write disjoint vectors and need no ordering (round 4: the fixups were a launch of
+// their own after the assembly, 7.9 us at config 2; as the assembly launch's trailing blocks the
+// step went 39.2-40.0 -> 37.6-37.8 us at config 2 and 414-417 -> 418-421 us at config 4,
+// profiles/r04xyz_encode_fused.json.  Tried on the way: a per-wavefront done counter so the
+// trailing blocks could take the queued spans -- 5,120 same-address atomics at the end of the
+// launch tripled it (79 us) -- and the trailing blocks resident beside the assembly (fewer
+// assembly blocks: 39.8-40.2 / 462-463 us).)
+__device__ __forceinline__ void fix_vectors(const EncArgs& a, uint64_t k, uint64_t wlo, uint64_t whi) {
+    const bool masked = a.masked != 0;
+    // frames k - 1, k, k + 1 in one trip (k - 1 clamped: its values are unused for k = 0)
+    const uint64_t kp = k > 0 ? k - 1 : 0;
+    const uint64_t Sp = gptr(a.wo)[kp] + a.wmis, S = gptr(a.wo)[k] + a.wmis, Sn = gptr(a.wo)[k + 1] + a.wmis;
+    const uint64_t op = gptr(a.off)[kp], o = gptr(a.off)[k], on = gptr(a.off)[k + 1];
+    const uint32_t keyp = masked ? gptr(a.keys)[kp] : 0u, key = masked ? gptr(a.keys)[k] : 0u;
+    const uint32_t b0 = a.b0 ? (uint32_t)gptr(a.b0)[k] : 0x82u;
+    const uint64_t len = on - o, hl = header_len(len, masked), pw = S + hl;
+    const uint64_t v0 = S & ~15ull, v1 = (pw - 1) & ~15ull;
+    const bool own0 = k == 0 || ((Sp + header_len(o - op, masked) - 1) & ~15ull) < v0;
+    // the usual case: the vectors hold only frame k - 1's payload tail, frame k's header and frame
+    // k's payload (frame k ends at or past the last one); the payload bytes by one load per frame
+    const bool simple = Sn >= v1 + 16 && (k == 0 || v0 >= S || v0 >= Sp + header_len(o - op, masked));
+    if (!simple) {   // small frames: the general walk
+        if (own0) compose_thread(a, v0, (k > 0 && v0 < S) ? (int64_t)k - 1 : (int64_t)k, wlo, whi);
+        if (v1 != v0) compose_thread(a, v1, (int64_t)k, wlo, whi);
+        return;
+    }
+    uint64_t hlo, hhi;
+    build_header(b0, len, masked, key, hlo, hhi);
+    auto vec = [&](uint64_t V) {
+        u32x4 out = shift_bytes(hlo, hhi, (int)((int64_t)S - (int64_t)V)) &
+                    select_range((int64_t)S - (int64_t)V, (int64_t)pw - (int64_t)V);
+        // frame k's payload bytes [pw, V + 16)
+        const int64_t plo = (int64_t)pw - (int64_t)V;
+        if (plo < 16 && len) {
+            const int64_t s0 = (int64_t)o - plo;
+            const int64_t phi = (int64_t)Sn - (int64_t)V;
+            u32x4 v;
+            if (s0 >= 0 && (uint64_t)s0 + 16 <= a.src_total) v = load_u<false>(a.src + s0);
+            else v = load_guarded(a, s0, plo < 0 ? 0 : (int)plo, phi > 16 ? 16 : (int)phi);
+            const uint32_t rk = rotr8(key, (uint64_t)(-plo));
+            const u32x4 kv = {rk, rk, rk, rk};
+            out |= (v ^ kv) & select_range(plo, phi);
+        }
+        // frame k - 1's payload bytes [V, S)
+        if (V < S && k > 0) {
+            const int64_t e = (int64_t)S - (int64_t)V;   // bytes of frame k - 1 in the vector
+            const int64_t s0 = (int64_t)o - e;           // its payload ends at o (= off[k])
+            u32x4 v;
+            if (s0 >= 0 && (uint64_t)s0 + 16 <= a.src_total) v = load_u<false>(a.src + s0);
+            else v = load_guarded(a, s0, 0, (int)e);
+            // phase of byte 0: its offset in frame k - 1's payload, s0 - op
+            const uint32_t rk = rotr8(keyp, (uint64_t)(s0 - (int64_t)op));
+            const u32x4 kv = {rk, rk, rk, rk};
+            out |= (v ^ kv) & select_range(0, e);
+        }
+        store_wire<false>(a, V, out, wlo, whi);
+    };
+    if (own0) vec(v0);
+    if (v1 != v0) vec(v1);
 }
 
 // Chunk = U spans.  Wavefront w of W takes chunks w, w+W, ...  Per trip: the table
 // of chunk c+W (issued a trip ago) is resolved and chunk c+W's loads are issued,
 // chunk c+2W's table is issued, then chunk c (loaded a trip ago) is stored.
 // W: wavefronts per SIMD the register budget must allow (launch_enc_u picks it per batch)
+// Blocks main_blocks .. gridDim.x - 1 (dispatched as the assembly blocks retire: its tail)
+// compose the vectors holding header bytes (fix_vectors, one thread per frame).  They share
+// no vector with the assembly's stores, so nothing orders the two.
+__device__ void fixup_block(const EncArgs& a, uint64_t wire_total) {
+    const uint64_t wlo = a.wmis, whi = a.wmis + wire_total;
+    const uint64_t fb = blockIdx.x - a.main_blocks, nfb = gridDim.x - a.main_blocks;
+    for (uint64_t k = fb * blockDim.x + threadIdx.x; k < a.n; k += nfb * blockDim.x) fix_vectors(a, k, wlo, whi);
+}
+
 template <int U, bool NT, int W>
 __global__ __launch_bounds__(256, W) void encode_frames_kernel(EncArgs a) {
+    const uint64_t wire_total = gptr(a.wo)[a.n];
+    if (blockIdx.x >= a.main_blocks) {   // block-uniform
+        fixup_block(a, wire_total);
+        return;
+    }
     constexpr uint64_t kWin = kSpan * U;
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wpb = blockDim.x / kWave;
-    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
+    const uint64_t nwaves = (uint64_t)a.main_blocks * wpb;
     const uint64_t wave = (uint64_t)blockIdx.x * wpb + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // uniform: scalar branches, exact vmcnt waits
-    const uint64_t wire_total = gptr(a.wo)[a.n];
     const uint64_t wlo = a.wmis, whi = a.wmis + wire_total;
     const uint64_t nwin = (whi + kWin - 1) / kWin;
     const double density = wire_total ? (double)a.n / (double)wire_total : 0.0;   // frames per wire byte
+    // spans the assembly cannot map (kSpanQueued: the first and last, spans the frame table does not
+    // cover, loads that would leave the payload): listed by lane 0 in the wavefront's own slice of
+    // the defer array (plain stores, read back by the same lane), composed after its windows
+    uint64_t* list = a.defer + wave * a.per_wave;
+    uint32_t nl = 0;   // wave-uniform
+    auto done = [&]() {
+        for (uint32_t i = 0; i < nl; ++i) {
+            uint64_t A0 = 0;
+            if (lane == 0) A0 = list[i];
+            A0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(A0 >> 32)) << 32) |
+                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)A0);
+            EncTable t;
+            enc_table_load(a, t, enc_locate(a, A0, wire_total, lane), lane);
+            const uint64_t Wq = A0 + 16ull * (uint64_t)lane;
+            const u32x4 v = compose_vec(a, t, A0, Wq, lane);
+            if (Wq < whi) store_wire<false>(a, Wq, v, wlo, whi);
+        }
+    };
 
     uint64_t c = wave;
     if (c >= nwin) return;
@@ -647,12 +783,13 @@ __global__ __launch_bounds__(256, W) void encode_frames_kernel(EncArgs a) {
         const uint64_t cn = c + nwaves;
         EncTable tn;
         if (cn < nwin) enc_table_issue(a, tn, guess(f, s, cn * kWin), lane);
-        finish_chunk<U, NT>(a, tc, A, wlo, whi, lane, pc);
+        finish_chunk<U, NT>(a, tc, A, wlo, whi, lane, pc, list, nl);
         if (cn >= nwin) break;
         c = cn;
         A = cn * kWin;
         tc = tn;
     }
+    done();
 }
 
 typedef unsigned __int128 u128;
@@ -673,58 +810,14 @@ __device__ __forceinline__ void put_bytes(NETC_GLOBAL uint8_t* w, u128 v, uint64
     }
 }
 
-// Frame k's header, and its payload bytes from the header's end to the end of the
-// 16-byte wire vector the header starts in (clipped to the frame): the bytes the
-// assembly kernel leaves wrong, since it maps a whole vector through the frame that
-// holds its first byte.  The compose kernel's vectors may cover some of the same
-// bytes, with the same values, so the two need no ordering.
-__device__ __forceinline__ void fix_frame(const EncArgs& a, uint64_t k) {
-    const bool masked = a.masked != 0;
-    const uint64_t w0 = gptr(a.wo)[k], p0 = gptr(a.off)[k];
-    const uint64_t len = gptr(a.off)[k + 1] - p0, hl = header_len(len, masked);
-    const uint32_t key = masked ? gptr(a.keys)[k] : 0u;
-    uint64_t lo, hi;
-    build_header(a.b0 ? (uint32_t)gptr(a.b0)[k] : 0x82u, len, masked, key, lo, hi);
-    NETC_GLOBAL uint8_t* w = gptr(a.wire_base) + a.wmis + w0;
-    if (!ENC_OK(4, w0 + hl + len, gptr(a.wo)[a.n])) return;
-    const uint64_t vend = (((w0 + a.wmis) | 15) + 1) - a.wmis;   // wire end of the header's vector
-    const uint64_t m = min(vend > w0 + hl ? vend - (w0 + hl) : 0ull, len);   // <= 15
-    // the payload bytes read before any byte is written (a load-store byte loop
-    // waits out each load in turn): one 16-B load, bytewise only at the buffer end
-    uint64_t dlo = 0, dhi = 0;
-    if (m) {
-        if (p0 + 16 <= a.src_total) {
-            const u32x4 d = load_u<false>(a.src + p0);
-            dlo = (uint64_t)d[0] | (uint64_t)d[1] << 32;
-            dhi = (uint64_t)d[2] | (uint64_t)d[3] << 32;
-        } else {
-            for (uint64_t i = 0; i < m; ++i) {
-                const uint64_t b = gptr(a.src)[p0 + i];
-                if (i < 8) dlo |= b << (8 * i);
-                else dhi |= b << (8 * (i - 8));
-            }
-        }
-        const uint64_t k2 = (uint64_t)key | (uint64_t)key << 32;   // phase 0 at p0
-        dlo ^= k2;
-        dhi ^= k2;
-    }
-    // header then payload bytes, hl + m <= 16 of them inside one 16-byte wire vector, written
-    // with the widest naturally aligned stores (at most 5, was one store per byte)
-    const u128 hmask = hl >= 16 ? ~(u128)0 : (((u128)1 << (8 * hl)) - 1);
-    const u128 pay = (u128)dhi << 64 | dlo;
-    put_bytes(w, (((u128)hi << 64 | lo) & hmask) | (hl < 16 ? pay << (8 * hl) : (u128)0), hl + m);
-}
-
-// The queued spans: each wavefront takes queue entries in turn and composes them;
-// then every frame's header bytes (fix_frame), one thread per frame.
+// Dense batches (all_spans): every span composed per lane, no assembly launch before this one.
 __global__ __launch_bounds__(256) void encode_queued_kernel(EncArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / kWave);
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint64_t count = min((uint64_t)*a.defer_count, a.defer_cap);
     const uint64_t wire_total = gptr(a.wo)[a.n];
     const uint64_t wlo = a.wmis, whi = a.wmis + wire_total;
-    if (a.all_spans) {
+    {
         // dense batch: no assembly launch before this one -- every span is composed
         // here, so no header fixups either.  A wave takes kDenseGroup consecutive
         // spans per trip: one search for the first, then each next span's table is
@@ -743,21 +836,6 @@ __global__ __launch_bounds__(256) void encode_queued_kernel(EncArgs a) {
                 if (W < whi) store_wire<false>(a, W, v, wlo, whi);
             }
         }
-        return;
-    }
-    // the header fixups first: their loads need nothing from the queue counter, so the
-    // dependent trips (frame descriptors, then the payload bytes after each header) do
-    // not wait behind the counter's
-    const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.n; k += nth) fix_frame(a, k);
-    for (uint64_t q = wave; q < count; q += nwaves) {
-        const uint64_t A0 = a.defer[q];
-        if (!ENC_OK(3, A0, whi)) continue;
-        EncTable t;
-        enc_table_load(a, t, enc_locate(a, A0, wire_total, lane), lane);
-        const uint64_t W = A0 + 16ull * (uint64_t)lane;
-        const u32x4 v = compose_vec(a, t, A0, W, lane);
-        if (W < whi) store_wire<false>(a, W, v, wlo, whi);
     }
 }
 
@@ -1239,13 +1317,16 @@ static hipError_t launch_enc_u(EncArgs a, uint64_t wire_bound, bool nt, int max_
         hipLaunchKernelGGL(encode_queued_kernel, dim3((unsigned)(gb < 8192 ? gb : 8192)), dim3(256), 0, stream, a);
         return hipGetLastError();
     }
-    if (nt) hipLaunchKernelGGL((encode_frames_kernel<U, true, W>), dim3(blocks), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((encode_frames_kernel<U, false, W>), dim3(blocks), dim3(256), 0, stream, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const uint64_t fix_blocks = (a.n + 255) / 256;   // one thread per frame, up to 64 frames each
-    const unsigned qb = (unsigned)(fix_blocks < 256 ? 256 : (fix_blocks > 4096 ? 4096 : fix_blocks));
-    hipLaunchKernelGGL(encode_queued_kernel, dim3(qb), dim3(256), 0, stream, a);
+    // the header fixups as trailing blocks of the same launch (fixup_block):
+    // one thread per frame up to 1,024 blocks
+    const uint64_t fix = (a.n + 255) / 256;
+    const uint64_t fix_blocks = fix < 64 ? 64 : (fix > 1024 ? 1024 : fix);
+    a.main_blocks = (uint32_t)blocks;
+    a.per_wave = (uint32_t)(((nwin + 4 * (uint64_t)blocks - 1) / (4 * (uint64_t)blocks)) * U);   // windows per wave x U
+    if ((uint64_t)a.per_wave * 4 * (uint64_t)blocks > a.defer_cap) return hipErrorInvalidValue;   // (sized with slack below)
+    const unsigned grid = (unsigned)(blocks + fix_blocks);
+    if (nt) hipLaunchKernelGGL((encode_frames_kernel<U, true, W>), dim3(grid), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((encode_frames_kernel<U, false, W>), dim3(grid), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -1257,7 +1338,9 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     const uint64_t tiles = scan_tiles_for(n, per);
     if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
     const uint64_t wmis = (uint64_t)(uintptr_t)wire & 15u;
-    const uint64_t spans = (wmis + wire_bound + kSpan - 1) / kSpan + 8;   // every span could be queued
+    // every span could be listed, in per-wavefront slices of the same length (+ slack: a wavefront's
+    // share of windows rounds up)
+    const uint64_t spans = (wmis + wire_bound + kSpan - 1) / kSpan + 8 + 4 * 4 * 8192;
     EncScratch sc;
     hipError_t e = scratch_for(stream, tiles, spans, sc);
     if (e != hipSuccess) return e;
