@@ -123,10 +123,36 @@ __device__ __forceinline__ void scan_value(int k, int i, uint64_t v) {   // a co
 #define SCAN_SCOPE(k) ScanStampScope scan_scope_guard(k)
 #define SCAN_STAMP(k, i) scan_stamp(k, i)
 #define SCAN_VALUE(k, i, v) scan_value(k, i, v)
+// K2's per-wavefront dense path: summed phase durations (100 MHz ticks) over every call, and calls
+__device__ unsigned long long g_dense_phase[8];
+extern "C" int netc_gpu_debug_dense_phases(unsigned long long* out8, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_dense_phase), sizeof(g_dense_phase));
+    if (reset) {
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dense_phase), z, sizeof(z));
+    }
+    return (int)e;
+}
+#define DENSE_T(i) uint64_t dense_t##i = (threadIdx.x & 63) == 0 ? __builtin_amdgcn_s_memrealtime() : 0
+#define DENSE_ADD(i, a, b) (dacc[i] += dense_t##b - dense_t##a)
+#define DENSE_COUNT() (dacc[7] += 1)
+#define DENSE_ACC uint64_t dacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define DENSE_ARG , uint64_t (&dacc)[8]
+#define DENSE_PASS , dacc
+#define DENSE_FLUSH() \
+    if ((threadIdx.x & 63) == 0 && dacc[7]) \
+        for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_dense_phase[i_], (unsigned long long)dacc[i_])
 #else
 #define SCAN_SCOPE(k) ((void)0)
 #define SCAN_STAMP(k, i) ((void)0)
 #define SCAN_VALUE(k, i, v) ((void)0)
+#define DENSE_T(i) ((void)0)
+#define DENSE_ADD(i, a, b) ((void)0)
+#define DENSE_COUNT() ((void)0)
+#define DENSE_ACC
+#define DENSE_ARG
+#define DENSE_PASS
+#define DENSE_FLUSH() ((void)0)
 #endif
 
 __device__ __forceinline__ uint64_t term(uint64_t type, uint64_t pos) { return kTerm | type << 61 | pos; }
@@ -864,13 +890,43 @@ __device__ __forceinline__ uint16_t dense_find(const DenseLds& d, uint32_t t) {
 
 // One queued node by the calling wavefront (see DenseLds); false (wave-uniform, nothing
 // written) leaves it to the block path.  qi: its queue index (anchor slot as the block path).
-__device__ bool dense_node(const ScanArgs& a, DenseLds& d, uint64_t node, uint32_t qi) {
-    if (!a.strict) return false;   // every position a candidate: the block path
+// a chunk's kWords words as the wavefront's registers: lane l holds 16-B vectors l + 64 i (the
+// next chunk's loads stay in flight while the current one is processed); false on an edge chunk
+// (the bytes past len must read as zero: wave_load_chunk's byte path then)
+struct ChunkRegs {
+    u32x4 v[(kWords / 4 + kWave - 1) / kWave];
+};
+__device__ __forceinline__ bool chunk_regs_load(const ScanArgs& a, uint64_t B, int lane, ChunkRegs& R) {
+    typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+    if (B + kChunk + 32 > a.len) return false;   // wave-uniform
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(R.v) / sizeof(R.v[0])); ++i) {
+        const int v = lane + kWave * i;
+        const int vc = v < kWords / 4 ? v : kWords / 4 - 1;   // (the clamped loads are not stored)
+        R.v[i] = *(const NETC_GLOBAL u32x4u*)(a.wire + B + 16 * (uint64_t)vc);
+    }
+    return true;
+}
+__device__ __forceinline__ void chunk_regs_store(uint32_t* words, const ChunkRegs& R, int lane) {
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(R.v) / sizeof(R.v[0])); ++i) {
+        const int v = lane + kWave * i;
+        if (v < kWords / 4) {
+            words[4 * v] = R.v[i][0];
+            words[4 * v + 1] = R.v[i][1];
+            words[4 * v + 2] = R.v[i][2];
+            words[4 * v + 3] = R.v[i][3];
+        }
+    }
+}
+
+// One queued node by the calling wavefront, its chunk's words already in d.words (see DenseLds);
+// false (wave-uniform, nothing written) leaves it to the block path.  qi: its queue index
+// (anchor slot as the block path).  x: the node's position (a.cand[node]).
+__device__ bool dense_node(const ScanArgs& a, DenseLds& d, uint64_t node, uint64_t x, uint32_t qi DENSE_ARG) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
-    wave_load_chunk(a, B, d.words, lane);
-    const uint64_t x = a.cand[node];   // in [B, B + kChunk): K2's walk started there
-    wave_lds_sync();
+    DENSE_T(1);
     // the lane's 64 positions [64 lane, 64 lane + 64) through the quick check
     uint64_t bits = 0;
 #pragma unroll
@@ -889,6 +945,8 @@ __device__ bool dense_node(const ScanArgs& a, DenseLds& d, uint64_t node, uint32
     d.pre[lane] = (uint16_t)at;
     for (; bits; bits &= bits - 1) d.pos[at++] = (uint16_t)(64 * lane + __builtin_ctzll(bits));
     wave_lds_sync();
+    DENSE_T(2);
+    const uint16_t e = x - B < kChunk ? dense_find(d, (uint32_t)(x - B)) : kNoLink;   // the entry's index
     // 1-hop successors, as indexes into pos
     for (uint32_t i = lane; i < m; i += kWave) {
         const uint32_t p = d.pos[i];
@@ -896,52 +954,77 @@ __device__ bool dense_node(const ScanArgs& a, DenseLds& d, uint64_t node, uint32
         d.s1[i] = (!(v & kTerm) && v < Bend) ? dense_find(d, (uint32_t)(v - B)) : kNoLink;
     }
     wave_lds_sync();
-    // 2, 4, 8 hops
-    const uint16_t* src = d.s1;
-    uint16_t* dst = d.sa;
+    DENSE_T(3);
+    // 2, 4, 8 hops (s8 in sa), then 16, 32, 64 (s64 in sb; s1 is reused for 32: the walk's last
+    // hops re-parse from the words instead)
+    uint16_t* const bufs[3] = {d.s1, d.sa, d.sb};
+    constexpr int kFrom[6] = {0, 1, 2, 1, 2, 0}, kTo[6] = {1, 2, 1, 2, 0, 2};
 #pragma unroll
-    for (int pass = 0; pass < 3; ++pass) {
+    for (int pass = 0; pass < 6; ++pass) {
+        const uint16_t* src = bufs[kFrom[pass]];
+        uint16_t* dst = bufs[kTo[pass]];
         for (uint32_t i = lane; i < m; i += kWave) {
             const uint16_t y = src[i];
             dst[i] = y == kNoLink ? kNoLink : src[y];
         }
         wave_lds_sync();
-        src = dst;
-        dst = dst == d.sa ? d.sb : d.sa;
     }
-    const uint16_t* s8 = src;   // (sa after three passes)
+    const uint16_t* s8 = d.sa;
+    const uint16_t* s64 = d.sb;
+    DENSE_T(4);
+    if (__builtin_amdgcn_readfirstlane((int)e) == (int)kNoLink) return false;   // wave-uniform (not listed)
+    // anchor j (every 8 frames from the entry) by lane j mod 64: s64^(j/8), then s8^(j%8)
+    const uint64_t q = (uint64_t)blockIdx.x * kBlkChunks + qi;
+    const bool keep = qi < (uint32_t)kBlkChunks && q < a.anc_cap;
+    uint16_t* anc = a.anc + (keep ? q : 0) * kAncSlot;
+    uint32_t na = 0;   // anchors (wave-uniform)
+    for (int it = 0;; ++it) {
+        const int j = lane + kWave * it;
+        uint32_t p = e;
+        for (int h = 0; h < j / 8 && p != kNoLink; ++h) p = s64[p];
+        for (int h = 0; h < j % 8 && p != kNoLink; ++h) p = s8[p];
+        const bool valid = p != kNoLink;
+        if (valid && keep && j < kAncMax) anc[j] = d.pos[p];
+        const uint64_t vm = __ballot(valid);
+        na += (uint32_t)__popcll(vm);
+        if (vm != ~0ull) break;   // (valid lanes are a prefix: anchor j exists when j + 1 does)
+    }
+    // the last anchor's position (lane (na - 1) % 64 of the last round holds it): recomputed by lane 0
     int ok = 0;
     if (lane == 0) {
-        const uint16_t e = x - B < kChunk ? dense_find(d, (uint32_t)(x - B)) : kNoLink;
-        if (e != kNoLink) {
-            ok = 1;
-            uint32_t p = e, hops = 0;
-            const uint64_t q = (uint64_t)blockIdx.x * kBlkChunks + qi;
-            const bool keep = qi < (uint32_t)kBlkChunks && q < a.anc_cap;
-            uint16_t* anc = a.anc + (keep ? q : 0) * kAncSlot;
-            int na = 0;
-            if (keep) anc[na++] = d.pos[p];
-            while (s8[p] != kNoLink) {
-                p = s8[p];
-                hops += kAncStride;
-                if (keep && na < kAncMax) anc[na++] = d.pos[p];
+        ok = 1;
+        uint32_t p = e;
+        for (uint32_t h = 0; h < (na - 1) / 8; ++h) p = s64[p];
+        for (uint32_t h = 0; h < (na - 1) % 8; ++h) p = s8[p];
+        uint32_t hops = (na - 1) * kAncStride;
+        if (keep) a.anc_n[q] = na < (uint32_t)kAncMax ? na : (uint32_t)kAncMax;
+        a.anq[node] = keep ? (uint32_t)q : ~0u;
+        // at most 7 listed frames on from it (the 8th would be another anchor), by parsing
+        uint64_t pp = B + d.pos[p], v;
+        for (;;) {
+            v = parse_at(a, pp, window_at(d.words, (int)(pp - B)), nullptr, nullptr);
+            if (v & kTerm) break;
+            ++hops;   // the frame at pp
+            if (v >= Bend) {   // its successor is past the chunk
+                v = term(kExit, v);
+                break;
             }
-            if (keep) a.anc_n[q] = (uint32_t)na;
-            a.anq[node] = keep ? (uint32_t)q : ~0u;
-            while (d.s1[p] != kNoLink) {
-                p = d.s1[p];
-                ++hops;
+            if (dense_find(d, (uint32_t)(v - B)) == kNoLink) {   // a position off the list: the chain dies there
+                v = parse_at(a, v, window_at(d.words, (int)(v - B)), nullptr, nullptr);
+                break;
             }
-            uint64_t v = parse_at(a, B + d.pos[p], window_at(d.words, (int)d.pos[p]), nullptr, nullptr);
-            if (!(v & kTerm)) {
-                ++hops;   // the last listed frame
-                if (v >= Bend) v = term(kExit, v);   // its successor is past the chunk
-                else   // a position off the list (it fails the quick check): the chain dies there
-                    v = parse_at(a, v, window_at(d.words, (int)(v - B)), nullptr, nullptr);
-            }
-            link_node(a, node, x, v, hops);
+            pp = v;
         }
+        DENSE_T(5);
+        link_node(a, node, x, v, hops);
+        DENSE_T(6);
+        DENSE_ADD(4, 4, 5);
+        DENSE_ADD(5, 5, 6);
     }
+    DENSE_ADD(1, 1, 2);
+    DENSE_ADD(2, 2, 3);
+    DENSE_ADD(3, 3, 4);
+    DENSE_COUNT();
     return __builtin_amdgcn_readfirstlane(ok) != 0;
 }
 
@@ -1006,11 +1089,28 @@ __device__ void links_body(const ScanArgs& a, LinksLds& sl) {
     SCAN_STAMP(1, 1);
     const int n = nq;
     if (n == 0) return;   // block-uniform
-    // dense chunks: one wavefront each (DenseLds), the block's wavefronts side by side
-    {
+    // dense chunks: one wavefront each (DenseLds), the block's wavefronts side by side; each
+    // wavefront's next chunk is loaded into registers while it works on the current one
+    if (a.strict) {   // (non-strict: every position a candidate, the block path)
         const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-        for (int qi = wv; qi < n; qi += kScanT / kWave)
-            if (dense_node(a, sl.w[wv], queue[qi], (uint32_t)qi) && (threadIdx.x & (kWave - 1)) == 0) queue[qi] = ~0u;
+        const int lane = threadIdx.x & (kWave - 1);
+        DenseLds& d = sl.w[wv];
+        DENSE_ACC;
+        ChunkRegs R;
+        bool rfast = wv < n && chunk_regs_load(a, (uint64_t)queue[wv] / kCand * kChunk, lane, R);
+        for (int qi = wv; qi < n; qi += kScanT / kWave) {
+            const uint64_t node = queue[qi];
+
+            const uint64_t x = a.cand[node];   // (before the prefetch: a wait for it must not wait for that)
+            if (rfast) chunk_regs_store(d.words, R, lane);
+            else wave_load_chunk(a, node / kCand * kChunk, d.words, lane);
+            const int qn = qi + kScanT / kWave;
+            rfast = qn < n && chunk_regs_load(a, (uint64_t)queue[qn] / kCand * kChunk, lane, R);
+            wave_lds_sync();
+            if (dense_node(a, d, node, x, (uint32_t)qi DENSE_PASS) && lane == 0) queue[qi] = ~0u;
+            wave_lds_sync();   // (the next chunk overwrites d)
+        }
+        DENSE_FLUSH();
     }
     __syncthreads();
     SCAN_STAMP(1, 2);   // dense chunks done

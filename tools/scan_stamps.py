@@ -41,6 +41,8 @@ def main():
     dev = torch.device("cuda", 0)
     stamps = torch.zeros(5 * BLOCKS * 8, dtype=torch.int64, device=dev)
     assert lib.netc_gpu_debug_scan_stamps(stamps.data_ptr()) == 0
+    if hasattr(lib, "netc_gpu_debug_dense_phases"):
+        lib.netc_gpu_debug_dense_phases.argtypes = [ctypes.c_void_p, ctypes.c_int]
     s = torch.cuda.Stream(dev)
     for wl in args.workloads.split(","):
         if wl.startswith("u"):   # uniform frames of int(wl[1:]) payload bytes, 64 MiB of payload
@@ -134,6 +136,14 @@ def main():
             })
         last = [r[4][0] + r[4][1] for r in spans if r[4][0] is not None]
         out["first_start_to_last_end_us"] = round(float(np.median(last)), 2)
+        if hasattr(lib, "netc_gpu_debug_dense_phases"):   # K2's per-wavefront dense path, summed over the reps
+            ph = (ctypes.c_ulonglong * 8)()
+            lib.netc_gpu_debug_dense_phases(ph, 1)
+            calls = ph[7]
+            if calls:
+                names = ["load", "quick_check+list", "successors", "doubling", "walk", "link_node"]
+                out["dense_phase_us_per_chunk"] = {nm: round(ph[i] / 100.0 / calls, 3) for i, nm in enumerate(names)}
+                out["dense_chunks_per_call"] = calls / (args.reps + 5)
         print(json.dumps(out), flush=True)
         del w
         torch.cuda.empty_cache()
