@@ -90,7 +90,7 @@ tools/libdiag_policy.so: tools/diag_policy.hip
 # sanitizer runtimes are preloaded and leak checking is off (the interpreter's own).
 ASAN_FLAGS := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined
 ASAN_TESTS := tests/test_host_framing.py tests/test_mask_cpu.py tests/test_oracle.py tests/test_scan_oracle.py tests/test_scan_host.py \
-              tests/test_utf8_oracle.py
+              tests/test_utf8_oracle.py tests/test_route.py
 build/asan/libnetc.so: $(HOST_SRCS) $(HOST_HDRS)
 	@mkdir -p build/asan
 	$(CC) $(ASAN_FLAGS) -Wall -fPIC -std=gnu11 -shared -o $@ $(HOST_SRCS) -lpthread
