@@ -752,9 +752,11 @@ __device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint
         // not a candidate: pruned by K1 (the chain dies at y), or its bucket overflowed
         if (next < 0 && !quick_reject(a, y)) atomicOr(a.ovf, kOvfLink);
     }
-    a.link[node] = next;
-    a.nterm[node] = v;
-    a.ncnt[node] = cnt;
+    // relaxed agent-scope (sc1) stores: K3a may read them in the same launch from another XCD
+    // (scan_links_fused), with sc1 loads only
+    __hip_atomic_store(&a.link[node], next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.nterm[node], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.ncnt[node], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Every position of the chunk that can start a header (strict: passes the quick
@@ -1053,9 +1055,13 @@ __device__ void links_body(const ScanArgs& a, LinksLds& sl) {
             for (int j = kCand - 1; j >= 0; --j)
                 if ((uint32_t)j < i && cs[j] == x) dup = j;   // the first earlier slot with x
             if (dup >= 0) {
-                a.link[s] = kDupLink;
-                a.ncnt[s] = 0;
-                if (a.ext[s]) a.ext[c * kCand + dup] = 1;
+                __hip_atomic_store(&a.link[s], kDupLink, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&a.ncnt[s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (a.ext[s]) {   // (K1's flag, the previous launch) passed on to the first slot: an atomic
+                    const uint64_t b = c * kCand + (uint64_t)dup;   // on the flag's 32-bit word (sc1 for K3a)
+                    __hip_atomic_fetch_or((uint32_t*)(a.ext + (b & ~3ull)), 1u << (8 * (b & 3)), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                }
             } else {
                 const uint64_t B = c * kChunk;
                 uint32_t cnt = 0;
@@ -1288,14 +1294,17 @@ __device__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
     // the chunk's counter, external flags, links and counts in one trip
     const bool live = c <= a.nc;
     const uint32_t cnt = live ? min(a.ccount[c], (uint32_t)kCand) : 0;
-    const uint64_t exf = live ? *(const uint64_t*)(a.ext + c * kCand) : 0;   // kCand == 8 flag bytes
+    // (K2's outputs by relaxed agent-scope loads: scan_links_fused hands them over in-launch)
+    const uint64_t exf = live ? __hip_atomic_load((const uint64_t*)(a.ext + c * kCand), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)
+                              : 0;   // kCand == 8 flag bytes
     int32_t lks[kCand];
     uint32_t nws[kCand];
     uint32_t rootm = 0;   // the slot holding the stream start
 #pragma unroll
     for (int j = 0; j < kCand; ++j) {
-        lks[j] = live ? a.link[c * kCand + j] : kDupLink;
-        nws[j] = live ? a.ncnt[c * kCand + j] : 0;
+        lks[j] = live ? __hip_atomic_load(&a.link[c * kCand + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kDupLink;
+        nws[j] = live ? __hip_atomic_load(&a.ncnt[c * kCand + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     }
     if (live && c == a.start / kChunk) {   // only the stream start's chunk holds the root
 #pragma unroll
@@ -1389,9 +1398,9 @@ __device__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
         TileExt e;
         e.slot = (uint32_t)(s0 + gsl[k]);
         e.w = W[k];
-        e.xl = a.link[last];
+        e.xl = __hip_atomic_load(&a.link[last], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         e.root = eroot[t];
-        e.term = a.nterm[last];
+        e.term = __hip_atomic_load(&a.nterm[last], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         put_text(&a.text[tile * kExt + t], e);
     }
     if (t == 0) __hip_atomic_store(&a.tcount[tile], (uint32_t)E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1710,18 +1719,23 @@ union FusedLds {
 };
 
 // true in every thread of the block that arrives last at *counter (of `expect`)
+// Round 4: the hand-offs need no fences.  Every byte a later phase of the launch reads is stored
+// with a relaxed agent-scope (sc1) store and read with sc1 loads only (link_node, the dup flags,
+// tiles_body's first trip and records, put_text / get_text); each wave waits for its stores, the
+// block's barrier follows, then one lane adds to the arrival counter (MI355X_MICROARCH.md,
+// cross-workgroup hand-offs).  The round-3 form -- a release fence by every block, an acquire by
+// the last -- wrote back each XCD's L2 per block and measured 261 us at config 2.
 __device__ __forceinline__ bool arrive_last(uint32_t* counter, uint32_t expect, int* flag) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this thread's results (release only: no L2 invalidate)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 stores have completed
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t old = atomicAdd(counter, 1u);
+        const uint32_t old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *flag = old == expect - 1;
-        if (*flag) atomicExch(counter, 0u);   // every block has arrived: reset for the next call
+        if (*flag)   // every block has arrived: reset for the next call
+            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    const bool last = *flag != 0;
-    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other blocks' results
-    return last;
+    return *flag != 0;
 }
 
 __global__ __launch_bounds__(kScanT) void scan_links_fused(ScanArgs a, uint64_t tiles, uint32_t blocks) {
@@ -2274,9 +2288,13 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     // K2, K3a, K3b: by default K2 and then K3a + K3b as one launch up to kMergeTiles (256) tiles
     // (scan_tiles_resolve), three launches above.  NETC_GPU_KNOB_SCAN_FUSE (tests and A/B):
     // 0 three launches at every size; 1 K2 + K3a + K3b as one launch up to kFuseTiles tiles
-    // (scan_links_fused: every block's agent-scope release is a buffer_wbl2 sc1 -- a write-back
-    // of its XCD's L2 -- and at config 2 a thousand blocks arrive: 128 us against 43 us for the
-    // three launches, profiles/r03b_scan_fuse_ab.json).
+    // (scan_links_fused.  Round 3 handed K2's outputs over with a release fence per block -- a
+    // write-back of its XCD's L2 -- and measured 128 us against 43 us at config 2,
+    // profiles/r03b_scan_fuse_ab.json.  Round 4 hands them over with sc1 stores and loads and no
+    // fence (arrive_last): 56 against 41 us at config 2, 123 against 81-84 us at config 4,
+    // profiles/r04gg_scan_fuse_sc1.json -- the tiles' K3a still waits for each tile's slowest K2
+    // block and K3b for the last tile, so the overlap saves little, while the launch runs at the
+    // fused LDS footprint and spills.  Not the default.)
     const int64_t fuse = knob(NETC_GPU_KNOB_SCAN_FUSE);
     if (fuse == 1 && tiles <= (uint64_t)kFuseTiles) {
         hipLaunchKernelGGL(scan_links_fused, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
