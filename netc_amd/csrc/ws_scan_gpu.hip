@@ -735,8 +735,22 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     if (ovf) atomicOr(a.ovf, kOvfSet);
 }
 
+// K2 -> K3a words: plain, or (SC1: scan_links_fused, K3a in the same launch, maybe on another XCD)
+// relaxed agent-scope stores and loads, which go through to the memory-side caches
+template <bool SC1, typename T>
+__device__ __forceinline__ void hand_st(T* p, T v) {
+    if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+template <bool SC1, typename T>
+__device__ __forceinline__ T hand_ld(const T* p) {
+    if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+
 // node -> the candidate its chain exits to (the first slot holding that position, or
 // -1) and the terminal where it ends
+template <bool SC1>
 __device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint64_t x, uint64_t v, uint32_t cnt) {
     int32_t next = -1;
     if (term_type(v) == kExit) {
@@ -752,11 +766,9 @@ __device__ __forceinline__ void link_node(const ScanArgs& a, uint64_t node, uint
         // not a candidate: pruned by K1 (the chain dies at y), or its bucket overflowed
         if (next < 0 && !quick_reject(a, y)) atomicOr(a.ovf, kOvfLink);
     }
-    // relaxed agent-scope (sc1) stores: K3a may read them in the same launch from another XCD
-    // (scan_links_fused), with sc1 loads only
-    __hip_atomic_store(&a.link[node], next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.nterm[node], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.ncnt[node], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hand_st<SC1>(&a.link[node], next);
+    hand_st<SC1>(&a.nterm[node], v);
+    hand_st<SC1>(&a.ncnt[node], cnt);
 }
 
 // Every position of the chunk that can start a header (strict: passes the quick
@@ -770,7 +782,7 @@ static constexpr int kAncStride = 8;                              // frames per 
 static constexpr int kAncMax = (int)(kChunk / 2 / kAncStride) + 1;   // a frame is 2 bytes or more
 static constexpr int kAncSlot = kAncMax + 1;                         // uint16 per slot (4-byte multiple)
 
-__device__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const uint32_t* words, uint16_t* l1,
+__device__ __forceinline__ const uint16_t* chunk_links16(const ScanArgs& a, uint64_t B, const uint32_t* words, uint16_t* l1,
                                          uint16_t* lj, uint16_t* lk16) {
     const int tid = threadIdx.x;
     const uint64_t Bend = B + kChunk;
@@ -925,7 +937,8 @@ __device__ __forceinline__ void chunk_regs_store(uint32_t* words, const ChunkReg
 // One queued node by the calling wavefront, its chunk's words already in d.words (see DenseLds);
 // false (wave-uniform, nothing written) leaves it to the block path.  qi: its queue index
 // (anchor slot as the block path).  x: the node's position (a.cand[node]).
-__device__ bool dense_node(const ScanArgs& a, DenseLds& d, uint64_t node, uint64_t x, uint32_t qi DENSE_ARG) {
+template <bool SC1>
+__device__ __forceinline__ bool dense_node(const ScanArgs& a, DenseLds& d, uint64_t node, uint64_t x, uint32_t qi DENSE_ARG) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
     DENSE_T(1);
@@ -1018,7 +1031,7 @@ __device__ bool dense_node(const ScanArgs& a, DenseLds& d, uint64_t node, uint64
             pp = v;
         }
         DENSE_T(5);
-        link_node(a, node, x, v, hops);
+        link_node<SC1>(a, node, x, v, hops);
         DENSE_T(6);
         DENSE_ADD(4, 4, 5);
         DENSE_ADD(5, 5, 6);
@@ -1030,7 +1043,8 @@ __device__ bool dense_node(const ScanArgs& a, DenseLds& d, uint64_t node, uint64
     return __builtin_amdgcn_readfirstlane(ok) != 0;
 }
 
-__device__ void links_body(const ScanArgs& a, LinksLds& sl) {
+template <bool SC1>
+__device__ __forceinline__ void links_body(const ScanArgs& a, LinksLds& sl) {
     uint32_t* words = sl.b.words;
     uint16_t* l1 = sl.b.l1;
     uint16_t* lj = sl.b.lj;
@@ -1055,12 +1069,15 @@ __device__ void links_body(const ScanArgs& a, LinksLds& sl) {
             for (int j = kCand - 1; j >= 0; --j)
                 if ((uint32_t)j < i && cs[j] == x) dup = j;   // the first earlier slot with x
             if (dup >= 0) {
-                __hip_atomic_store(&a.link[s], kDupLink, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&a.ncnt[s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (a.ext[s]) {   // (K1's flag, the previous launch) passed on to the first slot: an atomic
-                    const uint64_t b = c * kCand + (uint64_t)dup;   // on the flag's 32-bit word (sc1 for K3a)
-                    __hip_atomic_fetch_or((uint32_t*)(a.ext + (b & ~3ull)), 1u << (8 * (b & 3)), __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
+                hand_st<SC1>(&a.link[s], kDupLink);
+                hand_st<SC1>(&a.ncnt[s], 0u);
+                if (a.ext[s]) {   // (K1's flag, the previous launch) passed on to the first slot
+                    const uint64_t b = c * kCand + (uint64_t)dup;
+                    if constexpr (SC1)   // an atomic on the flag's 32-bit word
+                        __hip_atomic_fetch_or((uint32_t*)(a.ext + (b & ~3ull)), 1u << (8 * (b & 3)), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+                    else
+                        a.ext[b] = 1;
                 }
             } else {
                 const uint64_t B = c * kChunk;
@@ -1086,7 +1103,7 @@ __device__ void links_body(const ScanArgs& a, LinksLds& sl) {
                     queue[atomicAdd(&nq, 1)] = (uint32_t)s;
                 } else {
                     a.anq[s] = ~0u;
-                    link_node(a, s, x, v, cnt);
+                    link_node<SC1>(a, s, x, v, cnt);
                 }
             }
         }
@@ -1113,7 +1130,7 @@ __device__ void links_body(const ScanArgs& a, LinksLds& sl) {
             const int qn = qi + kScanT / kWave;
             rfast = qn < n && chunk_regs_load(a, (uint64_t)queue[qn] / kCand * kChunk, lane, R);
             wave_lds_sync();
-            if (dense_node(a, d, node, x, (uint32_t)qi DENSE_PASS) && lane == 0) queue[qi] = ~0u;
+            if (dense_node<SC1>(a, d, node, x, (uint32_t)qi DENSE_PASS) && lane == 0) queue[qi] = ~0u;
             wave_lds_sync();   // (the next chunk overwrites d)
         }
         DENSE_FLUSH();
@@ -1152,7 +1169,7 @@ __device__ void links_body(const ScanArgs& a, LinksLds& sl) {
                 v = term(kExit, v);
                 ++hops;
             }
-            link_node(a, node, x, v, hops);
+            link_node<SC1>(a, node, x, v, hops);
         }
         __syncthreads();
     }
@@ -1161,7 +1178,7 @@ __device__ void links_body(const ScanArgs& a, LinksLds& sl) {
 __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
     __shared__ LinksLds sl;
     SCAN_SCOPE(1);
-    links_body(a, sl);
+    links_body<false>(a, sl);
 }
 
 // exclusive prefix sum over a block of NT threads; the block total in *total
@@ -1273,7 +1290,8 @@ struct TilesLds {
     int skip;
 };
 
-__device__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
+template <bool SC1>
+__device__ __forceinline__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
     uint16_t* cid = st.cid;
     uint16_t* gsl = st.gsl;
     uint16_t* P = st.P;
@@ -1294,17 +1312,15 @@ __device__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
     // the chunk's counter, external flags, links and counts in one trip
     const bool live = c <= a.nc;
     const uint32_t cnt = live ? min(a.ccount[c], (uint32_t)kCand) : 0;
-    // (K2's outputs by relaxed agent-scope loads: scan_links_fused hands them over in-launch)
-    const uint64_t exf = live ? __hip_atomic_load((const uint64_t*)(a.ext + c * kCand), __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT)
-                              : 0;   // kCand == 8 flag bytes
+    // (SC1: K2's outputs handed over in the same launch, scan_links_fused)
+    const uint64_t exf = live ? hand_ld<SC1>((const uint64_t*)(a.ext + c * kCand)) : 0;   // kCand == 8 flag bytes
     int32_t lks[kCand];
     uint32_t nws[kCand];
     uint32_t rootm = 0;   // the slot holding the stream start
 #pragma unroll
     for (int j = 0; j < kCand; ++j) {
-        lks[j] = live ? __hip_atomic_load(&a.link[c * kCand + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kDupLink;
-        nws[j] = live ? __hip_atomic_load(&a.ncnt[c * kCand + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        lks[j] = live ? hand_ld<SC1>(&a.link[c * kCand + j]) : kDupLink;
+        nws[j] = live ? hand_ld<SC1>(&a.ncnt[c * kCand + j]) : 0;
     }
     if (live && c == a.start / kChunk) {   // only the stream start's chunk holds the root
 #pragma unroll
@@ -1398,9 +1414,9 @@ __device__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
         TileExt e;
         e.slot = (uint32_t)(s0 + gsl[k]);
         e.w = W[k];
-        e.xl = __hip_atomic_load(&a.link[last], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        e.xl = hand_ld<SC1>(&a.link[last]);
         e.root = eroot[t];
-        e.term = __hip_atomic_load(&a.nterm[last], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        e.term = hand_ld<SC1>(&a.nterm[last]);
         put_text(&a.text[tile * kExt + t], e);
     }
     if (t == 0) __hip_atomic_store(&a.tcount[tile], (uint32_t)E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1409,7 +1425,7 @@ __device__ void tiles_body(const ScanArgs& a, uint64_t tile, TilesLds& st) {
 __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
     __shared__ TilesLds st;
     SCAN_SCOPE(2);
-    tiles_body(a, blockIdx.x, st);
+    tiles_body<false>(a, blockIdx.x, st);
 }
 
 // Tile resolution (K3b): the external nodes of all tiles into LDS (tile by tile, in
@@ -1501,7 +1517,7 @@ __device__ void resolve_fast(uint16_t* succ, uint64_t* R, uint16_t* succ2, uint6
 // every thread of the block; on return (after a barrier) sm.bad / sm.why say whether the
 // parallel path holds, and R / mark / islast / toff answer per-tile queries
 template <int NT, int PER, int MAXT, int CAP>
-__device__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT, CAP, NT * PER>& sm) {
+__device__ __forceinline__ void resolve_tiles(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT, CAP, NT * PER>& sm) {
     const int t = threadIdx.x;
     if (tiles > (uint64_t)MAXT) {   // kernel-uniform
         if (t == 0) {
@@ -1686,7 +1702,7 @@ __device__ TileInfo tile_info(const ScanArgs& a, const ResolveLds<MAXT, CAP, PP>
 // K3b: one block resolves every tile, writes each tile's entry (tinfo) and whether K4
 // walks serially (flags[8], the reason in flags[9])
 template <int NT, int PER, int MAXT, int CAP>
-__device__ void resolve_body(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT, CAP, NT * PER>& sm) {
+__device__ __forceinline__ void resolve_body(const ScanArgs& a, uint64_t tiles, ResolveLds<MAXT, CAP, NT * PER>& sm) {
     resolve_tiles<NT, PER>(a, tiles, sm);
     if (!sm.bad)
         for (uint64_t tl = threadIdx.x; tl < tiles; tl += NT) a.tinfo[tl] = tile_info(a, sm, tl, true);
@@ -1742,12 +1758,12 @@ __global__ __launch_bounds__(kScanT) void scan_links_fused(ScanArgs a, uint64_t 
     __shared__ FusedLds sm;
     __shared__ int flag;
     SCAN_SCOPE(1);
-    links_body(a, sm.k2);
+    links_body<true>(a, sm.k2);
     constexpr uint32_t kPerTile = (uint32_t)(kTileChunks / kBlkChunks);
     const uint32_t tile = blockIdx.x / kPerTile;
     const uint32_t in_tile = min(blocks - tile * kPerTile, kPerTile);
     if (!arrive_last(a.tarr + tile, in_tile, &flag)) return;   // block-uniform
-    tiles_body(a, tile, sm.k3a);
+    tiles_body<true>(a, tile, sm.k3a);
     if (!arrive_last(a.flags + 12, (uint32_t)tiles, &flag)) return;
     resolve_body<kScanT, kFuseCap / kScanT>(a, tiles, sm.k3b);
 }
@@ -1776,7 +1792,7 @@ __global__ __launch_bounds__(kScanT) void scan_tiles_resolve(ScanArgs a, uint64_
     __shared__ MergedLds sm;
     __shared__ int last;
     SCAN_SCOPE(2);
-    tiles_body(a, blockIdx.x, sm.k3a);
+    tiles_body<false>(a, blockIdx.x, sm.k3a);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 stores have completed
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2291,10 +2307,12 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     // (scan_links_fused.  Round 3 handed K2's outputs over with a release fence per block -- a
     // write-back of its XCD's L2 -- and measured 128 us against 43 us at config 2,
     // profiles/r03b_scan_fuse_ab.json.  Round 4 hands them over with sc1 stores and loads and no
-    // fence (arrive_last): 56 against 41 us at config 2, 123 against 81-84 us at config 4,
-    // profiles/r04gg_scan_fuse_sc1.json -- the tiles' K3a still waits for each tile's slowest K2
+    // fence (arrive_last), hand_st / hand_ld on this launch only: 56 against 41 us at config 2,
+    // profiles/r04gg_scan_fuse_sc1.json; with the bodies inlined (no call, scratch 272 -> 36 B
+    // per lane) 43.3 against 41.3 us at config 2, 96 against 82 us at config 4,
+    // profiles/r04ii_scan_fuse.json -- the tiles' K3a still waits for each tile's slowest K2
     // block and K3b for the last tile, so the overlap saves little, while the launch runs at the
-    // fused LDS footprint and spills.  Not the default.)
+    // fused LDS footprint (4 blocks per CU against K2's 5).  Not the default.)
     const int64_t fuse = knob(NETC_GPU_KNOB_SCAN_FUSE);
     if (fuse == 1 && tiles <= (uint64_t)kFuseTiles) {
         hipLaunchKernelGGL(scan_links_fused, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
