@@ -140,6 +140,9 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *   MASK_TAPER         bytes at the end of a netc_gpu_mask_batch batch walked in one-step
  *                      windows instead of two-step ones, so the launch's last waves are
  *                      short and finish together [0]               (NETC_MASK_TAPER)
+ *   ENC_FIX            where netc_gpu_encode_frames composes the 16-B vectors holding header
+ *                      bytes: 0 trailing blocks of the assembly launch; 1 the wire-offsets
+ *                      scan (measured slower) [0]                   (NETC_ENC_FIX)
  */
 #define NETC_GPU_KNOB_ENC_DENSE_BYTES   1
 #define NETC_GPU_KNOB_ENC_SCAN_PER      2
@@ -149,6 +152,7 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
 #define NETC_GPU_KNOB_SCAN_FUSE         6
 #define NETC_GPU_KNOB_MASK_TAPER        7
 #define NETC_GPU_KNOB_ENC_SRC           8
+#define NETC_GPU_KNOB_ENC_FIX           9
 int netc_gpu_knob(int knob, int64_t value);
 
 /**

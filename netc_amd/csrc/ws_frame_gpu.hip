@@ -10,7 +10,7 @@
 // key always follows the MASK bit, also for an empty payload (RFC 6455 §5.2; the
 // reference omits it there, defect B9 in DESIGN.md).
 //
-// Three kernels on the caller's stream:
+// Two launches on the caller's stream:
 //   1. wire offsets: wo[j] = sum over k < j of (header_len(k) + len(k)), a
 //      single-pass chained scan over the frames (decoupled look-back, 64
 //      predecessors inspected at once);
@@ -19,14 +19,14 @@
 //      in ws_mask_gpu.hip.  A 64-entry frame table in VGPRs (wire start, payload
 //      offset, key, header byte of 64 consecutive frames) places each vector:
 //      one unaligned 16-B load, one XOR with the key of the frame holding the
-//      vector's first byte, rotated to its phase, one aligned store.  Spans the
-//      table does not cover (more than ~60 frames in 1 KiB) and the buffer edges
-//      are queued;
-//   3. the queued spans, composed byte-exactly per lane from every frame they
-//      touch; then per frame (one thread each) the header and the payload bytes
-//      after it in the header's vector, which step 2 mapped through the previous
-//      frame.  A batch averaging under 80 B of payload per frame skips step 2 and
-//      the per-frame fixups: step 3 composes every span.
+//      vector's first byte, rotated to its phase, one aligned store -- of the
+//      vectors that hold no header byte only.  Spans the table does not cover
+//      (more than ~60 frames in 1 KiB) and the buffer edges are listed per
+//      wavefront and composed byte-exactly by it after its chunks; the launch's
+//      trailing blocks compose, one thread per frame, the vectors holding each
+//      frame's header bytes (fix_vectors).
+//   A batch averaging under 80 B of payload per frame takes a compose launch
+//   instead of step 2 (encode_queued_kernel: every span composed per lane).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -74,69 +74,6 @@ __device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total) {
     return before + inc - v;
 }
 
-// One tile = kScanBlock frames.  The offsets go through LDS both ways so that every
-// global access is coalesced (thread t owns frames t*16 .. t*16+15 of the tile: read
-// straight from HBM, each load instruction would touch 64 cache lines, and with one
-// tile per CU that strided traffic, not the scan, set the kernel's time).
-template <int kScanPer>
-__global__ __launch_bounds__(kScanThreads) void wire_offsets_chained(const uint64_t* off, uint64_t n, uint32_t fixed,
-                                                                     uint64_t* wo, uint64_t* status, uint32_t epoch,
-                                                                     uint32_t* defer_count) {
-    constexpr uint64_t kScanBlock = (uint64_t)kScanThreads * kScanPer;   // frames per tile
-    __shared__ uint64_t tile_prefix;
-    __shared__ uint64_t v[kScanBlock + kScanBlock / kScanPer + 1];   // entry j at j + j / kScanPer
-    auto pos = [](uint32_t j) { return j + j / kScanPer; };
-    const uint64_t tile = blockIdx.x, base = tile * kScanBlock;
-    const uint32_t t0 = threadIdx.x * kScanPer;   // this thread's frames: base + t0 ..
-    if (tile == 0 && threadIdx.x == 0) *defer_count = 0;   // (a spare word of the scratch; no reader since round 4)
-#pragma unroll
-    for (int i = 0; i < kScanPer; ++i) {
-        const uint32_t j = i * kScanThreads + threadIdx.x;
-        v[pos(j)] = gptr(off)[base + j < n ? base + j : n];
-    }
-    if (threadIdx.x == 0) v[pos(kScanBlock)] = gptr(off)[base + kScanBlock < n ? base + kScanBlock : n];
-    const uint64_t off0 = gptr(off)[0];
-    __syncthreads();
-    uint64_t o[kScanPer + 1];
-#pragma unroll
-    for (int i = 0; i <= kScanPer; ++i) o[i] = v[pos(t0 + i)];
-    uint32_t e[kScanPer];
-    uint64_t s = 0;
-#pragma unroll
-    for (int i = 0; i < kScanPer; ++i) {
-        e[i] = base + t0 + i < n ? ext_len(o[i + 1] - o[i]) : 0u;
-        s += e[i];
-    }
-    uint64_t agg;
-    const uint64_t ex = block_exclusive_scan(s, &agg);   // its barriers also end the LDS reads above
-    if (threadIdx.x < kWave) {
-        const int lane = threadIdx.x;
-        if (lane == 0)
-            __hip_atomic_store(&status[tile], status_word(tile == 0 ? 2 : 1, epoch, agg), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t prefix = tile == 0 ? 0 : look_back(status, (int64_t)tile, epoch, lane);
-        if (lane == 0) {
-            if (tile) __hip_atomic_store(&status[tile], status_word(2, epoch, prefix + agg), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-            tile_prefix = prefix;
-        }
-    }
-    __syncthreads();
-    uint64_t run = tile_prefix + ex;
-#pragma unroll
-    for (int i = 0; i < kScanPer; ++i) {
-        const uint64_t j = base + t0 + i;
-        v[pos(t0 + i)] = (o[i] - off0) + (uint64_t)fixed * j + run;
-        run += e[i];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kScanPer; ++i) {
-        const uint32_t j = i * kScanThreads + threadIdx.x;
-        if (base + j <= n) gptr(wo)[base + j] = v[pos(j)];
-    }
-}
-
 // ---------------------------------------------------------------- assembly --
 
 struct EncArgs {
@@ -156,6 +93,7 @@ struct EncArgs {
     uint32_t all_spans;        // dense batch: the compose launch takes every span (no assembly launch)
     uint32_t main_blocks;      // encode_frames_kernel: blocks 0 .. main_blocks-1 assemble, the rest fix headers
     uint32_t per_wave;         // ... each assembly wavefront lists its unmapped spans at defer[wave * per_wave ..]
+    uint32_t fix_blocks;       // 1: the header vectors by trailing blocks of the assembly (0: by the scan, or none needed)
     // source-driven assembly (encode_src_kernel)
     const uint8_t* src_base;   // src rounded down to 16 (P coordinates: byte q of src is at P = q + smis)
     uint64_t smis;             // src & 15
@@ -608,15 +546,22 @@ __device__ __forceinline__ void finish_chunk(const EncArgs& a, const EncTable& t
 }
 
 // The wire vector at V (W coordinates, 16-aligned), byte-exact, by one thread: every frame from
-// j0 (the frame holding byte V) to the last one starting inside it -- header bytes from
-// build_header, payload bytes from one 16-B source load each -- then one store.
-__device__ void compose_thread(const EncArgs& a, uint64_t V, int64_t j0, uint64_t wlo, uint64_t whi) {
+// j0 (the frame holding byte V, its header at S, its payload at o) to the last one starting
+// inside it -- header bytes from build_header, payload bytes from one 16-B source load each --
+// then one store.  The later frames' starts follow from off[] alone (wo[j + 1] = wo[j] +
+// header_len + len), so this runs before wo[] is complete (in the wire-offsets scan); the wire
+// ends where frame n would start.
+__device__ __forceinline__ void compose_from(const EncArgs& a, uint64_t V, uint64_t j0, uint64_t S, uint64_t o, uint64_t wlo) {
     const bool masked = a.masked != 0;
     u32x4 out = {0, 0, 0, 0};
-    uint64_t S = gptr(a.wo)[j0] + a.wmis, o = gptr(a.off)[j0];
-    for (int64_t j = j0; j < (int64_t)a.n && S < V + 16; ++j) {
-        const uint64_t Sn = gptr(a.wo)[j + 1] + a.wmis, on = gptr(a.off)[j + 1];
-        const uint64_t len = on - o, pw = S + header_len(len, masked);
+    uint64_t whi = kInf;
+    for (uint64_t j = j0; S < V + 16; ++j) {
+        if (j >= a.n) {
+            whi = S;
+            break;
+        }
+        const uint64_t on = gptr(a.off)[j + 1];
+        const uint64_t len = on - o, pw = S + header_len(len, masked), Sn = pw + len;
         const uint32_t key = masked ? gptr(a.keys)[j] : 0u;
         const int64_t hs = (int64_t)(S - V), he = (int64_t)(pw - V), phi = (int64_t)(Sn - V);
         if (he > 0 && hs < 16) {
@@ -649,58 +594,208 @@ __device__ void compose_thread(const EncArgs& a, uint64_t V, int64_t j0, uint64_
 // trailing blocks could take the queued spans -- 5,120 same-address atomics at the end of the
 // launch tripled it (79 us) -- and the trailing blocks resident beside the assembly (fewer
 // assembly blocks: 39.8-40.2 / 462-463 us).)
-__device__ __forceinline__ void fix_vectors(const EncArgs& a, uint64_t k, uint64_t wlo, uint64_t whi) {
-    const bool masked = a.masked != 0;
-    // frames k - 1, k, k + 1 in one trip (k - 1 clamped: its values are unused for k = 0)
-    const uint64_t kp = k > 0 ? k - 1 : 0;
-    const uint64_t Sp = gptr(a.wo)[kp] + a.wmis, S = gptr(a.wo)[k] + a.wmis, Sn = gptr(a.wo)[k + 1] + a.wmis;
-    const uint64_t op = gptr(a.off)[kp], o = gptr(a.off)[k], on = gptr(a.off)[k + 1];
-    const uint32_t keyp = masked ? gptr(a.keys)[kp] : 0u, key = masked ? gptr(a.keys)[k] : 0u;
-    const uint32_t b0 = a.b0 ? (uint32_t)gptr(a.b0)[k] : 0x82u;
-    const uint64_t len = on - o, hl = header_len(len, masked), pw = S + hl;
-    const uint64_t v0 = S & ~15ull, v1 = (pw - 1) & ~15ull;
-    const bool own0 = k == 0 || ((Sp + header_len(o - op, masked) - 1) & ~15ull) < v0;
+// Frame k's header at S (W coordinates); its payload [o, on), frame k - 1's [op, o) (k > 0);
+// the keys of both and frame k's header byte.  fix_plan places the (one or two) vectors holding
+// frame k's header bytes that frame k owns -- the first is frame k - 1's when k - 1's header
+// reaches into it -- and issues their payload loads; fix_store composes and stores them.  The
+// split lets a thread issue the loads of several frames before its first store (the compiler
+// may not move a load above a store that could alias it: four frames fixed one after the other
+// were four round trips).  Every byte written lies in frames k - 1 and k (the simple case), or
+// comes from compose_from, so no wire end is needed here.
+struct FixGeo {   // frame k's fixup geometry (fix_geo)
+    uint64_t pw, Sn, len, v0, v1;
+    bool own0, simple;
+};
+
+__device__ __forceinline__ FixGeo fix_geo(const EncArgs& a, uint64_t k, uint64_t S, uint64_t op, uint64_t o, uint64_t on) {
+    FixGeo g;
+    g.len = on - o;
+    g.pw = S + header_len(g.len, a.masked != 0);
+    g.Sn = g.pw + g.len;
+    const uint64_t hpe = S - (o - op);   // frame k - 1's payload start (k > 0)
+    g.v0 = S & ~15ull;
+    g.v1 = (g.pw - 1) & ~15ull;
+    g.own0 = k == 0 || ((hpe - 1) & ~15ull) < g.v0;
     // the usual case: the vectors hold only frame k - 1's payload tail, frame k's header and frame
     // k's payload (frame k ends at or past the last one); the payload bytes by one load per frame
-    const bool simple = Sn >= v1 + 16 && (k == 0 || v0 >= S || v0 >= Sp + header_len(o - op, masked));
-    if (!simple) {   // small frames: the general walk
-        if (own0) compose_thread(a, v0, (k > 0 && v0 < S) ? (int64_t)k - 1 : (int64_t)k, wlo, whi);
-        if (v1 != v0) compose_thread(a, v1, (int64_t)k, wlo, whi);
+    g.simple = g.Sn >= g.v1 + 16 && (k == 0 || g.v0 >= S || g.v0 >= hpe);
+    return g;
+}
+
+__device__ __forceinline__ u32x4 fix_load(const EncArgs& a, int64_t s0, int lo, int hi) {
+    if (s0 >= 0 && (uint64_t)s0 + 16 <= a.src_total) return load_u<false>(a.src + s0);
+    return load_guarded(a, s0, lo, hi);
+}
+
+// the payload loads of the simple case: frame k's bytes for v0 (ld[0]) and v1 (ld[2]), frame
+// k - 1's tail for v0 (ld[1])
+__device__ __forceinline__ void fix_plan(const EncArgs& a, uint64_t k, uint64_t S, uint64_t op, uint64_t o, uint64_t on,
+                                         u32x4 (&ld)[3]) {
+    const FixGeo g = fix_geo(a, k, S, op, o, on);
+    ld[0] = ld[1] = ld[2] = u32x4{0, 0, 0, 0};
+    if (!g.simple) return;
+    const int64_t phi0 = (int64_t)g.Sn - (int64_t)g.v0, phi1 = (int64_t)g.Sn - (int64_t)g.v1;
+    const int64_t plo0 = (int64_t)g.pw - (int64_t)g.v0, plo1 = (int64_t)g.pw - (int64_t)g.v1;
+    if (g.own0) {
+        if (plo0 < 16 && g.len) ld[0] = fix_load(a, (int64_t)o - plo0, plo0 < 0 ? 0 : (int)plo0, phi0 > 16 ? 16 : (int)phi0);
+        if (g.v0 < S && k > 0) ld[1] = fix_load(a, (int64_t)o - ((int64_t)S - (int64_t)g.v0), 0, (int)((int64_t)S - (int64_t)g.v0));
+    }
+    if (g.v1 != g.v0 && plo1 < 16 && g.len)
+        ld[2] = fix_load(a, (int64_t)o - plo1, plo1 < 0 ? 0 : (int)plo1, phi1 > 16 ? 16 : (int)phi1);
+}
+
+__device__ __forceinline__ void fix_store(const EncArgs& a, uint64_t k, uint64_t S, uint64_t op, uint64_t o, uint64_t on,
+                                          uint32_t keyp, uint32_t key, uint32_t b0, const u32x4 (&ld)[3], uint64_t wlo) {
+    const bool masked = a.masked != 0;
+    const FixGeo g = fix_geo(a, k, S, op, o, on);
+    if (!g.simple) {   // small frames: the general walk
+        if (g.own0) {
+            if (k > 0 && g.v0 < S) compose_from(a, g.v0, k - 1, S - header_len(o - op, masked) - (o - op), op, wlo);
+            else compose_from(a, g.v0, k, S, o, wlo);
+        }
+        if (g.v1 != g.v0) compose_from(a, g.v1, k, S, o, wlo);
         return;
     }
     uint64_t hlo, hhi;
-    build_header(b0, len, masked, key, hlo, hhi);
-    auto vec = [&](uint64_t V) {
+    build_header(b0, g.len, masked, key, hlo, hhi);
+    auto vec = [&](uint64_t V, const u32x4& pa, const u32x4& pb) {
         u32x4 out = shift_bytes(hlo, hhi, (int)((int64_t)S - (int64_t)V)) &
-                    select_range((int64_t)S - (int64_t)V, (int64_t)pw - (int64_t)V);
+                    select_range((int64_t)S - (int64_t)V, (int64_t)g.pw - (int64_t)V);
         // frame k's payload bytes [pw, V + 16)
-        const int64_t plo = (int64_t)pw - (int64_t)V;
-        if (plo < 16 && len) {
-            const int64_t s0 = (int64_t)o - plo;
-            const int64_t phi = (int64_t)Sn - (int64_t)V;
-            u32x4 v;
-            if (s0 >= 0 && (uint64_t)s0 + 16 <= a.src_total) v = load_u<false>(a.src + s0);
-            else v = load_guarded(a, s0, plo < 0 ? 0 : (int)plo, phi > 16 ? 16 : (int)phi);
+        const int64_t plo = (int64_t)g.pw - (int64_t)V;
+        if (plo < 16 && g.len) {
             const uint32_t rk = rotr8(key, (uint64_t)(-plo));
             const u32x4 kv = {rk, rk, rk, rk};
-            out |= (v ^ kv) & select_range(plo, phi);
+            out |= (pa ^ kv) & select_range(plo, (int64_t)g.Sn - (int64_t)V);
         }
-        // frame k - 1's payload bytes [V, S)
+        // frame k - 1's payload bytes [V, S): its payload ends at o (= off[k]); the phase of
+        // byte 0 is its offset in frame k - 1's payload
         if (V < S && k > 0) {
-            const int64_t e = (int64_t)S - (int64_t)V;   // bytes of frame k - 1 in the vector
-            const int64_t s0 = (int64_t)o - e;           // its payload ends at o (= off[k])
-            u32x4 v;
-            if (s0 >= 0 && (uint64_t)s0 + 16 <= a.src_total) v = load_u<false>(a.src + s0);
-            else v = load_guarded(a, s0, 0, (int)e);
-            // phase of byte 0: its offset in frame k - 1's payload, s0 - op
-            const uint32_t rk = rotr8(keyp, (uint64_t)(s0 - (int64_t)op));
+            const int64_t e = (int64_t)S - (int64_t)V;
+            const uint32_t rk = rotr8(keyp, (uint64_t)((int64_t)o - e - (int64_t)op));
             const u32x4 kv = {rk, rk, rk, rk};
-            out |= (v ^ kv) & select_range(0, e);
+            out |= (pb ^ kv) & select_range(0, e);
         }
-        store_wire<false>(a, V, out, wlo, whi);
+        store_wire<false>(a, V, out, wlo, kInf);
     };
-    if (own0) vec(v0);
-    if (v1 != v0) vec(v1);
+    if (g.own0) vec(g.v0, ld[0], ld[1]);
+    if (g.v1 != g.v0) vec(g.v1, ld[2], ld[2]);
+}
+
+__device__ __forceinline__ void fix_vectors(const EncArgs& a, uint64_t k, uint64_t wlo) {
+    const bool masked = a.masked != 0;
+    // frame k's header start and frames k - 1, k, k + 1's payload offsets in one trip (k - 1
+    // clamped: its values are unused for k = 0)
+    const uint64_t kp = k > 0 ? k - 1 : 0;
+    const uint64_t S = gptr(a.wo)[k] + a.wmis;
+    const uint64_t op = gptr(a.off)[kp], o = gptr(a.off)[k], on = gptr(a.off)[k + 1];
+    const uint32_t keyp = masked ? gptr(a.keys)[kp] : 0u, key = masked ? gptr(a.keys)[k] : 0u;
+    const uint32_t b0 = a.b0 ? (uint32_t)gptr(a.b0)[k] : 0x82u;
+    const uint64_t opk = k > 0 ? op : o;
+    u32x4 ld[3];
+    fix_plan(a, k, S, opk, o, on, ld);
+    fix_store(a, k, S, opk, o, on, keyp, key, b0, ld, wlo);
+}
+
+// One tile = kScanBlock frames.  The offsets go through LDS both ways so that every
+// global access is coalesced (thread t owns frames t*16 .. t*16+15 of the tile: read
+// straight from HBM, each load instruction would touch 64 cache lines, and with one
+// tile per CU that strided traffic, not the scan, set the kernel's time).
+//
+// FIX (netc_gpu_encode_frames with NETC_GPU_KNOB_ENC_FIX = 1): the tile's frames then compose the 16-B wire vectors
+// holding their header bytes (fix_at), which the assembly launch after this one never stores.
+// Each thread owns frames base + t0 .. + kScanPer - 1 and holds their payload offsets, so a
+// frame's wire start is known the moment the tile's prefix is: its keys and header bytes are
+// loaded before the look-back, its payload vectors after it -- one trip more in this launch in
+// place of the assembly's trailing fixup blocks.  Slower on MI355X (see launch_encode_frames).
+template <int kScanPer, bool FIX>
+__global__ __launch_bounds__(kScanThreads) void wire_offsets_chained(const uint64_t* off, uint64_t n, uint32_t fixed,
+                                                                     uint64_t* wo, uint64_t* status, uint32_t epoch,
+                                                                     uint32_t* defer_count, EncArgs fa) {
+    constexpr uint64_t kScanBlock = (uint64_t)kScanThreads * kScanPer;   // frames per tile
+    __shared__ uint64_t tile_prefix;
+    __shared__ uint64_t v[kScanBlock + kScanBlock / kScanPer + 1];   // entry j at j + j / kScanPer
+    auto pos = [](uint32_t j) { return j + j / kScanPer; };
+    const uint64_t tile = blockIdx.x, base = tile * kScanBlock;
+    const uint32_t t0 = threadIdx.x * kScanPer;   // this thread's frames: base + t0 ..
+    if (tile == 0 && threadIdx.x == 0) *defer_count = 0;   // (a spare word of the scratch; no reader since round 4)
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+        const uint32_t j = i * kScanThreads + threadIdx.x;
+        v[pos(j)] = gptr(off)[base + j < n ? base + j : n];
+    }
+    if (threadIdx.x == 0) v[pos(kScanBlock)] = gptr(off)[base + kScanBlock < n ? base + kScanBlock : n];
+    const uint64_t off0 = gptr(off)[0];
+    // FIX: keys and header bytes of this thread's frames and of the frame before them
+    uint32_t key[kScanPer + 1], hb[kScanPer];
+    if constexpr (FIX) {
+        const uint64_t k0 = base + t0;
+#pragma unroll
+        for (int i = 0; i <= kScanPer; ++i) {
+            const uint64_t k = k0 + i - 1;   // i = 0: frame k0 - 1
+            key[i] = fa.masked && k0 + i >= 1 && k < n ? gptr(fa.keys)[k] : 0u;
+            if (i > 0) hb[i - 1] = fa.b0 && k < n ? (uint32_t)gptr(fa.b0)[k] : 0x82u;
+        }
+    }
+    __syncthreads();
+    uint64_t o[kScanPer + 1];
+#pragma unroll
+    for (int i = 0; i <= kScanPer; ++i) o[i] = v[pos(t0 + i)];
+    uint64_t op0 = 0;   // FIX: off[] of the frame before this thread's first
+    if constexpr (FIX) op0 = t0 > 0 ? v[pos(t0 - 1)] : (base > 0 ? gptr(off)[base - 1] : 0);
+    uint32_t e[kScanPer];
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+        e[i] = base + t0 + i < n ? ext_len(o[i + 1] - o[i]) : 0u;
+        s += e[i];
+    }
+    uint64_t agg;
+    const uint64_t ex = block_exclusive_scan(s, &agg);   // its barriers also end the LDS reads above
+    if (threadIdx.x < kWave) {
+        const int lane = threadIdx.x;
+        if (lane == 0)
+            __hip_atomic_store(&status[tile], status_word(tile == 0 ? 2 : 1, epoch, agg), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t prefix = tile == 0 ? 0 : look_back(status, (int64_t)tile, epoch, lane);
+        if (lane == 0) {
+            if (tile) __hip_atomic_store(&status[tile], status_word(2, epoch, prefix + agg), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+            tile_prefix = prefix;
+        }
+    }
+    __syncthreads();
+    uint64_t run = tile_prefix + ex;
+    uint64_t S[kScanPer];
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+        const uint64_t j = base + t0 + i;
+        S[i] = (o[i] - off0) + (uint64_t)fixed * j + run;
+        v[pos(t0 + i)] = S[i];
+        run += e[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+        const uint32_t j = i * kScanThreads + threadIdx.x;
+        if (base + j <= n) gptr(wo)[base + j] = v[pos(j)];
+    }
+    if constexpr (FIX) {   // two frames' loads at a time, then their stores (four: the loads went to scratch)
+        constexpr int G = kScanPer < 2 ? kScanPer : 2;
+#pragma unroll
+        for (int g = 0; g < kScanPer; g += G) {
+            u32x4 ld[G][3];
+#pragma unroll
+            for (int i = 0; i < G; ++i)
+                if (base + t0 + g + i < n)
+                    fix_plan(fa, base + t0 + g + i, S[g + i] + fa.wmis, g + i == 0 ? op0 : o[g + i - 1], o[g + i], o[g + i + 1], ld[i]);
+#pragma unroll
+            for (int i = 0; i < G; ++i)
+                if (base + t0 + g + i < n)
+                    fix_store(fa, base + t0 + g + i, S[g + i] + fa.wmis, g + i == 0 ? op0 : o[g + i - 1], o[g + i], o[g + i + 1],
+                              key[g + i], key[g + i + 1], hb[g + i], ld[i], fa.wmis);
+        }
+    }
 }
 
 // Chunk = U spans.  Wavefront w of W takes chunks w, w+W, ...  Per trip: the table
@@ -710,17 +805,17 @@ __device__ __forceinline__ void fix_vectors(const EncArgs& a, uint64_t k, uint64
 // Blocks main_blocks .. gridDim.x - 1 (dispatched as the assembly blocks retire: its tail)
 // compose the vectors holding header bytes (fix_vectors, one thread per frame).  They share
 // no vector with the assembly's stores, so nothing orders the two.
-__device__ void fixup_block(const EncArgs& a, uint64_t wire_total) {
-    const uint64_t wlo = a.wmis, whi = a.wmis + wire_total;
+__device__ void fixup_block(const EncArgs& a) {
+    const uint64_t wlo = a.wmis;
     const uint64_t fb = blockIdx.x - a.main_blocks, nfb = gridDim.x - a.main_blocks;
-    for (uint64_t k = fb * blockDim.x + threadIdx.x; k < a.n; k += nfb * blockDim.x) fix_vectors(a, k, wlo, whi);
+    for (uint64_t k = fb * blockDim.x + threadIdx.x; k < a.n; k += nfb * blockDim.x) fix_vectors(a, k, wlo);
 }
 
 template <int U, bool NT, int W>
 __global__ __launch_bounds__(256, W) void encode_frames_kernel(EncArgs a) {
     const uint64_t wire_total = gptr(a.wo)[a.n];
     if (blockIdx.x >= a.main_blocks) {   // block-uniform
-        fixup_block(a, wire_total);
+        fixup_block(a);
         return;
     }
     constexpr uint64_t kWin = kSpan * U;
@@ -1263,24 +1358,30 @@ static int scan_per(uint64_t n) {
 
 static uint64_t scan_tiles_for(uint64_t n, int per) { return n / ((uint64_t)kScanThreads * per) + 1; }   // frames 0 .. n
 
+// fa: the assembly's arguments when the scan also composes the header vectors (FIX), else null
 template <int PER>
 static hipError_t launch_scan_per(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream,
-                                  const EncScratch& sc) {
+                                  const EncScratch& sc, const EncArgs* fa) {
     const uint64_t tiles = scan_tiles_for(n, PER);
-    hipLaunchKernelGGL((wire_offsets_chained<PER>), dim3((unsigned)tiles), dim3(kScanThreads), 0, stream, off, n,
-                       (uint32_t)(2 + (masked ? 4 : 0)), wo, sc.status, sc.epoch,
-                       (uint32_t*)(sc.defer + sc.defer_cap));
+    const uint32_t fixed = 2 + (masked ? 4 : 0);
+    uint32_t* spare = (uint32_t*)(sc.defer + sc.defer_cap);
+    if (fa)
+        hipLaunchKernelGGL((wire_offsets_chained<PER, true>), dim3((unsigned)tiles), dim3(kScanThreads), 0, stream, off,
+                           n, fixed, wo, sc.status, sc.epoch, spare, *fa);
+    else
+        hipLaunchKernelGGL((wire_offsets_chained<PER, false>), dim3((unsigned)tiles), dim3(kScanThreads), 0, stream, off,
+                           n, fixed, wo, sc.status, sc.epoch, spare, EncArgs{});
     return hipGetLastError();
 }
 
 static hipError_t launch_scan(const uint64_t* off, uint64_t n, bool masked, uint64_t* wo, hipStream_t stream,
-                              const EncScratch& sc, int per) {
+                              const EncScratch& sc, int per, const EncArgs* fa) {
     switch (per) {
-        case 1: return launch_scan_per<1>(off, n, masked, wo, stream, sc);
-        case 2: return launch_scan_per<2>(off, n, masked, wo, stream, sc);
-        case 4: return launch_scan_per<4>(off, n, masked, wo, stream, sc);
-        case 8: return launch_scan_per<8>(off, n, masked, wo, stream, sc);
-        default: return launch_scan_per<16>(off, n, masked, wo, stream, sc);
+        case 1: return launch_scan_per<1>(off, n, masked, wo, stream, sc, fa);
+        case 2: return launch_scan_per<2>(off, n, masked, wo, stream, sc, fa);
+        case 4: return launch_scan_per<4>(off, n, masked, wo, stream, sc, fa);
+        case 8: return launch_scan_per<8>(off, n, masked, wo, stream, sc, fa);
+        default: return launch_scan_per<16>(off, n, masked, wo, stream, sc, fa);
     }
 }
 
@@ -1292,7 +1393,7 @@ hipError_t launch_wire_offsets(const uint64_t* off, uint64_t n, bool masked, uin
     EncScratch sc;
     hipError_t e = scratch_for(stream, tiles, 1, sc);
     if (e != hipSuccess) return e;
-    return launch_scan(off, n, masked, wo, stream, sc, per);
+    return launch_scan(off, n, masked, wo, stream, sc, per, nullptr);
 }
 
 // mean payload bytes per frame under which a batch takes the dense compose path
@@ -1317,10 +1418,10 @@ static hipError_t launch_enc_u(EncArgs a, uint64_t wire_bound, bool nt, int max_
         hipLaunchKernelGGL(encode_queued_kernel, dim3((unsigned)(gb < 8192 ? gb : 8192)), dim3(256), 0, stream, a);
         return hipGetLastError();
     }
-    // the header fixups as trailing blocks of the same launch (fixup_block):
-    // one thread per frame up to 1,024 blocks
+    // the header fixups as trailing blocks of the same launch (fixup_block), one thread per frame
+    // up to 1,024 blocks, unless the wire-offsets scan has composed them (ENC_FIX = 1)
     const uint64_t fix = (a.n + 255) / 256;
-    const uint64_t fix_blocks = fix < 64 ? 64 : (fix > 1024 ? 1024 : fix);
+    const uint64_t fix_blocks = !a.fix_blocks ? 0 : (fix < 64 ? 64 : (fix > 1024 ? 1024 : fix));
     a.main_blocks = (uint32_t)blocks;
     a.per_wave = (uint32_t)(((nwin + 4 * (uint64_t)blocks - 1) / (4 * (uint64_t)blocks)) * U);   // windows per wave x U
     if ((uint64_t)a.per_wave * 4 * (uint64_t)blocks > a.defer_cap) return hipErrorInvalidValue;   // (sized with slack below)
@@ -1334,7 +1435,20 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
                                 const uint64_t* off, const uint32_t* keys, const uint8_t* b0, uint64_t n, bool masked,
                                 uint64_t* wo, hipStream_t stream, const LaunchCfg& cfg) {
     if (n == 0) return hipMemsetAsync(wo, 0, sizeof(uint64_t), stream);
-    const int per = scan_per(n);
+    // frames averaging under dense_bytes() of payload: every span is composed per lane
+    // (the vector path would queue most spans and leave a header fixup per frame)
+    const bool all_spans = src_total < dense_bytes() * n;
+    const bool src_walk = !all_spans && knob(NETC_GPU_KNOB_ENC_SRC) == 1;
+    // the header vectors: composed by trailing blocks of the assembly launch (default), by the
+    // wire-offsets scan (NETC_GPU_KNOB_ENC_FIX = 1), or not at all (dense batches and the
+    // source-driven walk write every byte themselves).  The scan variant measured slower: config
+    // 2 40.5-47 us per step (1-4 frames per scan thread) against 37.3 with the trailing blocks,
+    // config 4 421-430 against 417-424 -- on the scan's critical path the fixups cost more than
+    // in the assembly's tail, where they fill the CUs its last waves leave (r04kk)
+    const bool fix_in_scan = !all_spans && !src_walk && knob(NETC_GPU_KNOB_ENC_FIX) == 1;
+    const bool fix_blocks = !all_spans && !src_walk && !fix_in_scan;
+    // (the scan with the fixups holds 8 frames per thread at most: 16 spilled)
+    const int per0 = scan_per(n), per = fix_in_scan && per0 > 8 ? 8 : per0;
     const uint64_t tiles = scan_tiles_for(n, per);
     if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
     const uint64_t wmis = (uint64_t)(uintptr_t)wire & 15u;
@@ -1344,7 +1458,6 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     EncScratch sc;
     hipError_t e = scratch_for(stream, tiles, spans, sc);
     if (e != hipSuccess) return e;
-    if ((e = launch_scan(off, n, masked, wo, stream, sc, per)) != hipSuccess) return e;
     EncArgs a;
     a.wmis = wmis;
     a.wire_base = wire - a.wmis;
@@ -1359,9 +1472,9 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     a.defer = sc.defer;
     a.defer_count = (uint32_t*)(sc.defer + sc.defer_cap);
     a.defer_cap = sc.defer_cap;
-    // frames averaging under dense_bytes() of payload: every span is composed per lane
-    // (the vector path would queue most spans and leave a header fixup per frame)
-    a.all_spans = src_total < dense_bytes() * n ? 1u : 0u;
+    a.all_spans = all_spans ? 1u : 0u;
+    a.fix_blocks = fix_blocks ? 1u : 0u;
+    if ((e = launch_scan(off, n, masked, wo, stream, sc, per, fix_in_scan ? &a : nullptr)) != hipSuccess) return e;
     const bool nt = cfg.flags < 0 || (cfg.flags & (kNtLoads | kNtStores));
     // Chunk size: netc_gpu_tune's unroll 8 selects 4 KiB, 2 or 4 select 2 KiB; the default
     // (unroll 1) takes 4 KiB up to 256 MiB of wire (C2 39.0-39.3 against 39.8-39.9 us, three
@@ -1373,7 +1486,7 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     // against 26.6 + 7.9 for the wire-driven kernel and the header fixups, config 4 428-438 us
     // against 404 + 8; its unaligned 16-B stores cost ~5 % at config 4 and the per-span frame
     // logic more than the fixup launch at config 2; profiles/r04c_encode_src_ab.json)
-    if (!a.all_spans && knob(NETC_GPU_KNOB_ENC_SRC) == 1) {
+    if (src_walk) {
         constexpr int K = 2;
         constexpr uint64_t kWin = kSpan * K;
         a.smis = (uint64_t)(uintptr_t)src & 15u;

@@ -73,15 +73,24 @@ def _payload(rng, n):
     return rng.integers(0, 256, n, dtype=np.uint8)
 
 
-# the assembly path: None = the default (wire-driven kernels + per-frame header fixups), "1" =
-# the source-driven walk writing headers in the same pass (NETC_GPU_KNOB_ENC_SRC, A/B path)
-PATHS = [None, "1"]
+# the assembly path: None = the default (wire-driven kernel; trailing blocks of the same launch
+# compose the vectors holding header bytes), "fixscan" = those vectors by the wire-offsets scan
+# (NETC_GPU_KNOB_ENC_FIX = 1), "src" = the source-driven walk writing headers in the same pass
+# (NETC_GPU_KNOB_ENC_SRC = 1); both A/B paths
+PATHS = [None, "fixscan", "src"]
+
+
+def _set_path(gpu_knob, path):
+    if path == "fixscan":
+        gpu_knob("ENC_FIX", 1)
+    elif path == "src":
+        gpu_knob("ENC_SRC", 1)
 
 
 @pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("masked", [True, False])
 def test_every_length_class(torch_cuda, gpu_knob, masked, path):
-    gpu_knob("ENC_SRC", path)
+    _set_path(gpu_knob, path)
     rng = np.random.default_rng(11)
     sizes = EDGE_SIZES + EDGE_SIZES[::-1]
     off = frames_from_sizes(sizes)
@@ -95,7 +104,7 @@ def test_every_length_class(torch_cuda, gpu_knob, masked, path):
 @pytest.mark.parametrize("wire_shift", [0, 1, 3, 7, 8, 13, 15])
 @pytest.mark.parametrize("src_shift", [0, 5, 12])
 def test_alignments(torch_cuda, gpu_knob, wire_shift, src_shift, path):
-    gpu_knob("ENC_SRC", path)
+    _set_path(gpu_knob, path)
     rng = np.random.default_rng(100 + wire_shift * 16 + src_shift)
     sizes = rng.integers(0, 3000, 300)
     off = frames_from_sizes(sizes)
@@ -132,7 +141,7 @@ def test_tiny_frames_many_per_span(torch_cuda):
 @pytest.mark.parametrize("path", PATHS)
 def test_payload_with_unframed_prefix(torch_cuda, gpu_knob, path):
     # frames need not start at payload byte 0: off[0] > 0 (bytes before it are not sent)
-    gpu_knob("ENC_SRC", path)
+    _set_path(gpu_knob, path)
     rng = np.random.default_rng(12)
     sizes = rng.integers(0, 2000, 50)
     off = frames_from_sizes(sizes, start=777)
@@ -157,7 +166,7 @@ def test_frame_starts_at_every_lane_byte(torch_cuda, gpu_knob, src_shift, path):
     # the source-driven lanes: a frame start at each byte j of a lane's 16 (one start per lane:
     # two overlapping 16-B stores + the header), two starts in one lane (frames of 1..15 B),
     # empty frames between long ones, and the batch ending on, inside and after a vector edge
-    gpu_knob("ENC_SRC", path)
+    _set_path(gpu_knob, path)
     rng = np.random.default_rng(77 + src_shift)
     sizes = []
     for j in range(16):
@@ -202,7 +211,7 @@ def test_empty_batch(torch_cuda):
 @pytest.mark.parametrize("path", PATHS)
 def test_c2_full_size(torch_cuda, gpu_knob, path):
     # config 2 shape: 65,536 x 1 KiB frames, independent keys
-    gpu_knob("ENC_SRC", path)
+    _set_path(gpu_knob, path)
     rng = np.random.default_rng(0x6E657463)
     n = 65536
     off = frames_from_sizes(np.full(n, 1024))
@@ -214,7 +223,7 @@ def test_c2_full_size(torch_cuda, gpu_knob, path):
 @pytest.mark.parametrize("path", PATHS)
 def test_mixed_64mib(torch_cuda, gpu_knob, path):
     # config 4 shape (sizes uniform in [256, 65536], unaligned), 64 MiB
-    gpu_knob("ENC_SRC", path)
+    _set_path(gpu_knob, path)
     rng = np.random.default_rng(44)
     sizes = rng.integers(256, 65537, 4096)
     off = frames_from_sizes(sizes)
@@ -265,7 +274,7 @@ def test_both_compose_paths(torch_cuda, gpu_knob, dense, masked, path):
     # and through the dense per-lane compose of every span (threshold above any mean):
     # uniform 16 / 8 / 1 B frames, empty frames, 0..30 B mixes, and long frames between
     gpu_knob("ENC_DENSE_BYTES", dense)
-    gpu_knob("ENC_SRC", path)
+    _set_path(gpu_knob, path)
     rng = np.random.default_rng(21)
     parts = [np.full(3000, 16), np.full(2000, 8), rng.integers(0, 31, 4000), np.full(1500, 1),
              np.array([126, 65536, 0, 0, 125, 3000]), np.zeros(700, dtype=np.int64), rng.integers(100, 300, 200)]
