@@ -207,6 +207,48 @@ def test_limits_and_errors():
         ne.Egress(slot_bytes=100)
 
 
+def test_send_to_closed_peer_reports_esend():
+    """send() failing (peer closed: EPIPE; MSG_NOSIGNAL, so no SIGPIPE) -> ESEND; the failed slot is
+    released and the ring keeps working"""
+    a, b = socket.socketpair()
+    b.close()
+    try:
+        with ne.Egress(slot_bytes=1 << 16, nslots=2) as eg:
+            assert eg.queue(bytes(1000), 2, b"\x01\x02\x03\x04", 1) == 0
+            with pytest.raises(NetcGpuError) as e:
+                eg.flush(a.fileno())
+            assert e.value.code == ne.NETC_WS_EGRESS_ESEND
+            msgs = [(bytes([7] * 300), 1, b"\x05\x06\x07\x08", 2)]
+            assert eg.queue(*msgs[0]) == 0
+            eg.submit()
+            assert drain(eg)[0] == oracle_wire(msgs)
+    finally:
+        a.close()
+
+
+def test_release_out_of_order_and_twice():
+    """wire batches released out of order; a second release of one is refused; slots refill in ring
+    order (a free slot behind a taken one waits for it)"""
+    lib = ne._bind(_lib.gpu())
+    msgs = [(bytes([i + 1] * 4000), 2, None, 1) for i in range(3)]
+    with ne.Egress(slot_bytes=4096, nslots=3) as eg:
+        for m in msgs:   # 4000 B each: every message after the first submits the slot before it
+            assert eg.queue(*m) == 0
+        eg.submit()
+        ws = [eg.next(), eg.next(), eg.next()]
+        assert b"".join(w.wire.tobytes() for w in ws) == oracle_wire(msgs)
+        raw1 = ws[1]._raw
+        ws[1].release()
+        assert lib.netc_ws_egress_release(eg._h, ctypes.byref(raw1)) < 0   # already released
+        extra = (bytes(10), 2, None, 1)
+        assert eg.queue(*extra) == ne.NETC_WS_EGRESS_FULL   # the next slot in ring order (0) is still taken
+        ws[0].release()
+        assert eg.queue(*extra) == 0
+        ws[2].release()
+        eg.submit()
+        assert drain(eg)[0] == oracle_wire([extra])
+
+
 class Reader:
     def __init__(self, sock):
         self.sock, self.out = sock, bytearray()
