@@ -4,6 +4,8 @@
 #   library and tools/libnetc_ws_gpu_prev.so (the previous kernel, NETC_GPU_LIB), 3 rounds;
 #   then rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE passes of the new C2 command.
 #   bash tools/gpu_ab_mask.sh TAG
+# (the comparison build is untracked: git worktree add /tmp/prev <commit> && make -C /tmp/prev
+#  netc_amd/lib/libnetc_ws_gpu.so, then copy it to the path below; PREV overrides the path)
 set -o pipefail
 TAG=${1:-ab}
 R=$GRAFT_REPO_ROOT
@@ -18,7 +20,7 @@ B="python -u bench.py --gpus 1 --steps 200 --warmup 20 --c5-gib 0 --cpu-seconds 
 for i in 1 2 3; do
   for WL in ${WLS:-c2 c4}; do
     timeout -k 10 300 $B --workload $WL > $OUT/new_${WL}_$i.json 2> $OUT/new_${WL}_$i.err || { echo NEWFAIL; tail -20 $OUT/new_${WL}_$i.err; exit 1; }
-    NETC_GPU_LIB=tools/libnetc_ws_gpu_prev.so timeout -k 10 300 $B --workload $WL > $OUT/prev_${WL}_$i.json 2> $OUT/prev_${WL}_$i.err || { echo PREVFAIL; tail -20 $OUT/prev_${WL}_$i.err; exit 1; }
+    NETC_GPU_LIB=${PREV:-tools/libnetc_ws_gpu_prev.so} timeout -k 10 300 $B --workload $WL > $OUT/prev_${WL}_$i.json 2> $OUT/prev_${WL}_$i.err || { echo PREVFAIL; tail -20 $OUT/prev_${WL}_$i.err; exit 1; }
   done
 done
 python3 - "$OUT" <<'EOF'
