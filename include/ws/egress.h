@@ -122,8 +122,13 @@ long netc_ws_egress_flush(struct netc_ws_egress *eg, int fd);
  * was created with NETC_WS_EGRESS_DEFER -- submits it and sends it before
  * returning, with ws_send_message's contract: 1 once sent, else the failing send()
  * result (-1; netc_errno_reason BADSEND, or the ring's code in netc_gpu_strerror).
- * Other sockets keep the CPU path.  Detach (which does not flush) before destroying
- * the ring.  0 or NETC_GPU_EINVAL.
+ * Other sockets keep the CPU path.  One ring serves one connection: attaching a ring
+ * that already serves another open socket, or one holding queued messages, fails
+ * with NETC_GPU_EINVAL, and the route refuses a call for any other socket.  Detach
+ * before destroying the ring: netc_ws_gpu_detach_send first sends every message a
+ * DEFER ring still holds (ws_send_message returned 1 for them) and returns 0, or
+ * the flush's negative code when they could not all be sent (the route is detached
+ * either way).  0 or a negative code.
  */
 int netc_ws_gpu_attach_send(int sockfd, struct netc_ws_egress *ring);
 int netc_ws_gpu_detach_send(int sockfd);

@@ -56,12 +56,15 @@ extern "C" {
 #endif
 
 /* -------------------------------------------------------------- errors -- */
-#define NETC_GPU_OK        0
-#define NETC_GPU_EINVAL   -1   /* bad argument (null buffer, bad sizes, partial overlap) */
-#define NETC_GPU_ENODEV   -2   /* no such device / HIP runtime has no GPU                */
-#define NETC_GPU_ELAUNCH  -3   /* kernel launch failed                                   */
-#define NETC_GPU_ERUNTIME -4   /* a HIP runtime call failed (memcpy, stream, event …)    */
-#define NETC_GPU_ENOMEM   -5   /* device or pinned host allocation failed                */
+/* Numbered apart from ws_parse_frame's WS_FRAME_PARSE_ERROR_* (-1..-3, include/ws/common.h:42-50),
+   which a GPU route returns through the kept API: a device failure must never read as
+   "payload too big" to netc's web layer (src/web/server.c:88-95). */
+#define NETC_GPU_OK          0
+#define NETC_GPU_EINVAL   -101   /* bad argument (null buffer, bad sizes, partial overlap) */
+#define NETC_GPU_ENODEV   -102   /* no such device / HIP runtime has no GPU                */
+#define NETC_GPU_ELAUNCH  -103   /* kernel launch failed                                   */
+#define NETC_GPU_ERUNTIME -104   /* a HIP runtime call failed (memcpy, stream, event …)    */
+#define NETC_GPU_ENOMEM   -105   /* device or pinned host allocation failed                */
 
 /** netc_errno_reason value set by a failing GPU entry (extends include/utils/error.h:28-45). */
 #define NETC_REASON_GPU   18
@@ -143,6 +146,10 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *   ENC_FIX            where netc_gpu_encode_frames composes the 16-B vectors holding header
  *                      bytes: 0 trailing blocks of the assembly launch; 1 the wire-offsets
  *                      scan (measured slower) [0]                   (NETC_ENC_FIX)
+ *   INJECT_FAULT       fault injection for tests: the ingest / egress ring submission this
+ *                      countdown reaches (0 = the next one) fails as NETC_GPU_ELAUNCH
+ *                      without launching, then the knob disarms itself [off]
+ *                                                                  (NETC_INJECT_FAULT)
  */
 #define NETC_GPU_KNOB_ENC_DENSE_BYTES   1
 #define NETC_GPU_KNOB_ENC_SCAN_PER      2
@@ -153,6 +160,7 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
 #define NETC_GPU_KNOB_MASK_TAPER        7
 #define NETC_GPU_KNOB_ENC_SRC           8
 #define NETC_GPU_KNOB_ENC_FIX           9
+#define NETC_GPU_KNOB_INJECT_FAULT     10
 int netc_gpu_knob(int knob, int64_t value);
 
 /**

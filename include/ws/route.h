@@ -25,6 +25,13 @@
  * send() result).  netc_ws_gpu_attach_send (include/ws/egress.h) attaches the GPU
  * egress ring this way.  A socket's receive and send routes are independent.
  *
+ * A route belongs to the connection it was attached to, not to the descriptor number:
+ * the table records the socket's identity (device, inode) at attach, and a lookup on a
+ * descriptor that now names another socket (the connection was closed without a detach
+ * and the number reused by accept()) finds no route -- the new connection gets the CPU
+ * path.  Attaching a different route to a socket that still has a live one fails with
+ * EBUSY (detach first); re-attaching the same (fn, ctx) is a no-op.
+ *
  * Threading: attach / detach / parse of ONE socket from one thread at a time
  * (as netc drives a connection); different sockets from any threads.  A route
  * must stay valid until it is detached.
@@ -43,26 +50,33 @@ struct ws_message;
 typedef int (*netc_ws_route_fn)(void *ctx, int sockfd, struct ws_frame_parsing_state *state,
                                 size_t max_payload_length);
 
-/** Route ws_parse_frame on sockfd to fn(ctx, ...).  0, or -1 (bad fd / null fn; errno = EINVAL / ENOMEM). */
+/** Route ws_parse_frame on sockfd to fn(ctx, ...).  0, or -1 (errno = EINVAL: bad or closed fd,
+ *  null fn; ENOMEM; EBUSY: another route serves this connection). */
 int netc_ws_route_attach(int sockfd, netc_ws_route_fn fn, void *ctx);
 
 /** Back to the CPU parser on sockfd.  0 (also when nothing was attached), -1 on a bad fd. */
 int netc_ws_route_detach(int sockfd);
 
-/** The route attached to sockfd, or NULL (*ctx filled when one is). */
+/** The route attached to sockfd's connection, or NULL (*ctx filled when one is). */
 netc_ws_route_fn netc_ws_route_get(int sockfd, void **ctx);
+
+/** The route recorded under the descriptor number, live or left by a closed connection (for detach). */
+netc_ws_route_fn netc_ws_route_get_raw(int sockfd, void **ctx);
 
 typedef int (*netc_ws_send_route_fn)(void *ctx, int sockfd, struct ws_message *message, uint8_t masking_key[4],
                                      size_t num_frames);
 
-/** Route ws_send_message on sockfd to fn(ctx, ...).  0, or -1 (bad fd / null fn; errno = EINVAL / ENOMEM). */
+/** Route ws_send_message on sockfd to fn(ctx, ...).  0, or -1 (errno as netc_ws_route_attach). */
 int netc_ws_send_route_attach(int sockfd, netc_ws_send_route_fn fn, void *ctx);
 
 /** Back to the CPU path on sockfd.  0 (also when nothing was attached), -1 on a bad fd. */
 int netc_ws_send_route_detach(int sockfd);
 
-/** The send route attached to sockfd, or NULL (*ctx filled when one is). */
+/** The send route attached to sockfd's connection, or NULL (*ctx filled when one is). */
 netc_ws_send_route_fn netc_ws_send_route_get(int sockfd, void **ctx);
+
+/** The send route recorded under the descriptor number, live or stale (for detach). */
+netc_ws_send_route_fn netc_ws_send_route_get_raw(int sockfd, void **ctx);
 
 #ifdef __cplusplus
 }

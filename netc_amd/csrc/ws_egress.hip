@@ -24,6 +24,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/uio.h>
 
 #include <new>
@@ -50,8 +51,10 @@ enum SlotState : int { kFree = 0, kFilling, kInflight, kTaken };
 
 struct EgressSlot {
     uint8_t* h_pay = nullptr;     // pinned: queued payload bytes (slot_bytes)
-    uint8_t* h_tab = nullptr;     // pinned: offsets [0, 8 (mf + 1)), keys and header bytes in their
-                                  // own regions while filling, packed behind the offsets at submit
+    uint8_t* h_tab = nullptr;     // offsets [0, 8 (mf + 1)), keys and header bytes in their own
+                                  // regions while filling
+    uint8_t* h_pack = nullptr;    // pinned: the table packed at submit (offsets | keys | header
+                                  // bytes), so a failed submission leaves h_tab intact for a retry
     uint8_t* h_wire = nullptr;    // pinned: the slot's wire bytes (D2H target)
     uint64_t* h_len = nullptr;    // pinned: the device's wire length (wo[n])
     uint8_t* d_pay = nullptr;
@@ -101,6 +104,8 @@ struct netc_ws_egress {
     int next_fill = 0;     // the slot to fill next (ring order)
     int fifo[16] = {0};    // submitted slots not yet handed out, in queue order
     int head = 0, count = 0;
+    int owner_fd = -1;     // the socket served through ws_send_message (netc_ws_gpu_attach_send)
+    uint64_t owner_dev = 0, owner_ino = 0;
 };
 
 namespace {
@@ -112,6 +117,7 @@ void free_slot(int device, EgressSlot& s) {
     }
     if (s.h_pay) (void)hipHostFree(s.h_pay);
     if (s.h_tab) (void)hipHostFree(s.h_tab);
+    if (s.h_pack) (void)hipHostFree(s.h_pack);
     if (s.h_wire) (void)hipHostFree(s.h_wire);
     if (s.h_len) (void)hipHostFree(s.h_len);
     if (s.d_pay) (void)hipFree(s.d_pay);
@@ -131,6 +137,7 @@ int alloc_slot(const netc_ws_egress* g, EgressSlot& s) {
         return api_fail_hip(NETC_GPU_ERUNTIME, "egress: stream / event create", e);
     if ((e = hipHostMalloc((void**)&s.h_pay, g->slot_bytes, hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc((void**)&s.h_tab, tab, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&s.h_pack, tab, hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc((void**)&s.h_wire, g->wire_cap, hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc((void**)&s.h_len, sizeof(uint64_t), hipHostMallocDefault)) != hipSuccess)
         return api_fail_hip(NETC_GPU_ENOMEM, "egress: pinned host allocation", e);
@@ -147,20 +154,23 @@ int submit_cur(netc_ws_egress* g) {
     if (g->cur < 0) return 0;
     EgressSlot& s = g->slots[g->cur];
     if (s.frames == 0) return 0;
+    if (netc_gpu::inject_fault())
+        return api_fail(NETC_GPU_ELAUNCH, "egress: injected fault (NETC_GPU_KNOB_INJECT_FAULT)");
     const uint64_t n = s.frames;
     // pack the table: offsets (n + 1) | keys (n) | header bytes (n), one H2D copy
-    uint64_t* off = (uint64_t*)s.h_tab;
-    uint8_t* keys = s.h_tab + (n + 1) * sizeof(uint64_t);
+    uint64_t* off = (uint64_t*)s.h_pack;
+    uint8_t* keys = s.h_pack + (n + 1) * sizeof(uint64_t);
     uint8_t* b0 = keys + n * sizeof(uint32_t);
     const bool masked = s.masked == 1;
-    if (masked) memmove(keys, s.h_tab + g->keys_at, n * sizeof(uint32_t));
-    memmove(b0, s.h_tab + g->b0_at, n);
+    memcpy(off, s.h_tab, n * sizeof(uint64_t));
+    if (masked) memcpy(keys, s.h_tab + g->keys_at, n * sizeof(uint32_t));
+    memcpy(b0, s.h_tab + g->b0_at, n);
     off[n] = s.fill;
-    const uint64_t tab = (uint64_t)(b0 + n - s.h_tab);
+    const uint64_t tab = (uint64_t)(b0 + n - s.h_pack);
     const uint64_t bound = s.fill + n * NETC_WS_MAX_HEADER(masked);
     hipError_t e;
     if ((s.fill && (e = hipMemcpyAsync(s.d_pay, s.h_pay, s.fill, hipMemcpyHostToDevice, s.stream)) != hipSuccess) ||
-        (e = hipMemcpyAsync(s.d_tab, s.h_tab, tab, hipMemcpyHostToDevice, s.stream)) != hipSuccess)
+        (e = hipMemcpyAsync(s.d_tab, s.h_pack, tab, hipMemcpyHostToDevice, s.stream)) != hipSuccess)
         return api_fail_hip(NETC_GPU_ERUNTIME, "egress: H2D copy", e);
     const uint8_t* d_keys = s.d_tab + (n + 1) * sizeof(uint64_t);
     if ((e = netc_gpu::launch_encode_frames(s.d_wire, bound, s.d_pay, s.fill, (const uint64_t*)s.d_tab,
@@ -382,6 +392,10 @@ long netc_ws_egress_flush(struct netc_ws_egress* g, int fd) {
 static int gpu_send_route(void* ctx, int sockfd, struct ws_message* message, uint8_t masking_key[4],
                           size_t num_frames) {
     netc_ws_egress* g = (netc_ws_egress*)ctx;
+    if (sockfd != g->owner_fd) {   // one ring, one connection: never another socket's bytes
+        api_fail(NETC_GPU_EINVAL, "send route: the ring serves socket %d, not %d", g->owner_fd, sockfd);
+        return -1;
+    }
     int r = netc_ws_egress_queue(g, message->buffer, message->payload_length, message->opcode, masking_key,
                                  num_frames);
     if (r == NETC_WS_EGRESS_FULL) {   // every slot queued or unsent: put the oldest on the socket
@@ -395,17 +409,68 @@ static int gpu_send_route(void* ctx, int sockfd, struct ws_message* message, uin
     return s < 0 ? -1 : 1;
 }
 
+static bool sock_identity(int fd, uint64_t* dev, uint64_t* ino) {
+    struct stat st;
+    if (fstat(fd, &st) != 0 || !S_ISSOCK(st.st_mode)) return false;
+    *dev = (uint64_t)st.st_dev;
+    *ino = (uint64_t)st.st_ino;
+    return true;
+}
+
+// a ring's messages queued but not yet on its socket (slots filling, on the GPU or finished)
+static bool has_queued(const netc_ws_egress* g) {
+    return g->count > 0 || (g->cur >= 0 && g->slots[g->cur].frames > 0);
+}
+
 int netc_ws_gpu_attach_send(int sockfd, struct netc_ws_egress* ring) {
     if (!ring) return api_fail(NETC_GPU_EINVAL, "attach_send: null ring");
+    uint64_t dev = 0, ino = 0;
+    if (!sock_identity(sockfd, &dev, &ino))
+        return api_fail(NETC_GPU_EINVAL, "attach_send: %d is not an open socket", sockfd);
+    if (ring->owner_fd >= 0) {
+        if (ring->owner_fd == sockfd && ring->owner_dev == dev && ring->owner_ino == ino) return 0;
+        uint64_t d2 = 0, i2 = 0;
+        if (sock_identity(ring->owner_fd, &d2, &i2) && d2 == ring->owner_dev && i2 == ring->owner_ino)
+            return api_fail(NETC_GPU_EINVAL, "attach_send: the ring already serves socket %d (one ring, one "
+                            "connection)", ring->owner_fd);
+        // its connection was closed without a detach
+        void* ctx = nullptr;
+        if (netc_ws_send_route_get_raw(ring->owner_fd, &ctx) && ctx == ring) (void)netc_ws_send_route_detach(ring->owner_fd);
+        ring->owner_fd = -1;
+    }
+    if (has_queued(ring))   // they were queued for another connection
+        return api_fail(NETC_GPU_EINVAL, "attach_send: the ring holds queued messages (flush or destroy it first)");
     if (netc_ws_send_route_attach(sockfd, gpu_send_route, ring) != 0)
-        return api_fail(NETC_GPU_EINVAL, "attach_send: socket %d out of range", sockfd);
+        return api_fail(NETC_GPU_EINVAL, "attach_send: socket %d: %s", sockfd,
+                        errno == EBUSY ? "another send route serves it" : "out of range");
+    ring->owner_fd = sockfd;
+    ring->owner_dev = dev;
+    ring->owner_ino = ino;
     return 0;
 }
 
 int netc_ws_gpu_detach_send(int sockfd) {
+    if (sockfd < 0) return api_fail(NETC_GPU_EINVAL, "detach_send: socket %d out of range", sockfd);
+    void* ctx = nullptr;
+    long flushed = 0;
+    if (netc_ws_send_route_get_raw(sockfd, &ctx) == gpu_send_route && ctx) {
+        netc_ws_egress* g = (netc_ws_egress*)ctx;
+        if (g->owner_fd == sockfd) {
+            // ws_send_message already returned 1 for a DEFER ring's queued messages: they go out now
+            uint64_t d = 0, i = 0;
+            if (has_queued(g)) {
+                if (sock_identity(sockfd, &d, &i) && d == g->owner_dev && i == g->owner_ino)
+                    flushed = netc_ws_egress_flush(g, sockfd);
+                else
+                    flushed = api_fail(NETC_WS_EGRESS_ESEND, "detach_send: socket %d was closed with queued "
+                                       "messages", sockfd);
+            }
+            g->owner_fd = -1;
+        }
+    }
     if (netc_ws_send_route_detach(sockfd) != 0)
         return api_fail(NETC_GPU_EINVAL, "detach_send: socket %d out of range", sockfd);
-    return 0;
+    return flushed < 0 ? (int)flushed : 0;
 }
 
 }  // extern "C"

@@ -535,8 +535,12 @@ __device__ __forceinline__ void finish_chunk(const EncArgs& a, const EncTable& t
         const uint64_t W = A0 + 16ull * (uint64_t)lane;
         if (sp.kind == kSpanNone) return;
         if (sp.kind == kSpanQueued) {   // wave-uniform: listed, composed after the wavefront's windows
-            if (lane == 0) list[nl] = A0;
-            ++nl;
+            // (bounded: the slice is sized from the host's wire bound; device offsets that break
+            // the contract -- not monotonic, or not ending at total_bytes -- must not write past it)
+            if (nl < a.per_wave) {
+                if (lane == 0) list[nl] = A0;
+                ++nl;
+            }
             return;
         }
         const u32x4 kv = {sp.rk, sp.rk, sp.rk, sp.rk};

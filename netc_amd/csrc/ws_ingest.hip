@@ -31,6 +31,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 
 #include <new>
 
@@ -51,6 +52,7 @@ using netc_gpu::api_fail_hip;
 namespace {
 
 constexpr int kBadRecv = 10;   // netc's BADRECV reason (include/utils/error.h)
+constexpr size_t kScratch = 1u << 20;   // discard buffer of the route on non-TCP sockets
 
 // Default scan choice per slot: the host header walk when the previous slot's frames
 // averaged at least this many bytes.  The walk costs the submitting thread one header
@@ -111,6 +113,18 @@ struct MessageState {
     size_t size = 0, cap = 0;
     uint8_t opcode = 0;          // the last non-continuation frame's opcode, as the reference
     int err = 0;                 // sticky message-level error (WS_FRAME_PARSE_ERROR_*)
+    uint64_t end_pos = 0;        // stream position just past the last delivered message
+};
+
+// the socket a ring serves through ws_parse_frame (netc_ws_gpu_attach), and how far the
+// route has taken bytes out of it: the route reads ahead with MSG_PEEK and removes bytes
+// from the socket only up to the end of the message it returns (see gpu_route)
+struct RouteState {
+    int fd = -1;                 // attached socket, -1 = none
+    uint64_t dev = 0, ino = 0;   // its identity at attach time (fstat), against fd reuse
+    int tcp = 0;                 // TCP: discard with MSG_TRUNC (no copy); else recv into scratch
+    uint64_t sock_pos = 0;       // stream bytes removed from the socket
+    uint8_t* scratch = nullptr;  // discard buffer for non-TCP sockets
 };
 
 }  // namespace
@@ -132,7 +146,9 @@ struct netc_ws_ingest {
     int sticky_after = -1; // ... once the batch of this slot has been handed out (-1: now)
     uint64_t max_frame = 0;   // max_frame_bytes (payload bytes per frame)
     bool closed = false;   // recv saw the peer close
+    uint64_t in_pos = 0;   // stream bytes taken into the ring (recv / peek / write)
     MessageState msg;
+    RouteState route;
 };
 
 namespace {
@@ -256,6 +272,8 @@ int submit_cur(netc_ws_ingest* g) {
     if (g->cur < 0) return 0;
     IngestSlot& s = g->slots[g->cur];
     if (s.fill == 0) return 0;   // nothing new: the carry alone cannot complete a frame
+    if (netc_gpu::inject_fault())
+        return api_fail(NETC_GPU_ELAUNCH, "ingest: injected fault (NETC_GPU_KNOB_INJECT_FAULT)");
     uint64_t carry = 0, pos = 0;
     const uint8_t* carry_src = nullptr;
     bool host_walk = g->scan_mode == NETC_WS_INGEST_SCAN_HOST;
@@ -400,13 +418,16 @@ int netc_ws_ingest_create(struct netc_ws_ingest** out, int device, size_t slot_b
 void netc_ws_ingest_destroy(struct netc_ws_ingest* g) {
     if (!g) return;
     free(g->msg.buf);   // a message not completed yet (delivered ones are the caller's)
+    free(g->route.scratch);
     DeviceGuard dg(g->device);
     for (int i = 0; i < g->nslots; ++i) free_slot(g->slots[i]);
     delete[] g->slots;
     delete g;
 }
 
-long netc_ws_ingest_recv(struct netc_ws_ingest* g, int fd) {
+// one recv() into the current slot; with peek (the ws_parse_frame route) MSG_PEEK: the bytes
+// stay in the socket until the route removes them (RouteState)
+static long ring_recv(netc_ws_ingest* g, int fd, bool peek) {
     if (!g) return api_fail(NETC_GPU_EINVAL, "ingest: null ingest");
     if (g->sticky) return sticky_now(g) ? g->sticky : api_fail(g->sticky, "ingest: the stream has ended (error)");
     DeviceGuard dg(g->device);
@@ -422,7 +443,7 @@ long netc_ws_ingest_recv(struct netc_ws_ingest* g, int fd) {
     uint8_t* dst = s.h_buf + g->carry_cap + s.fill;
     const size_t room = (size_t)(g->slot_bytes - s.fill);
     ssize_t r;
-    do r = recv(fd, dst, room, 0);
+    do r = recv(fd, dst, room, peek ? MSG_PEEK : 0);
     while (r < 0 && errno == EINTR);
     if (r < 0) {
         if (errno == EAGAIN || errno == EWOULDBLOCK) return 0;
@@ -438,14 +459,24 @@ long netc_ws_ingest_recv(struct netc_ws_ingest* g, int fd) {
         return api_fail(NETC_WS_INGEST_CLOSED, "ingest: the peer closed the connection");
     }
     s.fill += (uint64_t)r;
+    g->in_pos += (uint64_t)r;
     if (s.fill == g->slot_bytes) {
         if (int e = submit_cur(g)) return e;
     }
     return (long)r;
 }
 
+long netc_ws_ingest_recv(struct netc_ws_ingest* g, int fd) {
+    if (g && g->route.fd >= 0)
+        return api_fail(NETC_GPU_EINVAL, "ingest: the ring serves socket %d through ws_parse_frame "
+                        "(netc_ws_gpu_attach); detach it first", g->route.fd);
+    return ring_recv(g, fd, false);
+}
+
 long netc_ws_ingest_write(struct netc_ws_ingest* g, const void* data, size_t len) {
     if (!g || (len && !data)) return api_fail(NETC_GPU_EINVAL, "ingest: null argument");
+    if (g->route.fd >= 0)
+        return api_fail(NETC_GPU_EINVAL, "ingest: the ring serves socket %d through ws_parse_frame", g->route.fd);
     if (g->sticky) return api_fail(g->sticky, "ingest: the stream has ended (error)");
     DeviceGuard dg(g->device);
     if (dg.err != hipSuccess) return api_fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", dg.err);
@@ -459,6 +490,7 @@ long netc_ws_ingest_write(struct netc_ws_ingest* g, const void* data, size_t len
         memcpy(s.h_buf + g->carry_cap + s.fill, p + taken, k);
         s.fill += k;
         taken += k;
+        g->in_pos += k;
         if (s.fill == g->slot_bytes) {
             if (int e = submit_cur(g)) return e;
         }
@@ -594,6 +626,7 @@ int netc_ws_ingest_next_message(struct netc_ws_ingest* g, struct ws_message* mes
                 message->opcode = m.opcode;
                 message->buffer = m.buf;
                 message->payload_length = m.size;
+                m.end_pos = b.stream_offset + b.hdr[k + 1];
                 m.buf = nullptr;
                 m.size = m.cap = 0;
                 return 0;
@@ -604,25 +637,77 @@ int netc_ws_ingest_next_message(struct netc_ws_ingest* g, struct ws_message* mes
     }
 }
 
+// Remove the socket's bytes up to stream position `to` (<= in_pos: the ring holds a copy of
+// them, read with MSG_PEEK).  TCP discards them without a copy (recv with MSG_TRUNC and no
+// buffer); other stream sockets refuse that (EFAULT, nothing taken) and read into scratch.
+static int sock_consume(netc_ws_ingest* g, int fd, uint64_t to) {
+    RouteState& rs = g->route;
+    while (rs.sock_pos < to) {
+        const uint64_t want = to - rs.sock_pos;
+        ssize_t r;
+        if (rs.tcp) {
+            r = recv(fd, nullptr, (size_t)want, MSG_TRUNC | MSG_DONTWAIT);
+            if (r < 0 && errno == EFAULT) {
+                rs.tcp = 0;   // this socket copies: use the scratch from now on
+                continue;
+            }
+        } else {
+            if (!rs.scratch && !(rs.scratch = (uint8_t*)malloc(kScratch)))
+                return api_fail(NETC_GPU_ENOMEM, "ingest: discard buffer");
+            r = recv(fd, rs.scratch, (size_t)(want < kScratch ? want : kScratch), MSG_DONTWAIT);
+        }
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) {   // the bytes were peeked, so they are there: the socket has failed
+            const int saved = r < 0 ? errno : ECONNRESET;
+            api_fail(NETC_WS_INGEST_ERECV, "ingest: removing delivered bytes from socket %d: %s", fd,
+                     strerror(saved));
+            netc_errno_reason = kBadRecv;
+            errno = saved;
+            return NETC_WS_INGEST_ERECV;
+        }
+        rs.sock_pos += (uint64_t)r;
+    }
+    return 0;
+}
+
 // ws_parse_frame on a socket attached to a ring (include/ws/route.h): the reference's receive
-// contract (src/ws/common.c:134-348; caller src/web/server.c:86-140) served from the ring.
-// Buffered messages first; when none is complete, one recv() into the ring and again, until
-// a message is ready (0), the socket has nothing more now (1: wait for the next readiness
-// event), or the stream ended (< 0).  state->message gets the message as ws_parse_frame
-// would fill it (opcode, caller-owned malloc'd buffer, payload_length with a TEXT message's
-// NUL); the rest of the parser state is not used.
+// contract (src/ws/common.c:134-348) for its once-per-readiness-event caller
+// (src/tcp/server.c:72-75 -> src/web/server.c:86-98, which calls ws_parse_frame ONCE per
+// EPOLLIN and goes back to epoll_wait).
+//
+// The ring reads ahead -- one MSG_PEEK as large as the slot's room, then the GPU scan and
+// unmask over every frame in it -- but takes bytes out of the socket only up to the end of
+// the message it returns.  So while a complete message waits in the ring, its bytes are
+// still in the socket and the level-triggered event fires again: nothing is stranded when
+// the peer goes quiet.  Only once the ring holds no complete message (next_message says 1)
+// are the peeked bytes of the incomplete tail removed, and the socket peeked again past them.
+//   0   state->message filled as ws_parse_frame fills it (opcode, caller-owned malloc'd
+//       buffer, payload_length with a TEXT message's NUL); nothing else of the state is used
+//   1   the socket has nothing more now and the ring no complete message
+//   WS_FRAME_PARSE_ERROR_*   PAYLOAD_TOO_BIG against the caller's limit (or the ring's frame
+//       limit); INVALID_FRAME_LENGTH for a header strict mode rejects; RECV once the peer
+//       closed and every message before that was returned, or recv failed
+//   NETC_GPU_E*   a device / runtime failure (-101..-105: never one of the above)
 static int gpu_route(void* ctx, int sockfd, struct ws_frame_parsing_state* state, size_t max_payload_length) {
     netc_ws_ingest* g = (netc_ws_ingest*)ctx;
+    if (sockfd != g->route.fd)
+        return api_fail(NETC_GPU_EINVAL, "route: the ring serves socket %d, not %d", g->route.fd, sockfd);
     int full = 0;
     for (;;) {
         struct ws_message m;
         const int r = netc_ws_ingest_next_message(g, &m, max_payload_length, 1);
         if (r == 0) {
+            // the message's bytes leave the socket; later messages' stay (still readable).  A
+            // failing socket is reported by the next call's peek, after this message.
+            (void)sock_consume(g, sockfd, g->msg.end_pos);
             state->message = m;
             return 0;
         }
         if (r < 0) return r;
-        const long n = netc_ws_ingest_recv(g, sockfd);
+        // no complete message in the ring: the incomplete tail it holds leaves the socket,
+        // then one peek past it
+        if (int e = sock_consume(g, sockfd, g->in_pos)) return g->msg.err = message_code(e);
+        const long n = ring_recv(g, sockfd, true);
         if (n == 0) return 1;                              // drained: wait for readiness
         if (n > 0 || n == NETC_WS_INGEST_CLOSED) {         // (closed: what it sent is delivered first)
             full = 0;
@@ -631,18 +716,63 @@ static int gpu_route(void* ctx, int sockfd, struct ws_frame_parsing_state* state
         // no free slot: next_message releases slots as it consumes them; a ring that stays full
         // with no message completing cannot progress
         if (n == NETC_WS_INGEST_FULL && ++full < 3) continue;
-        return message_code((int)n);
+        return g->msg.err = message_code((int)n);
     }
+}
+
+// the identity of an open socket (device, inode), to tell a reused descriptor from the attached one
+static bool sock_identity(int fd, uint64_t* dev, uint64_t* ino) {
+    struct stat st;
+    if (fstat(fd, &st) != 0 || !S_ISSOCK(st.st_mode)) return false;
+    *dev = (uint64_t)st.st_dev;
+    *ino = (uint64_t)st.st_ino;
+    return true;
 }
 
 int netc_ws_gpu_attach(int sockfd, struct netc_ws_ingest* ring) {
     if (!ring) return api_fail(NETC_GPU_EINVAL, "attach: null ring");
-    if (netc_ws_route_attach(sockfd, gpu_route, ring) != 0)
-        return api_fail(NETC_GPU_EINVAL, "attach: socket %d out of range", sockfd);
+    uint64_t dev = 0, ino = 0;
+    if (!sock_identity(sockfd, &dev, &ino)) return api_fail(NETC_GPU_EINVAL, "attach: %d is not an open socket", sockfd);
+    RouteState& rs = ring->route;
+    if (rs.fd >= 0) {
+        uint64_t d2 = 0, i2 = 0;
+        const bool same = rs.fd == sockfd && rs.dev == dev && rs.ino == ino;
+        if (same) return 0;   // already serving this connection
+        if (sock_identity(rs.fd, &d2, &i2) && d2 == rs.dev && i2 == rs.ino)
+            return api_fail(NETC_GPU_EINVAL, "attach: the ring already serves socket %d (one ring, one connection)",
+                            rs.fd);
+        // its connection was closed without a detach: drop the stale route if it is still ours
+        void* ctx = nullptr;
+        if (netc_ws_route_get_raw(rs.fd, &ctx) && ctx == ring) (void)netc_ws_route_detach(rs.fd);
+        rs.fd = -1;
+    }
+    // a ring carries one connection's stream: a used one would splice two streams together
+    if (ring->in_pos != 0 || ring->closed || ring->sticky || ring->msg.err)
+        return api_fail(NETC_GPU_EINVAL, "attach: the ring has already carried a stream (create a fresh one)");
+    int type = 0, domain = 0;
+    socklen_t tl = sizeof type, dl = sizeof domain;
+    if (getsockopt(sockfd, SOL_SOCKET, SO_TYPE, &type, &tl) != 0 || type != SOCK_STREAM)
+        return api_fail(NETC_GPU_EINVAL, "attach: socket %d is not a stream socket", sockfd);
+    (void)getsockopt(sockfd, SOL_SOCKET, SO_DOMAIN, &domain, &dl);
+    const int r = netc_ws_route_attach(sockfd, gpu_route, ring);
+    if (r != 0)
+        return api_fail(NETC_GPU_EINVAL, "attach: socket %d: %s", sockfd,
+                        errno == EBUSY ? "another route serves it" : "out of range");
+    rs.fd = sockfd;
+    rs.dev = dev;
+    rs.ino = ino;
+    rs.tcp = domain == AF_INET || domain == AF_INET6;
+    rs.sock_pos = 0;
     return 0;
 }
 
 int netc_ws_gpu_detach(int sockfd) {
+    if (sockfd < 0) return api_fail(NETC_GPU_EINVAL, "detach: socket %d out of range", sockfd);
+    void* ctx = nullptr;
+    if (netc_ws_route_get_raw(sockfd, &ctx) == gpu_route && ctx) {
+        netc_ws_ingest* g = (netc_ws_ingest*)ctx;
+        if (g->route.fd == sockfd) g->route.fd = -1;
+    }
     if (netc_ws_route_detach(sockfd) != 0) return api_fail(NETC_GPU_EINVAL, "detach: socket %d out of range", sockfd);
     return 0;
 }

@@ -86,6 +86,8 @@ LaunchCfg api_cfg();                                         // snapshot of netc
 // measurement / test knobs (netc_gpu_knob, include/ws/mask.h NETC_GPU_KNOB_*): one atomic
 // word each, seeded once from the environment; < 0 = the built-in default
 int64_t knob(int k);
+// fault injection for tests (NETC_GPU_KNOB_INJECT_FAULT): true when this ring submission must fail
+bool inject_fault();
 // per-(device, stream) scratch of the public entries, released by netc_gpu_stream_release
 int release_enc_scratch(int device, hipStream_t stream);     // ws_frame_gpu.hip
 

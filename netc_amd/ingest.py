@@ -73,6 +73,10 @@ def _bind(lib):
     lib.netc_ws_ingest_next_message.restype = ctypes.c_int
     lib.netc_ws_ingest_scan_counts.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     lib.netc_ws_ingest_scan_counts.restype = ctypes.c_int
+    lib.netc_ws_gpu_attach.argtypes = [ctypes.c_int, vp]
+    lib.netc_ws_gpu_attach.restype = ctypes.c_int
+    lib.netc_ws_gpu_detach.argtypes = [ctypes.c_int]
+    lib.netc_ws_gpu_detach.restype = ctypes.c_int
     lib._ingest_bound = True
     return lib
 
@@ -187,6 +191,18 @@ class Ingest:
                   WS_FRAME_PARSE_ERROR_PAYLOAD_TOO_BIG):
             return rc, None, None
         _raise(rc)
+
+    def attach(self, sockfd: int) -> None:
+        """netc_ws_gpu_attach: libnetc's ws_parse_frame on sockfd is served from this ring (one
+        ring, one connection; a ring that has carried a stream cannot be attached)."""
+        rc = self._lib.netc_ws_gpu_attach(sockfd, self._h)
+        if rc:
+            _raise(rc)
+
+    def detach(self, sockfd: int) -> None:
+        rc = self._lib.netc_ws_gpu_detach(sockfd)
+        if rc:
+            _raise(rc)
 
     def close(self) -> None:
         if self._h:

@@ -20,11 +20,11 @@ import numpy as np
 from . import _lib
 
 NETC_GPU_OK = 0
-NETC_GPU_EINVAL = -1
-NETC_GPU_ENODEV = -2
-NETC_GPU_ELAUNCH = -3
-NETC_GPU_ERUNTIME = -4
-NETC_GPU_ENOMEM = -5
+NETC_GPU_EINVAL = -101
+NETC_GPU_ENODEV = -102
+NETC_GPU_ELAUNCH = -103
+NETC_GPU_ERUNTIME = -104
+NETC_GPU_ENOMEM = -105
 NETC_REASON_GPU = 18
 
 
@@ -110,7 +110,7 @@ def tune(unroll: int = 1, max_blocks: int = 0, flags: int = NETC_GPU_TUNE_AUTO) 
 
 
 KNOBS = {"ENC_DENSE_BYTES": 1, "ENC_SCAN_PER": 2, "SCAN_FAST_RANK": 3, "SCAN_ANCHOR_SLOTS": 4, "VAL_STEPS": 5, "SCAN_FUSE": 6,
-         "MASK_TAPER": 7, "ENC_SRC": 8, "ENC_FIX": 9}
+         "MASK_TAPER": 7, "ENC_SRC": 8, "ENC_FIX": 9, "INJECT_FAULT": 10}
 
 
 def set_knob(name: str, value: int) -> None:

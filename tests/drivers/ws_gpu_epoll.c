@@ -25,14 +25,17 @@
  *   client log: per sent message       u8 opcode, u8 masked, u8 key[4], u64 frames, u64 length, payload
  * Exit status 0 when every reply the client checks was right; stdout: one summary line.
  *
- * Route "parse" (5th argument): the server calls ONLY netc's own ws_parse_frame (libnetc.so),
- * exactly as src/web/server.c:86 does, with the ring attached to the socket by
- * netc_ws_gpu_attach (include/ws/ingest.h): ws_parse_frame then receives into
- * the ring and returns the GPU-unmasked messages; the server memsets its parser state after
- * each message (server.c:139-140) and calls again until it returns 1.  Route "ingest" (the
- * default): netc_ws_ingest_recv + netc_ws_ingest_next_message directly.
+ * Route "parse1" (5th argument): the server is netc's own loop -- per EPOLLIN it calls ONLY
+ * netc's ws_parse_frame (libnetc.so), exactly ONCE, and goes back to epoll_wait
+ * (src/tcp/server.c:72-75 -> src/web/server.c:86-98), with the ring attached to the socket by
+ * netc_ws_gpu_attach (include/ws/ingest.h): ws_parse_frame then reads ahead into the ring and
+ * returns the GPU-unmasked messages, leaving each later message's bytes in the socket so the
+ * level-triggered event fires again for it.  Route "parse": the same, calling
+ * ws_parse_frame again after a 0 until it returns 1.  Either way the server memsets its parser
+ * state after each message (server.c:139-140).  Route "ingest" (the default):
+ * netc_ws_ingest_recv + netc_ws_ingest_next_message directly.
  *
- * usage: ws_gpu_epoll SERVER_LOG CLIENT_LOG [auto|gpu|host] [slot_bytes] [ingest|parse]
+ * usage: ws_gpu_epoll SERVER_LOG CLIENT_LOG [auto|gpu|host] [slot_bytes] [ingest|parse|parse1]
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -94,7 +97,9 @@ struct server {
     int port;
     const char *log_path;
     int scan_flags;
-    int parse_route;           /* serve through ws_parse_frame on the attached socket */
+    int parse_route;           /* serve through ws_parse_frame on the attached socket: 1 until it
+                                  returns 1, 2 once per readiness event (netc's own loop) */
+    uint64_t events;           /* epoll wake-ups */
     size_t slot_bytes;
     int rc;                    /* 0 ok */
     uint64_t delivered, gpu_slots, host_slots;
@@ -153,9 +158,11 @@ static void *server_main(void *arg) {
         int n = epoll_wait(ep, &got, 1, 20000);
         if (n < 0 && errno == EINTR) continue;
         if (n <= 0) {
-            fprintf(stderr, "server: epoll_wait %s\n", n == 0 ? "timed out" : strerror(errno));
+            fprintf(stderr, "server: epoll_wait %s (%llu messages delivered)\n", n == 0 ? "timed out" : strerror(errno),
+                    (unsigned long long)S->delivered);
             goto out;
         }
+        ++S->events;
         if (!S->parse_route) {
             long r = netc_ws_ingest_recv(ing, fd);
             if (r == NETC_WS_INGEST_CLOSED) open = 0;   /* what it sent is still delivered below */
@@ -220,7 +227,7 @@ static void *server_main(void *arg) {
             }
             free(m.buffer);   /* the caller owns the message (src/web/server.c:139) */
             if (S->parse_route) memset(&st, 0, sizeof st);   /* src/web/server.c:140 */
-            if (!open) break;
+            if (!open || S->parse_route == 2) break;         /* netc: back to epoll_wait */
         }
         if (res < 0) {   /* malformed: on_ws_malformed_frame + close 1002 (src/web/server.c:88-95) */
             if (S->parse_route && res == WS_FRAME_PARSE_ERROR_RECV) {
@@ -309,7 +316,7 @@ int main(int argc, char **argv) {
     S.scan_flags = argc > 3 && !strcmp(argv[3], "gpu") ? NETC_WS_INGEST_SCAN_GPU
                    : argc > 3 && !strcmp(argv[3], "host") ? NETC_WS_INGEST_SCAN_HOST : 0;
     S.slot_bytes = argc > 4 ? (size_t)strtoull(argv[4], NULL, 10) : (size_t)1 << 20;
-    S.parse_route = argc > 5 && !strcmp(argv[5], "parse");
+    S.parse_route = argc > 5 && !strcmp(argv[5], "parse") ? 1 : argc > 5 && !strcmp(argv[5], "parse1") ? 2 : 0;
     if (netc_gpu_init(0) != 0) {   /* keep runtime initialisation off the event loop */
         fprintf(stderr, "netc_gpu_init: %s\n", netc_gpu_strerror());
         return 2;
@@ -406,8 +413,9 @@ int main(int argc, char **argv) {
     fclose(g_clog);
     pthread_join(th, NULL);
     printf("{\"server_rc\": %d, \"client_ok\": %d, \"delivered\": %llu, \"gpu_slots\": %llu, \"host_slots\": %llu, "
-           "\"route\": \"%s\"}\n",
+           "\"events\": %llu, \"route\": \"%s\"}\n",
            S.rc, !g_fail, (unsigned long long)S.delivered, (unsigned long long)S.gpu_slots,
-           (unsigned long long)S.host_slots, S.parse_route ? "parse" : "ingest");
+           (unsigned long long)S.host_slots, (unsigned long long)S.events,
+           S.parse_route == 2 ? "parse1" : S.parse_route ? "parse" : "ingest");
     return S.rc || g_fail;
 }

@@ -12,7 +12,11 @@ burst of 2,000 fragmented messages -- checking every reply with ws_parse_frame.
 
 Route "parse" runs the same server with ONLY netc's ws_parse_frame on its side: the socket is
 attached to the ring (netc_ws_gpu_attach), so libnetc.so's ws_parse_frame receives into the ring
-and returns the GPU-unmasked messages with the reference's 0 / 1 / < 0 contract.
+and returns the GPU-unmasked messages with the reference's 0 / 1 / < 0 contract.  Route "parse1"
+is netc's own loop exactly: ONE ws_parse_frame per EPOLLIN, then back to epoll_wait
+(reference src/tcp/server.c:72-75, src/web/server.c:86-98) -- the burst of 2,000 messages sent
+without waiting is then delivered only if the ring leaves every undelivered message's bytes in
+the socket; a stranded message shows up as the server's 20 s epoll timeout.
 
 Checked here, per scan mode of the ring and route:
   * the program's own checks (replies, pong payload, close echo, 16 MiB and burst hashes);
@@ -70,7 +74,8 @@ def read_client_log(path):
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("mode,route", [("auto", "ingest"), ("gpu", "ingest"), ("host", "ingest"),
-                                        ("auto", "parse"), ("gpu", "parse")])
+                                        ("auto", "parse"), ("gpu", "parse"), ("auto", "parse1"), ("gpu", "parse1"),
+                                        ("host", "parse1")])
 def test_epoll_server_on_gpu_ingest(tmp_path, mode, route):
     # route "parse": the server calls only netc's ws_parse_frame on a socket attached to the ring
     # (netc_ws_gpu_attach) -- the kept C API reaching the GPU
@@ -81,6 +86,8 @@ def test_epoll_server_on_gpu_ingest(tmp_path, mode, route):
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     assert summary["server_rc"] == 0 and summary["client_ok"] == 1
     assert summary["route"] == route
+    if route == "parse1":   # one call per wake-up: at least one wake-up per message
+        assert summary["events"] >= summary["delivered"]
     gpu_slots, host_slots = summary["gpu_slots"], summary["host_slots"]
     if mode == "gpu":
         assert host_slots == 0 and gpu_slots > 0

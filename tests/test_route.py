@@ -155,3 +155,40 @@ def test_send_route_serves_attached_socket_only():
         lib.netc_ws_send_route_detach(a.fileno())
         a.close()
         b.close()
+
+
+def test_route_belongs_to_the_connection_not_the_number():
+    """a route records its socket's identity; another route on a live socket
+    is refused (EBUSY); after the connection closes without a detach, the reused descriptor number
+    finds no route (the CPU parser serves the new connection) and may take a new route"""
+    import errno
+    import os
+    lib = host()
+    fn1 = ROUTE_FN(lambda *args: 1)
+    fn2 = ROUTE_FN(lambda *args: 1)
+    a, b = pair()
+    fd = b.fileno()
+    ctx = ctypes.c_void_p()
+    try:
+        assert lib.netc_ws_route_attach(fd, fn1, 11) == 0
+        assert lib.netc_ws_route_attach(fd, fn2, 22) == -1 and ctypes.get_errno() in (0, errno.EBUSY)
+        assert lib.netc_ws_route_attach(fd, fn1, 12) == -1           # same fn, other ctx: still another route
+        assert lib.netc_ws_route_get(fd, ctypes.byref(ctx)) and ctx.value == 11
+        a.close()
+        b.close()                                                     # no detach
+        c, d = pair()
+        if d.fileno() != fd:   # (the kernel usually hands out the same number by itself)
+            os.dup2(d.fileno(), fd)
+        try:
+            assert not lib.netc_ws_route_get(fd, ctypes.byref(ctx))   # stale: not served
+            assert lib.netc_ws_route_attach(fd, fn2, 22) == 0         # the new connection's route
+            assert lib.netc_ws_route_get(fd, ctypes.byref(ctx)) and ctx.value == 22
+            assert lib.netc_ws_route_detach(fd) == 0
+        finally:
+            if d.fileno() != fd:
+                os.close(fd)
+            c.close()
+            d.close()
+        assert lib.netc_ws_route_attach(fd, fn1, 11) == -1            # closed descriptor: EINVAL
+    finally:
+        lib.netc_ws_route_detach(fd)
