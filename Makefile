@@ -23,10 +23,12 @@ GPU_SRCS   := netc_amd/csrc/ws_mask_gpu.hip netc_amd/csrc/ws_frame_gpu.hip netc_
 GPU_HDRS   := netc_amd/csrc/ws_mask_gpu.h netc_amd/csrc/gpu_util.h include/ws/mask.h include/ws/frame.h include/ws/ingest.h \
               include/ws/route.h include/ws/common.h include/ws/egress.h
 
-.PHONY: all host gpu oracle diag clean asan
-all: host gpu oracle
+.PHONY: all host gpu oracle diag clean asan mock
+all: host gpu oracle mock
+mock: tests/bin/libnetc_ingest_mock.so
 host: $(LIBDIR)/libnetc.so
-gpu: $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc_ceiling.so tests/bin/ws_gpu_epoll tests/bin/ws_egress_bench
+gpu: $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc_ceiling.so tests/bin/ws_gpu_epoll tests/bin/ws_egress_bench \
+     tests/bin/ws_route_bench
 
 $(LIBDIR)/libnetc.so: $(HOST_SRCS) $(HOST_HDRS)
 	@mkdir -p $(LIBDIR)
@@ -51,19 +53,36 @@ $(LIBDIR)/libnetc_ceiling.so: netc_amd/csrc/ceiling.hip
 tests/bin/ws_gpu_epoll: tests/drivers/ws_gpu_epoll.c $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc.so $(HOST_HDRS)
 	@mkdir -p tests/bin
 	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -L$(LIBDIR) -lnetc_ws_gpu -lnetc -L/opt/rocm/lib -lamdhip64 \
-	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib -lpthread
+	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib -lpthread -ldl
 
 # send rates of the GPU egress ring beside the CPU ws_send_message (tools/bench_egress.py)
 tests/bin/ws_egress_bench: tests/drivers/ws_egress_bench.c $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc.so $(HOST_HDRS)
 	@mkdir -p tests/bin
 	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -L$(LIBDIR) -lnetc_ws_gpu -lnetc -L/opt/rocm/lib -lamdhip64 \
-	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib -lpthread
+	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib -lpthread -ldl
+
+# receive rates through ws_parse_frame over loopback TCP, netc's once-per-event loop: CPU path, GPU
+# route, the reference's own parser (tools/bench_routes.py)
+tests/bin/ws_route_bench: tests/drivers/ws_route_bench.c $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc.so $(HOST_HDRS)
+	@mkdir -p tests/bin
+	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -L$(LIBDIR) -lnetc_ws_gpu -lnetc -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib -lpthread -ldl
+
+# TEST ONLY: the ring's host code (ws_ingest.hip) over a host-memory mock of the HIP runtime
+# (tests/mockhip), so tests/test_route_mock.py drives the ingest ring and the ws_parse_frame route
+# on a machine without a GPU.  Never loaded by the product.
+tests/bin/libnetc_ingest_mock.so: netc_amd/csrc/ws_ingest.hip tests/mockhip/mock_gpu.cc tests/mockhip/hip/hip_runtime.h \
+                                  netc_amd/csrc/ws_mask_gpu.h $(LIBDIR)/libnetc.so $(HOST_HDRS)
+	@mkdir -p tests/bin
+	g++ -O1 -g -std=c++17 -fPIC -shared -Wall -Wno-unused-result -Itests/mockhip -x c++ netc_amd/csrc/ws_ingest.hip \
+	    -x none tests/mockhip/mock_gpu.cc -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -o $@
 
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(LIBDIR)/*.so build/*.o tests/bin/ws_gpu_epoll tests/bin/ws_egress_bench
+	rm -f $(LIBDIR)/*.so build/*.o tests/bin/ws_gpu_epoll tests/bin/ws_egress_bench tests/bin/ws_route_bench \
+	    tests/bin/libnetc_ingest_mock.so
 	$(MAKE) -C oracle clean
 
 # diagnostics (tools/, not part of the product)

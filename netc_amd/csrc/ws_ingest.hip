@@ -777,6 +777,20 @@ int netc_ws_gpu_detach(int sockfd) {
     return 0;
 }
 
+// diagnostics (tests): the ring's stream accounting
+int netc_ws_ingest_debug_state(const struct netc_ws_ingest* g, uint64_t* out8) {
+    if (!g || !out8) return NETC_GPU_EINVAL;
+    out8[0] = g->in_pos;
+    out8[1] = g->route.sock_pos;
+    out8[2] = g->msg.end_pos;
+    out8[3] = (uint64_t)g->count;
+    out8[4] = g->cur >= 0 ? g->slots[g->cur].fill : ~0ull;
+    out8[5] = g->msg.size;
+    out8[6] = (uint64_t)(int64_t)(g->sticky ? g->sticky : g->msg.err);
+    out8[7] = g->prev >= 0 ? g->slots[g->prev].pos + g->slots[g->prev].cut : 0;
+    return 0;
+}
+
 int netc_ws_ingest_scan_counts(const struct netc_ws_ingest* g, uint64_t* gpu, uint64_t* host) {
     if (!g || !gpu || !host) return NETC_GPU_EINVAL;
     *gpu = g->n_gpu;

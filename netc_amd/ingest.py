@@ -81,8 +81,10 @@ def _bind(lib):
     return lib
 
 
-def _raise(rc: int):
-    msg = _lib.gpu().netc_gpu_strerror()
+def _raise(rc: int, lib=None):
+    lib = lib if lib is not None else _lib.gpu()
+    lib.netc_gpu_strerror.restype = ctypes.c_char_p
+    msg = lib.netc_gpu_strerror()
     raise NetcGpuError(rc, msg.decode(errors="replace") if msg else "")
 
 
@@ -109,33 +111,35 @@ class Batch:
     def payload(self, k: int) -> Tuple[int, int]:
         """netc_ws_batch_payload: (offset into wire, length) of frame k's payload."""
         o, n = ctypes.c_uint64(0), ctypes.c_uint64(0)
-        rc = _lib.gpu().netc_ws_batch_payload(ctypes.byref(self._raw), k, ctypes.byref(o), ctypes.byref(n))
+        rc = self._owner._lib.netc_ws_batch_payload(ctypes.byref(self._raw), k, ctypes.byref(o), ctypes.byref(n))
         if rc:
             raise NetcGpuError(rc, f"frame {k} not in the batch")
         return int(o.value), int(n.value)
 
     def release(self) -> None:
         if self._raw is not None:
-            rc = _lib.gpu().netc_ws_ingest_release(self._owner._h, ctypes.byref(self._raw))
+            rc = self._owner._lib.netc_ws_ingest_release(self._owner._h, ctypes.byref(self._raw))
             self._raw = None
             if rc:
-                _raise(rc)
+                _raise(rc, self._owner._lib)
 
 
 class Ingest:
     """netc_ws_ingest_*: one connection's byte stream -> pinned slots -> GPU scan + unmask -> batches."""
 
     def __init__(self, device: int = 0, slot_bytes: int = 16 << 20, nslots: int = 4, max_frame_bytes: int = 65536,
-                 strict: bool = False, scan: str = "auto"):
-        """scan: "auto" (per slot by frame size, the C default), "gpu" or "host" (NETC_WS_INGEST_SCAN_*)."""
+                 strict: bool = False, scan: str = "auto", lib=None):
+        """scan: "auto" (per slot by frame size, the C default), "gpu" or "host" (NETC_WS_INGEST_SCAN_*).
+        lib: the library holding the ring (default libnetc_ws_gpu.so; the CPU tests pass the ring's host
+        code built over a mock HIP runtime, tests/mockhip)."""
         if scan not in _SCAN_FLAGS:
             raise ValueError(f"scan must be one of {sorted(_SCAN_FLAGS)}")
-        lib = _bind(_lib.gpu())
+        lib = _bind(lib if lib is not None else _lib.gpu())
         h = ctypes.c_void_p(0)
         rc = lib.netc_ws_ingest_create(ctypes.byref(h), device, slot_bytes, nslots, max_frame_bytes,
                                        (NETC_WS_INGEST_STRICT if strict else 0) | _SCAN_FLAGS[scan])
         if rc:
-            _raise(rc)
+            _raise(rc, self._lib)
         self._lib, self._h = lib, h
 
     def scan_counts(self) -> Tuple[int, int]:
@@ -143,14 +147,14 @@ class Ingest:
         g, h = ctypes.c_uint64(0), ctypes.c_uint64(0)
         rc = self._lib.netc_ws_ingest_scan_counts(self._h, ctypes.byref(g), ctypes.byref(h))
         if rc:
-            _raise(rc)
+            _raise(rc, self._lib)
         return int(g.value), int(h.value)
 
     def recv(self, fd: int) -> int:
         """netc_ws_ingest_recv: bytes read (> 0), 0 (would block), CLOSED or FULL; raises on other errors."""
         r = self._lib.netc_ws_ingest_recv(self._h, fd)
         if r < 0 and r not in (NETC_WS_INGEST_CLOSED, NETC_WS_INGEST_FULL):
-            _raise(int(r))
+            _raise(int(r), self._lib)
         return int(r)
 
     def write(self, data) -> int:
@@ -159,20 +163,20 @@ class Ingest:
                                    else data, dtype=np.uint8)
         r = self._lib.netc_ws_ingest_write(self._h, buf.ctypes.data if buf.size else None, buf.size)
         if r < 0 and r != NETC_WS_INGEST_FULL:
-            _raise(int(r))
+            _raise(int(r), self._lib)
         return int(r)
 
     def submit(self) -> None:
         rc = self._lib.netc_ws_ingest_submit(self._h)
         if rc:
-            _raise(rc)
+            _raise(rc, self._lib)
 
     def next(self, wait: bool = True) -> Optional[Batch]:
         """netc_ws_ingest_next: the oldest finished batch, or None; raises a stream error once it is due."""
         raw = _RawBatch()
         rc = self._lib.netc_ws_ingest_next(self._h, ctypes.byref(raw), 1 if wait else 0)
         if rc < 0:
-            _raise(rc)
+            _raise(rc, self._lib)
         return Batch(self, raw) if rc == 1 else None
 
     def next_message(self, max_payload_length: int = (1 << 64) - 1, wait: bool = True):
@@ -190,19 +194,19 @@ class Ingest:
         if rc in (1, WS_FRAME_PARSE_ERROR_RECV, WS_FRAME_PARSE_ERROR_INVALID_FRAME_LENGTH,
                   WS_FRAME_PARSE_ERROR_PAYLOAD_TOO_BIG):
             return rc, None, None
-        _raise(rc)
+        _raise(rc, self._lib)
 
     def attach(self, sockfd: int) -> None:
         """netc_ws_gpu_attach: libnetc's ws_parse_frame on sockfd is served from this ring (one
         ring, one connection; a ring that has carried a stream cannot be attached)."""
         rc = self._lib.netc_ws_gpu_attach(sockfd, self._h)
         if rc:
-            _raise(rc)
+            _raise(rc, self._lib)
 
     def detach(self, sockfd: int) -> None:
         rc = self._lib.netc_ws_gpu_detach(sockfd)
         if rc:
-            _raise(rc)
+            _raise(rc, self._lib)
 
     def close(self) -> None:
         if self._h:

@@ -14,11 +14,21 @@
  *   cpu_socket    libnetc's ws_send_message on the CPU path, same socketpair
  *   cpu_mem       the CPU path's work without the socket: header + netc_ws_mask of every frame
  *                 into one host wire buffer
- * One JSON line per leg on stdout.
+ *   ref_socket    the REFERENCE's own ws_send_message (oracle/_ref/libref_ws.so, compiled from
+ *                 /root/reference/src/ws/common.c at its flags, -O0; dlopen'd), same socket: a
+ *                 stated baseline.  TEXT messages of printable bytes from one NUL-terminated
+ *                 buffer: its masked BINARY path overflows the heap above 254 bytes (defect B1,
+ *                 src/ws/common.c:100) and its TEXT path copies with strdup (B3)
+ * Transport (argv[5]): "unix" (default) a socketpair, "tcp" a loopback TCP connection (TCP_NODELAY);
+ * a reader thread discards what arrives.  One JSON line per leg on stdout.
  *
- * usage: ws_egress_bench MSG_BYTES TOTAL_MIB [masked 0|1] [legs: comma list, default all]
+ * usage: ws_egress_bench MSG_BYTES TOTAL_MIB [masked 0|1] [legs: comma list, default all] [unix|tcp] [ref_lib]
  */
 #define _GNU_SOURCE
+#include <arpa/inet.h>
+#include <dlfcn.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -62,8 +72,24 @@ struct sockpair {
     pthread_t th;
 };
 
+static int g_tcp;
+
 static void sp_open(struct sockpair *s) {
-    if (socketpair(AF_UNIX, SOCK_STREAM, 0, s->fd)) {
+    if (g_tcp) {
+        int ls = socket(AF_INET, SOCK_STREAM, 0), one = 1;
+        struct sockaddr_in a = {.sin_family = AF_INET, .sin_port = 0};
+        a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+        socklen_t al = sizeof a;
+        s->fd[0] = socket(AF_INET, SOCK_STREAM, 0);
+        if (ls < 0 || bind(ls, (struct sockaddr *)&a, sizeof a) || listen(ls, 1) ||
+            getsockname(ls, (struct sockaddr *)&a, &al) || connect(s->fd[0], (struct sockaddr *)&a, sizeof a) ||
+            (s->fd[1] = accept(ls, NULL, NULL)) < 0) {
+            perror("tcp loopback");
+            exit(2);
+        }
+        close(ls);
+        setsockopt(s->fd[0], IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    } else if (socketpair(AF_UNIX, SOCK_STREAM, 0, s->fd)) {
         perror("socketpair");
         exit(2);
     }
@@ -114,7 +140,9 @@ int main(int argc, char **argv) {
     const size_t msg = (size_t)strtoull(argv[1], NULL, 0);
     const uint64_t total = strtoull(argv[2], NULL, 0) << 20;
     const int masked = argc > 3 ? atoi(argv[3]) : 1;
-    const char *legs = argc > 4 ? argv[4] : NULL;
+    const char *legs = argc > 4 && strcmp(argv[4], "all") ? argv[4] : NULL;
+    g_tcp = argc > 5 && !strcmp(argv[5], "tcp");
+    const char *ref_lib = argc > 6 ? argv[6] : "oracle/_ref/libref_ws.so";
     const uint64_t nmsg = total / msg;
     const size_t src_bytes = (size_t)(total < (64u << 20) ? total : (64u << 20));   /* reused round robin */
     const uint64_t per_src = src_bytes / msg;
@@ -246,6 +274,33 @@ int main(int argc, char **argv) {
         const double secs = now() - t0;
         report("cpu_mem", msg, nmsg, masked, wire_total, secs, 0);
         free(wire);
+    }
+    if (want(legs, "ref_socket")) {
+        typedef int (*ref_send_fn)(struct web_client *, struct ws_message *, uint8_t *, size_t);
+        void *h = dlopen(ref_lib, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
+        ref_send_fn ref_send = h ? (ref_send_fn)dlsym(h, "ws_send_message") : NULL;
+        if (!ref_send) {
+            fprintf(stderr, "ref: %s\n", dlerror());
+            return 1;
+        }
+        char *text = malloc(msg + 1);
+        for (size_t i = 0; i < msg; ++i) text[i] = (char)('a' + (i * 7) % 26);
+        text[msg] = 0;
+        struct sockpair sp;
+        sp_open(&sp);
+        memset(&tcp, 0, sizeof(tcp));
+        tcp.sockfd = sp.fd[0];
+        const double t0 = now();
+        for (uint64_t i = 0; i < nmsg; ++i) {
+            const uint64_t j = i % per_src;
+            m.opcode = WS_OPCODE_TEXT;   /* the reference's struct ws_message has the same layout */
+            m.payload_length = msg;
+            m.buffer = (uint8_t *)text;
+            if (ref_send((struct web_client *)&head, &m, masked ? keys + 4 * j : NULL, 1) != 1) return 1;
+        }
+        const double secs = now() - t0;
+        report("ref_socket", msg, nmsg, masked, wire_total, secs, sp_close(&sp));
+        free(text);
     }
     netc_ws_egress_destroy(eg);
     free(src);

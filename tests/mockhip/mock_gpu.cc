@@ -1,0 +1,69 @@
+// TEST INFRASTRUCTURE ONLY: host stand-ins for the netc_gpu:: kernel launches and C-ABI helpers
+// that ws_ingest.hip calls (see hip/hip_runtime.h here).  The frame scan is libnetc's host header
+// walk (netc_ws_scan_frames_host, pinned against the oracle in tests/test_scan_host.py); the
+// unmask is the reference's scalar loop (src/ws/common.c:317-323) over the frames it found.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "../../netc_amd/csrc/ws_mask_gpu.h"
+extern "C" {
+#include "../../include/ws/frame.h"
+extern __thread int netc_errno_reason;
+}
+
+namespace netc_gpu {
+namespace {
+char g_err[512];
+int g_fault = -1;
+}
+struct ScanScratch {
+    uint32_t diag;
+};
+ScanScratch* scan_scratch_new() { return new ScanScratch{0}; }
+void scan_scratch_free(ScanScratch* s) { delete s; }
+hipError_t scan_scratch_reserve(ScanScratch*, uint64_t, hipStream_t) { return hipSuccess; }
+const uint32_t* scan_scratch_diag_word(const ScanScratch* s) { return &s->diag; }
+hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start, bool strict, uint64_t* hdr,
+                              uint32_t* keys, uint8_t* b0, uint64_t max_frames, uint64_t* result, hipStream_t,
+                              ScanScratch*) {
+    return netc_ws_scan_frames_host(wire, len, start, strict ? NETC_WS_SCAN_STRICT : 0, hdr, keys, b0, max_frames,
+                                    result) == 0 ? hipSuccess : hipErrorInvalidValue;
+}
+hipError_t launch_unmask_scanned(uint8_t* wire, uint64_t, const uint64_t* hdr, const uint32_t* keys,
+                                 uint64_t max_frames, const uint64_t* result, hipStream_t, const LaunchCfg&) {
+    const uint64_t n = result[0] < max_frames ? result[0] : max_frames;
+    for (uint64_t k = 0; k < n; ++k) {
+        const uint64_t h = hdr[k];
+        const uint8_t second = wire[h + 1];
+        const uint64_t code = second & 0x7F;
+        if (!(second & 0x80)) continue;
+        const uint64_t p = h + 2 + (code == 126 ? 2 : code == 127 ? 8 : 0) + 4;
+        const uint8_t* key = wire + p - 4;
+        for (uint64_t i = p; i < hdr[k + 1]; ++i) wire[i] ^= key[(i - p) & 3];
+    }
+    return hipSuccess;
+}
+int api_fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    netc_errno_reason = NETC_REASON_GPU;
+    return code;
+}
+int api_fail_hip(int code, const char* what, hipError_t) { return api_fail(code, "%s: mock failure", what); }
+int api_check_device(int) { return 0; }
+LaunchCfg api_cfg() { return LaunchCfg(); }
+int64_t knob(int) { return -1; }
+bool inject_fault() {
+    if (g_fault < 0) return false;
+    return g_fault-- == 0;
+}
+}  // namespace netc_gpu
+
+extern "C" const char* netc_gpu_strerror(void) { return netc_gpu::g_err; }
+extern "C" int netc_mock_inject_fault(int countdown) {
+    netc_gpu::g_fault = countdown;
+    return 0;
+}

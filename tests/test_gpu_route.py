@@ -9,7 +9,7 @@ drive it exactly that way -- one ws_parse_frame per readiness of the socket -- a
   * every message the peer sent is delivered, and the socket stays readable while a complete
     message waits in the ring: nothing is stranded when the peer goes quiet after a burst
     (the driver fails the moment the socket is not readable with messages still owed);
-  * the messages equal, in order, the oracle's: the wire is built with oracle_encode_frame
+  * the messages equal, in order, the oracle's: the wire is built with oracle_encode_batch
     (the reference's send path, src/ws/common.c:53-125, pinned by the golden send vectors in
     tests/test_oracle.py) from known plaintexts, and each delivered message must be that
     plaintext (with the NUL the reference appends to TEXT, src/ws/common.c:340-344);
@@ -74,15 +74,20 @@ def script(rng, n, big=False):
 
 
 def wire_of(msgs):
-    """the oracle's frames of every message (a fragment per key, the reference's split)"""
+    """the oracle's frames of every message (a fragment per key, the reference's split) --
+    oracle_encode_batch, which gives a masked empty frame its key (RFC 6455 §5.2; the
+    reference's single-frame send omits it, defect B9, so its wire would not parse)"""
     w = bytearray()
     for op, p, nf, keys in msgs:
         split, rem = divmod(len(p), nf)
-        pos = 0
+        off = [0]
         for i in range(nf):
-            flen = split + (rem if i + 1 == nf else 0)
-            w += orc.encode_frame(p[pos:pos + flen], op if i == 0 else 0, keys[i], fin=i + 1 == nf)
-            pos += flen
+            off.append(off[-1] + split + (rem if i + 1 == nf else 0))
+        h0 = [(0x80 if i + 1 == nf else 0) | (op if i == 0 else 0) for i in range(nf)]
+        k32 = [int.from_bytes(k, "little") for k in keys]
+        wire, _ = orc.encode_batch(np.frombuffer(p, dtype=np.uint8), np.array(off, dtype=np.uint64),
+                                   np.array(k32, dtype=np.uint32), np.array(h0, dtype=np.uint8), True)
+        w += wire.tobytes()
     return bytes(w)
 
 
@@ -90,13 +95,23 @@ def expected(msgs):
     return [(op, p + (b"\0" if op == TEXT else b"")) for op, p, _, _ in msgs]
 
 
-def once_per_event(sock, ep, lib, n, limit, timeout=10.0):
+def ring_state(ing):
+    lib = ing._lib
+    out = (ctypes.c_uint64 * 8)()
+    lib.netc_ws_ingest_debug_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.netc_ws_ingest_debug_state(ing._h, out)
+    names = ["in_pos", "sock_pos", "end_pos", "batches", "cur_fill", "msg_size", "err", "scanned_to"]
+    return dict(zip(names, list(out)))
+
+
+def once_per_event(sock, ep, lib, n, limit, timeout=10.0, ing=None, sent=None):
     """netc's server loop: wait for readability, ONE ws_parse_frame, dispatch, repeat"""
     st = ParseState()
     got = []
     while len(got) < n:
         r, _, _ = select.select([sock], [], [], timeout)
-        assert r, f"stranded: {len(got)} of {n} messages delivered and the socket is not readable"
+        assert r, (f"stranded: {len(got)} of {n} messages delivered and the socket is not readable; "
+                   f"ring {ring_state(ing) if ing else None}, sent {sent}")
         rc = lib.ws_parse_frame(ctypes.byref(ep.client), ctypes.byref(st), limit)
         if rc == 0:
             m = st.message
@@ -104,7 +119,7 @@ def once_per_event(sock, ep, lib, n, limit, timeout=10.0):
             libc.free(m.buffer)                                      # src/web/server.c:139
             ctypes.memset(ctypes.byref(st), 0, ctypes.sizeof(st))    # src/web/server.c:140
         else:
-            assert rc == 1, f"ws_parse_frame returned {rc}: {nm._lib.gpu().netc_gpu_strerror()}"
+            assert rc == 1, f"ws_parse_frame returned {rc}"
     return got
 
 
@@ -121,12 +136,19 @@ def test_once_per_event_delivers_everything(kind, slot_bytes, scan):
     c, s = tcp_pair() if kind == "tcp" else pair()
     s.setblocking(False)
     ep = Endpoint(s)
-    sender = threading.Thread(target=c.sendall, args=(wire,))
+    sent = [0, len(wire)]
+
+    def send_all():
+        for i in range(0, len(wire), 1 << 16):
+            c.sendall(wire[i:i + (1 << 16)])
+            sent[0] = i + len(wire[i:i + (1 << 16)])
+
+    sender = threading.Thread(target=send_all)
     with ni.Ingest(slot_bytes=slot_bytes, nslots=4, max_frame_bytes=4 << 20, scan=scan) as ing:
         ing.attach(s.fileno())
         try:
             sender.start()
-            got = once_per_event(s, ep, lib, len(msgs), 64 << 20)
+            got = once_per_event(s, ep, lib, len(msgs), 64 << 20, ing=ing, sent=sent)
             sender.join()
             # everything delivered: the ring took every byte out of the socket
             assert not select.select([s], [], [], 0.2)[0]
