@@ -139,7 +139,7 @@ class Ingest:
         rc = lib.netc_ws_ingest_create(ctypes.byref(h), device, slot_bytes, nslots, max_frame_bytes,
                                        (NETC_WS_INGEST_STRICT if strict else 0) | _SCAN_FLAGS[scan])
         if rc:
-            _raise(rc, self._lib)
+            _raise(rc, lib)
         self._lib, self._h = lib, h
 
     def scan_counts(self) -> Tuple[int, int]:
