@@ -75,7 +75,7 @@ tests/bin/libnetc_ingest_mock.so: netc_amd/csrc/ws_ingest.hip tests/mockhip/mock
                                   netc_amd/csrc/ws_mask_gpu.h $(LIBDIR)/libnetc.so $(HOST_HDRS)
 	@mkdir -p tests/bin
 	g++ -O1 -g -std=c++17 -fPIC -shared -Wall -Wno-unused-result -Itests/mockhip -x c++ netc_amd/csrc/ws_ingest.hip \
-	    -x none tests/mockhip/mock_gpu.cc -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -o $@
+	    -x none tests/mockhip/mock_gpu.cc -L$(LIBDIR) -lnetc -Wl,-Bsymbolic -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -o $@
 
 oracle:
 	$(MAKE) -C oracle
