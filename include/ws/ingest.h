@@ -153,15 +153,23 @@ int netc_ws_ingest_next_message(struct netc_ws_ingest *ing, struct ws_message *m
 /**
  * Serve netc's own ws_parse_frame (libnetc.so) on `sockfd` from `ring` (include/ws/route.h):
  * while attached, ws_parse_frame(client, &state, limit) on that socket takes the next message
- * from the ring -- receiving with large recv() calls into the pinned slots, frames found and
- * unmasked on the GPU -- with the reference's contract (src/ws/common.c:134-348): 0 and
- * state->message filled (the caller frees message.buffer, src/web/server.c:139), 1 when the
- * socket has nothing more now, or WS_FRAME_PARSE_ERROR_* (PAYLOAD_TOO_BIG against `limit`,
- * RECV once the peer closed and every message was returned).  Other sockets keep the CPU
- * parser.  The ring reads ahead of the message it returns, so a caller driven by readiness
- * events calls ws_parse_frame again after a 0 until it returns 1 (the level-triggered event
- * does not fire for bytes already in the ring).  One thread per connection, as netc runs it;
- * detach before destroying the ring.  0 or NETC_GPU_EINVAL.
+ * from the ring -- frames found and unmasked on the GPU -- with the reference's contract
+ * (src/ws/common.c:134-348): 0 and state->message filled (the caller frees message.buffer,
+ * src/web/server.c:139), 1 when the socket has nothing more now, or WS_FRAME_PARSE_ERROR_*
+ * (PAYLOAD_TOO_BIG against `limit`, RECV once the peer closed and every message was
+ * returned); a device / runtime failure returns its NETC_GPU_E* code (-101..-105), never one of
+ * those.  netc's caller calls ws_parse_frame ONCE per EPOLLIN (src/tcp/server.c:72-75 ->
+ * src/web/server.c:86-98), and that is enough: the ring reads ahead with MSG_PEEK and takes the
+ * peeked bytes out of the socket all but one, which it leaves there while it holds bytes it has
+ * not delivered, so the level-triggered event fires again for every message already in the
+ * ring (a caller may also call again after a 0 until it gets 1).  While the caller works on a
+ * message, bytes that arrived since are sent to the GPU.  Other sockets keep the CPU parser.
+ * One ring serves one connection: attaching a ring that already serves another open socket,
+ * or one that has carried a stream, fails (NETC_GPU_EINVAL); so does a second ring on one
+ * socket.  netc_ws_ingest_recv / _write on an attached ring are refused.  A route left behind
+ * by a socket closed without a detach does not serve the next socket given its number.  One
+ * thread per connection, as netc runs it; detach before destroying the ring.  0 or
+ * NETC_GPU_EINVAL.
  */
 int netc_ws_gpu_attach(int sockfd, struct netc_ws_ingest *ring);
 int netc_ws_gpu_detach(int sockfd);

@@ -31,7 +31,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/socket.h>
+#include <sys/ioctl.h>
 #include <sys/stat.h>
+#include <sys/uio.h>
 
 #include <new>
 
@@ -59,6 +61,10 @@ constexpr size_t kScratch = 1u << 20;   // discard buffer of the route on non-TC
 // parse per frame (<= 1,024 per 16 MiB slot at this size); the GPU scan reads every byte
 // but costs the host nothing, so small frames stay on the GPU.
 constexpr uint64_t kHostWalkMean = 16384;
+// ... and for a slot of fewer bytes than this, whatever its frames: the GPU scan's fixed cost
+// (its launches, ~20 us) is more than the walk of the few frames such a slot can hold, and a
+// small slot is a latency case (one message submitted as it arrives)
+constexpr uint64_t kHostWalkBytes = 64 * 1024;
 
 enum SlotState : int { kFree = 0, kFilling, kInflight, kTaken };
 
@@ -288,6 +294,7 @@ int submit_cur(netc_ws_ingest* g) {
         if (g->scan_mode == 0)
             host_walk = p.frames == 0 || p.cut / p.frames >= kHostWalkMean || (!g->strict && unchecked_headers(p));
     }
+    if (g->scan_mode == 0 && carry + s.fill < kHostWalkBytes) host_walk = true;
     if (carry > g->carry_cap) return set_sticky(g, NETC_WS_INGEST_TOO_BIG, g->prev);
     // the carried bytes are raw in the previous slot (the unmask stops at its last
     // complete frame, its copy back rewrites them unchanged)
@@ -425,9 +432,11 @@ void netc_ws_ingest_destroy(struct netc_ws_ingest* g) {
     delete g;
 }
 
-// one recv() into the current slot; with peek (the ws_parse_frame route) MSG_PEEK: the bytes
-// stay in the socket until the route removes them (RouteState)
-static long ring_recv(netc_ws_ingest* g, int fd, bool peek) {
+// One recv() into the current slot; the bytes read (> 0), 0 when the socket has none now, or a
+// code.  skip >= 0 (the ws_parse_frame route): MSG_PEEK, the bytes stay in the socket until the
+// route removes them (RouteState), and the first `skip` bytes the socket holds -- already in the
+// ring, its hostage byte -- go to a scratch byte instead of the slot.
+static long ring_recv(netc_ws_ingest* g, int fd, int skip = -1) {
     if (!g) return api_fail(NETC_GPU_EINVAL, "ingest: null ingest");
     if (g->sticky) return sticky_now(g) ? g->sticky : api_fail(g->sticky, "ingest: the stream has ended (error)");
     DeviceGuard dg(g->device);
@@ -443,8 +452,21 @@ static long ring_recv(netc_ws_ingest* g, int fd, bool peek) {
     uint8_t* dst = s.h_buf + g->carry_cap + s.fill;
     const size_t room = (size_t)(g->slot_bytes - s.fill);
     ssize_t r;
-    do r = recv(fd, dst, room, peek ? MSG_PEEK : 0);
-    while (r < 0 && errno == EINTR);
+    if (skip < 0) {
+        do r = recv(fd, dst, room, 0);
+        while (r < 0 && errno == EINTR);
+    } else {
+        uint8_t held[1];
+        struct iovec iov[2] = {{held, (size_t)skip}, {dst, room}};
+        struct msghdr mh;
+        memset(&mh, 0, sizeof mh);
+        mh.msg_iov = skip ? iov : iov + 1;
+        mh.msg_iovlen = skip ? 2 : 1;
+        do r = recvmsg(fd, &mh, MSG_PEEK);
+        while (r < 0 && errno == EINTR);
+        if (r > 0 && r <= skip) return 0;   // only what the ring already has
+        if (r > 0) r -= skip;
+    }
     if (r < 0) {
         if (errno == EAGAIN || errno == EWOULDBLOCK) return 0;
         const int saved = errno;
@@ -470,7 +492,7 @@ long netc_ws_ingest_recv(struct netc_ws_ingest* g, int fd) {
     if (g && g->route.fd >= 0)
         return api_fail(NETC_GPU_EINVAL, "ingest: the ring serves socket %d through ws_parse_frame "
                         "(netc_ws_gpu_attach); detach it first", g->route.fd);
-    return ring_recv(g, fd, false);
+    return ring_recv(g, fd);
 }
 
 long netc_ws_ingest_write(struct netc_ws_ingest* g, const void* data, size_t len) {
@@ -570,6 +592,21 @@ static int message_code(int r) {
     }
 }
 
+// a new message whose frames up to FIN are all in the batch: its buffer at its exact size
+// (the payloads + a NUL), so the appends never reallocate and copy it again
+static void msg_reserve_exact(MessageState& m, const netc_ws_batch& b, uint64_t k) {
+    uint64_t need = 1;
+    for (uint64_t j = k, stop = k + 1024 < b.nframes ? k + 1024 : b.nframes; j < stop; ++j) {
+        uint64_t off = 0, len = 0;
+        (void)netc_ws_batch_payload(&b, j, &off, &len);
+        need += len;
+        if (b.b0[j] & 0x80) {
+            if ((m.buf = (uint8_t*)malloc(need))) m.cap = need;
+            return;
+        }
+    }
+}
+
 static bool msg_append(MessageState& m, const uint8_t* p, size_t n) {
     if (m.size + n > m.cap || !m.buf) {
         size_t cap = m.cap ? m.cap : 64;
@@ -616,6 +653,7 @@ int netc_ws_ingest_next_message(struct netc_ws_ingest* g, struct ws_message* mes
             if (op != WS_OPCODE_CONTINUE) m.opcode = op;                        // :163-164
             if (len + m.size > max_payload_length)                             // :210-211, :261-262
                 return m.err = WS_FRAME_PARSE_ERROR_PAYLOAD_TOO_BIG;
+            if (!m.buf) msg_reserve_exact(m, b, k);
             if (!msg_append(m, b.wire + off, (size_t)len))
                 return m.err = api_fail(NETC_GPU_ENOMEM, "ingest: message buffer");
             if (b0 & 0x80) {                                                    // FIN: the message (:340-346)
@@ -675,12 +713,16 @@ static int sock_consume(netc_ws_ingest* g, int fd, uint64_t to) {
 // (src/tcp/server.c:72-75 -> src/web/server.c:86-98, which calls ws_parse_frame ONCE per
 // EPOLLIN and goes back to epoll_wait).
 //
-// The ring reads ahead -- one MSG_PEEK as large as the slot's room, then the GPU scan and
-// unmask over every frame in it -- but takes bytes out of the socket only up to the end of
-// the message it returns.  So while a complete message waits in the ring, its bytes are
-// still in the socket and the level-triggered event fires again: nothing is stranded when
-// the peer goes quiet.  Only once the ring holds no complete message (next_message says 1)
-// are the peeked bytes of the incomplete tail removed, and the socket peeked again past them.
+// The ring reads ahead -- MSG_PEEK as large as the slot's room, then the GPU scan and unmask
+// over every frame in it -- and then takes the peeked bytes out of the socket (recv with
+// MSG_TRUNC: no copy) all but the last one.  That byte, the hostage, stays in the socket as long
+// as the ring holds bytes it has not delivered: the level-triggered event keeps firing for them,
+// so a complete message never waits in the ring while the peer is quiet, and the socket buffer
+// is still drained at once (the peer is not throttled by bytes the ring already has).  The
+// hostage is released when the ring has delivered everything it read, or when it holds no
+// complete message and the socket nothing new.  The next peek reads the hostage into a scratch
+// byte (it is in the ring already).  While the caller works on a message, bytes that have
+// arrived since go to the GPU (`pump`), so the next batch is in flight in the meantime.
 //   0   state->message filled as ws_parse_frame fills it (opcode, caller-owned malloc'd
 //       buffer, payload_length with a TEXT message's NUL); nothing else of the state is used
 //   1   the socket has nothing more now and the ring no complete message
@@ -688,6 +730,35 @@ static int sock_consume(netc_ws_ingest* g, int fd, uint64_t to) {
 //       limit); INVALID_FRAME_LENGTH for a header strict mode rejects; RECV once the peer
 //       closed and every message before that was returned, or recv failed
 //   NETC_GPU_E*   a device / runtime failure (-101..-105: never one of the above)
+
+// peek what the socket has past the ring's bytes into the ring, then take it out of the socket
+// but for the hostage; returns new bytes (> 0), 0 when nothing new, or a code (CLOSED, ...)
+static long route_take(netc_ws_ingest* g, int fd) {
+    RouteState& rs = g->route;
+    const int held = (int)(g->in_pos - rs.sock_pos);   // 0 or 1
+    long n = ring_recv(g, fd, held);
+    if (n > 0) {
+        if (int e = sock_consume(g, fd, g->in_pos - 1)) return e;
+        return n;
+    }
+    if (n == 0 && held) {   // only the hostage: release it and look once more
+        if (int e = sock_consume(g, fd, g->in_pos)) return e;
+        n = ring_recv(g, fd, 0);
+        if (n > 0) {
+            if (int e = sock_consume(g, fd, g->in_pos - 1)) return e;
+        }
+    }
+    return n;
+}
+
+// while the caller works on a delivered message: bytes that arrived since go to the GPU now
+static void route_pump(netc_ws_ingest* g, int fd) {
+    if (g->count != 0 || g->sticky) return;   // a batch is already on its way, or the stream is over
+    int avail = 0;
+    if (ioctl(fd, FIONREAD, &avail) != 0 || avail <= (int)(g->in_pos - g->route.sock_pos)) return;
+    if (route_take(g, fd) > 0) (void)netc_ws_ingest_submit(g);   // (a failure resurfaces on the next call)
+}
+
 static int gpu_route(void* ctx, int sockfd, struct ws_frame_parsing_state* state, size_t max_payload_length) {
     netc_ws_ingest* g = (netc_ws_ingest*)ctx;
     if (sockfd != g->route.fd)
@@ -697,17 +768,16 @@ static int gpu_route(void* ctx, int sockfd, struct ws_frame_parsing_state* state
         struct ws_message m;
         const int r = netc_ws_ingest_next_message(g, &m, max_payload_length, 1);
         if (r == 0) {
-            // the message's bytes leave the socket; later messages' stay (still readable).  A
-            // failing socket is reported by the next call's peek, after this message.
-            (void)sock_consume(g, sockfd, g->msg.end_pos);
+            // everything the ring read is delivered: the hostage goes too (a failing socket is
+            // reported by the next call, after this message)
+            if (g->msg.end_pos == g->in_pos && !g->msg.buf) (void)sock_consume(g, sockfd, g->in_pos);
+            else route_pump(g, sockfd);
             state->message = m;
             return 0;
         }
         if (r < 0) return r;
-        // no complete message in the ring: the incomplete tail it holds leaves the socket,
-        // then one peek past it
-        if (int e = sock_consume(g, sockfd, g->in_pos)) return g->msg.err = message_code(e);
-        const long n = ring_recv(g, sockfd, true);
+        // no complete message in the ring: read on
+        const long n = route_take(g, sockfd);
         if (n == 0) return 1;                              // drained: wait for readiness
         if (n > 0 || n == NETC_WS_INGEST_CLOSED) {         // (closed: what it sent is delivered first)
             full = 0;
