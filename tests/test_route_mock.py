@@ -129,3 +129,27 @@ def test_peer_waits_for_each_reply(mock, msg_bytes):
     c.close()
     s.close()
     assert got == [(op, p) for op, p, _, _ in msgs]
+
+
+# ---------------------------------------------------------------- the shared ring (hub) --
+
+@pytest.fixture
+def hub_mock(mock, monkeypatch):
+    from tests import test_gpu_hub as H
+    monkeypatch.setattr(H, "HUB_LIB", mock)
+    return H
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("nconn,nmsg,slot", [(64, 40, 1 << 20), (16, 60, 128 << 10)])
+def test_hub_many_connections(hub_mock, nconn, nmsg, slot):
+    hub_mock.test_hub_many_connections(nconn, nmsg, slot)
+
+
+@pytest.mark.timeout(60)
+def test_hub_unix_sockets_and_big_frames(hub_mock):
+    hub_mock.test_hub_unix_sockets_and_big_frames()
+
+
+def test_hub_attach_rules(hub_mock):
+    hub_mock.test_hub_attach_rules()
