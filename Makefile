@@ -92,8 +92,8 @@ clean:
 	$(MAKE) -C oracle clean
 
 # diagnostics (tools/, not part of the product)
-diag: tools/libdiag_stream.so tools/libnetc_ws_gpu_stamps.so tools/libdiag_order.so tools/libdiag_policy.so \
-      tools/libnetc_ws_gpu_checks.so tools/libscan_k1only.so tools/libscan_k1exp.so
+diag: tools/libdiag_stream.so tools/libnetc_ws_gpu_stamps.so tools/libnetc_ws_gpu_checks.so tools/libscan_k1only.so \
+      tools/libscan_k1exp.so
 tools/libdiag_stream.so: tools/diag_stream.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 tools/libnetc_ws_gpu_stamps.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
@@ -104,10 +104,6 @@ tools/libscan_k1only.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
 	$(HIPCC) $(HIPFLAGS) -DNETC_SCAN_K1_ONLY -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 tools/libscan_k1exp.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
 	$(HIPCC) $(HIPFLAGS) -DNETC_SCAN_K1_EXP -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
-tools/libdiag_order.so: tools/diag_order.hip
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
-tools/libdiag_policy.so: tools/diag_policy.hip
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 
 # ASan + UBSan over the host C (the reference had two heap overflows on this
 # path, B1 src/ws/common.c:100 and B6 :306-315; this proves the rebuilt parser has none).

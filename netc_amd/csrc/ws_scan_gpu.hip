@@ -1722,10 +1722,10 @@ __global__ __launch_bounds__(kResolveT) void scan_resolve(ScanArgs a, uint64_t t
 // K2 on its 16 chunks; the last of a tile's blocks to finish (an arrival counter per
 // tile) runs K3a for that tile, while other tiles' blocks are still in K2; the last tile
 // to finish K3a (one more counter) runs K3b over all of them.  Two launch boundaries
-// and their cold trips fewer, and K3a overlapped with K2.  Each arrival is a release
-// fence by every thread, then one atomic; the block that arrives last resets the
-// counter for the next call and acquires before reading the other blocks' results.
-// The phases' LDS share one union (36 KB: 4 blocks per CU).
+// and their cold trips fewer, and K3a overlapped with K2.  Each arrival is one atomic
+// after the block's own sc1 stores have completed (arrive_last below: no fences); the
+// block that arrives last resets the counter for the next call and reads the other
+// blocks' results with sc1 loads.  The phases' LDS share one union (36 KB: 4 blocks per CU).
 static constexpr int kFuseTiles = 512;   // 512 MiB of stream
 static constexpr int kFuseCap = 1024;    // external nodes
 union FusedLds {

@@ -1,0 +1,52 @@
+"""Many connections on one event loop: the GPU hub (include/ws/hub.h) against libnetc's CPU
+ws_parse_frame and the reference's own parser (VERDICT r4 "next" #7).
+
+Runs tests/bin/ws_hub_server (tests/drivers/ws_hub_server.c) per configuration and leg: CONNS
+loopback TCP connections, MSGS messages each of 0..MAX bytes (1-3 fragments, PINGs), sent round
+robin by 4 client threads with libnetc's ws_send_message; the server calls ws_parse_frame once per
+readable socket per loop iteration (netc's loop, reference src/tcp/server.c:30-75 ->
+src/web/server.c:69-98).  Per-connection delivery is checked by hash against what each client
+sent.  One JSON line per run (stdout and --out).
+
+    python tools/bench_hub.py [--configs 256x400x1024,1024x100x1024,64x200x16384] [--out FILE]
+"""
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "bin", "ws_hub_server")
+REF = os.path.join(ROOT, "oracle", "_ref", "libref_ws.so")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="256x400x1024,1024x100x1024,64x200x16384,16x100x262144")
+    ap.add_argument("--legs", default="hub,cpu,ref")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    if not os.path.exists(EXE):
+        sys.exit(f"{EXE} missing: run make")
+    out = open(args.out, "a") if args.out else None
+    for cfg in args.configs.split(","):
+        conns, msgs, mx = cfg.split("x")
+        for leg in args.legs.split(","):
+            if leg == "ref" and not os.path.exists(REF):
+                continue
+            r = subprocess.run([EXE, leg, conns, msgs, mx], capture_output=True, text=True, timeout=600, cwd=ROOT)
+            if r.returncode:
+                sys.exit(f"{cfg} {leg}: rc {r.returncode}: {r.stderr[-2000:]}")
+            rec = json.loads(r.stdout.strip().splitlines()[-1])
+            rec.pop("conn_hash", None)
+            line = json.dumps(rec)
+            print(line, flush=True)
+            if out:
+                out.write(line + "\n")
+                out.flush()
+
+
+if __name__ == "__main__":
+    main()

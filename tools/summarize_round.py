@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""gpurun_out/<tag>/ (tools/gpu_round.sh) -> the committed evidence under profiles/:
+"""gpurun_out/<tag>/ (tools/gpu_record.sh) -> the committed evidence under profiles/:
 
   profiles/<tag>_c2_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary, as produced
   profiles/<tag>_c2_summary.json       the mask kernel: launches, rocprof mean duration (all
@@ -50,7 +50,7 @@ def main():
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(prof, f"{args.tag}_{wl}_kernel_stats.csv"))
     bpath = os.path.join(src, "bench.json")
-    if not os.path.exists(bpath):   # tools/gpu_round2.sh names it per workload
+    if not os.path.exists(bpath):   # the record driver names it per workload
         bpath = os.path.join(src, f"bench_{wl}.json")
     bench = json.loads(open(bpath).read().strip().splitlines()[-1])
     total = bench["config"]["batch_bytes_per_gpu"]
