@@ -9,7 +9,7 @@
 #   prof      rocprofv3 trace + FETCH_SIZE / WRITE_SIZE passes of the headline, summarised into
 #             profiles/ by tools/summarize_round.py on the CPU side afterwards  -> TAG_c2/
 #   rows      the SURVEY §8(f) rows (tools/prof_rows.sh)          -> rows_TAG/
-#   c3        bench.py --workload c3 with FETCH_SIZE / WRITE_SIZE passes            -> TAG_c3/
+#   wl        bench.py --workload W (WLS, default "c3 c4") with FETCH_SIZE / WRITE_SIZE passes -> TAG_W/
 #   routes    tools/bench_routes.py (the kept API over loopback TCP) -> TAG/routes.jsonl
 #   hub       tools/bench_hub.py + a rocprofv3 trace of the hub leg  -> TAG/hub.jsonl, TAG_hub/
 # Every GPU step runs under its own time limit; the chain stops at the first failure.
@@ -57,15 +57,17 @@ for s in ${STEPS:-tests smoke bench}; do
   rows)
     TAG=$TAG bash tools/prof_rows.sh > $OUT/rows.log 2>&1 || { echo ROWSFAIL; tail -20 $OUT/rows.log; exit 1; }
     tail -3 $OUT/rows.log ;;
-  c3)
-    D=$R/gpurun_out/${TAG}_c3
+  wl)
+    for W in ${WLS:-c3 c4}; do
+    D=$R/gpurun_out/${TAG}_$W
     mkdir -p $D
-    CMD="python3 $R/bench.py --gpus 1 --steps 10 --warmup 3 --c5-gib 0 --cpu-seconds 0 --no-pipelined-probe --workload c3"
-    (cd /tmp && timeout -k 10 300 $CMD > $D/bench.json 2> $D/bench.err) || { echo C3FAIL; tail -20 $D/bench.err; exit 1; }
-    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- $CMD > $D/trace.log 2>&1) || { echo C3TRACEFAIL; tail -20 $D/trace.log; exit 1; }
-    (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "mask_np_kernel" --output-format csv -d $D/pmc_fetch -o run -- $CMD --no-copy-ceiling > $D/pmc_fetch.log 2>&1) || { echo C3FETCHFAIL; tail -20 $D/pmc_fetch.log; exit 1; }
-    (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "mask_np_kernel" --output-format csv -d $D/pmc_write -o run -- $CMD --no-copy-ceiling > $D/pmc_write.log 2>&1) || { echo C3WRITEFAIL; tail -20 $D/pmc_write.log; exit 1; }
-    cat $D/bench.json | cut -c1-300 ;;
+    CMD="python3 $R/bench.py --gpus 1 --steps 10 --warmup 3 --c5-gib 0 --cpu-seconds 0 --no-pipelined-probe --workload $W"
+    (cd /tmp && timeout -k 10 300 $CMD > $D/bench.json 2> $D/bench.err) || { echo WLFAIL; tail -20 $D/bench.err; exit 1; }
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- $CMD > $D/trace.log 2>&1) || { echo WLTRACEFAIL; tail -20 $D/trace.log; exit 1; }
+    (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "mask_np_kernel" --output-format csv -d $D/pmc_fetch -o run -- $CMD --no-copy-ceiling > $D/pmc_fetch.log 2>&1) || { echo WLFETCHFAIL; tail -20 $D/pmc_fetch.log; exit 1; }
+    (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "mask_np_kernel" --output-format csv -d $D/pmc_write -o run -- $CMD --no-copy-ceiling > $D/pmc_write.log 2>&1) || { echo WLWRITEFAIL; tail -20 $D/pmc_write.log; exit 1; }
+    cut -c1-300 $D/bench.json
+    done ;;
   routes)
     timeout -k 10 600 python3 -u tools/bench_routes.py --out $OUT/routes.jsonl > $OUT/routes.log 2>&1 || { echo ROUTESFAIL; tail -20 $OUT/routes.log; exit 1; }
     tail -2 $OUT/routes.log | cut -c1-200 ;;
