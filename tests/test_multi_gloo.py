@@ -71,3 +71,61 @@ def test_gloo_sharded_batch_matches_oracle(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert ok
+
+
+def _hip_worker(rank, world, port, result_q):
+    """As _worker, but each rank masks its shard with the HIP batch kernel (netc_gpu_mask_batch) on
+    GPU rank % device_count -- one process per GPU as bench.py runs them; with one GPU the ranks
+    share it, which is what this rehearses (the N-rank path had only ever
+    masked with the host entry)."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+
+        from netc_amd import mask as nm
+        from netc_amd import synth
+
+        dev = rank % torch.cuda.device_count()
+        torch.cuda.set_device(dev)
+        off = synth.mixed_offsets(24 << 20, 256, 65536, seed=91)
+        keys = synth.random_keys(off.size - 1, 91)
+        payload = synth.host_payload(int(off[-1]), 91)
+        cuts = nm.shard_frames(off, world)
+        base, soff, skeys = shard_view(off, keys, cuts, rank)
+        end = int(off[cuts[rank + 1]])
+        src = torch.from_numpy(payload[base:end].copy()).to(f"cuda:{dev}")
+        dst = torch.empty_like(src)
+        d_off = torch.from_numpy(soff.astype(np.int64)).to(f"cuda:{dev}")
+        d_keys = torch.from_numpy(skeys.astype(np.int32)).to(f"cuda:{dev}")
+        nm.mask_batch(dst, src, d_off, d_keys)
+        torch.cuda.synchronize()
+        parts = [None] * world
+        dist.all_gather_object(parts, (rank, base, dst.cpu().numpy().tobytes()))
+        if rank == 0:
+            from oracle import oracle as orc
+
+            whole = b"".join(p[2] for p in sorted(parts))
+            result_q.put(whole == orc.mask_batch(payload, off, keys).tobytes())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_sharded_batch_on_hip(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hip_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert ok
