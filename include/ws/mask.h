@@ -145,7 +145,11 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *                      short and finish together [0]               (NETC_MASK_TAPER)
  *   ENC_FIX            where netc_gpu_encode_frames composes the 16-B vectors holding header
  *                      bytes: 0 trailing blocks of the assembly launch; 1 the wire-offsets
- *                      scan (measured slower) [0]                   (NETC_ENC_FIX)
+ *                      scan (measured slower); 2 the assembly's own wavefronts after their
+ *                      windows [0]                                  (NETC_ENC_FIX)
+ *   ENC_PROBE          entries of the frame assembly's first table probe per chunk, when dense:
+ *                      0 always 64 (round 4's table), > 0 that many more than the default
+ *                      (expected frames + 10) [default]             (NETC_ENC_PROBE)
  *   INJECT_FAULT       fault injection for tests: the ingest / egress ring submission this
  *                      countdown reaches (0 = the next one) fails as NETC_GPU_ELAUNCH
  *                      without launching, then the knob disarms itself [off]
@@ -161,6 +165,7 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
 #define NETC_GPU_KNOB_ENC_SRC           8
 #define NETC_GPU_KNOB_ENC_FIX           9
 #define NETC_GPU_KNOB_INJECT_FAULT     10
+#define NETC_GPU_KNOB_ENC_PROBE        11
 int netc_gpu_knob(int knob, int64_t value);
 
 /**

@@ -94,12 +94,14 @@ struct EncArgs {
     uint32_t main_blocks;      // encode_frames_kernel: blocks 0 .. main_blocks-1 assemble, the rest fix headers
     uint32_t per_wave;         // ... each assembly wavefront lists its unmapped spans at defer[wave * per_wave ..]
     uint32_t fix_blocks;       // 1: the header vectors by trailing blocks of the assembly (0: by the scan, or none needed)
+    uint32_t fix_tail;         // 1: ... by the assembly wavefronts themselves, after their windows (ENC_FIX = 2)
     // source-driven assembly (encode_src_kernel)
     const uint8_t* src_base;   // src rounded down to 16 (P coordinates: byte q of src is at P = q + smis)
     uint64_t smis;             // src & 15
     uint64_t nwin;             // windows of the source walk
     double density;            // frames per payload byte (table-base guesses)
     int32_t probe_e;           // entries of a window's first table probe (<= 64)
+    int32_t probe_bias;        // wire-driven assembly: frames the probe's base sits before the density guess
     const uint32_t* keys_ld;   // keys, or any readable array when unmasked (loads are never branched around)
     const uint8_t* b0_ld;      // b0, or any readable array when null
 };
@@ -114,11 +116,19 @@ struct EncTable {
     uint64_t poff;    // payload offset off[v] (clamped)
     uint32_t key;
     uint32_t b0;
-    uint64_t last;    // start of entry 63 (uniform)
+    uint64_t last;    // start of entry e - 1 (uniform)
     bool tail;        // entry for frame n is in the table
+    int e;            // entries held: 64, or fewer for a chunk's first probe (uniform); lanes >= e: start inf
 };
 
-__device__ __forceinline__ void enc_entry(const EncArgs& a, int64_t v, EncTable& t) {
+__device__ __forceinline__ void enc_entry(const EncArgs& a, int64_t v, EncTable& t, bool held = true) {
+    if (!held) {   // past the probe's entries: nothing loaded (the loads below are skipped for the lane)
+        t.start = kInf;
+        t.poff = 0;
+        t.key = 0;
+        t.b0 = 0x82u;
+        return;
+    }
     const int64_t n = (int64_t)a.n;
     const int64_t vo = v < 0 ? 0 : (v > n ? n : v);
     const int64_t vk = v < 0 ? 0 : (v >= n ? (n > 0 ? n - 1 : 0) : v);
@@ -131,13 +141,14 @@ __device__ __forceinline__ void enc_entry(const EncArgs& a, int64_t v, EncTable&
     t.b0 = b0;
 }
 
-__device__ __forceinline__ void enc_table_issue(const EncArgs& a, EncTable& t, int64_t kb, int lane) {
+__device__ __forceinline__ void enc_table_issue(const EncArgs& a, EncTable& t, int64_t kb, int lane, int e = kWave) {
     t.kb = kb;
-    enc_entry(a, kb + lane, t);
-    t.tail = kb + (kWave - 1) >= (int64_t)a.n;
+    t.e = e;
+    enc_entry(a, kb + lane, t, lane < e);
+    t.tail = kb + (e - 1) >= (int64_t)a.n;
 }
 
-__device__ __forceinline__ void enc_table_finish(EncTable& t) { t.last = readlane64(t.start, kWave - 1); }
+__device__ __forceinline__ void enc_table_finish(EncTable& t) { t.last = readlane64(t.start, t.e - 1); }
 
 __device__ __forceinline__ void enc_table_load(const EncArgs& a, EncTable& t, int64_t kb, int lane) {
     enc_table_issue(a, t, kb, lane);
@@ -182,7 +193,7 @@ __device__ int64_t enc_locate(const EncArgs& a, uint64_t W, uint64_t wire_total,
 __device__ __forceinline__ void enc_resolve(const EncArgs& a, EncTable& t, uint64_t W, uint64_t wire_total,
                                             int lane) {
     const uint64_t m = __ballot(t.start <= W);
-    if (!(m != 0 && (t.tail || m != ~0ull))) enc_table_load(a, t, enc_locate(a, W, wire_total, lane), lane);
+    if (!(m != 0 && (t.tail || __popcll(m) < t.e))) enc_table_load(a, t, enc_locate(a, W, wire_total, lane), lane);
 }
 
 // The frame header as 16 little-endian bytes (h <= 14 used), wave-uniform:
@@ -335,10 +346,10 @@ __device__ __forceinline__ FrameInfo frame_info_lane(const EncArgs& a, const Enc
 // while this one is composed; entry 62 is shared by two windows and its bytes are
 // ORed twice with the same values.  On entry entry 0 of t starts at or before A0.
 __device__ u32x4 compose_vec(const EncArgs& a, EncTable& t, uint64_t A0, uint64_t W, int lane) {
-    constexpr int kLast = kWave - 2;   // last usable entry
     const uint64_t Aend = A0 + kSpan;
     u32x4 out = {0, 0, 0, 0};
     for (;;) {
+        const int kLast = t.e - 2;   // last usable entry (uniform)
         const bool more = !t.tail && t.last < Aend;   // wave-uniform
         EncTable tn;
         if (more) enc_table_issue(a, tn, t.kb + kLast, lane);
@@ -484,7 +495,7 @@ __device__ __forceinline__ void plan_chunk(const EncArgs& a, const EncTable& t, 
             l0 = __popcll(__ballot(t.start <= A0)) - 1;
             const uint64_t bm = __ballot(t.start > A0 && t.start < Aend);
             nb = __popcll(bm);
-            const bool covered = (t.tail || t.last >= Aend) && l0 >= 0 && l0 + nb + 2 <= kWave - 1;
+            const bool covered = (t.tail || t.last >= Aend) && l0 >= 0 && l0 + nb + 2 <= t.e - 1;
             if (!covered || A0 < wlo || Aend > whi || t.kb + l0 < 0 || t.kb + l0 + nb >= (int64_t)a.n) break;
             if (nb == 0) {
                 // one frame covers the span: everything is wave-uniform
@@ -849,13 +860,22 @@ __global__ __launch_bounds__(256, W) void encode_frames_kernel(EncArgs a) {
         }
     };
 
+    // ENC_FIX = 2: the header vectors by the assembly's own wavefronts once their windows are
+    // stored (64 frames a wavefront, one per lane: fix_vectors), instead of trailing blocks
+    auto tail_fix = [&]() {
+        if (!a.fix_tail) return;
+        for (uint64_t k = wave * kWave + (uint64_t)lane; k < a.n; k += nwaves * kWave) fix_vectors(a, k, wlo);
+    };
     uint64_t c = wave;
-    if (c >= nwin) return;
+    if (c >= nwin) {
+        tail_fix();
+        return;
+    }
     // table base for the chunk at A from a frame f_known starting at s_known,
     // biased 24 frames back (the spread of independent random sizes)
     auto guess = [&](int64_t f_known, uint64_t s_known, uint64_t A) -> int64_t {
         if (A < a.wmis) return -1;
-        int64_t g = f_known + (int64_t)((double)(A - s_known) * density) - 24;
+        int64_t g = f_known + (int64_t)((double)(A - s_known) * density) - a.probe_bias;
         g = g < -1 ? -1 : g;
         return g > (int64_t)a.n ? (int64_t)a.n : g;
     };
@@ -870,7 +890,7 @@ __global__ __launch_bounds__(256, W) void encode_frames_kernel(EncArgs a) {
     // so that 4+ wavefronts per SIMD keep the loads in flight instead.
     EncTable tc;
     uint64_t A = c * kWin;
-    enc_table_issue(a, tc, guess(0, a.wmis, A), lane);
+    enc_table_issue(a, tc, guess(0, a.wmis, A), lane, a.probe_e);
     for (;;) {
         enc_table_finish(tc);
         enc_resolve(a, tc, A, wire_total, lane);
@@ -881,7 +901,7 @@ __global__ __launch_bounds__(256, W) void encode_frames_kernel(EncArgs a) {
         known(tc, A, f, s);
         const uint64_t cn = c + nwaves;
         EncTable tn;
-        if (cn < nwin) enc_table_issue(a, tn, guess(f, s, cn * kWin), lane);
+        if (cn < nwin) enc_table_issue(a, tn, guess(f, s, cn * kWin), lane, a.probe_e);
         finish_chunk<U, NT>(a, tc, A, wlo, whi, lane, pc, list, nl);
         if (cn >= nwin) break;
         c = cn;
@@ -889,6 +909,7 @@ __global__ __launch_bounds__(256, W) void encode_frames_kernel(EncArgs a) {
         tc = tn;
     }
     done();
+    tail_fix();
 }
 
 typedef unsigned __int128 u128;
@@ -1426,6 +1447,21 @@ static hipError_t launch_enc_u(EncArgs a, uint64_t wire_bound, bool nt, int max_
     // up to 1,024 blocks, unless the wire-offsets scan has composed them (ENC_FIX = 1)
     const uint64_t fix = (a.n + 255) / 256;
     const uint64_t fix_blocks = !a.fix_blocks ? 0 : (fix < 64 ? 64 : (fix > 1024 ? 1024 : fix));
+    // each chunk's first table probe: as many entries as the frames a chunk is expected to touch
+    // (+ the bias and a margin) when that is a few -- dense batches (config 2: 10 of 64 entries,
+    // the rest of the 64-entry table loads were the launch's excess counter traffic) -- else 64
+    // entries from 24 frames before the density guess (random sizes).  A probe that misses is
+    // replaced by a full table from the binary search (enc_resolve).
+    const double reach = (double)(kSpan * U) * ((double)a.n / (double)(wire_bound ? wire_bound : 1));
+    const int64_t pk = knob(NETC_GPU_KNOB_ENC_PROBE);
+    if (pk == 0 || reach < 1.0 || reach > (double)(kWave - 16)) {
+        a.probe_e = kWave;
+        a.probe_bias = 24;
+    } else {
+        a.probe_bias = 2;
+        a.probe_e = (int)reach + 10 + (pk > 0 ? (int)pk : 0);
+        if (a.probe_e > kWave) a.probe_e = kWave;
+    }
     a.main_blocks = (uint32_t)blocks;
     a.per_wave = (uint32_t)(((nwin + 4 * (uint64_t)blocks - 1) / (4 * (uint64_t)blocks)) * U);   // windows per wave x U
     if ((uint64_t)a.per_wave * 4 * (uint64_t)blocks > a.defer_cap) return hipErrorInvalidValue;   // (sized with slack below)
@@ -1450,7 +1486,8 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     // config 4 421-430 against 417-424 -- on the scan's critical path the fixups cost more than
     // in the assembly's tail, where they fill the CUs its last waves leave (r04kk)
     const bool fix_in_scan = !all_spans && !src_walk && knob(NETC_GPU_KNOB_ENC_FIX) == 1;
-    const bool fix_blocks = !all_spans && !src_walk && !fix_in_scan;
+    const bool fix_tail = !all_spans && !src_walk && knob(NETC_GPU_KNOB_ENC_FIX) == 2;
+    const bool fix_blocks = !all_spans && !src_walk && !fix_in_scan && !fix_tail;
     // (the scan with the fixups holds 8 frames per thread at most: 16 spilled)
     const int per0 = scan_per(n), per = fix_in_scan && per0 > 8 ? 8 : per0;
     const uint64_t tiles = scan_tiles_for(n, per);
@@ -1478,6 +1515,7 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     a.defer_cap = sc.defer_cap;
     a.all_spans = all_spans ? 1u : 0u;
     a.fix_blocks = fix_blocks ? 1u : 0u;
+    a.fix_tail = fix_tail ? 1u : 0u;
     if ((e = launch_scan(off, n, masked, wo, stream, sc, per, fix_in_scan ? &a : nullptr)) != hipSuccess) return e;
     const bool nt = cfg.flags < 0 || (cfg.flags & (kNtLoads | kNtStores));
     // Chunk size: netc_gpu_tune's unroll 8 selects 4 KiB, 2 or 4 select 2 KiB; the default

@@ -77,12 +77,14 @@ def _payload(rng, n):
 # compose the vectors holding header bytes), "fixscan" = those vectors by the wire-offsets scan
 # (NETC_GPU_KNOB_ENC_FIX = 1), "src" = the source-driven walk writing headers in the same pass
 # (NETC_GPU_KNOB_ENC_SRC = 1); both A/B paths
-PATHS = [None, "fixscan", "src"]
+PATHS = [None, "fixscan", "fixtail", "src"]
 
 
 def _set_path(gpu_knob, path):
     if path == "fixscan":
         gpu_knob("ENC_FIX", 1)
+    elif path == "fixtail":
+        gpu_knob("ENC_FIX", 2)
     elif path == "src":
         gpu_knob("ENC_SRC", 1)
 
