@@ -488,7 +488,9 @@ int hub_route(void* ctx, int sockfd, struct ws_frame_parsing_state* state, size_
         struct ws_message m;
         int r = deliver(h, c, &m, max_payload_length);
         if (r == 0) {
-            if (c.ranges.empty()) (void)sock_consume(c, c.in_pos);   // nothing of it left: no hostage
+            // nothing of it left -- no frames, no error still to report (its bytes are in the
+            // socket as far as the caller is concerned): no hostage
+            if (c.ranges.empty() && !c.pending) (void)sock_consume(c, c.in_pos);
             state->message = m;
             return 0;
         }
@@ -510,7 +512,7 @@ int hub_route(void* ctx, int sockfd, struct ws_frame_parsing_state* state, size_
             continue;
         }
         if (n == 0) {
-            if (c.ranges.empty()) (void)sock_consume(c, c.in_pos);
+            if (c.ranges.empty() && !c.pending) (void)sock_consume(c, c.in_pos);
             return 1;
         }
         if (n == NETC_WS_INGEST_CLOSED) {

@@ -164,3 +164,113 @@ def test_hub_server_256_connections_equals_cpu_parser():
         assert out[leg]["conn_hash"] == out["hub"]["conn_hash"]
     hub = out["hub"]
     assert hub["frames"] >= 256 * 200 and hub["max_conns_per_launch"] >= 16, hub
+
+
+def _call(lib, ep, st, limit=1 << 20, tries=200):
+    """ws_parse_frame once per readiness until it returns something other than 1 (or tries run out)"""
+    rc = 1
+    for _ in range(tries):
+        if not select.select([ep.sock], [], [], 2)[0]:
+            return 1
+        rc = lib.ws_parse_frame(ctypes.byref(ep.client), ctypes.byref(st), limit)
+        if rc != 1:
+            return rc
+    return rc
+
+
+def _take(st):
+    m = st.message
+    out = (int(m.opcode), ctypes.string_at(m.buffer, m.payload_length))
+    libc.free(m.buffer)
+    ctypes.memset(ctypes.byref(st), 0, ctypes.sizeof(st))
+    return out
+
+
+@pytest.mark.timeout(60)
+def test_hub_stream_errors_after_the_messages_before_them():
+    """per connection, as the reference's parser and the single-connection ring: every complete
+    message before a bad frame is delivered first, then the error, and it stays; other
+    connections of the hub go on (strict: an unmasked client frame; a frame over the hub's
+    limit; a message over the caller's limit; the peer closing)"""
+    lib = _lib.host()
+    good = [(G.TEXT, b"first", 1, [b"\x01\x02\x03\x04"]), (G.BINARY, bytes(range(200)), 2, [b"\x05\x06\x07\x08"] * 2)]
+    unmasked = bytes([0x81, 0x03]) + b"abc"
+    big = G.wire_of([(G.BINARY, bytes(5000), 1, [b"\x09\x09\x09\x09"])])
+    pairs = [G.tcp_pair() for _ in range(4)]
+    with make_hub(slot_bytes=64 << 10, nslots=4, max_frame_bytes=4096, strict=True) as hub:
+        eps, sts = [], []
+        for c, s in pairs:
+            s.setblocking(False)
+            hub.attach(s.fileno())
+            eps.append(Endpoint(s))
+            sts.append(ParseState())
+        try:
+            pairs[0][0].sendall(G.wire_of(good) + unmasked)          # strict: MASK clear
+            pairs[1][0].sendall(G.wire_of(good) + big)               # 5,000 B > the hub's 4,096
+            pairs[2][0].sendall(G.wire_of(good))                     # fine, then closes
+            pairs[2][0].shutdown(socket.SHUT_WR)
+            pairs[3][0].sendall(G.wire_of(good))                     # fine, stays open
+            want = G.expected(good)
+            for c in range(4):
+                for m in want:
+                    assert _call(lib, eps[c], sts[c], limit=1 << 20) == 0, c
+                    assert _take(sts[c]) == m
+            assert _call(lib, eps[0], sts[0]) == ni_codes.INVALID
+            assert _call(lib, eps[0], sts[0]) == ni_codes.INVALID   # sticky
+            assert _call(lib, eps[1], sts[1]) == ni_codes.TOO_BIG
+            assert _call(lib, eps[2], sts[2]) == ni_codes.RECV
+            assert _call(lib, eps[3], sts[3], tries=3) == 1          # nothing more, still open
+            # a message over the caller's limit (src/ws/common.c:210-211)
+            pairs[3][0].sendall(G.wire_of([(G.BINARY, bytes(3000), 1, [b"\x0a\x0b\x0c\x0d"])]))
+            assert _call(lib, eps[3], sts[3], limit=2000) == ni_codes.TOO_BIG
+        finally:
+            for _, s in pairs:
+                hub.detach(s.fileno())
+    for a, b in pairs:
+        a.close()
+        b.close()
+
+
+@pytest.mark.timeout(60)
+def test_hub_detach_with_frames_pending():
+    """a connection detached while its frames sit in the shared slots: the other connections'
+    messages still arrive, the slots return to the pool (many more messages pass through 2 slots)"""
+    lib = _lib.host()
+    rng = np.random.default_rng(12)
+    pairs = [G.tcp_pair() for _ in range(3)]
+    with make_hub(slot_bytes=32 << 10, nslots=2, max_frame_bytes=8192) as hub:
+        eps, sts = [], []
+        for c, s in pairs:
+            s.setblocking(False)
+            hub.attach(s.fileno())
+            eps.append(Endpoint(s))
+            sts.append(ParseState())
+        try:
+            msgs = [(G.BINARY, rng.integers(0, 256, 700, dtype=np.uint8).tobytes(), 1,
+                     [bytes(rng.integers(0, 256, 4, dtype=np.uint8))]) for _ in range(60)]
+            for c, _ in pairs:
+                c.sendall(G.wire_of(msgs[:5]))
+            # connection 0 reads its frames into the hub, then is dropped with them undelivered
+            assert _call(lib, eps[0], sts[0], tries=1) in (0, 1)
+            hub.detach(pairs[0][1].fileno())
+            got = {1: [], 2: []}
+            for i in range(5, 60):
+                for c in (1, 2):
+                    pairs[c][0].sendall(G.wire_of([msgs[i]]))
+            for c in (1, 2):
+                while len(got[c]) < 60:
+                    rc = _call(lib, eps[c], sts[c])
+                    assert rc == 0, (c, len(got[c]), rc)
+                    got[c].append(_take(sts[c]))
+            assert got[1] == got[2] == G.expected(msgs)
+            assert hub.stats()["connections"] == 2
+        finally:
+            for _, s in pairs[1:]:
+                hub.detach(s.fileno())
+    for a, b in pairs:
+        a.close()
+        b.close()
+
+
+class ni_codes:
+    RECV, INVALID, TOO_BIG = -1, -2, -3

@@ -299,3 +299,33 @@ def test_route_does_not_outlive_its_connection():
                 os.close(fd)
             c.close()
             d.close()
+
+
+@pytest.mark.timeout(60)
+def test_route_errors_after_the_messages_before_them():
+    """a strict ring: the messages before an unmasked client frame first, then
+    WS_FRAME_PARSE_ERROR_INVALID_FRAME_LENGTH, sticky; a frame over the ring's limit likewise
+    ends in PAYLOAD_TOO_BIG -- all with one call per readiness (the socket stays readable until
+    the error is reported)"""
+    lib = _lib.host()
+    good = [(TEXT, b"first", 1, [b"\x01\x02\x03\x04"]), (BINARY, bytes(range(200)), 2, [b"\x05\x06\x07\x08"] * 2)]
+    for tail, want_rc, kw in ((bytes([0x81, 0x03]) + b"abc", -2, dict(strict=True)),
+                              (wire_of([(BINARY, bytes(5000), 1, [b"\x09\x09\x09\x09"])]), -3,
+                               dict(max_frame_bytes=4096))):
+        c, s = tcp_pair()
+        s.setblocking(False)
+        ep = Endpoint(s)
+        with ni.Ingest(slot_bytes=1 << 16, nslots=2, **kw) as ing:
+            ing.attach(s.fileno())
+            try:
+                c.sendall(wire_of(good) + tail)
+                got = once_per_event(s, ep, lib, len(good), 1 << 20)
+                assert got == expected(good)
+                st = ParseState()
+                assert select.select([s], [], [], 5)[0], "the error's bytes must keep the socket readable"
+                assert lib.ws_parse_frame(ctypes.byref(ep.client), ctypes.byref(st), 1 << 20) == want_rc
+                assert lib.ws_parse_frame(ctypes.byref(ep.client), ctypes.byref(st), 1 << 20) == want_rc
+            finally:
+                ing.detach(s.fileno())
+        c.close()
+        s.close()

@@ -153,3 +153,15 @@ def test_hub_unix_sockets_and_big_frames(hub_mock):
 
 def test_hub_attach_rules(hub_mock):
     hub_mock.test_hub_attach_rules()
+
+
+def test_hub_stream_errors_after_the_messages_before_them(hub_mock):
+    hub_mock.test_hub_stream_errors_after_the_messages_before_them()
+
+
+def test_hub_detach_with_frames_pending(hub_mock):
+    hub_mock.test_hub_detach_with_frames_pending()
+
+
+def test_route_errors_after_the_messages_before_them(mock):
+    G.test_route_errors_after_the_messages_before_them()
