@@ -68,6 +68,33 @@ int netc_gpu_encode_frames(int device, void *d_wire, size_t wire_capacity, uint6
                            const uint32_t *d_keys, const uint8_t *d_header0, size_t nframes, int masked,
                            void *stream);
 
+/** Length classes for netc_gpu_encode_frames_class: the extended-length bytes of every frame. */
+#define NETC_WS_CLASS_7BIT  0   /* every payload 0..125 bytes     (header 2 B + key)  */
+#define NETC_WS_CLASS_16BIT 2   /* every payload 126..65535 bytes (header 4 B + key)  */
+#define NETC_WS_CLASS_64BIT 8   /* every payload 65536 bytes or more (10 B + key)     */
+
+/** d_wire_offsets[nframes] after netc_gpu_encode_frames_class when a frame broke the class. */
+#define NETC_WS_WIRE_INVALID UINT64_MAX
+
+/**
+ * netc_gpu_encode_frames for a batch whose frames all lie in one length class, as the caller
+ * promises (length_class: NETC_WS_CLASS_*) -- e.g. a broadcast of equal-sized messages, or a
+ * batch a host packer saw every length of.  The wire offsets are then affine in the payload
+ * offsets, d_wire_offsets[k] = (offsets[k] - offsets[0]) + k * (2 + length_class + (masked ? 4 :
+ * 0)), so the assembly computes them itself and writes them: one launch, where
+ * netc_gpu_encode_frames runs a prefix scan over the frames before it.
+ *
+ * The promise is checked for every frame.  If a frame breaks it, d_wire_offsets[nframes] reads
+ * NETC_WS_WIRE_INVALID once the call's work is done and the wire bytes are unspecified; no byte
+ * outside the wire bound is written.  A batch that takes the general path (one averaging under 80
+ * payload bytes per frame, or one the measurement knobs send to another path) runs the scan and
+ * is exact whatever its frames are.  Other arguments and errors as netc_gpu_encode_frames.
+ */
+int netc_gpu_encode_frames_class(int device, void *d_wire, size_t wire_capacity, uint64_t *d_wire_offsets,
+                                 const void *d_payload, size_t total_bytes, const uint64_t *d_frame_offsets,
+                                 const uint32_t *d_keys, const uint8_t *d_header0, size_t nframes, int masked,
+                                 int length_class, void *stream);
+
 /* ---------------------------------------------------------- receive side -- */
 
 /** netc_gpu_scan_frames flag: reject what RFC 6455 forbids from a client (see below). */

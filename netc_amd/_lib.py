@@ -110,6 +110,9 @@ def gpu() -> ctypes.CDLL:
             lib.netc_gpu_encode_frames.argtypes = [ctypes.c_int, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp, vp,
                                                    vp, ctypes.c_size_t, ctypes.c_int, vp]
             lib.netc_gpu_encode_frames.restype = ctypes.c_int
+            lib.netc_gpu_encode_frames_class.argtypes = [ctypes.c_int, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t,
+                                                         vp, vp, vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, vp]
+            lib.netc_gpu_encode_frames_class.restype = ctypes.c_int
             lib.netc_gpu_scan_frames.argtypes = [ctypes.c_int, vp, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int, vp,
                                                  vp, vp, ctypes.c_size_t, vp, vp]
             lib.netc_gpu_scan_frames.restype = ctypes.c_int

@@ -9,7 +9,8 @@
 //
 //   H2D     the payload bytes, then the packed table (offsets | keys | header bytes: one copy)
 //   encode  launch_encode_frames (ws_frame_gpu.hip): wire offsets, then every frame's header,
-//           key and masked payload back to back
+//           key and masked payload back to back -- one launch when every frame of the slot is
+//           in one length class (the host saw each length: the offsets are affine, no scan)
 //   D2H     the wire bytes into the slot's page-locked wire buffer (the host knows their
 //           count: it summed the header lengths while queueing) and the device's own wire
 //           length beside them, checked against it when the slot is taken; event "done"
@@ -69,6 +70,8 @@ struct EgressSlot {
     uint64_t frames = 0;
     uint64_t messages = 0;
     uint64_t wire = 0;            // wire bytes of the queued frames
+    int ext = -2;                 // the frames' extended-length bytes: one class (0, 2, 8), mixed (-1),
+                                  // none yet (-2); one class: the assembly launches without its scan
 };
 
 struct DeviceGuard {
@@ -175,7 +178,8 @@ int submit_cur(netc_ws_egress* g) {
     const uint8_t* d_keys = s.d_tab + (n + 1) * sizeof(uint64_t);
     if ((e = netc_gpu::launch_encode_frames(s.d_wire, bound, s.d_pay, s.fill, (const uint64_t*)s.d_tab,
                                             (const uint32_t*)d_keys, d_keys + n * sizeof(uint32_t), n, masked,
-                                            s.d_wo, s.stream, netc_gpu::api_cfg())) != hipSuccess)
+                                            s.d_wo, s.stream, netc_gpu::api_cfg(), s.ext >= 0 ? s.ext : -1)) !=
+        hipSuccess)
         return api_fail_hip(e == hipErrorOutOfMemory ? NETC_GPU_ENOMEM : NETC_GPU_ELAUNCH, "egress: frame assembly",
                             e);
     *s.h_len = ~0ull;
@@ -199,6 +203,7 @@ int acquire(netc_ws_egress* g) {
     s.state = kFilling;
     s.masked = -1;
     s.fill = s.frames = s.messages = s.wire = 0;
+    s.ext = -2;
     g->cur = g->next_fill;
     g->next_fill = (g->next_fill + 1) % g->nslots;
     return 0;
@@ -318,6 +323,8 @@ int netc_ws_egress_queue(struct netc_ws_egress* g, const void* payload, size_t l
         if (masked) keys[i] = key32;
         b0[i] = (uint8_t)((last ? 0x80 : 0x00) | (i == 0 ? (opcode & 0x0F) : WS_OPCODE_CONTINUE));   // :55-61
         wire += header_len(flen, masked) + flen;
+        const int ext = flen <= 125 ? 0 : (flen <= 0xFFFF ? 2 : 8);
+        s.ext = s.ext == -2 || s.ext == ext ? ext : -1;
     }
     s.fill += len;
     s.frames += nf;

@@ -104,7 +104,24 @@ struct EncArgs {
     int32_t probe_bias;        // wire-driven assembly: frames the probe's base sits before the density guess
     const uint32_t* keys_ld;   // keys, or any readable array when unmasked (loads are never branched around)
     const uint8_t* b0_ld;      // b0, or any readable array when null
+    // one length class (netc_gpu_encode_frames_class): the wire offsets are affine in the payload
+    // offsets, wo[k] = off[k] - off[0] + hstride * k, so the assembly computes them instead of
+    // reading wo[] and no scan launch runs before it; its trailing fixup blocks write wo[] and
+    // check every frame's class
+    uint32_t affine;
+    uint32_t ext;              // ... the class's extended-length bytes (0, 2 or 8)
+    uint64_t hstride;          // ... header + key bytes of every frame
+    uint64_t off0;             // ... off[0] (loaded by the kernel)
+    uint64_t* wo_out;          // ... wo[] as the fixup blocks write it
+    uint32_t* fix_done;        // ... fixup blocks retired + 0x10000 per block that met a frame outside
+                               //     the class; zero between calls (the last block resets it)
 };
+
+// wire offset of frame k (k <= n): from wo[], or affine in off[k] (one length class)
+__device__ __forceinline__ uint64_t wire_at(const EncArgs& a, uint64_t k) {
+    if (a.affine) return gptr(a.off)[k] - a.off0 + a.hstride * k;
+    return gptr(a.wo)[k];
+}
 
 // spans per wave trip of the dense compose launch
 static constexpr int kDenseGroup = 4;
@@ -132,8 +149,8 @@ __device__ __forceinline__ void enc_entry(const EncArgs& a, int64_t v, EncTable&
     const int64_t n = (int64_t)a.n;
     const int64_t vo = v < 0 ? 0 : (v > n ? n : v);
     const int64_t vk = v < 0 ? 0 : (v >= n ? (n > 0 ? n - 1 : 0) : v);
-    const uint64_t wo = gptr(a.wo)[vo];
     t.poff = gptr(a.off)[vo];
+    const uint64_t wo = a.affine ? t.poff - a.off0 + a.hstride * (uint64_t)vo : gptr(a.wo)[vo];
     const uint32_t key = a.masked ? gptr(a.keys)[vk] : 0u;
     const uint32_t b0 = a.b0 ? (uint32_t)gptr(a.b0)[vk] : 0x82u;
     t.start = v < 0 ? 0 : (v <= n ? wo + a.wmis : kInf);
@@ -169,7 +186,7 @@ __device__ int64_t enc_locate(const EncArgs& a, uint64_t W, uint64_t wire_total,
         const int64_t base = g - 31 * kStride;
         const int64_t idx = base + (int64_t)lane * kStride;
         const bool valid = idx >= 0 && idx <= (int64_t)a.n;
-        const uint64_t val = valid ? gptr(a.wo)[idx] : 0;
+        const uint64_t val = valid ? wire_at(a, (uint64_t)idx) : 0;
         const uint64_t le = __ballot(valid && val <= q);
         const uint64_t gt = __ballot(valid && val > q);
         if (le) L = base + (int64_t)(63 - __builtin_clzll(le)) * kStride;
@@ -180,7 +197,7 @@ __device__ int64_t enc_locate(const EncArgs& a, uint64_t W, uint64_t wire_total,
         const int64_t step = (H - lo + kWave - 1) / kWave;
         const int64_t idx = lo + (int64_t)lane * step;
         const bool valid = idx < H;
-        const uint64_t val = valid ? gptr(a.wo)[idx] : kInf;
+        const uint64_t val = valid ? wire_at(a, (uint64_t)idx) : kInf;
         const uint64_t le = __ballot(valid && val <= q);
         const uint64_t gt = __ballot(valid && val > q);
         if (le) L = lo + (int64_t)(63 - __builtin_clzll(le)) * step;
@@ -702,8 +719,8 @@ __device__ __forceinline__ void fix_vectors(const EncArgs& a, uint64_t k, uint64
     // frame k's header start and frames k - 1, k, k + 1's payload offsets in one trip (k - 1
     // clamped: its values are unused for k = 0)
     const uint64_t kp = k > 0 ? k - 1 : 0;
-    const uint64_t S = gptr(a.wo)[k] + a.wmis;
     const uint64_t op = gptr(a.off)[kp], o = gptr(a.off)[k], on = gptr(a.off)[k + 1];
+    const uint64_t S = (a.affine ? o - a.off0 + a.hstride * k : gptr(a.wo)[k]) + a.wmis;
     const uint32_t keyp = masked ? gptr(a.keys)[kp] : 0u, key = masked ? gptr(a.keys)[k] : 0u;
     const uint32_t b0 = a.b0 ? (uint32_t)gptr(a.b0)[k] : 0x82u;
     const uint64_t opk = k > 0 ? op : o;
@@ -820,15 +837,42 @@ __global__ __launch_bounds__(kScanThreads) void wire_offsets_chained(const uint6
 // Blocks main_blocks .. gridDim.x - 1 (dispatched as the assembly blocks retire: its tail)
 // compose the vectors holding header bytes (fix_vectors, one thread per frame).  They share
 // no vector with the assembly's stores, so nothing orders the two.
+// One length class (a.affine): the same threads write wo[k] and check frame k's class; a frame
+// outside it gets no header vectors (the wire is then unspecified, and no byte is written outside
+// [wire, wire + the bound)).  The last fixup block to retire writes wo[n]: the wire length, or
+// UINT64_MAX when any block met such a frame -- one atomic word carries both the count and the
+// verdict, so no fence orders them.
 __device__ void fixup_block(const EncArgs& a) {
     const uint64_t wlo = a.wmis;
     const uint64_t fb = blockIdx.x - a.main_blocks, nfb = gridDim.x - a.main_blocks;
-    for (uint64_t k = fb * blockDim.x + threadIdx.x; k < a.n; k += nfb * blockDim.x) fix_vectors(a, k, wlo);
+    int broken = 0;
+    for (uint64_t k = fb * blockDim.x + threadIdx.x; k < a.n; k += nfb * blockDim.x) {
+        if (a.affine) {
+            const uint64_t o = gptr(a.off)[k], on = gptr(a.off)[k + 1];
+            gptr(a.wo_out)[k] = o - a.off0 + a.hstride * k;
+            if (on < o || ext_len(on - o) != a.ext) {
+                broken = 1;
+                continue;
+            }
+        }
+        fix_vectors(a, k, wlo);
+    }
+    if (!a.affine) return;
+    broken = __syncthreads_or(broken);
+    if (threadIdx.x == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(a.fix_done, 1u + (broken ? 0x10000u : 0u), __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        if ((old & 0xFFFFu) == (uint32_t)nfb - 1) {
+            gptr(a.wo_out)[a.n] = (old >> 16) || broken ? ~0ull : wire_at(a, a.n);
+            __hip_atomic_store(a.fix_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 template <int U, bool NT, int W>
 __global__ __launch_bounds__(256, W) void encode_frames_kernel(EncArgs a) {
-    const uint64_t wire_total = gptr(a.wo)[a.n];
+    if (a.affine) a.off0 = gptr(a.off)[0];
+    const uint64_t wire_total = wire_at(a, a.n);
     if (blockIdx.x >= a.main_blocks) {   // block-uniform
         fixup_block(a);
         return;
@@ -1337,6 +1381,11 @@ static hipError_t scratch_for(hipStream_t stream, uint64_t tiles, uint64_t spans
         uint64_t want = sc.defer_cap ? 2 * sc.defer_cap : 4096;
         while (want < spans) want *= 2;
         if ((e = hipMalloc(&p, (want + 1) * sizeof(uint64_t))) != hipSuccess) return e;
+        // the word past the spans: the scan's spare word, then the fixup blocks' counter (fix_done)
+        if ((e = hipMemsetAsync(p + want, 0, sizeof(uint64_t), stream)) != hipSuccess) {
+            (void)hipFree(p);
+            return e;
+        }
         if (sc.defer) sc.retired.push_back(sc.defer);
         sc.defer = p;
         sc.defer_cap = want;
@@ -1473,7 +1522,7 @@ static hipError_t launch_enc_u(EncArgs a, uint64_t wire_bound, bool nt, int max_
 
 hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_t* src, uint64_t src_total,
                                 const uint64_t* off, const uint32_t* keys, const uint8_t* b0, uint64_t n, bool masked,
-                                uint64_t* wo, hipStream_t stream, const LaunchCfg& cfg) {
+                                uint64_t* wo, hipStream_t stream, const LaunchCfg& cfg, int ext_class) {
     if (n == 0) return hipMemsetAsync(wo, 0, sizeof(uint64_t), stream);
     // frames averaging under dense_bytes() of payload: every span is composed per lane
     // (the vector path would queue most spans and leave a header fixup per frame)
@@ -1516,7 +1565,19 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     a.all_spans = all_spans ? 1u : 0u;
     a.fix_blocks = fix_blocks ? 1u : 0u;
     a.fix_tail = fix_tail ? 1u : 0u;
-    if ((e = launch_scan(off, n, masked, wo, stream, sc, per, fix_in_scan ? &a : nullptr)) != hipSuccess) return e;
+    // One length class (ext_class 0, 2 or 8: netc_gpu_encode_frames_class): on the default path
+    // the wire offsets are affine and the trailing fixup blocks write them -- no scan launch, whose
+    // ~5 us at config 2 the assembly waited for.  The other paths run the scan, which needs no
+    // class and is exact whatever the frames are.
+    a.affine = ext_class >= 0 && fix_blocks ? 1u : 0u;
+    a.ext = ext_class >= 0 ? (uint32_t)ext_class : 0u;
+    a.hstride = 2u + (masked ? 4u : 0u) + a.ext;
+    a.off0 = 0;
+    a.fix_done = a.defer_count + 1;
+    a.wo_out = wo;
+    if (!a.affine &&
+        (e = launch_scan(off, n, masked, wo, stream, sc, per, fix_in_scan ? &a : nullptr)) != hipSuccess)
+        return e;
     const bool nt = cfg.flags < 0 || (cfg.flags & (kNtLoads | kNtStores));
     // Chunk size: netc_gpu_tune's unroll 8 selects 4 KiB, 2 or 4 select 2 KiB; the default
     // (unroll 1) takes 4 KiB up to 256 MiB of wire (C2 39.0-39.3 against 39.8-39.9 us, three

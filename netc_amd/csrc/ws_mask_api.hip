@@ -342,10 +342,9 @@ int netc_gpu_mask_batch_multi(int nshards, const int* devices, void* const* d_ds
     return 0;
 }
 
-int netc_gpu_encode_frames(int device, void* d_wire, size_t wire_capacity, uint64_t* d_wire_offsets,
-                           const void* d_payload, size_t total_bytes, const uint64_t* d_frame_offsets,
-                           const uint32_t* d_keys, const uint8_t* d_header0, size_t nframes, int masked,
-                           void* stream) {
+static int encode_frames(int device, void* d_wire, size_t wire_capacity, uint64_t* d_wire_offsets, const void* d_payload,
+                         size_t total_bytes, const uint64_t* d_frame_offsets, const uint32_t* d_keys,
+                         const uint8_t* d_header0, size_t nframes, int masked, int ext_class, void* stream) {
     if (int r = check_device(device)) return r;
     if (!d_wire_offsets) return fail(NETC_GPU_EINVAL, "null wire offsets");
     if (nframes && (!d_frame_offsets || !d_wire)) return fail(NETC_GPU_EINVAL, "null frame buffer");
@@ -368,9 +367,28 @@ int netc_gpu_encode_frames(int device, void* d_wire, size_t wire_capacity, uint6
     if (g.err != hipSuccess) return fail_hip(NETC_GPU_ERUNTIME, "hipSetDevice", g.err);
     hipError_t e = netc_gpu::launch_encode_frames((uint8_t*)d_wire, bound, (const uint8_t*)d_payload, total_bytes,
                                                   d_frame_offsets, d_keys, d_header0, nframes, masked != 0,
-                                                  d_wire_offsets, (hipStream_t)stream, cfg_now());
+                                                  d_wire_offsets, (hipStream_t)stream, cfg_now(), ext_class);
     if (e != hipSuccess) return fail_hip(NETC_GPU_ELAUNCH, "frame assembly launch", e);
     return 0;
+}
+
+int netc_gpu_encode_frames(int device, void* d_wire, size_t wire_capacity, uint64_t* d_wire_offsets,
+                           const void* d_payload, size_t total_bytes, const uint64_t* d_frame_offsets,
+                           const uint32_t* d_keys, const uint8_t* d_header0, size_t nframes, int masked,
+                           void* stream) {
+    return encode_frames(device, d_wire, wire_capacity, d_wire_offsets, d_payload, total_bytes, d_frame_offsets,
+                         d_keys, d_header0, nframes, masked, -1, stream);
+}
+
+int netc_gpu_encode_frames_class(int device, void* d_wire, size_t wire_capacity, uint64_t* d_wire_offsets,
+                                 const void* d_payload, size_t total_bytes, const uint64_t* d_frame_offsets,
+                                 const uint32_t* d_keys, const uint8_t* d_header0, size_t nframes, int masked,
+                                 int length_class, void* stream) {
+    if (length_class != NETC_WS_CLASS_7BIT && length_class != NETC_WS_CLASS_16BIT &&
+        length_class != NETC_WS_CLASS_64BIT)
+        return fail(NETC_GPU_EINVAL, "unknown length class %d (NETC_WS_CLASS_7BIT, _16BIT or _64BIT)", length_class);
+    return encode_frames(device, d_wire, wire_capacity, d_wire_offsets, d_payload, total_bytes, d_frame_offsets,
+                         d_keys, d_header0, nframes, masked, length_class, stream);
 }
 
 int netc_gpu_scan_frames(int device, const void* d_wire, size_t len, uint64_t start, int flags, uint64_t* d_hdr,

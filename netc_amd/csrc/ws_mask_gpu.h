@@ -93,6 +93,8 @@ int release_enc_scratch(int device, hipStream_t stream);     // ws_frame_gpu.hip
 
 hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_t* src, uint64_t src_total,
                                 const uint64_t* off, const uint32_t* keys, const uint8_t* b0, uint64_t n, bool masked,
-                                uint64_t* wo, hipStream_t stream, const LaunchCfg& cfg);
+                                uint64_t* wo, hipStream_t stream, const LaunchCfg& cfg, int ext_class = -1);
+// ext_class: -1, or every frame's extended-length bytes (0, 2, 8) as the caller promises
+// (netc_gpu_encode_frames_class; wo[n] = UINT64_MAX after the call if a frame breaks it)
 
 }  // namespace netc_gpu

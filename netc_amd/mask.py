@@ -226,12 +226,29 @@ def wire_size(offsets: np.ndarray, masked: bool) -> int:
     return int(_lib.host().netc_ws_wire_size(_ptr(off), off.size - 1, 1 if masked else 0))
 
 
+# include/ws/frame.h: length classes of netc_gpu_encode_frames_class (extended-length bytes)
+NETC_WS_CLASS_7BIT, NETC_WS_CLASS_16BIT, NETC_WS_CLASS_64BIT = 0, 2, 8
+NETC_WS_WIRE_INVALID = (1 << 64) - 1
+
+
+def length_class(offsets: np.ndarray) -> Optional[int]:
+    """The one NETC_WS_CLASS_* every frame of host offsets lies in, or None when they are mixed."""
+    ln = np.diff(np.asarray(offsets, dtype=np.uint64))
+    if ln.size == 0:
+        return None
+    cls = np.where(ln <= 125, 0, np.where(ln <= 0xFFFF, 2, 8))
+    return int(cls[0]) if (cls == cls[0]).all() else None
+
+
 def encode_frames(wire, wire_offsets, src, offsets, keys=None, header0=None, masked: bool = True, stream=None,
-                  device: Optional[int] = None) -> None:
+                  device: Optional[int] = None, length_class: Optional[int] = None) -> None:
     """netc_gpu_encode_frames: headers + keys + masked payloads of every frame into `wire` (device tensors).
 
     wire: uint8, >= wire_bound(src.numel(), n, masked) bytes; wire_offsets: int64, n + 1 (output);
     header0: uint8 per frame (FIN | RSV | opcode) or None for 0x82; keys: packed key32 (masked only).
+    length_class: a NETC_WS_CLASS_* every frame lies in, as the caller promises
+    (netc_gpu_encode_frames_class: one launch; wire_offsets[n] reads NETC_WS_WIRE_INVALID after
+    the call when a frame breaks it), or None.
     """
     import torch
 
@@ -256,9 +273,15 @@ def encode_frames(wire, wire_offsets, src, offsets, keys=None, header0=None, mas
             raise ValueError("header0 must be nframes uint8")
         hp = header0.data_ptr()
     dev = src.device.index if device is None else device
-    _check(_lib.gpu().netc_gpu_encode_frames(dev, wire.data_ptr(), wire.numel(), wire_offsets.data_ptr(),
-                                             src.data_ptr(), src.numel(), offsets.data_ptr(), kp, hp, n,
-                                             1 if masked else 0, _stream_handle(stream)))
+    if length_class is None:
+        _check(_lib.gpu().netc_gpu_encode_frames(dev, wire.data_ptr(), wire.numel(), wire_offsets.data_ptr(),
+                                                 src.data_ptr(), src.numel(), offsets.data_ptr(), kp, hp, n,
+                                                 1 if masked else 0, _stream_handle(stream)))
+    else:
+        _check(_lib.gpu().netc_gpu_encode_frames_class(dev, wire.data_ptr(), wire.numel(), wire_offsets.data_ptr(),
+                                                       src.data_ptr(), src.numel(), offsets.data_ptr(), kp, hp, n,
+                                                       1 if masked else 0, int(length_class),
+                                                       _stream_handle(stream)))
 
 
 NETC_WS_SCAN_STRICT = 1

@@ -35,7 +35,8 @@ def frames_from_sizes(sizes, start=0):
     return off
 
 
-def run_encode(torch, payload, off, keys, header0=None, masked=True, wire_shift=0, src_shift=0, check=True):
+def run_encode(torch, payload, off, keys, header0=None, masked=True, wire_shift=0, src_shift=0, check=True,
+               length_class=None):
     total = payload.size
     n = off.size - 1
     src_buf = torch.full((total + 2 * GUARD,), 0x5A, dtype=torch.uint8, device="cuda")
@@ -47,7 +48,7 @@ def run_encode(torch, payload, off, keys, header0=None, masked=True, wire_shift=
     wo = torch.full((n + 1,), -1, dtype=torch.int64, device="cuda")
     keys_t = _dev(torch, np.asarray(keys, dtype=np.uint32)) if masked else None
     h_t = torch.from_numpy(np.ascontiguousarray(header0, dtype=np.uint8)).cuda() if header0 is not None else None
-    nm.encode_frames(wire, wo, src, _dev(torch, off), keys_t, h_t, masked=masked)
+    nm.encode_frames(wire, wo, src, _dev(torch, off), keys_t, h_t, masked=masked, length_class=length_class)
     torch.cuda.synchronize()
     exp_wire, exp_wo = orc.encode_batch(payload, off, keys if masked else None, header0, masked)
     got_wo = wo.cpu().numpy().view(np.uint64)
@@ -306,3 +307,127 @@ def test_dense_compose_edges(torch_cuda, gpu_knob, wire_shift, src_shift, masked
     payload = _payload(rng, int(off[-1]))
     keys = rng.integers(0, 2**32, len(sizes), dtype=np.uint64).astype(np.uint32)
     run_encode(torch_cuda, payload, off, keys, masked=masked, wire_shift=wire_shift, src_shift=src_shift)
+
+
+# ------------------------------------------------ one length class (netc_gpu_encode_frames_class) --
+# Every frame in one header class: the wire offsets are affine in the payload offsets, the assembly
+# launch computes and writes them (no scan launch).  Same bar as above: wire bytes and offsets
+# bit-exact against oracle_encode_batch, nothing written outside the wire.
+
+CLASS_SIZES = {
+    nm.NETC_WS_CLASS_7BIT: (80, 126),          # mean >= 80 B: the vector path (below it, the dense path)
+    nm.NETC_WS_CLASS_16BIT: (126, 65536),
+    nm.NETC_WS_CLASS_64BIT: (65536, 200000),
+}
+
+
+@pytest.mark.parametrize("cls", sorted(CLASS_SIZES))
+@pytest.mark.parametrize("masked", [True, False])
+@pytest.mark.parametrize("shifts", [(0, 0), (5, 3), (15, 9)])
+def test_one_class(torch_cuda, cls, masked, shifts):
+    rng = np.random.default_rng(500 + cls * 8 + shifts[0] + masked)
+    lo, hi = CLASS_SIZES[cls]
+    n = {0: 3000, 2: 400, 8: 24}[cls]
+    sizes = rng.integers(lo, hi, n)
+    sizes[:2] = [lo, hi - 1]   # the class edges
+    off = frames_from_sizes(sizes, start=int(rng.integers(0, 40)))
+    assert nm.length_class(off) == cls
+    payload = _payload(rng, int(off[-1]) + 7)
+    keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    h0 = rng.choice(np.array([0x81, 0x82, 0x01, 0x00, 0x80], dtype=np.uint8), n)
+    run_encode(torch_cuda, payload, off, keys, header0=h0, masked=masked, wire_shift=shifts[0], src_shift=shifts[1],
+               length_class=cls)
+
+
+def test_one_class_c2_full_size(torch_cuda):
+    # config 2: 65,536 x 1 KiB, every frame in the 16-bit class -- 256 fixup blocks share the counter
+    rng = np.random.default_rng(0x6E657463)
+    n = 65536
+    off = frames_from_sizes(np.full(n, 1024))
+    payload = _payload(rng, int(off[-1]))
+    keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    run_encode(torch_cuda, payload, off, keys, length_class=nm.NETC_WS_CLASS_16BIT)
+
+
+@pytest.mark.parametrize("path", PATHS[1:] + ["dense"])
+def test_one_class_on_the_general_paths(torch_cuda, gpu_knob, path):
+    # where the call takes another path (the knobs, or a batch averaging < 80 B) the scan runs
+    # and the result is exact -- also when a frame breaks the promise
+    if path == "dense":
+        gpu_knob("ENC_DENSE_BYTES", "100000")
+    else:
+        _set_path(gpu_knob, path)
+    rng = np.random.default_rng(61)
+    sizes = rng.integers(126, 3000, 300)
+    sizes[100] = 5   # outside the 16-bit class
+    off = frames_from_sizes(sizes)
+    payload = _payload(rng, int(off[-1]))
+    keys = rng.integers(0, 2**32, sizes.size, dtype=np.uint64).astype(np.uint32)
+    run_encode(torch_cuda, payload, off, keys, wire_shift=3, length_class=nm.NETC_WS_CLASS_16BIT)
+
+
+def _broken(torch, sizes, cls, masked=True, wire_shift=0):
+    rng = np.random.default_rng(len(sizes) + cls)
+    off = frames_from_sizes(sizes)
+    total = int(off[-1])
+    n = len(sizes)
+    src = torch.from_numpy(_payload(rng, total)).cuda()
+    cap = nm.wire_bound(total, n, masked)
+    wire_buf = torch.full((cap + 2 * GUARD,), SENTINEL, dtype=torch.uint8, device="cuda")
+    wire = wire_buf[GUARD + wire_shift: GUARD + wire_shift + cap]
+    wo = torch.full((n + 1,), -1, dtype=torch.int64, device="cuda")
+    keys = _dev(torch, rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)) if masked else None
+    nm.encode_frames(wire, wo, src, _dev(torch, off), keys, masked=masked, length_class=cls)
+    torch.cuda.synchronize()
+    whole = wire_buf.cpu().numpy()
+    assert (whole[:GUARD + wire_shift] == SENTINEL).all(), "write before the wire"
+    assert (whole[GUARD + wire_shift + cap:] == SENTINEL).all(), "write past the wire bound"
+    return wo.cpu().numpy().view(np.uint64)
+
+
+@pytest.mark.parametrize("where", ["first", "middle", "last", "many"])
+@pytest.mark.parametrize("masked", [True, False])
+def test_one_class_broken_promise(torch_cuda, where, masked):
+    # a frame outside the promised class: wire_offsets[n] = NETC_WS_WIRE_INVALID, no stray write
+    sizes = np.full(20000, 1024)
+    pick = {"first": [0], "middle": [9999], "last": [19999], "many": list(range(3, 20000, 997))}[where]
+    for i, k in enumerate(pick):
+        sizes[k] = [100, 70000, 0][i % 3]
+    wo = _broken(torch_cuda, sizes, nm.NETC_WS_CLASS_16BIT, masked=masked, wire_shift=7)
+    assert int(wo[-1]) == nm.NETC_WS_WIRE_INVALID
+
+
+def test_one_class_counter_resets(torch_cuda):
+    # the fixup blocks' counter is left zero by every call, broken or not: calls in a row on one
+    # stream with grids of different sizes each give their own verdict
+    torch = torch_cuda
+    for n, bad in [(5000, False), (300, True), (70000, False), (64, True), (64, False), (30000, True), (1, False)]:
+        sizes = np.full(n, 200)
+        if bad:
+            sizes[n // 2] = 7
+        wo = _broken(torch, sizes, nm.NETC_WS_CLASS_16BIT)
+        if bad:
+            assert int(wo[-1]) == nm.NETC_WS_WIRE_INVALID
+        else:
+            assert int(wo[-1]) == nm.wire_size(frames_from_sizes(sizes), True)
+    rng = np.random.default_rng(3)
+    sizes = rng.integers(126, 5000, 2000)
+    off = frames_from_sizes(sizes)
+    run_encode(torch, _payload(rng, int(off[-1])), off, rng.integers(0, 2**32, 2000, dtype=np.uint64).astype(np.uint32),
+               length_class=nm.NETC_WS_CLASS_16BIT)
+
+
+def test_one_class_errors(torch_cuda):
+    torch = torch_cuda
+    src = torch.zeros(1000, dtype=torch.uint8, device="cuda")
+    off = torch.tensor([0, 500, 1000], dtype=torch.int64, device="cuda")
+    keys = torch.zeros(2, dtype=torch.int32, device="cuda")
+    wo = torch.zeros(3, dtype=torch.int64, device="cuda")
+    wire = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    for bad in (-1, 1, 3, 4, 16):
+        with pytest.raises(nm.NetcGpuError) as e:
+            nm.encode_frames(wire, wo, src, off, keys, length_class=bad)
+        assert e.value.code == nm.NETC_GPU_EINVAL
+    nm.encode_frames(wire, wo, src, off, keys, length_class=nm.NETC_WS_CLASS_16BIT)
+    torch.cuda.synchronize()
+    assert int(wo.cpu()[-1]) == 1000 + 2 * 8

@@ -2,7 +2,9 @@
 """Send-side frame assembly (netc_gpu_encode_frames) throughput, one GPU.
 
 Per step: the wire-offset scan + the assembly kernel over one batch (configs 2 and 4
-shapes: 65,536 x 1 KiB, and 1 GiB of 256 B..64 KiB frames), masked.  Algorithmic
+shapes: 65,536 x 1 KiB, and 1 GiB of 256 B..64 KiB frames), masked.  --entry class times
+netc_gpu_encode_frames_class instead (one launch: affine wire offsets) on the workloads whose
+frames are all in one length class (config 2).  Algorithmic
 bytes = payload read + wire written (+ 8 B/frame offsets read, + 8 B/frame wire
 offsets written, reported, not counted).  GPU time from two events around K steps
 on one stream; batches rotate over >= 1 GiB of distinct payload.  One JSON line per
@@ -30,6 +32,8 @@ def main():
                                                        "a huge value: one chunk per wavefront over a covering grid)")
     ap.add_argument("--flags", default="-1", help="netc_gpu_tune flags values (-1: auto, non-temporal payload "
                                                   "loads and stores; 8: plain loads and stores)")
+    ap.add_argument("--entry", default="scan", help="comma list: scan (netc_gpu_encode_frames), class "
+                                                    "(netc_gpu_encode_frames_class, one-class workloads only)")
     args = ap.parse_args()
 
     import torch
@@ -38,7 +42,7 @@ def main():
     from netc_amd import mask as nm
 
     dev = torch.device("cuda", 0)
-    entry = _lib.gpu().netc_gpu_encode_frames
+    lib = _lib.gpu()
     s = torch.cuda.Stream(dev)
     sh = s.cuda_stream
     for wl in args.workloads.split(","):
@@ -54,14 +58,24 @@ def main():
         wire_len = nm.wire_size(off, True)
         torch.cuda.synchronize()
 
+        cls = nm.length_class(off)
+
         def step(i):
-            rc = entry(0, wires[i % 2].data_ptr(), cap, wo.data_ptr(), srcs[i % nb].data_ptr(), total,
-                       off_t.data_ptr(), keys_t.data_ptr(), None, n, 1, sh)
+            if entry == "class":
+                rc = lib.netc_gpu_encode_frames_class(0, wires[i % 2].data_ptr(), cap, wo.data_ptr(),
+                                                      srcs[i % nb].data_ptr(), total, off_t.data_ptr(),
+                                                      keys_t.data_ptr(), None, n, 1, cls, sh)
+            else:
+                rc = lib.netc_gpu_encode_frames(0, wires[i % 2].data_ptr(), cap, wo.data_ptr(), srcs[i % nb].data_ptr(),
+                                                total, off_t.data_ptr(), keys_t.data_ptr(), None, n, 1, sh)
             if rc:
                 raise RuntimeError(nm._lib.gpu().netc_gpu_strerror())
 
-        for unroll, mb, fl in [(int(u), int(m), int(f)) for u in args.unroll.split(",") for m in args.max_blocks.split(",")
-                               for f in args.flags.split(",")]:
+        for entry, unroll, mb, fl in [(e, int(u), int(m), int(f)) for e in args.entry.split(",")
+                                      for u in args.unroll.split(",") for m in args.max_blocks.split(",")
+                                      for f in args.flags.split(",")]:
+            if entry == "class" and cls is None:
+                continue
             nm.tune(unroll, mb, fl)
             K = args.steps if wl == "c2" else max(10, args.steps // 5)
             with torch.cuda.stream(s):
@@ -86,7 +100,7 @@ def main():
                 exp = orc.encode_frame(src_h[lo:hi].tobytes(), 2, int(keys[k]).to_bytes(4, "little"))
                 bad += wire[int(wo_h[k]): int(wo_h[k + 1])].tobytes() != exp
             alg = total + wire_len
-            print(json.dumps({"workload": wl, "unroll": unroll, "max_blocks": mb, "flags": fl, "frames": int(n), "payload_bytes": int(total), "wire_bytes": int(wire_len),
+            print(json.dumps({"workload": wl, "entry": entry, "unroll": unroll, "max_blocks": mb, "flags": fl, "frames": int(n), "payload_bytes": int(total), "wire_bytes": int(wire_len),
                               "us_per_step": round(us, 2), "achieved_GBps": round(alg / (us * 1e-6) / 1e9, 1),
                               "frac_of_8TBps": round(alg / (us * 1e-6) / 8e12, 4),
                               "payload_GiBps": round(total / (us * 1e-6) / 2**30, 1),
