@@ -847,15 +847,17 @@ __device__ void fixup_block(const EncArgs& a) {
     const uint64_t fb = blockIdx.x - a.main_blocks, nfb = gridDim.x - a.main_blocks;
     int broken = 0;
     for (uint64_t k = fb * blockDim.x + threadIdx.x; k < a.n; k += nfb * blockDim.x) {
+        bool fix = true;
+        uint64_t o = 0;
         if (a.affine) {
-            const uint64_t o = gptr(a.off)[k], on = gptr(a.off)[k + 1];
-            gptr(a.wo_out)[k] = o - a.off0 + a.hstride * k;
-            if (on < o || ext_len(on - o) != a.ext) {
-                broken = 1;
-                continue;
-            }
+            o = gptr(a.off)[k];
+            const uint64_t on = gptr(a.off)[k + 1];
+            fix = on >= o && ext_len(on - o) == a.ext;
+            broken |= fix ? 0 : 1;
         }
-        fix_vectors(a, k, wlo);
+        if (fix) fix_vectors(a, k, wlo);   // (one call site: a second inlined copy spills the kernel)
+        // (wo[k] stored last: a store before fix_vectors would make it reload off[])
+        if (a.affine) gptr(a.wo_out)[k] = o - a.off0 + a.hstride * k;
     }
     if (!a.affine) return;
     broken = __syncthreads_or(broken);
