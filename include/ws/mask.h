@@ -104,9 +104,8 @@ int netc_gpu_init(int device);
  * selects round 1's walk — one resident round of workgroups striding over the
  * chunks — where max_blocks caps the workgroups (0 = exactly the workgroups the
  * device holds at once); max_blocks is ignored otherwise.  The frame assembly of
- * include/ws/frame.h reads the same knob: unroll 8 selects 4 KiB chunks there, 2
- * or 4 select 2 KiB, the default 4 KiB up to 256 MiB of wire and 2 KiB above, and
- * it always walks persistently.  Diagnostic knob.  The
+ * include/ws/frame.h reads the same knob: 2 or 4 select 2 KiB chunks there, any
+ * other value 4 KiB (the default), and it always walks persistently.  Diagnostic knob.  The
  * shape is one atomic word: a launch on another thread sees the old shape or the
  * new one, never a mix.
  */

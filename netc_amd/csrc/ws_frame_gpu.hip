@@ -1581,11 +1581,12 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
         (e = launch_scan(off, n, masked, wo, stream, sc, per, fix_in_scan ? &a : nullptr)) != hipSuccess)
         return e;
     const bool nt = cfg.flags < 0 || (cfg.flags & (kNtLoads | kNtStores));
-    // Chunk size: netc_gpu_tune's unroll 8 selects 4 KiB, 2 or 4 select 2 KiB; the default
-    // (unroll 1) takes 4 KiB up to 256 MiB of wire (C2 39.0-39.3 against 39.8-39.9 us, three
-    // rounds, profiles/r03r_enc_chunk.json) and 2 KiB above (C4 416-417 against 422-423 us).
-    // 2 KiB: 7 wavefronts per SIMD up to 256 MiB (72 VGPRs), 6 above (76 VGPRs; C4 418 vs 425
-    // us at 7, 424 at 8 with spills; profiles/r02k_ab_enc_occupancy.json)
+    // Chunk size: 4 KiB chunks, 5 wavefronts per SIMD by default; netc_gpu_tune's unroll 2 or 4
+    // select 2 KiB chunks at 6 wavefronts (A/B only).  Round 3 took 2 KiB above 256 MiB of wire
+    // (C4 416-417 against 422-423 us then); the kernel has grown since, and at 6 wavefronts the
+    // 2 KiB form spills 18 VGPRs to scratch: C4 435-437 us against 421-423 for 4 KiB (round 5,
+    // three interleaved rounds, profiles/r05_kernels/encode_c4_chunk.json).  C2 39.0-39.3 against
+    // 39.8-39.9 us (profiles/r03r_enc_chunk.json).
     // NETC_GPU_KNOB_ENC_SRC = 1: the source-driven walk (round 4 experiment, kept for A/B: parity
     // green, but slower than the wire-driven kernels at both shapes measured -- config 2 35.3 us
     // against 26.6 + 7.9 for the wire-driven kernel and the header fixups, config 4 428-438 us
@@ -1609,10 +1610,8 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
         else hipLaunchKernelGGL((encode_src_kernel<K, false>), dim3((unsigned)blocks), dim3(256), 0, stream, a);
         return hipGetLastError();
     }
-    const bool small = wire_bound <= (256ull << 20);
-    if (cfg.unroll >= 8 || (cfg.unroll <= 1 && small)) return launch_enc_u<4, 5>(a, wire_bound, nt, cfg.max_blocks, stream);
-    if (small) return launch_enc_u<2, 7>(a, wire_bound, nt, cfg.max_blocks, stream);
-    return launch_enc_u<2, 6>(a, wire_bound, nt, cfg.max_blocks, stream);
+    if (cfg.unroll == 2 || cfg.unroll == 4) return launch_enc_u<2, 6>(a, wire_bound, nt, cfg.max_blocks, stream);
+    return launch_enc_u<4, 5>(a, wire_bound, nt, cfg.max_blocks, stream);
 }
 
 }  // namespace netc_gpu
