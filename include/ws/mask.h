@@ -105,7 +105,8 @@ int netc_gpu_init(int device);
  * chunks — where max_blocks caps the workgroups (0 = exactly the workgroups the
  * device holds at once); max_blocks is ignored otherwise.  The frame assembly of
  * include/ws/frame.h reads the same knob: 2 or 4 select 2 KiB chunks there, any
- * other value 4 KiB (the default), and it always walks persistently.  Diagnostic knob.  The
+ * other value 4 KiB (the default; pipelined above 256 MiB, knob ENC_PF), and it
+ * always walks persistently.  Diagnostic knob.  The
  * shape is one atomic word: a launch on another thread sees the old shape or the
  * new one, never a mix.
  */
@@ -149,6 +150,10 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *   ENC_PROBE          entries of the frame assembly's first table probe per chunk, when dense:
  *                      0 always 64 (round 4's table), > 0 that many more than the default
  *                      (expected frames + 10) [default]             (NETC_ENC_PROBE)
+ *   ENC_PF             the frame assembly's walk software-pipelined -- a chunk's payload loads
+ *                      issued before the previous chunk is stored: 0 never; 1 2 KiB chunks at
+ *                      5 wavefronts per SIMD; 2 4 KiB chunks at 4 [2 above 256 MiB of wire,
+ *                      else 0]                                      (NETC_ENC_PF)
  *   INJECT_FAULT       fault injection for tests: the ingest / egress ring submission this
  *                      countdown reaches (0 = the next one) fails as NETC_GPU_ELAUNCH
  *                      without launching, then the knob disarms itself [off]
@@ -165,6 +170,7 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
 #define NETC_GPU_KNOB_ENC_FIX           9
 #define NETC_GPU_KNOB_INJECT_FAULT     10
 #define NETC_GPU_KNOB_ENC_PROBE        11
+#define NETC_GPU_KNOB_ENC_PF           12
 int netc_gpu_knob(int knob, int64_t value);
 
 /**

@@ -871,7 +871,10 @@ __device__ void fixup_block(const EncArgs& a) {
     }
 }
 
-template <int U, bool NT, int W>
+// PF (knob ENC_PF): the walk software-pipelined -- chunk c + W's table is resolved and its loads
+// issued before chunk c is stored, so a wavefront keeps two chunks of loads in flight (one plan
+// more in registers).
+template <int U, bool NT, int W, bool PF = false>
 __global__ __launch_bounds__(256, W) void encode_frames_kernel(EncArgs a) {
     if (a.affine) a.off0 = gptr(a.off)[0];
     const uint64_t wire_total = wire_at(a, a.n);
@@ -937,6 +940,37 @@ __global__ __launch_bounds__(256, W) void encode_frames_kernel(EncArgs a) {
     EncTable tc;
     uint64_t A = c * kWin;
     enc_table_issue(a, tc, guess(0, a.wmis, A), lane, a.probe_e);
+    if constexpr (PF) {
+        enc_table_finish(tc);
+        enc_resolve(a, tc, A, wire_total, lane);
+        Plan<U> pc;
+        plan_chunk<U, NT>(a, tc, A, wlo, whi, lane, pc);
+        int64_t f;
+        uint64_t s;
+        known(tc, A, f, s);
+        uint64_t cn = c + nwaves;
+        if (cn < nwin) enc_table_issue(a, tc, guess(f, s, cn * kWin), lane, a.probe_e);   // tc: chunk cn's table
+        for (;;) {
+            const bool more = cn < nwin;   // wave-uniform
+            const uint64_t An = cn * kWin;
+            Plan<U> pn;
+            if (more) {
+                enc_table_finish(tc);
+                enc_resolve(a, tc, An, wire_total, lane);
+                plan_chunk<U, NT>(a, tc, An, wlo, whi, lane, pn);
+                known(tc, An, f, s);
+                if (cn + nwaves < nwin) enc_table_issue(a, tc, guess(f, s, (cn + nwaves) * kWin), lane, a.probe_e);
+            }
+            finish_chunk<U, NT>(a, tc, A, wlo, whi, lane, pc, list, nl);   // (finish_chunk reads no table)
+            if (!more) break;
+            pc = pn;
+            A = An;
+            cn += nwaves;
+        }
+        done();
+        tail_fix();
+        return;
+    }
     for (;;) {
         enc_table_finish(tc);
         enc_resolve(a, tc, A, wire_total, lane);
@@ -1326,14 +1360,14 @@ __global__ __launch_bounds__(256) void encode_src_kernel(EncArgs a) {
     }
 }
 
-template <int U, bool NT, int W>
+template <int U, bool NT, int W, bool PF>
 static int enc_resident_blocks() {
     static int cache[64] = {0};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
     if (cache[dev] > 0) return cache[dev];
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, encode_frames_kernel<U, NT, W>, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, encode_frames_kernel<U, NT, W, PF>, 256, 0) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 || cus <= 0)
         return 1024;
     cache[dev] = per_cu * cus;
@@ -1480,11 +1514,11 @@ static uint64_t dense_bytes() {
     return k >= 0 ? (uint64_t)k : (uint64_t)80;
 }
 
-template <int U, int W>
+template <int U, int W, bool PF = false>
 static hipError_t launch_enc_u(EncArgs a, uint64_t wire_bound, bool nt, int max_blocks, hipStream_t stream) {
     const uint64_t nwin = (a.wmis + wire_bound + kSpan * U - 1) / (kSpan * U);
     const uint64_t cap = (uint64_t)(max_blocks > 0 ? max_blocks
-                                                  : (nt ? enc_resident_blocks<U, true, W>() : enc_resident_blocks<U, false, W>()));
+                                                  : (nt ? enc_resident_blocks<U, true, W, PF>() : enc_resident_blocks<U, false, W, PF>()));
     const uint64_t want = (nwin + 3) / 4;
     const int blocks = (int)(want < cap ? want : cap);
     if (blocks <= 0) return hipSuccess;
@@ -1517,8 +1551,8 @@ static hipError_t launch_enc_u(EncArgs a, uint64_t wire_bound, bool nt, int max_
     a.per_wave = (uint32_t)(((nwin + 4 * (uint64_t)blocks - 1) / (4 * (uint64_t)blocks)) * U);   // windows per wave x U
     if ((uint64_t)a.per_wave * 4 * (uint64_t)blocks > a.defer_cap) return hipErrorInvalidValue;   // (sized with slack below)
     const unsigned grid = (unsigned)(blocks + fix_blocks);
-    if (nt) hipLaunchKernelGGL((encode_frames_kernel<U, true, W>), dim3(grid), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((encode_frames_kernel<U, false, W>), dim3(grid), dim3(256), 0, stream, a);
+    if (nt) hipLaunchKernelGGL((encode_frames_kernel<U, true, W, PF>), dim3(grid), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((encode_frames_kernel<U, false, W, PF>), dim3(grid), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -1610,6 +1644,15 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
         else hipLaunchKernelGGL((encode_src_kernel<K, false>), dim3((unsigned)blocks), dim3(256), 0, stream, a);
         return hipGetLastError();
     }
+    // The software-pipelined walk (4 KiB chunks, 4 wavefronts per SIMD) above 256 MiB of wire: C4
+    // 416.2-416.8 us against 422.8-424.2, while at C2 it loses (41.1-41.3 against 38.0-38.5 us:
+    // ~4 chunks per wavefront, the deeper prologue is not repaid).  2 KiB chunks pipelined at 5
+    // wavefronts lose at both (C2 40.9-41.1, C4 425.3-426.7 us).  Three interleaved rounds, one
+    // box, profiles/r05_kernels/encode_pf_ab.json.  NETC_GPU_KNOB_ENC_PF: 0 never, 1 / 2 always.
+    const int64_t pf = knob(NETC_GPU_KNOB_ENC_PF);
+    if (pf == 1) return launch_enc_u<2, 5, true>(a, wire_bound, nt, cfg.max_blocks, stream);
+    if (pf == 2 || (pf < 0 && cfg.unroll <= 1 && wire_bound > (256ull << 20)))
+        return launch_enc_u<4, 4, true>(a, wire_bound, nt, cfg.max_blocks, stream);
     if (cfg.unroll == 2 || cfg.unroll == 4) return launch_enc_u<2, 6>(a, wire_bound, nt, cfg.max_blocks, stream);
     return launch_enc_u<4, 5>(a, wire_bound, nt, cfg.max_blocks, stream);
 }

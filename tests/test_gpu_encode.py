@@ -77,8 +77,9 @@ def _payload(rng, n):
 # the assembly path: None = the default (wire-driven kernel; trailing blocks of the same launch
 # compose the vectors holding header bytes), "fixscan" = those vectors by the wire-offsets scan
 # (NETC_GPU_KNOB_ENC_FIX = 1), "src" = the source-driven walk writing headers in the same pass
-# (NETC_GPU_KNOB_ENC_SRC = 1); both A/B paths
-PATHS = [None, "fixscan", "fixtail", "src"]
+# (NETC_GPU_KNOB_ENC_SRC = 1), "pf1" / "pf2" = the software-pipelined walk (NETC_GPU_KNOB_ENC_PF);
+# all A/B paths
+PATHS = [None, "fixscan", "fixtail", "src", "pf1", "pf2"]
 
 
 def _set_path(gpu_knob, path):
@@ -88,6 +89,8 @@ def _set_path(gpu_knob, path):
         gpu_knob("ENC_FIX", 2)
     elif path == "src":
         gpu_knob("ENC_SRC", 1)
+    elif path in ("pf1", "pf2"):   # the software-pipelined walk (ENC_PF): 2 KiB / 4 KiB chunks
+        gpu_knob("ENC_PF", int(path[2]))
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -339,8 +342,10 @@ def test_one_class(torch_cuda, cls, masked, shifts):
                length_class=cls)
 
 
-def test_one_class_c2_full_size(torch_cuda):
+@pytest.mark.parametrize("path", [None, "pf1", "pf2"])
+def test_one_class_c2_full_size(torch_cuda, gpu_knob, path):
     # config 2: 65,536 x 1 KiB, every frame in the 16-bit class -- 256 fixup blocks share the counter
+    _set_path(gpu_knob, path)
     rng = np.random.default_rng(0x6E657463)
     n = 65536
     off = frames_from_sizes(np.full(n, 1024))
@@ -349,7 +354,7 @@ def test_one_class_c2_full_size(torch_cuda):
     run_encode(torch_cuda, payload, off, keys, length_class=nm.NETC_WS_CLASS_16BIT)
 
 
-@pytest.mark.parametrize("path", PATHS[1:] + ["dense"])
+@pytest.mark.parametrize("path", ["fixscan", "fixtail", "src", "dense"])
 def test_one_class_on_the_general_paths(torch_cuda, gpu_knob, path):
     # where the call takes another path (the knobs, or a batch averaging < 80 B) the scan runs
     # and the result is exact -- also when a frame breaks the promise

@@ -26,8 +26,10 @@ READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
 HOT = [
     "void netc_gpu::mask_np_kernel<1, 2, true, true, false, netc_gpu::Args>",   # the headline (config 2)
     "void netc_gpu::mask_np_kernel<",
-    "void netc_gpu::encode_frames_kernel<4, true, 5>",
-    "void netc_gpu::encode_frames_kernel<4, false, 5>",
+    "void netc_gpu::encode_frames_kernel<4, true, 5, false>",
+    "void netc_gpu::encode_frames_kernel<4, false, 5, false>",
+    "void netc_gpu::encode_frames_kernel<4, true, 4, true>",    # pipelined, above 256 MiB of wire
+    "void netc_gpu::encode_frames_kernel<4, false, 4, true>",
     "void netc_gpu::wire_offsets_chained<4, false>",
     "void netc_gpu::wire_offsets_chained<16, false>",
     "netc_gpu::scan_links(",
@@ -41,7 +43,7 @@ HOT = [
 # reached only through netc_gpu_tune or NETC_GPU_KNOB_* (A/B paths), not held at zero
 KNOB_ONLY = [
     "void netc_gpu::mask_frames_kernel<",      # round-1 walk (NETC_GPU_TUNE_PERSISTENT)
-    "void netc_gpu::encode_frames_kernel<2,",  # 2 KiB chunks (netc_gpu_tune unroll 2 / 4)
+    "void netc_gpu::encode_frames_kernel<2,",  # 2 KiB chunks (netc_gpu_tune unroll 2 / 4; ENC_PF = 1)
     "void netc_gpu::wire_offsets_chained<16, true>",   # fixups in the scan (ENC_FIX = 1)
     "void netc_gpu::wire_offsets_chained<1, true>",
     "netc_gpu::scan_links_fused(",             # NETC_GPU_KNOB_SCAN_FUSE = 1
