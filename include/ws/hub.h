@@ -33,6 +33,12 @@
  * readable sockets, whose frames join the same slot, and the next call for the connection
  * submits the slot and delivers.  A slot that fills is submitted at once.
  *
+ * Back-pressure: frames a connection has not yet been handed hold their slot.  When every slot
+ * holds undelivered frames, a call for a connection with nothing pending reads nothing and
+ * returns 1 (its socket stays readable) until the others drain -- a connection whose messages are
+ * never asked for should be detached (its frames are then dropped) rather than left attached.
+ * Reads never block: the route peeks with MSG_DONTWAIT, on blocking sockets too.
+ *
  * Threading: a hub is driven by one thread -- the event loop's, as netc's server runs one loop
  * for all of its clients.  Errors as in include/ws/mask.h.
  */

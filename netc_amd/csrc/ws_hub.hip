@@ -342,6 +342,7 @@ long take(netc_ws_hub* h, HubConn& c, uint64_t* frames) {
     size_t room = (size_t)(h->slot_bytes - seg - c.carry_len);
     if (room > kPeek) room = kPeek;
     const int held = (int)(c.in_pos - c.sock_pos);
+    if (held > 1) return api_fail(NETC_GPU_ERUNTIME, "hub: %d bytes held in socket %d", held, c.fd);
     ssize_t r;
     for (int pass = 0;; ++pass) {
         uint8_t skip[1];
@@ -351,7 +352,7 @@ long take(netc_ws_hub* h, HubConn& c, uint64_t* frames) {
         memset(&mh, 0, sizeof mh);
         mh.msg_iov = k ? iov : iov + 1;
         mh.msg_iovlen = k ? 2 : 1;
-        do r = recvmsg(c.fd, &mh, MSG_PEEK);
+        do r = recvmsg(c.fd, &mh, MSG_PEEK | MSG_DONTWAIT);   // (never blocks the loop, blocking socket or not)
         while (r < 0 && errno == EINTR);
         if (r > 0 && r <= k) {   // only the hostage: release it and look once more
             if (pass == 0 && held) {

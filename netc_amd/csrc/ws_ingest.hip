@@ -457,12 +457,15 @@ static long ring_recv(netc_ws_ingest* g, int fd, int skip = -1) {
         while (r < 0 && errno == EINTR);
     } else {
         uint8_t held[1];
+        if (skip > (int)sizeof held) return api_fail(NETC_GPU_ERUNTIME, "ingest: %d bytes held in the socket", skip);
         struct iovec iov[2] = {{held, (size_t)skip}, {dst, room}};
         struct msghdr mh;
         memset(&mh, 0, sizeof mh);
         mh.msg_iov = skip ? iov : iov + 1;
         mh.msg_iovlen = skip ? 2 : 1;
-        do r = recvmsg(fd, &mh, MSG_PEEK);
+        // MSG_DONTWAIT: the route peeks again after releasing its hostage, when the socket may
+        // hold nothing -- a blocking socket must not stall the caller's loop there
+        do r = recvmsg(fd, &mh, MSG_PEEK | MSG_DONTWAIT);
         while (r < 0 && errno == EINTR);
         if (r > 0 && r <= skip) return 0;   // only what the ring already has
         if (r > 0) r -= skip;

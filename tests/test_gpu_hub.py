@@ -272,5 +272,11 @@ def test_hub_detach_with_frames_pending():
         b.close()
 
 
+@pytest.mark.timeout(60)
+def test_hub_blocking_socket_never_stalls_the_loop():
+    with make_hub(slot_bytes=1 << 20, nslots=2) as hub:
+        G.blocking_socket_case(hub.attach, hub.detach)
+
+
 class ni_codes:
     RECV, INVALID, TOO_BIG = -1, -2, -3

@@ -207,6 +207,44 @@ def test_trickle_one_byte_at_a_time_then_close():
     assert got == expected(msgs)
 
 
+def blocking_socket_case(attach, detach):
+    """A socket left BLOCKING (netc makes its sockets non-blocking, but a caller may not): a call
+    that finds only part of a frame must return 1 at once -- the route releases its hostage and
+    peeks again, and that peek must not wait for the peer -- and the message comes whole once
+    the rest arrives.  A timer sends the rest after 3 s, so a call that blocks ends then and
+    fails the timing check instead of hanging the test."""
+    lib = _lib.host()
+    msgs = [(BINARY, bytes(range(256)) * 40, 1, [b"\x01\x02\x03\x04"]), (TEXT, b"after", 1, [b"\x05\x06\x07\x08"])]
+    wire = wire_of(msgs)
+    c, s = tcp_pair()   # s stays blocking
+    ep = Endpoint(s)
+    attach(s.fileno())
+    rest = threading.Timer(3.0, lambda: c.sendall(wire[3000:]))
+    try:
+        c.sendall(wire[:3000])
+        assert select.select([s], [], [], 5)[0]
+        st = ParseState()
+        rest.start()
+        t0 = time.monotonic()
+        rc = lib.ws_parse_frame(ctypes.byref(ep.client), ctypes.byref(st), 1 << 20)
+        took = time.monotonic() - t0
+        assert rc == 1 and took < 1.0, f"rc {rc} after {took:.2f} s: the call waited for the peer"
+        rest.join()
+        got = once_per_event(s, ep, lib, len(msgs), 1 << 20)
+        assert got == expected(msgs)
+    finally:
+        rest.cancel()
+        detach(s.fileno())
+        c.close()
+        s.close()
+
+
+@pytest.mark.timeout(60)
+def test_blocking_socket_never_stalls_the_loop():
+    with ni.Ingest(slot_bytes=1 << 16, nslots=2) as ing:
+        blocking_socket_case(ing.attach, ing.detach)
+
+
 @pytest.mark.timeout(60)
 def test_device_failure_is_not_a_parse_error():
     """an injected launch failure (NETC_GPU_KNOB_INJECT_FAULT) reaches ws_parse_frame's caller

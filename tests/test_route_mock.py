@@ -163,5 +163,13 @@ def test_hub_detach_with_frames_pending(hub_mock):
     hub_mock.test_hub_detach_with_frames_pending()
 
 
+def test_blocking_socket_never_stalls_the_loop(mock):
+    G.test_blocking_socket_never_stalls_the_loop()
+
+
+def test_hub_blocking_socket_never_stalls_the_loop(hub_mock):
+    hub_mock.test_hub_blocking_socket_never_stalls_the_loop()
+
+
 def test_route_errors_after_the_messages_before_them(mock):
     G.test_route_errors_after_the_messages_before_them()
