@@ -21,7 +21,7 @@ run_tool() {   # name, regex, args...
     (cd /tmp && timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$rx" --output-format csv \
         -d "$OUT/pmc_write_$name" -o run -- python3 "$R/tools/$name.py" "$@" > "$OUT/pmc_write_$name.log" 2>&1) || return $?
 }
-run_tool bench_encode "encode|wire_offsets" --steps 50 || exit $?
+run_tool bench_encode "encode|wire_offsets" --steps 50 --unroll 1 --entry scan,class || exit $?   # the default shapes
 run_tool bench_validate "mask_np_kernel|utf8" --steps 30 || exit $?
 run_tool bench_scan "scan_" --steps 20 || exit $?
 timeout -k 10 400 python3 tools/bench_stream.py > "$OUT/bench_stream.json" 2> "$OUT/bench_stream.err" || exit $?
