@@ -23,7 +23,15 @@
  *
  * With VERIFY = 1 the server also regenerates every message and compares it byte for byte.
  *
- * usage: ws_hub_server hub|cpu|ref CONNS MSGS MAX_BYTES [slot_bytes|0] [VERIFY 0|1] [ref_lib]
+ * CHUNK (0: off) prerenders the clients' traffic: before the clock starts, each client renders
+ * every message of its connections into memory -- the frames ws_send_message sends (the
+ * reference's split, src/ws/common.c:42-49; one key, each frame masked from its own first byte);
+ * the per-connection hashes check them -- and, timed, sends them round robin over its
+ * connections, CHUNK bytes per send().  The clients
+ * then cost a send per CHUNK, not a frame's ws_send_message, so the rate is the server's.  The
+ * output also carries "clients_seconds": when the last client finished sending.
+ *
+ * usage: ws_hub_server hub|cpu|ref CONNS MSGS MAX_BYTES [slot_bytes|0] [VERIFY 0|1] [ref_lib|-] [CHUNK]
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -125,14 +133,74 @@ static int g_verify;
 static int g_conns;
 static size_t g_msgs;
 static int *g_cfd;
+static size_t g_chunk;                 /* CHUNK: prerendered traffic, bytes per send() (0: off) */
+static pthread_barrier_t g_start;      /* CHUNK: the clients have rendered; the clock starts */
+static uint64_t g_clients_end;         /* when the last client finished sending (ns) */
+static pthread_mutex_t g_end_mu = PTHREAD_MUTEX_INITIALIZER;
 
 struct client_arg {
     int first, count;
 };
 
+static void client_done(void) {
+    const uint64_t t = now_ns();
+    pthread_mutex_lock(&g_end_mu);
+    if (t > g_clients_end) g_clients_end = t;
+    pthread_mutex_unlock(&g_end_mu);
+}
+
+/* every byte of [p, p + n) on fd (blocking socket) */
+static void send_all(int fd, const uint8_t *p, size_t n) {
+    while (n) {
+        const ssize_t r = send(fd, p, n, MSG_NOSIGNAL);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) {
+            perror("client send");
+            exit(4);
+        }
+        p += r;
+        n -= (size_t)r;
+    }
+}
+
+struct wire {
+    uint8_t *p;
+    size_t n, cap, at;
+};
+
+/* append the frames of one message as ws_send_message sends them (masked) */
+static void render(struct wire *w, uint8_t op, const uint8_t *msg, size_t len, size_t frames, const uint8_t key[4]) {
+    const size_t split = len / frames, rem = len % frames;
+    for (size_t f = 0; f < frames; ++f) {
+        const int last = f + 1 == frames;
+        const size_t fl = split + (last ? rem : 0), at = f * split;
+        if (w->cap - w->n < fl + 14) {
+            while (w->cap - w->n < fl + 14) w->cap = w->cap ? 2 * w->cap : 1 << 20;
+            if (!(w->p = realloc(w->p, w->cap))) exit(4);
+        }
+        uint8_t *q = w->p + w->n;
+        *q++ = (uint8_t)((last ? 0x80 : 0) | (f == 0 ? op : WS_OPCODE_CONTINUE));
+        if (fl <= 125) {
+            *q++ = (uint8_t)(0x80 | fl);
+        } else if (fl <= 0xFFFF) {
+            *q++ = 0x80 | 126;
+            *q++ = (uint8_t)(fl >> 8);
+            *q++ = (uint8_t)fl;
+        } else {
+            *q++ = 0x80 | 127;
+            for (int b = 7; b >= 0; --b) *q++ = (uint8_t)((uint64_t)fl >> (8 * b));
+        }
+        memcpy(q, key, 4);
+        q += 4;
+        for (size_t i = 0; i < fl; ++i) q[i] = msg[at + i] ^ key[i & 3];
+        w->n = (size_t)(q + fl - w->p);
+    }
+}
+
 static void *client_main(void *p) {
     struct client_arg *a = p;
     struct peer *peers = calloc((size_t)a->count, sizeof(struct peer));
+    struct wire *wires = g_chunk ? calloc((size_t)a->count, sizeof(struct wire)) : NULL;
     for (int k = 0; k < a->count; ++k) {
         peers[k].tcp.sockfd = g_cfd[a->first + k];
         peers[k].head.tcp_client = &peers[k].tcp;
@@ -148,6 +216,10 @@ static void *client_main(void *p) {
             fill(&s, buf);
             buf[s.len] = 0;   /* a TEXT message is delivered with a NUL appended (src/ws/common.c:342) */
             g_want[c] = msg_hash(g_want[c], s.op, buf, s.len + (s.op == WS_OPCODE_TEXT));
+            if (g_chunk) {
+                render(&wires[k], s.op, buf, s.len, s.frames, key);
+                continue;
+            }
             struct ws_message m;
             ws_build_message(&m, s.op, s.len, buf);
             if (ws_send_message((struct web_client *)&peers[k].head, &m, key, s.frames) != 1) {
@@ -157,6 +229,23 @@ static void *client_main(void *p) {
         }
     }
     free(buf);
+    if (g_chunk) {
+        pthread_barrier_wait(&g_start);   /* rendered: the clock starts */
+        for (size_t left = 1; left;) {
+            left = 0;
+            for (int k = 0; k < a->count; ++k) {
+                struct wire *w = &wires[k];
+                if (w->at == w->n) continue;
+                const size_t n = w->n - w->at < g_chunk ? w->n - w->at : g_chunk;
+                send_all(g_cfd[a->first + k], w->p + w->at, n);
+                w->at += n;
+                left += w->n - w->at;
+            }
+        }
+        for (int k = 0; k < a->count; ++k) free(wires[k].p);
+        free(wires);
+    }
+    client_done();
     free(peers);
     return NULL;
 }
@@ -175,7 +264,8 @@ int main(int argc, char **argv) {
     const size_t slot_bytes = argc > 5 && strtoull(argv[5], NULL, 10) ? (size_t)strtoull(argv[5], NULL, 10)
                                                                      : (size_t)16 << 20;
     g_verify = argc > 6 && atoi(argv[6]);
-    const char *ref_lib = argc > 7 ? argv[7] : "oracle/_ref/libref_ws.so";
+    const char *ref_lib = argc > 7 && strcmp(argv[7], "-") ? argv[7] : "oracle/_ref/libref_ws.so";
+    g_chunk = argc > 8 ? (size_t)strtoull(argv[8], NULL, 10) : 0;
     const int is_hub = !strcmp(leg, "hub"), is_ref = !strcmp(leg, "ref");
     if (!is_hub && !is_ref && strcmp(leg, "cpu")) return 2;
     if (g_conns < 4 || g_conns % 4) {
@@ -240,11 +330,16 @@ int main(int argc, char **argv) {
     uint8_t *want = malloc(g_max + 16);
     pthread_t th[4];
     struct client_arg ca[4];
-    const uint64_t t0 = now_ns();
+    if (g_chunk) pthread_barrier_init(&g_start, NULL, 5);
+    uint64_t t0 = now_ns();
     for (int t = 0; t < 4; ++t) {
         ca[t].first = t * (g_conns / 4);
         ca[t].count = g_conns / 4;
         pthread_create(&th[t], NULL, client_main, &ca[t]);
+    }
+    if (g_chunk) {   /* the clients render first; the clock starts when all have */
+        pthread_barrier_wait(&g_start);
+        t0 = now_ns();
     }
     const size_t total = (size_t)g_conns * g_msgs;
     size_t done = 0, bad = 0;
@@ -318,15 +413,16 @@ int main(int argc, char **argv) {
         netc_ws_hub_destroy(hub);
     }
     const double secs = (double)(t1 - t0) * 1e-9;
+    const double csecs = g_clients_end > t0 ? (double)(g_clients_end - t0) * 1e-9 : 0.0;
     size_t mismatched = 0;
     for (int c = 0; c < g_conns; ++c) mismatched += hash[c] != g_want[c];
     printf("{\"leg\": \"%s\", \"conns\": %d, \"msgs_per_conn\": %zu, \"max_bytes\": %zu, \"messages\": %zu, "
            "\"payload_bytes\": %llu, \"seconds\": %.6f, \"msgs_per_s\": %.1f, \"gib_per_s\": %.4f, \"bad\": %zu, "
-           "\"mismatched\": %zu, \"verified\": %d, "
+           "\"mismatched\": %zu, \"verified\": %d, \"chunk\": %zu, \"clients_seconds\": %.6f, "
            "\"events\": %llu, \"ref_spins\": %llu, \"launches\": %llu, \"frames\": %llu, \"max_conns_per_launch\": %llu, "
            "\"mean_conns_per_launch\": %.2f, \"mean_frames_per_launch\": %.1f, \"conn_hash\": [",
            leg, g_conns, g_msgs, g_max, total, (unsigned long long)bytes, secs, (double)total / secs,
-           (double)bytes / secs / (double)(1ull << 30), bad, mismatched, g_verify, (unsigned long long)events, (unsigned long long)spins,
+           (double)bytes / secs / (double)(1ull << 30), bad, mismatched, g_verify, g_chunk, csecs, (unsigned long long)events, (unsigned long long)spins,
            (unsigned long long)hs.launches, (unsigned long long)hs.frames, (unsigned long long)hs.max_connections,
            hs.launches ? (double)hs.connection_slots / (double)hs.launches : 0.0,
            hs.launches ? (double)hs.frames / (double)hs.launches : 0.0);

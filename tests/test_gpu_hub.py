@@ -146,17 +146,19 @@ def test_hub_attach_rules():
 
 
 @pytest.mark.timeout(300)
-def test_hub_server_256_connections_equals_cpu_parser():
+@pytest.mark.parametrize("chunk", ["0", "65536"])
+def test_hub_server_256_connections_equals_cpu_parser(chunk):
     """tests/drivers/ws_hub_server.c: 256 TCP connections, 200 messages each (0-1024 B, 1-3
     fragments, PINGs), netc's loop; every message regenerated and compared; the per-connection
     results of the hub equal those of libnetc's CPU ws_parse_frame and of the reference's own
-    parser (when oracle/_ref is present)"""
+    parser (when oracle/_ref is present).  chunk 65536: the clients' frames rendered in memory
+    beforehand and sent 64 KiB per send() (many messages per read on the server side)"""
     assert os.path.exists(EXE), "tests/bin/ws_hub_server missing: run make"
     out = {}
     legs = ["hub", "cpu"] + (["ref"] if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libref_ws.so")) else [])
     for leg in legs:
-        r = subprocess.run([EXE, leg, "256", "200", "1024", "0", "1"], capture_output=True, text=True, timeout=240,
-                           cwd=ROOT)
+        r = subprocess.run([EXE, leg, "256", "200", "1024", "0", "1", "-", chunk], capture_output=True, text=True,
+                           timeout=240, cwd=ROOT)
         assert r.returncode == 0, f"{leg}: rc {r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}"
         out[leg] = json.loads(r.stdout.strip().splitlines()[-1])
         assert out[leg]["bad"] == 0 and out[leg]["mismatched"] == 0 and out[leg]["verified"] == 1

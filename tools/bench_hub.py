@@ -8,7 +8,12 @@ readable socket per loop iteration (netc's loop, reference src/tcp/server.c:30-7
 src/web/server.c:69-98).  Per-connection delivery is checked by hash against what each client
 sent.  One JSON line per run (stdout and --out).
 
-    python tools/bench_hub.py [--configs 256x400x1024,1024x100x1024,64x200x16384] [--out FILE]
+--chunks 0,65536 adds prerendered client traffic (CHUNK bytes per send(), rendered before the clock
+starts; tests/drivers/ws_hub_server.c): with 0 the 4 client threads run ws_send_message per message
+inside the timed region, and "clients_seconds" in each line shows whether they, not the server,
+set the pace.
+
+    python tools/bench_hub.py [--configs 256x400x1024,1024x100x1024,64x200x16384] [--chunks 0] [--out FILE]
 """
 
 import argparse
@@ -26,6 +31,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="256x400x1024,1024x100x1024,64x200x16384,16x100x262144")
     ap.add_argument("--legs", default="hub,cpu,ref")
+    ap.add_argument("--chunks", default="0,65536", help="client send chunk sizes (0: live ws_send_message)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     if not os.path.exists(EXE):
@@ -33,10 +39,11 @@ def main():
     out = open(args.out, "a") if args.out else None
     for cfg in args.configs.split(","):
         conns, msgs, mx = cfg.split("x")
-        for leg in args.legs.split(","):
+        for chunk, leg in [(c, l) for c in args.chunks.split(",") for l in args.legs.split(",")]:
             if leg == "ref" and not os.path.exists(REF):
                 continue
-            r = subprocess.run([EXE, leg, conns, msgs, mx], capture_output=True, text=True, timeout=600, cwd=ROOT)
+            r = subprocess.run([EXE, leg, conns, msgs, mx, "0", "0", "-", chunk], capture_output=True, text=True,
+                               timeout=600, cwd=ROOT)
             if r.returncode:
                 sys.exit(f"{cfg} {leg}: rc {r.returncode}: {r.stderr[-2000:]}")
             rec = json.loads(r.stdout.strip().splitlines()[-1])
