@@ -86,9 +86,11 @@ int netc_gpu_encode_frames(int device, void *d_wire, size_t wire_capacity, uint6
  *
  * The promise is checked for every frame.  If a frame breaks it, d_wire_offsets[nframes] reads
  * NETC_WS_WIRE_INVALID once the call's work is done and the wire bytes are unspecified; no byte
- * outside the wire bound is written.  A batch that takes the general path (one averaging under 80
- * payload bytes per frame, or one the measurement knobs send to another path) runs the scan and
- * is exact whatever its frames are.  Other arguments and errors as netc_gpu_encode_frames.
+ * outside the wire bound is written.  A batch that takes the general path -- one averaging under
+ * 80 payload bytes per frame, one whose wire bound exceeds 256 MiB (there the scan costs less
+ * than the one-launch form saves), or one the measurement knobs send to another path -- runs the
+ * scan and is exact whatever its frames are.  Other arguments and errors as
+ * netc_gpu_encode_frames.
  */
 int netc_gpu_encode_frames_class(int device, void *d_wire, size_t wire_capacity, uint64_t *d_wire_offsets,
                                  const void *d_payload, size_t total_bytes, const uint64_t *d_frame_offsets,

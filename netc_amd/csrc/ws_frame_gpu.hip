@@ -1603,9 +1603,13 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     a.fix_tail = fix_tail ? 1u : 0u;
     // One length class (ext_class 0, 2 or 8: netc_gpu_encode_frames_class): on the default path
     // the wire offsets are affine and the trailing fixup blocks write them -- no scan launch, whose
-    // ~5 us at config 2 the assembly waited for.  The other paths run the scan, which needs no
-    // class and is exact whatever the frames are.
-    a.affine = ext_class >= 0 && fix_blocks ? 1u : 0u;
+    // ~5 us at config 2 the assembly waited for.  Up to 256 MiB of wire: the affine form costs the
+    // assembly itself a little per chunk (config 2 kernel 35.3 against 33.7 us, the step 35.3
+    // against 38.4), and at config 4's 1 GiB more than the scan it saves (424.4-427.7 against
+    // 419.2-419.6 us a step; profiles/r05_kernels/encode_class.json).  The other paths run the scan,
+    // which needs no class and is exact whatever the frames are.
+    const bool one_launch_ok = wire_bound <= (256ull << 20);
+    a.affine = ext_class >= 0 && fix_blocks && one_launch_ok ? 1u : 0u;
     a.ext = ext_class >= 0 ? (uint32_t)ext_class : 0u;
     a.hstride = 2u + (masked ? 4u : 0u) + a.ext;
     a.off0 = 0;

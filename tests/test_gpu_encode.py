@@ -371,6 +371,20 @@ def test_one_class_on_the_general_paths(torch_cuda, gpu_knob, path):
     run_encode(torch_cuda, payload, off, keys, wire_shift=3, length_class=nm.NETC_WS_CLASS_16BIT)
 
 
+def test_one_class_above_256_mib_takes_the_scan(torch_cuda):
+    # a wire bound over 256 MiB: the scan runs (it costs less there than the one-launch form
+    # saves), so the result is exact even with a frame outside the promised class
+    rng = np.random.default_rng(71)
+    n = 262144
+    sizes = np.full(n, 1030)
+    sizes[1000] = 99
+    off = frames_from_sizes(sizes)
+    assert nm.wire_bound(int(off[-1]), n, True) > (256 << 20)
+    payload = _payload(rng, int(off[-1]))
+    keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    run_encode(torch_cuda, payload, off, keys, length_class=nm.NETC_WS_CLASS_16BIT)
+
+
 def _broken(torch, sizes, cls, masked=True, wire_shift=0):
     rng = np.random.default_rng(len(sizes) + cls)
     off = frames_from_sizes(sizes)
