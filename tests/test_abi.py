@@ -69,6 +69,29 @@ def test_libraries_load_without_gpu():
     assert nm.device_count() >= 0
 
 
+def test_length_class_and_wire_size_helpers():
+    """host helpers around netc_gpu_encode_frames_class: the one length class of a batch (or None)
+    and the exact wire size it implies -- affine in the offsets when the class is one"""
+    import numpy as np
+    from netc_amd import mask as nm
+
+    def offs(sizes, start=0):
+        return np.concatenate([[start], start + np.cumsum(sizes)]).astype(np.uint64)
+
+    assert nm.length_class(offs([0, 5, 125])) == nm.NETC_WS_CLASS_7BIT
+    assert nm.length_class(offs([126, 1024, 65535])) == nm.NETC_WS_CLASS_16BIT
+    assert nm.length_class(offs([65536, 1 << 20])) == nm.NETC_WS_CLASS_64BIT
+    assert nm.length_class(offs([125, 126])) is None
+    assert nm.length_class(offs([65535, 65536])) is None
+    assert nm.length_class(offs([])) is None
+    for sizes, cls in (([7] * 9, 0), ([1024] * 65, 2), ([70000, 65536], 8)):
+        for masked in (True, False):
+            o = offs(sizes, start=13)
+            n = len(sizes)
+            affine = int(o[-1] - o[0]) + n * (2 + cls + (4 if masked else 0))
+            assert nm.wire_size(o, masked) == affine
+
+
 LAYOUT_C = r"""
 #include <stdio.h>
 #include <stddef.h>
