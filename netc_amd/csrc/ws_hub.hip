@@ -91,6 +91,8 @@ struct HubConn {
     uint64_t last_gen = 0;               // the slot filling this connection last added frames to
     int err = 0;                         // sticky (delivered)
     int pending = 0;                     // an error found behind frames not yet delivered
+    bool carry_frames = false;           // the carry may hold complete frames (a full frame table
+                                         // stopped the walk): walked before new bytes, hostage kept
     bool closed = false;
     uint8_t* scratch = nullptr;
 };
@@ -343,7 +345,11 @@ long take(netc_ws_hub* h, HubConn& c, uint64_t* frames) {
     if (room > kPeek) room = kPeek;
     const int held = (int)(c.in_pos - c.sock_pos);
     if (held > 1) return api_fail(NETC_GPU_ERUNTIME, "hub: %d bytes held in socket %d", held, c.fd);
+    // a carry with complete frames is walked even when the socket has nothing new, and the
+    // hostage stays: the caller must come back for those frames' messages
+    const bool stale = c.carry_frames;
     ssize_t r;
+    bool eof = false;
     for (int pass = 0;; ++pass) {
         uint8_t skip[1];
         const int k = (int)(c.in_pos - c.sock_pos);
@@ -355,30 +361,39 @@ long take(netc_ws_hub* h, HubConn& c, uint64_t* frames) {
         do r = recvmsg(c.fd, &mh, MSG_PEEK | MSG_DONTWAIT);   // (never blocks the loop, blocking socket or not)
         while (r < 0 && errno == EINTR);
         if (r > 0 && r <= k) {   // only the hostage: release it and look once more
-            if (pass == 0 && held) {
+            if (pass == 0 && held && !stale) {
                 if (int e = sock_consume(c, c.in_pos)) return e;
                 continue;
             }
-            return 0;
+            r = 0;
+            break;
         }
         if (r > 0) r -= k;
+        else if (r == 0) eof = true;
         break;
     }
     if (r < 0) {
-        if (errno == EAGAIN || errno == EWOULDBLOCK) return 0;
-        const int saved = errno;
-        api_fail(NETC_WS_INGEST_ERECV, "hub: recv on socket %d: %s", c.fd, strerror(saved));
-        netc_errno_reason = kBadRecv;
-        errno = saved;
-        return NETC_WS_INGEST_ERECV;
+        if (errno != EAGAIN && errno != EWOULDBLOCK) {
+            const int saved = errno;
+            api_fail(NETC_WS_INGEST_ERECV, "hub: recv on socket %d: %s", c.fd, strerror(saved));
+            netc_errno_reason = kBadRecv;
+            errno = saved;
+            return NETC_WS_INGEST_ERECV;
+        }
+        r = 0;
     }
-    if (r == 0) return api_fail(NETC_WS_INGEST_CLOSED, "hub: socket %d: the peer closed the connection", c.fd);
+    if (r == 0 && !stale) {
+        if (eof) return api_fail(NETC_WS_INGEST_CLOSED, "hub: socket %d: the peer closed the connection", c.fd);
+        return 0;
+    }
     c.in_pos += (uint64_t)r;
     const uint64_t len = c.carry_len + (uint64_t)r;
     uint64_t cut = 0;
     int err = 0;
-    const uint64_t n = walk(h, s, dst, seg, len, h->max_frames - s.nframes, &cut, &err);
+    const uint64_t cap = h->max_frames - s.nframes;
+    const uint64_t n = walk(h, s, dst, seg, len, cap, &cut, &err);
     if (err) c.pending = err;
+    c.carry_frames = !err && n == cap && cut < len;   // a full table: complete frames may follow
     if (n) {
         c.ranges.push_back(Range{cur, s.gen, s.nframes, n, 0});
         s.nframes += n;
@@ -394,10 +409,11 @@ long take(netc_ws_hub* h, HubConn& c, uint64_t* frames) {
     if (tail && !grow(c.carry, c.carry_cap, tail)) return api_fail(NETC_GPU_ENOMEM, "hub: carry buffer");
     if (tail) memmove(c.carry, dst + cut, tail);
     c.carry_len = tail;
-    if (int e = sock_consume(c, c.in_pos - 1)) return e;
+    if (c.in_pos > c.sock_pos + 1)
+        if (int e = sock_consume(c, c.in_pos - 1)) return e;
     *frames = n;
-    if (s.fill + 4096 > h->slot_bytes) (void)submit(h);   // full: on its way now (errors resurface)
-    return r;
+    if (s.fill + 4096 > h->slot_bytes || c.carry_frames) (void)submit(h);   // full: on its way now (errors resurface)
+    return r > 0 ? r : (n > 0 || c.carry_frames ? 1 : 0);   // > 0: progress (new bytes or carried frames)
 }
 
 bool m_append(HubConn& c, const uint8_t* p, size_t n) {
@@ -489,9 +505,9 @@ int hub_route(void* ctx, int sockfd, struct ws_frame_parsing_state* state, size_
         struct ws_message m;
         int r = deliver(h, c, &m, max_payload_length);
         if (r == 0) {
-            // nothing of it left -- no frames, no error still to report (its bytes are in the
-            // socket as far as the caller is concerned): no hostage
-            if (c.ranges.empty() && !c.pending) (void)sock_consume(c, c.in_pos);
+            // nothing of it left -- no frames, no error still to report, no carried frames (its
+            // bytes are in the socket as far as the caller is concerned): no hostage
+            if (c.ranges.empty() && !c.pending && !c.carry_frames) (void)sock_consume(c, c.in_pos);
             state->message = m;
             return 0;
         }
@@ -513,7 +529,7 @@ int hub_route(void* ctx, int sockfd, struct ws_frame_parsing_state* state, size_
             continue;
         }
         if (n == 0) {
-            if (c.ranges.empty() && !c.pending) (void)sock_consume(c, c.in_pos);
+            if (c.ranges.empty() && !c.pending && !c.carry_frames) (void)sock_consume(c, c.in_pos);
             return 1;
         }
         if (n == NETC_WS_INGEST_CLOSED) {

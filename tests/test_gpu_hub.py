@@ -274,6 +274,18 @@ def test_hub_detach_with_frames_pending():
         b.close()
 
 
+@pytest.mark.timeout(120)
+def test_hub_table_fills_before_the_bytes():
+    """the flood of empty frames (test_gpu_route.flood_of_empty_frames) on a hub with the smallest
+    slot: one peek holds far more frames than a slot's frame table, so each take records what
+    fits and carries the rest -- complete frames included -- walking them before new bytes and
+    keeping the hostage meanwhile (round 5: without that, the carried frames were stranded)"""
+    with make_hub(slot_bytes=65536 + 14 + 4096, nslots=2, max_frame_bytes=65536) as hub:
+        G.flood_of_empty_frames(lambda: hub)
+        st = hub.stats()
+    assert st["frames"] >= 30000 and st["launches"] > 10, st
+
+
 @pytest.mark.timeout(60)
 def test_hub_blocking_socket_never_stalls_the_loop():
     with make_hub(slot_bytes=1 << 20, nslots=2) as hub:

@@ -207,6 +207,38 @@ def test_trickle_one_byte_at_a_time_then_close():
     assert got == expected(msgs)
 
 
+def flood_of_empty_frames(make_ctx, n=30000):
+    """a flood of empty masked frames (6 B each) with one large message between: far more frames
+    per read than a small slot's frame table holds -- every message arrives, in order, under
+    netc's once-per-event loop"""
+    lib = _lib.host()
+    c, s = tcp_pair()
+    s.setblocking(False)
+    ep = Endpoint(s)
+    msgs = [(BINARY if i % 3 else TEXT, b"", 1, [bytes([i & 0xFF, 1, 2, 3])]) for i in range(n)]
+    msgs[n // 4] = (BINARY, bytes(range(256)) * 200, 2, [b"\x11\x22\x33\x44"] * 2)
+    wire = wire_of(msgs)
+    ctx = make_ctx()
+    ctx.attach(s.fileno())
+    try:
+        th = threading.Thread(target=lambda: c.sendall(wire))
+        th.start()
+        got = once_per_event(s, ep, lib, len(msgs), 1 << 20)
+        th.join()
+    finally:
+        ctx.detach(s.fileno())
+        c.close()
+        s.close()
+    assert got == expected(msgs)
+    return ctx
+
+
+@pytest.mark.timeout(120)
+def test_flood_of_empty_frames():
+    with ni.Ingest(slot_bytes=1 << 16, nslots=3, max_frame_bytes=65536) as ing:
+        flood_of_empty_frames(lambda: ing)
+
+
 def blocking_socket_case(attach, detach):
     """A socket left BLOCKING (netc makes its sockets non-blocking, but a caller may not): a call
     that finds only part of a frame must return 1 at once -- the route releases its hostage and

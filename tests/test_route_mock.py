@@ -167,6 +167,14 @@ def test_blocking_socket_never_stalls_the_loop(mock):
     G.test_blocking_socket_never_stalls_the_loop()
 
 
+def test_flood_of_empty_frames(mock):
+    G.test_flood_of_empty_frames()
+
+
+def test_hub_table_fills_before_the_bytes(hub_mock):
+    hub_mock.test_hub_table_fills_before_the_bytes()
+
+
 def test_hub_blocking_socket_never_stalls_the_loop(hub_mock):
     hub_mock.test_hub_blocking_socket_never_stalls_the_loop()
 
