@@ -286,6 +286,12 @@ def test_hub_table_fills_before_the_bytes():
     assert st["frames"] >= 30000 and st["launches"] > 10, st
 
 
+@pytest.mark.timeout(120)
+def test_hub_client_side_unmasked_frames():
+    with make_hub(slot_bytes=1 << 20, nslots=3, max_frame_bytes=1 << 17) as hub:
+        G.client_side_case(lambda: hub)
+
+
 @pytest.mark.timeout(60)
 def test_hub_blocking_socket_never_stalls_the_loop():
     with make_hub(slot_bytes=1 << 20, nslots=2) as hub:

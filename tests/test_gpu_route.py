@@ -91,6 +91,22 @@ def wire_of(msgs):
     return bytes(w)
 
 
+def wire_of_unmasked(msgs):
+    """the same frames unmasked, as netc's server sends them to its clients (ws_send_message with
+    no key, src/ws/common.c:40; src/web/client.c:25 parses them)"""
+    w = bytearray()
+    for op, p, nf, _ in msgs:
+        split, rem = divmod(len(p), nf)
+        off = [0]
+        for i in range(nf):
+            off.append(off[-1] + split + (rem if i + 1 == nf else 0))
+        h0 = [(0x80 if i + 1 == nf else 0) | (op if i == 0 else 0) for i in range(nf)]
+        wire, _ = orc.encode_batch(np.frombuffer(p, dtype=np.uint8), np.array(off, dtype=np.uint64), None,
+                                   np.array(h0, dtype=np.uint8), False)
+        w += wire.tobytes()
+    return bytes(w)
+
+
 def expected(msgs):
     return [(op, p + (b"\0" if op == TEXT else b"")) for op, p, _, _ in msgs]
 
@@ -237,6 +253,36 @@ def flood_of_empty_frames(make_ctx, n=30000):
 def test_flood_of_empty_frames():
     with ni.Ingest(slot_bytes=1 << 16, nslots=3, max_frame_bytes=65536) as ing:
         flood_of_empty_frames(lambda: ing)
+
+
+def client_side_case(make_ctx):
+    """netc's client side (src/web/client.c:25): a non-strict ring or hub on the client's socket
+    receives the server's UNMASKED frames; every message arrives as sent"""
+    lib = _lib.host()
+    rng = np.random.default_rng(23)
+    msgs = script(rng, 120)
+    wire = wire_of_unmasked(msgs)
+    c, s = tcp_pair()
+    s.setblocking(False)
+    ep = Endpoint(s)
+    ctx = make_ctx()
+    ctx.attach(s.fileno())
+    try:
+        th = threading.Thread(target=lambda: c.sendall(wire))
+        th.start()
+        got = once_per_event(s, ep, lib, len(msgs), 1 << 20)
+        th.join()
+    finally:
+        ctx.detach(s.fileno())
+        c.close()
+        s.close()
+    assert got == expected(msgs)
+
+
+@pytest.mark.timeout(120)
+def test_client_side_unmasked_frames():
+    with ni.Ingest(slot_bytes=1 << 20, nslots=3, max_frame_bytes=1 << 17, strict=False) as ing:
+        client_side_case(lambda: ing)
 
 
 def blocking_socket_case(attach, detach):

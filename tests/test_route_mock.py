@@ -171,6 +171,14 @@ def test_flood_of_empty_frames(mock):
     G.test_flood_of_empty_frames()
 
 
+def test_client_side_unmasked_frames(mock):
+    G.test_client_side_unmasked_frames()
+
+
+def test_hub_client_side_unmasked_frames(hub_mock):
+    hub_mock.test_hub_client_side_unmasked_frames()
+
+
 def test_hub_table_fills_before_the_bytes(hub_mock):
     hub_mock.test_hub_table_fills_before_the_bytes()
 
