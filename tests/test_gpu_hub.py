@@ -26,6 +26,7 @@ import select
 import socket
 import subprocess
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -284,6 +285,68 @@ def test_hub_table_fills_before_the_bytes():
         G.flood_of_empty_frames(lambda: hub)
         st = hub.stats()
     assert st["frames"] >= 30000 and st["launches"] > 10, st
+
+
+@pytest.mark.timeout(120)
+def test_hub_many_connections_trickle_then_close():
+    """8 connections whose peers send 1-7 bytes at a time with pauses (headers, keys and payloads
+    cut anywhere, the pieces of different connections interleaved), then close: per connection
+    every message in order, then WS_FRAME_PARSE_ERROR_RECV (src/ws/common.c:151-154)"""
+    lib = _lib.host()
+    rng = np.random.default_rng(29)
+    nconn = 8
+    pairs = [G.tcp_pair() for _ in range(nconn)]
+    msgs = [G.script(rng, 10) for _ in range(nconn)]
+    wires = [G.wire_of(m) for m in msgs]
+
+    def trickle():
+        pos = [0] * nconn
+        while any(pos[c] < len(wires[c]) for c in range(nconn)):
+            for c in range(nconn):
+                if pos[c] >= len(wires[c]):
+                    continue
+                n = int(rng.integers(1, 8)) if pos[c] < 300 else 40000
+                pairs[c][0].sendall(wires[c][pos[c]:pos[c] + n])
+                pos[c] += n
+                if pos[c] >= len(wires[c]):
+                    pairs[c][0].shutdown(socket.SHUT_WR)
+            time.sleep(0.001)
+
+    got = [[] for _ in range(nconn)]
+    codes = [None] * nconn
+    with make_hub(slot_bytes=1 << 20, nslots=4, max_frame_bytes=1 << 17) as hub:
+        socks = [s for _, s in pairs]
+        eps, sts = [], []
+        for s in socks:
+            s.setblocking(False)
+            hub.attach(s.fileno())
+            eps.append(Endpoint(s))
+            sts.append(ParseState())
+        index = {s.fileno(): c for c, s in enumerate(socks)}
+        th = threading.Thread(target=trickle)
+        th.start()
+        try:
+            while any(x is None for x in codes):
+                live = [s for c, s in enumerate(socks) if codes[c] is None]
+                ready, _, _ = select.select(live, [], [], 10)
+                assert ready, f"stranded: {[len(g) for g in got]} delivered, codes {codes}"
+                for s in ready:
+                    c = index[s.fileno()]
+                    rc = lib.ws_parse_frame(ctypes.byref(eps[c].client), ctypes.byref(sts[c]), 1 << 20)
+                    if rc == 0:
+                        got[c].append(_take(sts[c]))
+                    elif rc != 1:
+                        codes[c] = rc
+            th.join()
+        finally:
+            for s in socks:
+                hub.detach(s.fileno())
+    for a, b in pairs:
+        a.close()
+        b.close()
+    for c in range(nconn):
+        assert got[c] == G.expected(msgs[c]), c
+        assert codes[c] == ni_codes.RECV, codes
 
 
 @pytest.mark.timeout(120)

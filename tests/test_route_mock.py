@@ -179,6 +179,10 @@ def test_hub_client_side_unmasked_frames(hub_mock):
     hub_mock.test_hub_client_side_unmasked_frames()
 
 
+def test_hub_many_connections_trickle_then_close(hub_mock):
+    hub_mock.test_hub_many_connections_trickle_then_close()
+
+
 def test_hub_table_fills_before_the_bytes(hub_mock):
     hub_mock.test_hub_table_fills_before_the_bytes()
 
