@@ -122,6 +122,9 @@ long netc_ws_egress_flush(struct netc_ws_egress *eg, int fd);
  * was created with NETC_WS_EGRESS_DEFER -- submits it and sends it before
  * returning, with ws_send_message's contract: 1 once sent, else the failing send()
  * result (-1; netc_errno_reason BADSEND, or the ring's code in netc_gpu_strerror).
+ * A message larger than the ring's slot_bytes (or in more frames than a slot
+ * holds) is refused with -1 and NETC_WS_EGRESS_TOO_BIG in netc_gpu_strerror:
+ * size the ring's slots for the connection's largest message.
  * Other sockets keep the CPU path.  One ring serves one connection: attaching a ring
  * that already serves another open socket, or one holding queued messages, fails
  * with NETC_GPU_EINVAL, and the route refuses a call for any other socket.  Detach

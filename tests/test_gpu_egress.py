@@ -379,6 +379,38 @@ def test_detach_flushes_deferred_messages():
     assert got == cpu
 
 
+def test_send_route_refuses_a_message_over_the_slot():
+    """ws_send_message on an attached socket with a message larger than the ring's slot: -1 and
+    NETC_WS_EGRESS_TOO_BIG in the error text, nothing of it on the socket, and the next messages
+    go out as before (include/ws/egress.h: size the slots for the largest message)"""
+    from netc_amd import mask as nm
+    lib = _lib.host()
+    a, b = pair()
+    rd = Reader(b)
+    ep = Endpoint(a)
+    small = [(b"before", 1, b"\x01\x02\x03\x04", 1)]
+    after = [(b"after" * 100, 2, b"\x05\x06\x07\x08", 2)]
+    big = bytes(100000)
+    with ne.Egress(slot_bytes=1 << 16, nslots=2) as eg:
+        eg.attach(a.fileno())
+        try:
+            send_through(lib, ep, small)
+            buf = ctypes.create_string_buffer(big, len(big) + 1)
+            m = WsMessage()
+            lib.ws_build_message(ctypes.byref(m), 2, len(big), buf)
+            kb = (ctypes.c_uint8 * 4)(9, 9, 9, 9)
+            assert lib.ws_send_message(ctypes.byref(ep.client), ctypes.byref(m), kb, 1) == -1
+            assert b"exceeds a slot" in nm._lib.gpu().netc_gpu_strerror()
+            send_through(lib, ep, after)
+        finally:
+            eg.detach(a.fileno())
+    a.shutdown(socket.SHUT_WR)
+    got = rd.join()
+    a.close()
+    b.close()
+    assert got == b"".join(send_wire(p, op, key, nf)[1] for p, op, key, nf in small + after)
+
+
 def test_egress_injected_fault_reports_and_recovers():
     """a failing submission (NETC_GPU_KNOB_INJECT_FAULT) is reported as NETC_GPU_ELAUNCH and leaves
     the slot's queued messages intact: the retried submission sends exactly the oracle's wire
