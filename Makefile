@@ -19,9 +19,9 @@ HIPFLAGS   ?= -O3 -g -fPIC -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-r
 HOST_SRCS  := $(wildcard netc_amd/csrc/host/*.c)
 HOST_HDRS  := $(wildcard include/*.h include/*/*.h)
 GPU_SRCS   := netc_amd/csrc/ws_mask_gpu.hip netc_amd/csrc/ws_frame_gpu.hip netc_amd/csrc/ws_scan_gpu.hip netc_amd/csrc/ws_ingest.hip netc_amd/csrc/ws_egress.hip \
-              netc_amd/csrc/ws_mask_api.hip netc_amd/csrc/ws_hub.hip
+              netc_amd/csrc/ws_mask_api.hip netc_amd/csrc/ws_hub.hip netc_amd/csrc/ws_egress_hub.hip
 GPU_HDRS   := netc_amd/csrc/ws_mask_gpu.h netc_amd/csrc/gpu_util.h include/ws/mask.h include/ws/frame.h include/ws/ingest.h \
-              include/ws/route.h include/ws/common.h include/ws/egress.h include/ws/hub.h
+              include/ws/route.h include/ws/common.h include/ws/egress.h include/ws/hub.h include/ws/egress_hub.h
 
 .PHONY: all host gpu oracle diag clean asan mock
 all: host gpu oracle mock
@@ -71,10 +71,10 @@ tests/bin/ws_route_bench: tests/drivers/ws_route_bench.c $(LIBDIR)/libnetc_ws_gp
 # TEST ONLY: the ring's host code (ws_ingest.hip) over a host-memory mock of the HIP runtime
 # (tests/mockhip), so tests/test_route_mock.py drives the ingest ring and the ws_parse_frame route
 # on a machine without a GPU.  Never loaded by the product.
-tests/bin/libnetc_ingest_mock.so: netc_amd/csrc/ws_ingest.hip netc_amd/csrc/ws_hub.hip tests/mockhip/mock_gpu.cc tests/mockhip/hip/hip_runtime.h \
+tests/bin/libnetc_ingest_mock.so: netc_amd/csrc/ws_ingest.hip netc_amd/csrc/ws_hub.hip netc_amd/csrc/ws_egress_hub.hip tests/mockhip/mock_gpu.cc tests/mockhip/hip/hip_runtime.h \
                                   netc_amd/csrc/ws_mask_gpu.h $(LIBDIR)/libnetc.so $(HOST_HDRS)
 	@mkdir -p tests/bin
-	g++ -O1 -g -std=c++17 -fPIC -shared -Wall -Wno-unused-result -Itests/mockhip -x c++ netc_amd/csrc/ws_ingest.hip netc_amd/csrc/ws_hub.hip \
+	g++ -O1 -g -std=c++17 -fPIC -shared -Wall -Wno-unused-result -Itests/mockhip -x c++ netc_amd/csrc/ws_ingest.hip netc_amd/csrc/ws_hub.hip netc_amd/csrc/ws_egress_hub.hip \
 	    -x none tests/mockhip/mock_gpu.cc -L$(LIBDIR) -lnetc -Wl,-Bsymbolic -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -o $@
 
 # many connections on one event loop, one GPU hub (tests/test_gpu_hub.py, tools/bench_hub.py)

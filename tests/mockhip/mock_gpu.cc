@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
 
 #include "../../netc_amd/csrc/ws_mask_gpu.h"
 extern "C" {
@@ -44,6 +45,44 @@ hipError_t launch_unmask_scanned(uint8_t* wire, uint64_t, const uint64_t* hdr, c
     }
     return hipSuccess;
 }
+// the frame assembly (include/ws/frame.h, netc_gpu_encode_frames): each frame's header, key and
+// masked payload back to back, frame by frame (src/ws/common.c:55-125 without B1/B2); with a
+// length class, a frame outside it sets wo[n] to UINT64_MAX as the kernel's check does
+hipError_t launch_encode_frames(uint8_t* wire, uint64_t, const uint8_t* src, uint64_t, const uint64_t* off,
+                                const uint32_t* keys, const uint8_t* b0, uint64_t n, bool masked, uint64_t* wo,
+                                hipStream_t, const LaunchCfg&, int ext_class) {
+    uint64_t w = 0;
+    bool broken = false;
+    for (uint64_t k = 0; k < n; ++k) {
+        const uint64_t len = off[k + 1] - off[k];
+        const int ext = len <= 125 ? 0 : (len <= 0xFFFF ? 2 : 8);
+        broken |= ext_class >= 0 && ext != ext_class;
+        wo[k] = w;
+        uint8_t* p = wire + w;
+        *p++ = b0 ? b0[k] : 0x82;
+        if (ext == 0) {
+            *p++ = (uint8_t)((masked ? 0x80 : 0) | len);
+        } else if (ext == 2) {
+            *p++ = (uint8_t)((masked ? 0x80 : 0) | 126);
+            *p++ = (uint8_t)(len >> 8);
+            *p++ = (uint8_t)len;
+        } else {
+            *p++ = (uint8_t)((masked ? 0x80 : 0) | 127);
+            for (int b = 7; b >= 0; --b) *p++ = (uint8_t)(len >> (8 * b));
+        }
+        uint8_t key[4] = {0, 0, 0, 0};
+        if (masked) {
+            memcpy(key, &keys[k], 4);
+            memcpy(p, key, 4);
+            p += 4;
+        }
+        for (uint64_t i = 0; i < len; ++i) p[i] = src[off[k] + i] ^ key[i & 3];
+        w = (uint64_t)(p + len - wire);
+    }
+    wo[n] = broken ? ~0ull : w;
+    return hipSuccess;
+}
+int release_enc_scratch(int, hipStream_t) { return 0; }
 int api_fail(int code, const char* fmt, ...) {
     va_list ap;
     va_start(ap, fmt);

@@ -1,0 +1,223 @@
+"""One GPU send ring shared by many connections (include/ws/egress_hub.h): the send side of the hub.
+
+netc's server answers its clients from one event loop; each ws_send_message (reference
+src/ws/common.c:36-131) frames, masks and send()s one message.  With every socket attached to an
+egress hub, the messages of all connections share the hub's slots: one frame-assembly launch per
+slot, then one sendmsg() per connection per slot.  Checked here:
+
+  * per connection, the bytes that arrive are exactly the frames of what it sent, in order --
+    the oracle's wire (oracle_encode_batch: the reference's send path with B1/B2 fixed, pinned by
+    the golden send vectors in tests/test_oracle.py; tests/test_gpu_egress.py pins libnetc's CPU
+    ws_send_message to the same bytes), masked and unmasked connections mixed, 1-3 fragments,
+    sizes across the 7-, 16- and 64-bit length forms;
+  * launches span messages of many connections (the hub's counters);
+  * detach sends what was queued, and the socket then takes the CPU path;
+  * a peer that went away fails only its own connection: its next ws_send_message returns -1;
+  * a message larger than a slot is refused, and nothing of it is sent.
+
+tests/test_route_mock.py runs these on the CPU, over the mock HIP runtime.
+"""
+
+import ctypes
+import socket
+import threading
+
+import numpy as np
+import pytest
+
+from netc_amd import _lib
+from netc_amd import egress as ne
+from netc_amd import hub as nh
+from netc_amd.mask import NETC_GPU_EINVAL, NetcGpuError
+from tests import test_gpu_route as G
+from tests.wsutil import Endpoint, WsMessage, pair
+
+pytestmark = pytest.mark.gpu
+HUB_LIB = None   # the library holding the hub (None: libnetc_ws_gpu.so; the CPU tests set the mock)
+
+
+def make(**kw):
+    return nh.EgressHub(lib=HUB_LIB, **kw)
+
+
+class Reader:
+    def __init__(self, sock):
+        self.sock, self.out = sock, bytearray()
+        self.th = threading.Thread(target=self.run)
+        self.th.start()
+
+    def run(self):
+        while True:
+            try:
+                d = self.sock.recv(1 << 20)
+            except OSError:
+                break
+            if not d:
+                break
+            self.out.extend(d)
+
+    def join(self):
+        self.th.join()
+        return bytes(self.out)
+
+
+def send(lib, ep, op, payload, key, nf):
+    buf = ctypes.create_string_buffer(bytes(payload), len(payload) + 1)
+    m = WsMessage()
+    lib.ws_build_message(ctypes.byref(m), op, len(payload), buf)
+    kb = (ctypes.c_uint8 * 4)(*key) if key is not None else None
+    return lib.ws_send_message(ctypes.byref(ep.client), ctypes.byref(m), kb, nf)
+
+
+def wire(msgs):
+    """the frames of (op, payload, frames, key or None) messages, as ws_send_message sends them"""
+    out = b""
+    for op, p, nf, key in msgs:
+        one = [(op, p, nf, [key] * nf)]
+        out += G.wire_of(one) if key is not None else G.wire_of_unmasked(one)
+    return out
+
+
+def message(rng, big=False):
+    sizes = [0, 1, 17, 125, 126, 700, 1024, 3000] + ([65535, 70000] if big else [])
+    op = int(rng.choice([G.TEXT, G.BINARY]))
+    ln = int(rng.choice(sizes))
+    nf = int(rng.choice([1, 1, 2, 3]))
+    return op, rng.integers(0, 256, ln, dtype=np.uint8).tobytes(), nf
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("nconn,rounds,slot", [(64, 30, 1 << 20), (16, 40, 64 << 10), (256, 6, 1 << 20)])
+def test_many_connections_interleaved(nconn, rounds, slot):
+    lib = _lib.host()
+    rng = np.random.default_rng(nconn * 100 + rounds)
+    pairs = [pair() for _ in range(nconn)]
+    readers = [Reader(b) for _, b in pairs]
+    eps = [Endpoint(a) for a, _ in pairs]
+    sent = [[] for _ in range(nconn)]
+    with make(slot_bytes=slot, nslots=3) as hub:
+        for a, _ in pairs:
+            hub.attach(a.fileno())
+        try:
+            for r in range(rounds):
+                for c in rng.permutation(nconn)[: max(1, nconn // 2)]:
+                    op, p, nf = message(rng, big=slot > (64 << 10))
+                    key = rng.integers(0, 256, 4, dtype=np.uint8).tobytes() if c % 3 else None   # a third unmasked
+                    assert send(lib, eps[c], op, p, key, nf) == 1
+                    sent[c].append((op, p, nf, key))
+                if r % 5 == 4:   # the server's loop flushes once per iteration
+                    hub.flush()
+            hub.flush()
+            st = hub.stats()
+        finally:
+            for a, _ in pairs:
+                hub.detach(a.fileno())
+    for a, _ in pairs:
+        a.shutdown(socket.SHUT_WR)
+    got = [rd.join() for rd in readers]
+    for a, b in pairs:
+        a.close()
+        b.close()
+    for c in range(nconn):
+        assert got[c] == wire(sent[c]), f"connection {c}: {len(got[c])} bytes against {len(wire(sent[c]))}"
+    total = sum(len(m) for m in sent)
+    assert st["messages"] == total and st["launches"] < total, st
+    assert st["max_connections"] > 1, st
+    assert st["send_errors"] == 0 and st["connections"] == nconn
+
+
+@pytest.mark.timeout(60)
+def test_detach_sends_what_was_queued_then_cpu_path():
+    lib = _lib.host()
+    rng = np.random.default_rng(5)
+    (a, b), (c, d) = pair(), pair()
+    ra, rc = Reader(b), Reader(d)
+    ea, ec = Endpoint(a), Endpoint(c)
+    msgs_a = [message(rng) + (bytes([1, 2, 3, 4]),) for _ in range(20)]
+    msgs_c = [message(rng) + (bytes([5, 6, 7, 8]),) for _ in range(20)]
+    with make(slot_bytes=1 << 20, nslots=2) as hub:
+        hub.attach(a.fileno())
+        hub.attach(c.fileno())
+        for (op, p, nf, key), (op2, p2, nf2, key2) in zip(msgs_a, msgs_c):
+            assert send(lib, ea, op, p, key, nf) == 1
+            assert send(lib, ec, op2, p2, key2, nf2) == 1
+        hub.detach(a.fileno())   # everything queued goes out first (both connections' bytes)
+        tail = [(G.BINARY, b"cpu path", 1, bytes([9, 9, 9, 9]))]
+        assert send(lib, ea, *[tail[0][i] for i in (0, 1, 3, 2)]) == 1   # not routed any more
+        assert hub.stats()["connections"] == 1
+        hub.detach(c.fileno())
+    a.shutdown(socket.SHUT_WR)
+    c.shutdown(socket.SHUT_WR)
+    got_a, got_c = ra.join(), rc.join()
+    for s in (a, b, c, d):
+        s.close()
+    assert got_a == wire([(op, p, nf, key) for op, p, nf, key in msgs_a] + tail)
+    assert got_c == wire([(op, p, nf, key) for op, p, nf, key in msgs_c])
+
+
+@pytest.mark.timeout(60)
+def test_a_peer_gone_fails_only_its_connection():
+    lib = _lib.host()
+    (a, b), (c, d) = pair(), pair()
+    rc = Reader(d)
+    ea, ec = Endpoint(a), Endpoint(c)
+    b.close()   # a's peer is gone
+    key = bytes([1, 2, 3, 4])
+    with make(slot_bytes=1 << 20, nslots=2) as hub:
+        hub.attach(a.fileno())
+        hub.attach(c.fileno())
+        try:
+            assert send(lib, ea, G.BINARY, b"lost" * 100, key, 1) == 1   # queued: the failure comes at the flush
+            assert send(lib, ec, G.BINARY, b"kept" * 100, key, 1) == 1
+            hub.flush()
+            st = hub.stats()
+            assert st["send_errors"] == 1, st
+            assert send(lib, ea, G.BINARY, b"again", key, 1) == -1       # its send() failed
+            assert send(lib, ec, G.TEXT, b"still fine", key, 2) == 1
+            hub.flush()
+        finally:
+            hub.detach(a.fileno())
+            hub.detach(c.fileno())
+    c.shutdown(socket.SHUT_WR)
+    got = rc.join()
+    a.close()
+    c.close()
+    d.close()
+    assert got == wire([(G.BINARY, b"kept" * 100, 1, key), (G.TEXT, b"still fine", 2, key)])
+
+
+@pytest.mark.timeout(60)
+def test_rules_and_limits():
+    """one send route per socket (a socket an egress ring serves is refused; re-attaching to the
+    same hub is a no-op); a message over the slot is refused with nothing sent"""
+    from netc_amd import mask as nm
+    lib = _lib.host()
+    a, b = pair()
+    rd = Reader(b)
+    ep = Endpoint(a)
+    key = bytes([7, 7, 7, 7])
+    with make(slot_bytes=64 << 10, nslots=2) as hub:
+        if HUB_LIB is None:   # (the egress ring lives in the GPU library only)
+            with ne.Egress(slot_bytes=1 << 16, nslots=2) as eg:
+                eg.attach(a.fileno())
+                with pytest.raises(NetcGpuError) as e:
+                    hub.attach(a.fileno())
+                assert e.value.code == NETC_GPU_EINVAL
+                eg.detach(a.fileno())
+        hub.attach(a.fileno())
+        hub.attach(a.fileno())
+        try:
+            assert send(lib, ep, G.BINARY, b"small", key, 1) == 1
+            assert send(lib, ep, G.BINARY, bytes(100000), key, 1) == -1
+            assert b"exceeds a slot" in hub._lib.netc_gpu_strerror()
+            assert send(lib, ep, G.BINARY, b"after", key, 1) == 1
+        finally:
+            hub.detach(a.fileno())
+    with pytest.raises(NetcGpuError):
+        make(slot_bytes=1024)
+    a.shutdown(socket.SHUT_WR)
+    got = rd.join()
+    a.close()
+    b.close()
+    assert got == wire([(G.BINARY, b"small", 1, key), (G.BINARY, b"after", 1, key)])
+    assert nm.NETC_GPU_EINVAL == NETC_GPU_EINVAL

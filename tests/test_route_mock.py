@@ -193,3 +193,30 @@ def test_hub_blocking_socket_never_stalls_the_loop(hub_mock):
 
 def test_route_errors_after_the_messages_before_them(mock):
     G.test_route_errors_after_the_messages_before_them()
+
+
+# ---------------------------------------------------------- the shared send ring (egress hub) --
+
+@pytest.fixture
+def egress_hub_mock(mock, monkeypatch):
+    from tests import test_gpu_egress_hub as E
+    monkeypatch.setattr(E, "HUB_LIB", mock)
+    return E
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("nconn,rounds,slot", [(64, 30, 1 << 20), (16, 40, 64 << 10)])
+def test_egress_hub_many_connections_interleaved(egress_hub_mock, nconn, rounds, slot):
+    egress_hub_mock.test_many_connections_interleaved(nconn, rounds, slot)
+
+
+def test_egress_hub_detach_sends_what_was_queued_then_cpu_path(egress_hub_mock):
+    egress_hub_mock.test_detach_sends_what_was_queued_then_cpu_path()
+
+
+def test_egress_hub_a_peer_gone_fails_only_its_connection(egress_hub_mock):
+    egress_hub_mock.test_a_peer_gone_fails_only_its_connection()
+
+
+def test_egress_hub_rules_and_limits(egress_hub_mock):
+    egress_hub_mock.test_rules_and_limits()
