@@ -19,7 +19,10 @@ tests/test_route_mock.py runs these on the CPU, over the mock HIP runtime.
 """
 
 import ctypes
+import json
+import os
 import socket
+import subprocess
 import threading
 
 import numpy as np
@@ -221,3 +224,23 @@ def test_rules_and_limits():
     b.close()
     assert got == wire([(G.BINARY, b"small", 1, key), (G.BINARY, b"after", 1, key)])
     assert nm.NETC_GPU_EINVAL == NETC_GPU_EINVAL
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("masked", ["0", "1"])
+def test_egress_hub_server_256_connections(masked):
+    """tests/drivers/ws_egress_hub_server.c: 256 TCP connections answered 60 times each from one
+    loop through the egress hub (flushed per iteration); every connection's bytes hashed by its
+    client equal the frames the server expects (the same rendering that libnetc's CPU leg and
+    the reference's own ws_send_message leg match)"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "bin", "ws_egress_hub_server")
+    assert os.path.exists(exe), "tests/bin/ws_egress_hub_server missing: run make"
+    for leg in ("hub", "cpu"):
+        r = subprocess.run([exe, leg, "256", "60", "1024", masked], capture_output=True, text=True, timeout=240,
+                           cwd=root)
+        assert r.returncode == 0, f"{leg}: rc {r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}"
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["mismatched"] == 0 and d["messages"] == 256 * 60, d
+        if leg == "hub":
+            assert d["launches"] >= 1 and d["max_conns_per_launch"] >= 64 and d["send_errors"] == 0, d

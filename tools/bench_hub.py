@@ -14,6 +14,12 @@ inside the timed region, and "clients_seconds" in each line shows whether they, 
 set the pace.
 
     python tools/bench_hub.py [--configs 256x400x1024,1024x100x1024,64x200x16384] [--chunks 0] [--out FILE]
+
+--send runs the send side instead (tests/bin/ws_egress_hub_server, include/ws/egress_hub.h): CONNS
+connections answered ROUNDS times each from one loop with netc's ws_send_message -- through one
+GPU egress hub (flushed once per loop iteration), libnetc's CPU path, or the reference's own
+ws_send_message; 4 client threads check every connection's bytes by hash.  --send-configs
+CONNSxROUNDSxMAX.
 """
 
 import argparse
@@ -24,6 +30,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "tests", "bin", "ws_hub_server")
+SEND_EXE = os.path.join(ROOT, "tests", "bin", "ws_egress_hub_server")
 REF = os.path.join(ROOT, "oracle", "_ref", "libref_ws.so")
 
 
@@ -33,7 +40,12 @@ def main():
     ap.add_argument("--legs", default="hub,cpu,ref")
     ap.add_argument("--chunks", default="0,65536", help="client send chunk sizes (0: live ws_send_message)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--send", action="store_true", help="the send side (egress hub) instead")
+    ap.add_argument("--send-configs", default="256x100x1024,1024x40x1024,64x100x16384,16x40x262144")
+    ap.add_argument("--masked", type=int, default=0, help="send side: masked frames (the client side; no ref leg)")
     args = ap.parse_args()
+    if args.send:
+        return send_side(args)
     if not os.path.exists(EXE):
         sys.exit(f"{EXE} missing: run make")
     out = open(args.out, "a") if args.out else None
@@ -49,6 +61,26 @@ def main():
             rec = json.loads(r.stdout.strip().splitlines()[-1])
             rec.pop("conn_hash", None)
             line = json.dumps(rec)
+            print(line, flush=True)
+            if out:
+                out.write(line + "\n")
+                out.flush()
+
+
+def send_side(args):
+    if not os.path.exists(SEND_EXE):
+        sys.exit(f"{SEND_EXE} missing: run make")
+    out = open(args.out, "a") if args.out else None
+    for cfg in args.send_configs.split(","):
+        conns, rounds, mx = cfg.split("x")
+        for leg in args.legs.split(","):
+            if leg == "ref" and (args.masked or not os.path.exists(REF)):
+                continue
+            r = subprocess.run([SEND_EXE, leg, conns, rounds, mx, str(args.masked)], capture_output=True, text=True,
+                               timeout=600, cwd=ROOT)
+            if r.returncode:
+                sys.exit(f"send {cfg} {leg}: rc {r.returncode}: {r.stderr[-2000:]}")
+            line = r.stdout.strip().splitlines()[-1]
             print(line, flush=True)
             if out:
                 out.write(line + "\n")
