@@ -13,7 +13,8 @@
  *         messages of printable bytes, unmasked (its masked BINARY path overflows the heap
  *         above 254 bytes: defect B1, src/ws/common.c:100)
  * Messages: size uniform in [0, MAX_BYTES], 1-3 frames, from an LCG seeded by (connection,
- * index), unmasked (server to client) unless MASKED = 1.
+ * index), unmasked (server to client) unless MASKED = 1.  BURST (default 1): messages to each
+ * client per loop iteration (a server fanning out updates), ROUNDS x BURST messages in all.
  *
  * Clients (4 threads, CONNS / 4 sockets each, epoll): read every byte and hash it per
  * connection (FNV-1a over the byte stream).  The server renders the frames it expects on each
@@ -22,7 +23,7 @@
  * fails unless every connection's hashes match.  The clock runs from the first send to the last
  * byte received.  One JSON line on stdout.
  *
- * usage: ws_egress_hub_server hub|cpu|ref CONNS ROUNDS MAX_BYTES [MASKED 0|1] [slot_bytes|0] [ref_lib]
+ * usage: ws_egress_hub_server hub|cpu|ref CONNS ROUNDS MAX_BYTES [MASKED 0|1] [slot_bytes|0] [ref_lib|-] [BURST]
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -183,7 +184,9 @@ int main(int argc, char **argv) {
     g_max = (size_t)strtoull(argv[4], NULL, 10);
     const int masked = argc > 5 && atoi(argv[5]);
     const size_t slot_bytes = argc > 6 && strtoull(argv[6], NULL, 10) ? (size_t)strtoull(argv[6], NULL, 10) : (size_t)16 << 20;
-    const char *ref_lib = argc > 7 ? argv[7] : "oracle/_ref/libref_ws.so";
+    const char *ref_lib = argc > 7 && strcmp(argv[7], "-") ? argv[7] : "oracle/_ref/libref_ws.so";
+    const size_t burst = argc > 8 && atoi(argv[8]) > 0 ? (size_t)atoi(argv[8]) : 1;
+    const size_t nmsg = rounds * burst;   /* messages per connection */
     const int is_hub = !strcmp(leg, "hub"), is_ref = !strcmp(leg, "ref");
     if (!is_hub && !is_ref && strcmp(leg, "cpu")) return 2;
     if (g_conns < 4 || g_conns % 4) {
@@ -246,7 +249,7 @@ int main(int argc, char **argv) {
     uint8_t *buf = malloc(g_max + 16);
     uint64_t payload = 0, messages = 0;
     for (int c = 0; c < g_conns; ++c)
-        for (size_t i = 0; i < rounds; ++i) {
+        for (size_t i = 0; i < nmsg; ++i) {
             size_t len, frames;
             uint8_t op, key[4];
             message(c, i, buf, &len, &frames, &op, key);
@@ -267,14 +270,17 @@ int main(int argc, char **argv) {
     /* the server's loop: one message to every client per iteration, then (hub) the flush */
     for (size_t i = 0; i < rounds; ++i) {
         for (int c = 0; c < g_conns; ++c) {
-            size_t len, frames;
-            uint8_t op, key[4];
-            message(c, i, buf, &len, &frames, &op, key);
-            struct ws_message m;
-            ws_build_message(&m, op, len, buf);
-            if (snd((struct web_client *)&sp[c].head, &m, masked ? key : NULL, frames) != 1) {
-                fprintf(stderr, "server: connection %d: ws_send_message failed (%s)\n", c, hub ? netc_gpu_strerror() : "");
-                return 3;
+            for (size_t b = 0; b < burst; ++b) {
+                size_t len, frames;
+                uint8_t op, key[4];
+                message(c, i * burst + b, buf, &len, &frames, &op, key);
+                struct ws_message m;
+                ws_build_message(&m, op, len, buf);
+                if (snd((struct web_client *)&sp[c].head, &m, masked ? key : NULL, frames) != 1) {
+                    fprintf(stderr, "server: connection %d: ws_send_message failed (%s)\n", c,
+                            hub ? netc_gpu_strerror() : "");
+                    return 3;
+                }
             }
         }
         if (hub && netc_ws_egress_hub_flush(hub) < 0) {
@@ -294,11 +300,11 @@ int main(int argc, char **argv) {
     size_t mismatched = 0;
     for (int c = 0; c < g_conns; ++c) mismatched += g_got_hash[c] != want_hash[c];
     const double secs = (double)(g_last_ns - t0) * 1e-9;
-    printf("{\"leg\": \"%s\", \"conns\": %d, \"rounds\": %zu, \"max_bytes\": %zu, \"masked\": %d, \"messages\": %llu, "
+    printf("{\"leg\": \"%s\", \"conns\": %d, \"rounds\": %zu, \"burst\": %zu, \"max_bytes\": %zu, \"masked\": %d, \"messages\": %llu, "
            "\"payload_bytes\": %llu, \"seconds\": %.6f, \"server_seconds\": %.6f, \"msgs_per_s\": %.1f, "
            "\"gib_per_s\": %.4f, \"mismatched\": %zu, \"launches\": %llu, \"max_conns_per_launch\": %llu, "
            "\"mean_conns_per_launch\": %.2f, \"sendmsg_calls\": %llu, \"send_errors\": %llu}\n",
-           leg, g_conns, rounds, g_max, masked, (unsigned long long)messages, (unsigned long long)payload, secs,
+           leg, g_conns, rounds, burst, g_max, masked, (unsigned long long)messages, (unsigned long long)payload, secs,
            (double)(t_sent - t0) * 1e-9, (double)messages / secs, (double)payload / secs / (double)(1ull << 30),
            mismatched, (unsigned long long)hs.launches, (unsigned long long)hs.max_connections,
            hs.launches ? (double)hs.connection_slots / (double)hs.launches : 0.0,

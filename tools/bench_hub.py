@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--send", action="store_true", help="the send side (egress hub) instead")
     ap.add_argument("--send-configs", default="256x100x1024,1024x40x1024,64x100x16384,16x40x262144")
+    ap.add_argument("--bursts", default="1,8", help="send side: messages per connection per loop iteration")
     ap.add_argument("--masked", type=int, default=0, help="send side: masked frames (the client side; no ref leg)")
     args = ap.parse_args()
     if args.send:
@@ -73,11 +74,11 @@ def send_side(args):
     out = open(args.out, "a") if args.out else None
     for cfg in args.send_configs.split(","):
         conns, rounds, mx = cfg.split("x")
-        for leg in args.legs.split(","):
+        for burst, leg in [(b, l) for b in args.bursts.split(",") for l in args.legs.split(",")]:
             if leg == "ref" and (args.masked or not os.path.exists(REF)):
                 continue
-            r = subprocess.run([SEND_EXE, leg, conns, rounds, mx, str(args.masked)], capture_output=True, text=True,
-                               timeout=600, cwd=ROOT)
+            r = subprocess.run([SEND_EXE, leg, conns, str(max(1, int(rounds) // int(burst))), mx, str(args.masked), "0",
+                                "-", burst], capture_output=True, text=True, timeout=600, cwd=ROOT)
             if r.returncode:
                 sys.exit(f"send {cfg} {leg}: rc {r.returncode}: {r.stderr[-2000:]}")
             line = r.stdout.strip().splitlines()[-1]
