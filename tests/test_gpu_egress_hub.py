@@ -244,3 +244,74 @@ def test_egress_hub_server_256_connections(masked):
         assert d["mismatched"] == 0 and d["messages"] == 256 * 60, d
         if leg == "hub":
             assert d["launches"] >= 1 and d["max_conns_per_launch"] >= 64 and d["send_errors"] == 0, d
+
+
+@pytest.mark.timeout(120)
+def test_slots_run_out_between_flushes():
+    """two small slots and no flush for a long while: with no slot free the oldest is sent from
+    inside ws_send_message, over and over; every connection's bytes still come in order"""
+    lib = _lib.host()
+    rng = np.random.default_rng(77)
+    nconn = 32
+    pairs = [pair() for _ in range(nconn)]
+    readers = [Reader(b) for _, b in pairs]
+    eps = [Endpoint(a) for a, _ in pairs]
+    sent = [[] for _ in range(nconn)]
+    with make(slot_bytes=8192, nslots=2, max_frames=64) as hub:
+        for a, _ in pairs:
+            hub.attach(a.fileno())
+        try:
+            for _ in range(600):
+                c = int(rng.integers(0, nconn))
+                op, p, nf = message(rng)
+                key = bytes(rng.integers(0, 256, 4, dtype=np.uint8)) if c % 2 else None
+                assert send(lib, eps[c], op, p, key, nf) == 1
+                sent[c].append((op, p, nf, key))
+            hub.flush()
+            st = hub.stats()
+        finally:
+            for a, _ in pairs:
+                hub.detach(a.fileno())
+    for a, _ in pairs:
+        a.shutdown(socket.SHUT_WR)
+    got = [rd.join() for rd in readers]
+    for a, b in pairs:
+        a.close()
+        b.close()
+    for c in range(nconn):
+        assert got[c] == wire(sent[c]), c
+    assert st["launches"] > 20, st
+
+
+@pytest.mark.timeout(60)
+def test_descriptor_reused_after_a_close_without_detach():
+    """a connection closed without a detach leaves its queued messages behind; the next socket
+    given the same descriptor number is a new connection: attaching it drops the old one's bytes
+    (nowhere to go), and only the new connection's messages reach the new peer"""
+    import os as _os
+    lib = _lib.host()
+    key = bytes([3, 1, 4, 1])
+    with make(slot_bytes=1 << 20, nslots=2) as hub:
+        a, b = pair()
+        hub.attach(a.fileno())
+        assert send(lib, Endpoint(a), G.BINARY, b"old connection", key, 1) == 1   # queued
+        fd = a.fileno()
+        a.close()
+        b.close()
+        x, y = pair()
+        if x.fileno() != fd:   # (the kernel usually hands out the same number by itself)
+            _os.dup2(x.fileno(), fd)
+            x.close()
+            x = socket.socket(fileno=fd)
+        rd = Reader(y)
+        try:
+            hub.attach(x.fileno())
+            assert send(lib, Endpoint(x), G.TEXT, b"new connection", key, 2) == 1
+            hub.flush()
+        finally:
+            hub.detach(x.fileno())
+        x.shutdown(socket.SHUT_WR)
+        got = rd.join()
+        x.close()
+        y.close()
+    assert got == wire([(G.TEXT, b"new connection", 2, key)])

@@ -220,3 +220,11 @@ def test_egress_hub_a_peer_gone_fails_only_its_connection(egress_hub_mock):
 
 def test_egress_hub_rules_and_limits(egress_hub_mock):
     egress_hub_mock.test_rules_and_limits()
+
+
+def test_egress_hub_slots_run_out_between_flushes(egress_hub_mock):
+    egress_hub_mock.test_slots_run_out_between_flushes()
+
+
+def test_egress_hub_descriptor_reused_after_a_close_without_detach(egress_hub_mock):
+    egress_hub_mock.test_descriptor_reused_after_a_close_without_detach()
