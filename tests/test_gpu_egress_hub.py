@@ -315,3 +315,46 @@ def test_descriptor_reused_after_a_close_without_detach():
         x.close()
         y.close()
     assert got == wire([(G.TEXT, b"new connection", 2, key)])
+
+
+def fault_then_recover(arm, disarm):
+    """a failing submission (injected) fails the flush with NETC_GPU_ELAUNCH and leaves the queued
+    messages in their slot: the next flush sends them once each, in order -- nothing lost, nothing
+    twice"""
+    from netc_amd import mask as nm
+    lib = _lib.host()
+    a, b = pair()
+    rd = Reader(b)
+    ep = Endpoint(a)
+    rng = np.random.default_rng(8)
+    msgs = [message(rng) + (bytes([i, 2, 3, 4]),) for i in range(12)]
+    with make(slot_bytes=1 << 20, nslots=2) as hub:
+        hub.attach(a.fileno())
+        try:
+            for op, p, nf, key in msgs[:6]:
+                assert send(lib, ep, op, p, key, nf) == 1
+            arm()
+            try:
+                with pytest.raises(NetcGpuError) as e:
+                    hub.flush()
+                assert e.value.code == nm.NETC_GPU_ELAUNCH
+            finally:
+                disarm()
+            for op, p, nf, key in msgs[6:]:
+                assert send(lib, ep, op, p, key, nf) == 1
+            hub.flush()
+        finally:
+            hub.detach(a.fileno())
+    a.shutdown(socket.SHUT_WR)
+    got = rd.join()
+    a.close()
+    b.close()
+    assert got == wire(msgs)
+
+
+@pytest.mark.timeout(60)
+def test_injected_fault_then_recovery():
+    from netc_amd import mask as nm
+    _lib.gpu().netc_gpu_knob.restype = ctypes.c_int
+    fault_then_recover(lambda: _lib.gpu().netc_gpu_knob(nm.KNOBS["INJECT_FAULT"], 0),
+                       lambda: _lib.gpu().netc_gpu_knob(nm.KNOBS["INJECT_FAULT"], -1))
