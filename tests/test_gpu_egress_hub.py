@@ -358,3 +358,74 @@ def test_injected_fault_then_recovery():
     _lib.gpu().netc_gpu_knob.restype = ctypes.c_int
     fault_then_recover(lambda: _lib.gpu().netc_gpu_knob(nm.KNOBS["INJECT_FAULT"], 0),
                        lambda: _lib.gpu().netc_gpu_knob(nm.KNOBS["INJECT_FAULT"], -1))
+
+
+@pytest.mark.timeout(180)
+def test_echo_server_both_hubs():
+    """netc's server loop with both hubs: every client's masked messages come in through the
+    receive hub (one ws_parse_frame per readable socket per iteration) and go back out through
+    the egress hub (ws_send_message, unmasked as a server sends, one flush per iteration); each
+    client gets back exactly the frames of what it sent"""
+    import select
+    from tests.wsutil import ParseState, libc
+    lib = _lib.host()
+    rng = np.random.default_rng(99)
+    nconn, nmsg = 32, 25
+    pairs = [G.tcp_pair() for _ in range(nconn)]
+    msgs = [[message(rng) for _ in range(nmsg)] for _ in range(nconn)]
+    keys = [[bytes(rng.integers(0, 256, 4, dtype=np.uint8)) for _ in range(nmsg)] for _ in range(nconn)]
+    readers = [Reader(c) for c, _ in pairs]
+
+    def client():
+        for i in range(nmsg):
+            for c in range(nconn):
+                op, p, nf = msgs[c][i]
+                pairs[c][0].sendall(G.wire_of([(op, p, nf, [keys[c][i]] * nf)]))
+
+    socks = [s for _, s in pairs]
+    with nh.Hub(lib=HUB_LIB, slot_bytes=1 << 20, nslots=4) as rx, make(slot_bytes=1 << 20, nslots=3) as tx:
+        for s in socks:
+            s.setblocking(False)
+            rx.attach(s.fileno())
+            tx.attach(s.fileno())
+        eps = [Endpoint(s) for s in socks]
+        sts = [ParseState() for _ in socks]
+        index = {s.fileno(): c for c, s in enumerate(socks)}
+        th = threading.Thread(target=client)
+        th.start()
+        try:
+            left = nconn * nmsg
+            while left:
+                ready, _, _ = select.select(socks, [], [], 10)
+                assert ready, f"stranded: {nconn * nmsg - left} of {nconn * nmsg}"
+                for s in ready:
+                    c = index[s.fileno()]
+                    rc = lib.ws_parse_frame(ctypes.byref(eps[c].client), ctypes.byref(sts[c]), 1 << 20)
+                    if rc == 0:
+                        m = sts[c].message
+                        n = m.payload_length - (1 if m.opcode == G.TEXT else 0)   # (the NUL the reference appends)
+                        echo = WsMessage()
+                        lib.ws_build_message(ctypes.byref(echo), m.opcode, n, m.buffer)
+                        assert lib.ws_send_message(ctypes.byref(eps[c].client), ctypes.byref(echo), None, 1) == 1
+                        libc.free(m.buffer)
+                        ctypes.memset(ctypes.byref(sts[c]), 0, ctypes.sizeof(sts[c]))
+                        left -= 1
+                    else:
+                        assert rc == 1, rc
+                tx.flush()   # once per loop iteration
+            th.join()
+            st = tx.stats()
+        finally:
+            for s in socks:
+                rx.detach(s.fileno())
+                tx.detach(s.fileno())
+    for c, s in pairs:
+        s.shutdown(socket.SHUT_WR)
+    got = [rd.join() for rd in readers]
+    for c, s in pairs:
+        c.close()
+        s.close()
+    for c in range(nconn):
+        want = wire([(op, p, 1, None) for op, p, _ in msgs[c]])
+        assert got[c] == want, c
+    assert st["messages"] == nconn * nmsg and st["max_connections"] > 1, st

@@ -232,3 +232,7 @@ def test_egress_hub_descriptor_reused_after_a_close_without_detach(egress_hub_mo
 
 def test_egress_hub_injected_fault_then_recovery(egress_hub_mock, mock):
     egress_hub_mock.fault_then_recover(lambda: mock.netc_mock_inject_fault(0), lambda: mock.netc_mock_inject_fault(-1))
+
+
+def test_egress_hub_echo_server_both_hubs(egress_hub_mock):
+    egress_hub_mock.test_echo_server_both_hubs()
