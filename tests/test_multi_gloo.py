@@ -1,4 +1,4 @@
-"""N > 1 path on CPU: world_size-2 gloo ranks each take a byte-balanced shard of one frame batch
+"""N > 1 path on CPU: world_size-2 (and 3, 8: the driver's 8-GPU node, an odd split) gloo ranks each take a byte-balanced shard of one frame batch
 (netc_shard_frames), rebase it exactly as a GPU shard is rebased (bench.py / netc_gpu_mask_batch_multi),
 mask it with the host entry netc_ws_mask, and the gathered result must equal the oracle on the
 whole batch.  No collective touches the data path except the final check's gather."""
@@ -58,7 +58,7 @@ def _worker(rank, world, port, result_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gloo_sharded_batch_matches_oracle(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
