@@ -28,7 +28,7 @@ all: host gpu oracle mock
 mock: tests/bin/libnetc_ingest_mock.so
 host: $(LIBDIR)/libnetc.so
 gpu: $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc_ceiling.so tests/bin/ws_gpu_epoll tests/bin/ws_egress_bench \
-     tests/bin/ws_route_bench tests/bin/ws_hub_server tests/bin/ws_egress_hub_server
+     tests/bin/ws_route_bench tests/bin/ws_hub_server tests/bin/ws_egress_hub_server tests/bin/ws_echo_server
 
 $(LIBDIR)/libnetc.so: $(HOST_SRCS) $(HOST_HDRS)
 	@mkdir -p $(LIBDIR)
@@ -79,6 +79,12 @@ tests/bin/libnetc_ingest_mock.so: netc_amd/csrc/ws_ingest.hip netc_amd/csrc/ws_h
 
 # many connections on one event loop, one GPU hub (tests/test_gpu_hub.py, tools/bench_hub.py)
 tests/bin/ws_hub_server: tests/drivers/ws_hub_server.c $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc.so $(HOST_HDRS)
+	@mkdir -p tests/bin
+	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -L$(LIBDIR) -lnetc_ws_gpu -lnetc -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib -lpthread -ldl
+
+# an echo server in netc's shape, GPU both ways (receive hub in, egress hub out)
+tests/bin/ws_echo_server: tests/drivers/ws_echo_server.c $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc.so $(HOST_HDRS)
 	@mkdir -p tests/bin
 	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -L$(LIBDIR) -lnetc_ws_gpu -lnetc -L/opt/rocm/lib -lamdhip64 \
 	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib -lpthread -ldl

@@ -428,3 +428,22 @@ def test_echo_server_both_hubs():
         want = wire([(op, p, 1, None) for op, p, _ in msgs[c]])
         assert got[c] == want, c
     assert st["messages"] == nconn * nmsg and st["max_connections"] > 1, st
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("chunk", ["0", "65536"])
+def test_echo_server_driver(chunk):
+    """tests/drivers/ws_echo_server.c: 256 TCP connections, 40 masked requests each, echoed by a
+    netc-shaped loop through the receive hub and the egress hub; every connection's reply bytes
+    hashed against the expected frames, beside libnetc's CPU leg"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "bin", "ws_echo_server")
+    assert os.path.exists(exe), "tests/bin/ws_echo_server missing: run make"
+    for leg in ("hub", "cpu"):
+        r = subprocess.run([exe, leg, "256", "40", "1024", chunk], capture_output=True, text=True, timeout=240,
+                           cwd=root)
+        assert r.returncode == 0, f"{leg}: rc {r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}"
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["mismatched"] == 0 and d["messages"] == 256 * 40, d
+        if leg == "hub":
+            assert d["rx_launches"] >= 1 and d["tx_launches"] >= 1 and d["tx_max_conns_per_launch"] > 1, d

@@ -41,12 +41,16 @@ def main():
     ap.add_argument("--chunks", default="0,65536", help="client send chunk sizes (0: live ws_send_message)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--send", action="store_true", help="the send side (egress hub) instead")
+    ap.add_argument("--echo", action="store_true", help="the echo server (both hubs) instead: --echo-configs")
+    ap.add_argument("--echo-configs", default="256x200x1024x0,256x200x1024x65536,1024x50x1024x65536,64x100x16384x65536")
     ap.add_argument("--send-configs", default="256x100x1024,1024x40x1024,64x100x16384,16x40x262144")
     ap.add_argument("--bursts", default="1,8", help="send side: messages per connection per loop iteration")
     ap.add_argument("--masked", type=int, default=0, help="send side: masked frames (the client side; no ref leg)")
     args = ap.parse_args()
     if args.send:
         return send_side(args)
+    if args.echo:
+        return echo(args)
     if not os.path.exists(EXE):
         sys.exit(f"{EXE} missing: run make")
     out = open(args.out, "a") if args.out else None
@@ -62,6 +66,22 @@ def main():
             rec = json.loads(r.stdout.strip().splitlines()[-1])
             rec.pop("conn_hash", None)
             line = json.dumps(rec)
+            print(line, flush=True)
+            if out:
+                out.write(line + "\n")
+                out.flush()
+
+
+def echo(args):
+    exe = os.path.join(ROOT, "tests", "bin", "ws_echo_server")
+    out = open(args.out, "a") if args.out else None
+    for cfg in args.echo_configs.split(","):
+        conns, msgs, mx, chunk = cfg.split("x")
+        for leg in ("hub", "cpu"):
+            r = subprocess.run([exe, leg, conns, msgs, mx, chunk], capture_output=True, text=True, timeout=600, cwd=ROOT)
+            if r.returncode:
+                sys.exit(f"echo {cfg} {leg}: rc {r.returncode}: {r.stderr[-2000:]}")
+            line = r.stdout.strip().splitlines()[-1]
             print(line, flush=True)
             if out:
                 out.write(line + "\n")
