@@ -76,6 +76,9 @@ int netc_ws_gpu_detach_send_hub(int sockfd);
  * Every queued message framed on the GPU and sent: the filling slot is submitted, then each
  * slot in queue order is waited for and its connections' bytes are sent.  Bytes sent (>= 0), or
  * a negative code for a device failure.  Per-connection send failures do not fail the flush.
+ * A slot whose wire the device does not vouch for (its wire length is not the host's) fails
+ * each of its connections as a failed send does, and the flush returns NETC_GPU_ERUNTIME after
+ * sending the later slots; the hub goes on serving the other connections.
  */
 long netc_ws_egress_hub_flush(struct netc_ws_egress_hub *hub);
 

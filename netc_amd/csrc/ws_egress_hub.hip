@@ -243,16 +243,31 @@ int send_iov(netc_ws_egress_hub* h, int fd, struct iovec* iov, size_t cnt) {
     return 0;
 }
 
-// wait for the oldest submitted slot and put its connections' bytes on their sockets; bytes sent
-long send_oldest(netc_ws_egress_hub* h) {
+// wait for the oldest submitted slot and put its connections' bytes on their sockets; bytes sent.
+// *dropped: the slot finished but its wire is not what was queued (the device's wire length differs
+// from the host's); then each of its connections fails as on a failed send -- its bytes are gone,
+// its next ws_send_message returns -1 and netc closes it -- and the slot is free for the others,
+// so one bad slot does not hold up every later flush.  A failed wait (the device itself) stays
+// sticky: the slot is left where it is.
+long send_oldest(netc_ws_egress_hub* h, bool* dropped) {
+    *dropped = false;
     const int i = h->fifo.front();
     EhSlot& s = h->slots[i];
     hipError_t e = hipEventSynchronize(s.done);
     if (e != hipSuccess) return api_fail_hip(NETC_GPU_ERUNTIME, "egress hub: slot wait", e);
-    if (*s.h_len != s.wire)
-        return api_fail(NETC_GPU_ERUNTIME, "egress hub: the device's wire length %llu is not the host's %llu",
-                        (unsigned long long)*s.h_len, (unsigned long long)s.wire);
     h->fifo.pop_front();
+    if (*s.h_len != s.wire) {
+        for (const Span& sp : s.spans)
+            if (sp.conn && !sp.conn->failed) {
+                sp.conn->failed = EIO;
+                h->st.send_errors++;
+            }
+        s.spans.clear();
+        s.state = kFree;
+        *dropped = true;
+        return api_fail(NETC_GPU_ERUNTIME, "egress hub: the device's wire length %llu is not the host's %llu; "
+                        "the slot's connections fail", (unsigned long long)*s.h_len, (unsigned long long)s.wire);
+    }
     // per connection, its runs in the wire, in queue order (consecutive messages: one run)
     std::vector<EhConn*> order;
     for (const Span& sp : s.spans) {
@@ -300,8 +315,9 @@ int acquire(netc_ws_egress_hub* h) {
             return 0;
         }
         if (h->fifo.empty()) return api_fail(NETC_GPU_ERUNTIME, "egress hub: no slot to send");
-        const long r = send_oldest(h);
-        if (r < 0) return (int)r;
+        bool dropped = false;
+        const long r = send_oldest(h, &dropped);
+        if (r < 0 && !dropped) return (int)r;   // (dropped: its connections learn it on their next call)
     }
 }
 
@@ -357,15 +373,18 @@ int queue(netc_ws_egress_hub* h, EhConn* c, const void* payload, size_t len, uin
     return 0;
 }
 
+// every queued byte out; a dropped slot is reported (its code) once the later slots are sent
 long flush(netc_ws_egress_hub* h) {
     if (int e = submit(h)) return e;
-    long sent = 0;
+    long sent = 0, err = 0;
     while (!h->fifo.empty()) {
-        const long r = send_oldest(h);
-        if (r < 0) return r;
-        sent += r;
+        bool dropped = false;
+        const long r = send_oldest(h, &dropped);
+        if (r < 0 && !dropped) return r;
+        if (r < 0) err = r;
+        else sent += r;
     }
-    return sent;
+    return err ? err : sent;
 }
 
 bool sock_identity(int fd, uint64_t* dev, uint64_t* ino) {

@@ -17,6 +17,7 @@ namespace netc_gpu {
 namespace {
 char g_err[512];
 int g_fault = -1;
+int g_bad_wire = -1;   // netc_mock_bad_wire: the assembly launch this many launches on reports no wire
 }
 struct ScanScratch {
     uint32_t diag;
@@ -79,6 +80,7 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t, const uint8_t* src, uin
         for (uint64_t i = 0; i < len; ++i) p[i] = src[off[k] + i] ^ key[i & 3];
         w = (uint64_t)(p + len - wire);
     }
+    if (g_bad_wire >= 0 && g_bad_wire-- == 0) broken = true;
     wo[n] = broken ? ~0ull : w;
     return hipSuccess;
 }
@@ -104,5 +106,11 @@ bool inject_fault() {
 extern "C" const char* netc_gpu_strerror(void) { return netc_gpu::g_err; }
 extern "C" int netc_mock_inject_fault(int countdown) {
     netc_gpu::g_fault = countdown;
+    return 0;
+}
+// the frame assembly launch `countdown` launches from now writes wo[n] = UINT64_MAX (a wire the
+// device does not vouch for, as a broken length-class promise reports it); -1 disarms
+extern "C" int netc_mock_bad_wire(int countdown) {
+    netc_gpu::g_bad_wire = countdown;
     return 0;
 }

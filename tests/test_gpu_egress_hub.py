@@ -351,6 +351,51 @@ def fault_then_recover(arm, disarm):
     assert got == wire(msgs)
 
 
+def bad_wire_fails_only_its_slot(arm, disarm):
+    """a slot whose wire the device does not vouch for (wire length mismatch) fails its own
+    connections as a failed send would -- their next ws_send_message returns -1 -- and the flush
+    reports it after sending the later slots; a connection with nothing in that slot, and the
+    hub, go on"""
+    from netc_amd import mask as nm
+    lib = _lib.host()
+    (a, b), (c, d) = pair(), pair()
+    ra, rc = Reader(b), Reader(d)
+    ea, ec = Endpoint(a), Endpoint(c)
+    rng = np.random.default_rng(12)
+    first = [message(rng) + (bytes([9, 8, 7, i]),) for i in range(4)]
+    later = [message(rng) + (bytes([1, 2, 3, i]),) for i in range(6)]
+    with make(slot_bytes=1 << 20, nslots=2) as hub:
+        hub.attach(a.fileno())
+        hub.attach(c.fileno())
+        try:
+            for op, p, nf, key in first:   # connection a only: the slot that goes bad
+                assert send(lib, ea, op, p, key, nf) == 1
+            arm()
+            try:
+                with pytest.raises(NetcGpuError) as e:
+                    hub.flush()
+                assert e.value.code == nm.NETC_GPU_ERUNTIME
+            finally:
+                disarm()
+            op, p, nf, key = later[0]
+            assert send(lib, ea, op, p, key, nf) == -1   # its bytes are gone: the connection failed
+            for op, p, nf, key in later:
+                assert send(lib, ec, op, p, key, nf) == 1
+            assert hub.flush() > 0
+            st = hub.stats()
+        finally:
+            hub.detach(a.fileno())
+            hub.detach(c.fileno())
+    for s in (a, c):
+        s.shutdown(socket.SHUT_WR)
+    got_a, got_c = ra.join(), rc.join()
+    for s in (a, b, c, d):
+        s.close()
+    assert got_a == b""
+    assert got_c == wire(later)
+    assert st["send_errors"] == 1, st
+
+
 @pytest.mark.timeout(60)
 def test_injected_fault_then_recovery():
     from netc_amd import mask as nm

@@ -236,3 +236,7 @@ def test_egress_hub_injected_fault_then_recovery(egress_hub_mock, mock):
 
 def test_egress_hub_echo_server_both_hubs(egress_hub_mock):
     egress_hub_mock.test_echo_server_both_hubs()
+
+
+def test_egress_hub_bad_wire_fails_only_its_slot(egress_hub_mock, mock):
+    egress_hub_mock.bad_wire_fails_only_its_slot(lambda: mock.netc_mock_bad_wire(0), lambda: mock.netc_mock_bad_wire(-1))
