@@ -452,7 +452,15 @@ __device__ __forceinline__ void append_cand(const ScanArgs& a, uint64_t x, bool 
 // a lane of the last vector of a chunk whose 16 positions can exit the chunk with a
 // 7-bit length: p + 2 + 4 + 125 >= chunk end  <=>  offset >= 3965 (lane 55 holds 3952-3967)
 static constexpr int kNearLane = 55;
-static constexpr int kQCap = 256;   // K1: exit-capable candidates queued per chunk (more: serial walk)
+// K1's LDS per 4-wave block: each wave's chunk (+ the 16 bytes after it, all a window at offset
+// 4095 reads), exit set and candidate queue.  At 248 queue entries the block takes 20,480 B, so 8
+// blocks (32 waves, the SIMDs' limit) fit a CU's 160 KiB where the 20,992 B of a 32-byte tail and
+// 256 entries allowed 7.  NETC_K1_SLIM=0 restores that layout (A/B builds).
+#ifndef NETC_K1_SLIM
+#define NETC_K1_SLIM 1
+#endif
+static constexpr int kQCap = NETC_K1_SLIM ? 248 : 256;   // K1: exit-capable candidates queued per chunk (more: serial walk)
+static constexpr int kStageWords = NETC_K1_SLIM ? (int)((kChunk + 16) / 4) : kWords;
 static constexpr int kCheapMax = 64;   // K1: more from the cheap selection: the full quick check instead
 
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
@@ -508,7 +516,7 @@ __device__ __forceinline__ u32x4 k1_load(const uint8_t* p) {
 
 template <bool NT>
 __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
-    __shared__ uint32_t stage[4][kWords];      // per wave: its chunk's bytes (+ 32 after)
+    __shared__ uint32_t stage[4][kStageWords];   // per wave: its chunk's bytes (+ 16 after)
     __shared__ unsigned long long set[4][kSet];
     __shared__ uint16_t queue[4][kQCap];
 #ifdef NETC_SCAN_K1_EXP
