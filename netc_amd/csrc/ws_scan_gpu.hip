@@ -7,7 +7,8 @@
 //
 // Frame starts form a chain: the next header follows the current frame's payload.
 // The stream is cut into chunks of C = 4 KiB, chunks into tiles of 256 (1 MiB).
-// Five launches:
+// Five launches (four up to 256 tiles = 256 MiB of stream, where K3b runs in the last K3a block to
+// arrive: scan_tiles_resolve):
 //   K1  scan_exits    one wavefront per chunk, straight from HBM (16-B loads, no
 //                     LDS staging): the strict quick check on bytes 0-1 of every
 //                     position, 4 positions per 5 VALU operations (SWAR).  A chain
