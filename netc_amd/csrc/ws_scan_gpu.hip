@@ -462,6 +462,8 @@ static constexpr int kNearLane = 55;
 #endif
 static constexpr int kQCap = NETC_K1_SLIM ? 248 : 256;   // K1: exit-capable candidates queued per chunk (more: serial walk)
 static constexpr int kStageWords = NETC_K1_SLIM ? (int)((kChunk + 16) / 4) : kWords;
+static_assert(!NETC_K1_SLIM || 4 * (4 * kStageWords + 8 * kSet + 2 * kQCap) <= 20480,
+              "K1: a 4-wave block must stay within 20,480 B of LDS (8 blocks per CU)");
 static constexpr int kCheapMax = 64;   // K1: more from the cheap selection: the full quick check instead
 
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
