@@ -76,9 +76,10 @@ def _code_objects(path):
     return objs
 
 
-def kernel_resources(path=LIB):
-    """{demangled kernel name: (vgpr_count, vgpr_spill_count, private_segment_fixed_size)}"""
-    res = {}
+def kernel_resources(path=LIB, lds_out=None):
+    """{demangled kernel name: (vgpr_count, vgpr_spill_count, private_segment_fixed_size)};
+    lds_out, if given, receives {demangled name: group_segment_fixed_size}"""
+    res, lds = {}, {}
     for obj in _code_objects(path):
         with tempfile.NamedTemporaryFile(suffix=".co") as f:
             f.write(obj)
@@ -91,8 +92,11 @@ def kernel_resources(path=LIB):
                 return int(re.search(rf"\.{k}:\s+(\d+)", blk).group(1))
 
             res[name] = (field("vgpr_count"), field("vgpr_spill_count"), field("private_segment_fixed_size"))
+            lds[name] = field("group_segment_fixed_size")
     names = list(res)
     dem = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True, check=True).stdout.split("\n")
+    if lds_out is not None:
+        lds_out.update({d: lds[m] for m, d in zip(names, dem)})
     return {d: res[m] for m, d in zip(names, dem)}
 
 
@@ -118,3 +122,16 @@ def test_hot_kernels_do_not_spill(resources):
         if any(k.startswith(p) for p in HOT) and (spills or scratch):
             bad.append(f"{k}: {vgprs} VGPRs, {spills} spilled, {scratch} B scratch per lane")
     assert not bad, "kernels on a default path spill:\n" + "\n".join(bad)
+
+
+def test_scan_k1_fits_eight_blocks_per_cu():
+    """K1 (scan_exits) at 20,480 B of LDS per 4-wave block: 8 blocks, the SIMDs' 32 waves, fit a
+    CU's 160 KiB (C4 scan 81.2 -> 80.1 us against the 20,608-B layout)"""
+    if not os.path.exists(LIB) or not os.path.exists(READELF):
+        pytest.skip("libnetc_ws_gpu.so or llvm-readelf missing")
+    lds = {}
+    kernel_resources(lds_out=lds)
+    k1 = {k: v for k, v in lds.items() if k.startswith("void netc_gpu::scan_exits<")}
+    assert len(k1) == 2, k1
+    for k, v in k1.items():
+        assert 0 < v <= 20480, f"{k}: {v} B of LDS"
