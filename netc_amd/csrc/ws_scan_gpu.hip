@@ -80,13 +80,17 @@ static constexpr int kMaxTiles = 8192;                        // K3b: tiles (8 G
 #ifndef NETC_SCAN_BLK
 #define NETC_SCAN_BLK 32   // A/B builds
 #endif
-#ifndef NETC_SCAN_EMIT
-#define NETC_SCAN_EMIT 32
-#endif
 static constexpr int kBlkChunks = NETC_SCAN_BLK;              // K2: chunks per block
-static constexpr int kEmitChunks = NETC_SCAN_EMIT;            // K4: chunks per block
+// K4: chunks per block.  32 up to 128 MiB of stream (8,192 chunks at C2: 64 per block measured
+// 43.2 against 42.5 us, r03i2); 64 above, where most chunks hold no node and the blocks themselves
+// are the cost (C4: 2,049 blocks of 32 take 1.6 rounds at 5 per CU; 1,025 of 64 fit one).  Knob
+// SCAN_EMIT_CHUNKS picks either for any stream (tests, A/B).
+static constexpr int kEmitChunks = 32;
+static constexpr int kEmitChunksBig = 64;
+static constexpr uint64_t kEmitBigAbove = 32768;   // chunks (128 MiB)
 static_assert(kBlkChunks * kCand <= 256 && kTileChunks % kBlkChunks == 0, "K2: one thread per node slot");
 static_assert(kEmitChunks <= 256 && kTileChunks % kEmitChunks == 0, "K4: one thread per chunk, blocks inside a tile");
+static_assert(kEmitChunksBig <= 256 && kTileChunks % kEmitChunksBig == 0, "K4: one thread per chunk, blocks inside a tile");
 static constexpr int32_t kDupLink = -2;                       // K2: slot repeats an earlier slot's position
 static constexpr int kWalkHops = 64;                          // K2 / K4: frames walked one by one
 static constexpr int kList = 8;                               // K2 -> K4: frames recorded per node
@@ -1881,7 +1885,7 @@ __device__ __forceinline__ void put_frame(const ScanArgs& a, uint64_t k, uint64_
     }
 }
 
-// K4: the chunks' descriptors, kEmitChunks chunks per block.  Thread t < kEmitChunks
+// K4: the chunks' descriptors, EC chunks per block (kEmitChunks or kEmitChunksBig).  Thread t < EC
 // takes chunk t: its true entry is the node whose path bits hold the tile entry's bit;
 // a chunk of at most kWalkHops frames is walked by that thread (header bytes from
 // global memory).  Longer ones: with K2' anchors one wavefront per chunk, lane u
@@ -1893,6 +1897,7 @@ __device__ __forceinline__ void put_frame(const ScanArgs& a, uint64_t k, uint64_
 static constexpr int kEmitGroup = 32;
 static constexpr uint16_t kNoFrame = 0xFFFF;
 
+template <int EC>
 __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) {
     __shared__ uint32_t words[kWords];
     __shared__ union {
@@ -1913,14 +1918,14 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
     uint16_t* const lk16 = lu.b.lk16;
     __shared__ uint16_t anchor[kChunk / kStride + 1];
     __shared__ int nanchor, nqa, nqb;
-    __shared__ uint32_t qa_node[kEmitChunks], qb_node[kEmitChunks], qa_slot[kEmitChunks];
-    __shared__ uint64_t qa_base[kEmitChunks], qb_base[kEmitChunks];
+    __shared__ uint32_t qa_node[EC], qb_node[EC], qa_slot[EC];
+    __shared__ uint64_t qa_base[EC], qb_base[EC];
     __shared__ TileInfo bti;
     __shared__ int fbs;
     SCAN_SCOPE(4);
     (void)tiles;
     const int tid = threadIdx.x;
-    const uint64_t tile = (uint64_t)blockIdx.x * kEmitChunks / kTileChunks;   // kEmitChunks divides kTileChunks
+    const uint64_t tile = (uint64_t)blockIdx.x * EC / kTileChunks;   // EC divides kTileChunks
     if (tid == 0) {
         fbs = __hip_atomic_load(&a.flags[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
         bti = a.tinfo[tile];
@@ -1930,8 +1935,8 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
     }
     __syncthreads();
     const bool fb = fbs != 0;
-    if (tid < kEmitChunks) {
-        const uint64_t c = (uint64_t)blockIdx.x * kEmitChunks + tid;
+    if (tid < EC) {
+        const uint64_t c = (uint64_t)blockIdx.x * EC + tid;
         if (c <= a.nc) {
             // the chunk's counter, path bits, W, counts and positions, and its tile's entry, in one trip
             const uint32_t cnt = min(a.ccount[c], (uint32_t)kCand);
@@ -2335,8 +2340,13 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         hipLaunchKernelGGL(scan_tiles, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a);
         hipLaunchKernelGGL(scan_resolve, dim3(1), dim3(kResolveT), 0, stream, a, tiles);
     }
-    hipLaunchKernelGGL(scan_emit, dim3((unsigned)((chunks + kEmitChunks - 1) / kEmitChunks)), dim3(kScanT), 0, stream, a,
-                       tiles);
+    const int64_t ek = knob(NETC_GPU_KNOB_SCAN_EMIT_CHUNKS);
+    if (ek == kEmitChunksBig || (ek != kEmitChunks && chunks > kEmitBigAbove))
+        hipLaunchKernelGGL(scan_emit<kEmitChunksBig>, dim3((unsigned)((chunks + kEmitChunksBig - 1) / kEmitChunksBig)),
+                           dim3(kScanT), 0, stream, a, tiles);
+    else
+        hipLaunchKernelGGL(scan_emit<kEmitChunks>, dim3((unsigned)((chunks + kEmitChunks - 1) / kEmitChunks)), dim3(kScanT),
+                           0, stream, a, tiles);
     e = hipGetLastError();
     if (e != hipSuccess) s.dirty = true;   // a launch failed: the flags may be left set (lock still held)
     return e;

@@ -120,6 +120,21 @@ def layout(include_dir):
         return json.loads(subprocess.run([exe], capture_output=True, text=True, check=True).stdout)
 
 
+def test_every_knob_is_accepted_and_no_other():
+    """netc_gpu_knob (include/ws/mask.h): each NETC_GPU_KNOB_* the header declares, and the Python
+    mirror's names, is accepted (set, then restored to its default); 0 and the next index are not"""
+    from netc_amd import mask as nm
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "ws",
+                            "mask.h")).read()
+    declared = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define NETC_GPU_KNOB_(\w+)\s+(\d+)", hdr)}
+    assert declared == nm.KNOBS
+    g = _lib.gpu()
+    for k in declared.values():
+        assert g.netc_gpu_knob(k, -1) == 0, k
+    assert g.netc_gpu_knob(0, -1) != 0
+    assert g.netc_gpu_knob(max(declared.values()) + 1, -1) != 0
+
+
 def test_struct_layout_is_the_reference_layout():
     mine = layout(INCLUDE)
     golden = json.load(open(os.path.join(ROOT, "tests", "golden", "ws_layout.json")))

@@ -269,9 +269,10 @@ def test_repeat_calls_same_stream(torch_cuda):
         run_scan(torch_cuda, wire)
 
 
+@pytest.mark.parametrize("emit", [None, "64"])
 @pytest.mark.parametrize("slots", [None, "0", "3"])
 @pytest.mark.parametrize("masked,strict", [(True, True), (False, False)])
-def test_dense_chunks_parallel_walks(torch_cuda, gpu_knob, masked, strict, slots):
+def test_dense_chunks_parallel_walks(torch_cuda, gpu_knob, masked, strict, slots, emit):
     # chunks of 64+ frames (K2' and K4b': 16-hop links, anchored emit): uniform 16 / 8 B
     # payloads, empty frames (2-byte unmasked / 6-byte masked wire frames: up to 2,048
     # per chunk), mixes, and a long frame between; then truncations and start offsets
@@ -279,6 +280,7 @@ def test_dense_chunks_parallel_walks(torch_cuda, gpu_knob, masked, strict, slots
     # K2' anchor slots (None: one per chunk, K4b' emits from them; "0": none, every
     # dense chunk goes through the LDS emit; "3": both paths in one call)
     gpu_knob("SCAN_ANCHOR_SLOTS", slots)
+    gpu_knob("SCAN_EMIT_CHUNKS", emit)   # "64": the emit blocks of streams over 128 MiB
     rng = np.random.default_rng(41 + masked)
     sizes = np.concatenate([np.full(3000, 16), np.full(2500, 8), np.zeros(3000, dtype=np.int64),
                             rng.integers(0, 20, 3000), [70000], np.full(1000, 1)])
@@ -349,3 +351,34 @@ def test_fused_and_separate_launches(torch_cuda, gpu_knob, fuse):
         run_scan(torch_cuda, mixed[:int(wo[1500]) + 5], parallel=True)
         run_scan(torch_cuda, mixed, start=int(wo[2222]), parallel=True)
         run_scan(torch_cuda, big[:4096 * 300 + 7], parallel=True)     # a partial last tile
+
+
+@pytest.mark.parametrize("emit", ["64", "32"])
+def test_emit_block_sizes(torch_cuda, gpu_knob, emit):
+    """K4 (scan_emit) takes 32 chunks per block up to 128 MiB of stream and 64 above (knob
+    SCAN_EMIT_CHUNKS forces either): the C2 and C4 shapes, tiny frames, mixed sizes with 64-bit
+    lengths, non-strict streams, truncations, start offsets and the serial fallback, both ways"""
+    gpu_knob("SCAN_EMIT_CHUNKS", emit)
+    rng = np.random.default_rng(77)
+    wire, _ = _stream(rng, np.full(65536, 1024))
+    assert run_scan(torch_cuda, wire, parallel=True) == 65536
+    wire, _ = _stream(rng, rng.integers(256, 65537, 2000))
+    assert run_scan(torch_cuda, wire, parallel=True) == 2000
+    wire, _ = _stream(rng, rng.integers(0, 4, 20000))
+    assert run_scan(torch_cuda, wire, parallel=True) == 20000
+    sizes = np.concatenate([rng.integers(0, 5000, 300), rng.integers(0, 130, 300), [65535, 65536, 200000]])
+    rng.shuffle(sizes)
+    wire, wo = _stream(rng, sizes)
+    assert run_scan(torch_cuda, wire, parallel=True) == sizes.size
+    for cut in (1, int(wo[50]) + 1, int(wo[300]) + 3, wire.size - 1):
+        run_scan(torch_cuda, wire[:cut], parallel=True)
+    for st in (int(wo[1]), int(wo[477])):
+        run_scan(torch_cuda, wire, start=st, parallel=True)
+    wire, _ = _stream(rng, rng.integers(0, 126, 3000), masked=False)
+    assert run_scan(torch_cuda, wire, strict=False, parallel=True) == 3000
+    rec = b"".join(bytes.fromhex("82fe") + (5000 + i % 997).to_bytes(2, "big") + bytes(4) for i in range(997))
+    inner = np.tile(np.frombuffer(rec, dtype=np.uint8), 40)
+    off = np.array([0, inner.size, inner.size + 10], dtype=np.uint64)
+    payload = np.concatenate([inner, rng.integers(0, 256, 10, dtype=np.uint8)])
+    wire, _ = orc.encode_batch(payload, off, np.array([0, 0x01020304], dtype=np.uint32), None, True)
+    assert run_scan(torch_cuda, wire) == 2   # capacity overflow: the serial walk in K4

@@ -36,7 +36,7 @@ HOT = [
     "netc_gpu::scan_tiles_resolve(",
     "netc_gpu::scan_tiles(",
     "netc_gpu::scan_resolve(",
-    "netc_gpu::scan_emit(",
+    "void netc_gpu::scan_emit<",
     "void netc_gpu::scan_exits<",
     "netc_gpu::utf8_messages(",
 ]
