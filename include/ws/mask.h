@@ -154,8 +154,8 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *                      issued before the previous chunk is stored: 0 never; 1 2 KiB chunks at
  *                      5 wavefronts per SIMD; 2 4 KiB chunks at 4 [2 above 256 MiB of wire,
  *                      else 0]                                      (NETC_ENC_PF)
- *   SCAN_EMIT_CHUNKS   chunks per block of the frame scan's emit phase: 32 or 64 [32 up to
- *                      128 MiB of stream, 64 above]                 (NETC_SCAN_EMIT_CHUNKS)
+ *   SCAN_BLOCK_CHUNKS  chunks per block of the frame scan's link and emit phases: 32 or 64
+ *                      [32 up to 128 MiB of stream, 64 above]       (NETC_SCAN_BLOCK_CHUNKS)
  *   INJECT_FAULT       fault injection for tests: the ingest / egress ring submission this
  *                      countdown reaches (0 = the next one) fails as NETC_GPU_ELAUNCH
  *                      without launching, then the knob disarms itself [off]
@@ -173,7 +173,7 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
 #define NETC_GPU_KNOB_INJECT_FAULT     10
 #define NETC_GPU_KNOB_ENC_PROBE        11
 #define NETC_GPU_KNOB_ENC_PF           12
-#define NETC_GPU_KNOB_SCAN_EMIT_CHUNKS 13
+#define NETC_GPU_KNOB_SCAN_BLOCK_CHUNKS 13
 int netc_gpu_knob(int knob, int64_t value);
 
 /**

@@ -54,7 +54,7 @@ void knobs_init() {
     static const char* const env[kKnobs] = {nullptr, "NETC_ENC_DENSE_BYTES", "NETC_ENC_SCAN_PER", "NETC_SCAN_FAST_RANK",
                                             "NETC_SCAN_ANCHOR_SLOTS", "NETC_VAL_STEPS", "NETC_SCAN_FUSE", "NETC_MASK_TAPER",
                                             "NETC_ENC_SRC", "NETC_ENC_FIX", "NETC_INJECT_FAULT",
-                                            "NETC_ENC_PROBE", "NETC_ENC_PF", "NETC_SCAN_EMIT_CHUNKS"};
+                                            "NETC_ENC_PROBE", "NETC_ENC_PF", "NETC_SCAN_BLOCK_CHUNKS"};
     for (int k = 0; k < kKnobs; ++k) {
         const char* e = env[k] ? getenv(env[k]) : nullptr;
         g_knob[k].store(e && *e ? (int64_t)strtoll(e, nullptr, 10) : -1, std::memory_order_relaxed);

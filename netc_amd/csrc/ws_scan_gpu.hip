@@ -81,16 +81,18 @@ static constexpr int kMaxTiles = 8192;                        // K3b: tiles (8 G
 #define NETC_SCAN_BLK 32   // A/B builds
 #endif
 static constexpr int kBlkChunks = NETC_SCAN_BLK;              // K2: chunks per block
-// K4: chunks per block.  32 up to 128 MiB of stream (8,192 chunks at C2: 64 per block measured
-// 43.2 against 42.5 us, r03i2); 64 above, where most chunks hold no node and the blocks themselves
-// are the cost (C4: 2,049 blocks of 32 take 1.6 rounds at 5 per CU; 1,025 of 64 fit one).  Knob
-// SCAN_EMIT_CHUNKS picks either for any stream (tests, A/B).
-static constexpr int kEmitChunks = 32;
-static constexpr int kEmitChunksBig = 64;
-static constexpr uint64_t kEmitBigAbove = 32768;   // chunks (128 MiB)
+// K2 and K4 take twice the chunks per block above 128 MiB of stream, where most chunks hold no
+// node and the blocks themselves are the cost (C4: 2,049 blocks of 32 take 1.6 rounds at 5 per
+// CU; 1,025 of 64 fit one); K2 then runs two node slots per thread.  Up to 128 MiB 32 stay (C2:
+// 64 per K4 block measured 43.2 against 42.5 us, r03i2).  Knob SCAN_BLOCK_CHUNKS picks either for
+// any stream (tests, A/B).
+static constexpr int kEmitChunks = 32;          // K4: chunks per block
+static constexpr int kBlkChunksBig = 64;        // K2 and K4 above kBigBlocksAbove chunks
+static constexpr uint64_t kBigBlocksAbove = 32768;   // chunks (128 MiB)
 static_assert(kBlkChunks * kCand <= 256 && kTileChunks % kBlkChunks == 0, "K2: one thread per node slot");
 static_assert(kEmitChunks <= 256 && kTileChunks % kEmitChunks == 0, "K4: one thread per chunk, blocks inside a tile");
-static_assert(kEmitChunksBig <= 256 && kTileChunks % kEmitChunksBig == 0, "K4: one thread per chunk, blocks inside a tile");
+static_assert(kBlkChunksBig <= 256 && kTileChunks % kBlkChunksBig == 0 && kBlkChunksBig * kCand < 0xFFFF,
+              "K2 / K4: a thread per chunk (K4), node slots as 16-bit indexes (K2), blocks inside a tile");
 static constexpr int32_t kDupLink = -2;                       // K2: slot repeats an earlier slot's position
 static constexpr int kWalkHops = 64;                          // K2 / K4: frames walked one by one
 static constexpr int kList = 8;                               // K2 -> K4: frames recorded per node
@@ -844,7 +846,7 @@ __device__ __forceinline__ const uint16_t* chunk_links16(const ScanArgs& a, uint
     return src;
 }
 
-// K2: nodes of kBlkChunks chunks per block, one thread per slot: a repeated position
+// K2: nodes of BC chunks per block (kBlkChunks, or kBlkChunksBig: two slots per thread), one thread per slot: a repeated position
 // defers to its first slot (passing on its external flag); a node's chain is walked
 // from global memory to the candidate it exits to.  Chains of more than kWalkHops
 // frames in the chunk are finished by the whole block afterwards: the chunk's 16-hop
@@ -873,7 +875,9 @@ struct DenseLds {
     uint16_t sb[kDenseCand];
 };
 
-struct LinksLds {
+// BC chunks per block: kBlkChunks, or kBlkChunksBig for big streams (two node slots per thread)
+template <int BC>
+struct LinksLdsT {
     union {
         struct {
             uint32_t words[kWords];
@@ -883,9 +887,11 @@ struct LinksLds {
         } b;
         DenseLds w[kScanT / kWave];
     };
-    uint32_t queue[kBlkChunks * kCand];   // queued nodes; ~0u once the wavefront path took one
+    uint16_t queue[BC * kCand];   // queued nodes (slot in the block); kQTaken once the wavefront path took one
     int nq;
 };
+using LinksLds = LinksLdsT<kBlkChunks>;
+static constexpr uint16_t kQTaken = 0xFFFF;
 
 // the wavefront's LDS ops so far are visible to its other lanes
 __device__ __forceinline__ void wave_lds_sync() {
@@ -952,7 +958,7 @@ __device__ __forceinline__ void chunk_regs_store(uint32_t* words, const ChunkReg
 // One queued node by the calling wavefront, its chunk's words already in d.words (see DenseLds);
 // false (wave-uniform, nothing written) leaves it to the block path.  qi: its queue index
 // (anchor slot as the block path).  x: the node's position (a.cand[node]).
-template <bool SC1>
+template <bool SC1, int BC>
 __device__ __forceinline__ bool dense_node(const ScanArgs& a, DenseLds& d, uint64_t node, uint64_t x, uint32_t qi DENSE_ARG) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
@@ -1004,8 +1010,8 @@ __device__ __forceinline__ bool dense_node(const ScanArgs& a, DenseLds& d, uint6
     DENSE_T(4);
     if (__builtin_amdgcn_readfirstlane((int)e) == (int)kNoLink) return false;   // wave-uniform (not listed)
     // anchor j (every 8 frames from the entry) by lane j mod 64: s64^(j/8), then s8^(j%8)
-    const uint64_t q = (uint64_t)blockIdx.x * kBlkChunks + qi;
-    const bool keep = qi < (uint32_t)kBlkChunks && q < a.anc_cap;
+    const uint64_t q = (uint64_t)blockIdx.x * BC + qi;
+    const bool keep = qi < (uint32_t)BC && q < a.anc_cap;
     uint16_t* anc = a.anc + (keep ? q : 0) * kAncSlot;
     uint32_t na = 0;   // anchors (wave-uniform)
     for (int it = 0;; ++it) {
@@ -1058,19 +1064,20 @@ __device__ __forceinline__ bool dense_node(const ScanArgs& a, DenseLds& d, uint6
     return __builtin_amdgcn_readfirstlane(ok) != 0;
 }
 
-template <bool SC1>
-__device__ __forceinline__ void links_body(const ScanArgs& a, LinksLds& sl) {
+template <bool SC1, int BC>
+__device__ __forceinline__ void links_body(const ScanArgs& a, LinksLdsT<BC>& sl) {
     uint32_t* words = sl.b.words;
     uint16_t* l1 = sl.b.l1;
     uint16_t* lj = sl.b.lj;
     uint16_t* lk16 = sl.b.lk16;
-    uint32_t* queue = sl.queue;
+    uint16_t* queue = sl.queue;
+    const uint64_t blk0 = (uint64_t)blockIdx.x * (BC * kCand);   // the block's first node slot
     int& nq = sl.nq;
     const int tid = threadIdx.x;
     if (tid == 0) nq = 0;
     __syncthreads();
-    if (tid < kBlkChunks * kCand) {
-        const uint64_t s = (uint64_t)blockIdx.x * (kBlkChunks * kCand) + tid, c = s / kCand;
+    for (int t = tid; t < BC * kCand; t += kScanT) {   // (two slots per thread when BC = 64)
+        const uint64_t s = blk0 + (uint64_t)t, c = s / kCand;
         const uint32_t i = (uint32_t)(s % kCand);
         // the counter, the bucket (one line) and the external flags in one trip
         const uint32_t cc = c <= a.nc ? a.ccount[c] : 0;
@@ -1115,7 +1122,7 @@ __device__ __forceinline__ void links_body(const ScanArgs& a, LinksLds& sl) {
                         v = walk_frames<false>(a, B, nullptr, at, kWalkHops - kProbeHops, emit);
                 }
                 if (v == 0) {
-                    queue[atomicAdd(&nq, 1)] = (uint32_t)s;
+                    queue[atomicAdd(&nq, 1)] = (uint16_t)(s - blk0);
                 } else {
                     a.anq[s] = ~0u;
                     link_node<SC1>(a, s, x, v, cnt);
@@ -1135,17 +1142,17 @@ __device__ __forceinline__ void links_body(const ScanArgs& a, LinksLds& sl) {
         DenseLds& d = sl.w[wv];
         DENSE_ACC;
         ChunkRegs R;
-        bool rfast = wv < n && chunk_regs_load(a, (uint64_t)queue[wv] / kCand * kChunk, lane, R);
+        bool rfast = wv < n && chunk_regs_load(a, (blk0 + queue[wv]) / kCand * kChunk, lane, R);
         for (int qi = wv; qi < n; qi += kScanT / kWave) {
-            const uint64_t node = queue[qi];
+            const uint64_t node = blk0 + queue[qi];
 
             const uint64_t x = a.cand[node];   // (before the prefetch: a wait for it must not wait for that)
             if (rfast) chunk_regs_store(d.words, R, lane);
             else wave_load_chunk(a, node / kCand * kChunk, d.words, lane);
             const int qn = qi + kScanT / kWave;
-            rfast = qn < n && chunk_regs_load(a, (uint64_t)queue[qn] / kCand * kChunk, lane, R);
+            rfast = qn < n && chunk_regs_load(a, (blk0 + queue[qn]) / kCand * kChunk, lane, R);
             wave_lds_sync();
-            if (dense_node<SC1>(a, d, node, x, (uint32_t)qi DENSE_PASS) && lane == 0) queue[qi] = ~0u;
+            if (dense_node<SC1, BC>(a, d, node, x, (uint32_t)qi DENSE_PASS) && lane == 0) queue[qi] = kQTaken;
             wave_lds_sync();   // (the next chunk overwrites d)
         }
         DENSE_FLUSH();
@@ -1153,8 +1160,8 @@ __device__ __forceinline__ void links_body(const ScanArgs& a, LinksLds& sl) {
     __syncthreads();
     SCAN_STAMP(1, 2);   // dense chunks done
     for (int qi = 0; qi < n; ++qi) {
-        if (queue[qi] == ~0u) continue;   // block-uniform: taken by a wavefront
-        const uint64_t node = queue[qi], chunk = node / kCand, B = chunk * kChunk;
+        if (queue[qi] == kQTaken) continue;   // block-uniform: taken by a wavefront
+        const uint64_t node = blk0 + queue[qi], chunk = node / kCand, B = chunk * kChunk;
         load_chunk(a, B, words);
         chunk_links16(a, B, words, l1, lj, lk16);
         const uint16_t* l8 = lj;   // the 8-hop links (the pass before the last)
@@ -1163,8 +1170,8 @@ __device__ __forceinline__ void links_body(const ScanArgs& a, LinksLds& sl) {
             uint32_t p = (uint32_t)(x - B), hops = 0;
             // the walk's positions every 8 frames are K4's anchors if this node turns out
             // to be its chunk's true entry: kept in the block's slots while they last
-            const uint64_t q = (uint64_t)blockIdx.x * kBlkChunks + qi;
-            const bool keep = qi < kBlkChunks && q < a.anc_cap;
+            const uint64_t q = (uint64_t)blockIdx.x * BC + qi;
+            const bool keep = qi < BC && q < a.anc_cap;
             uint16_t* anc = a.anc + (keep ? q : 0) * kAncSlot;
             int na = 0;
             if (keep) anc[na++] = (uint16_t)p;
@@ -1190,10 +1197,11 @@ __device__ __forceinline__ void links_body(const ScanArgs& a, LinksLds& sl) {
     }
 }
 
+template <int BC>
 __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
-    __shared__ LinksLds sl;
+    __shared__ LinksLdsT<BC> sl;
     SCAN_SCOPE(1);
-    links_body<false>(a, sl);
+    links_body<false, BC>(a, sl);
 }
 
 // exclusive prefix sum over a block of NT threads; the block total in *total
@@ -1773,7 +1781,7 @@ __global__ __launch_bounds__(kScanT) void scan_links_fused(ScanArgs a, uint64_t 
     __shared__ FusedLds sm;
     __shared__ int flag;
     SCAN_SCOPE(1);
-    links_body<true>(a, sm.k2);
+    links_body<true, kBlkChunks>(a, sm.k2);
     constexpr uint32_t kPerTile = (uint32_t)(kTileChunks / kBlkChunks);
     const uint32_t tile = blockIdx.x / kPerTile;
     const uint32_t in_tile = min(blocks - tile * kPerTile, kPerTile);
@@ -1885,7 +1893,7 @@ __device__ __forceinline__ void put_frame(const ScanArgs& a, uint64_t k, uint64_
     }
 }
 
-// K4: the chunks' descriptors, EC chunks per block (kEmitChunks or kEmitChunksBig).  Thread t < EC
+// K4: the chunks' descriptors, EC chunks per block (kEmitChunks or kBlkChunksBig).  Thread t < EC
 // takes chunk t: its true entry is the node whose path bits hold the tile entry's bit;
 // a chunk of at most kWalkHops frames is walked by that thread (header bytes from
 // global memory).  Longer ones: with K2' anchors one wavefront per chunk, lane u
@@ -2330,19 +2338,27 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     // block and K3b for the last tile, so the overlap saves little, while the launch runs at the
     // fused LDS footprint (4 blocks per CU against K2's 5).  Not the default.)
     const int64_t fuse = knob(NETC_GPU_KNOB_SCAN_FUSE);
-    if (fuse == 1 && tiles <= (uint64_t)kFuseTiles) {
+    const int64_t bk = knob(NETC_GPU_KNOB_SCAN_BLOCK_CHUNKS);
+    const bool big = bk == kBlkChunksBig || (bk != kBlkChunks && chunks > kBigBlocksAbove);
+    auto links = [&]() {
+        if (big)
+            hipLaunchKernelGGL(scan_links<kBlkChunksBig>, dim3((unsigned)((chunks + kBlkChunksBig - 1) / kBlkChunksBig)),
+                               dim3(kScanT), 0, stream, a);
+        else
+            hipLaunchKernelGGL(scan_links<kBlkChunks>, dim3(blk), dim3(kScanT), 0, stream, a);
+    };
+    if (fuse == 1 && tiles <= (uint64_t)kFuseTiles) {   // (32 chunks per K2 block: the tiles' arrival counts)
         hipLaunchKernelGGL(scan_links_fused, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
     } else if (fuse != 0 && tiles <= (uint64_t)kMergeTiles) {
-        hipLaunchKernelGGL(scan_links, dim3(blk), dim3(kScanT), 0, stream, a);
+        links();
         hipLaunchKernelGGL(scan_tiles_resolve, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a, tiles);
     } else {
-        hipLaunchKernelGGL(scan_links, dim3(blk), dim3(kScanT), 0, stream, a);
+        links();
         hipLaunchKernelGGL(scan_tiles, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a);
         hipLaunchKernelGGL(scan_resolve, dim3(1), dim3(kResolveT), 0, stream, a, tiles);
     }
-    const int64_t ek = knob(NETC_GPU_KNOB_SCAN_EMIT_CHUNKS);
-    if (ek == kEmitChunksBig || (ek != kEmitChunks && chunks > kEmitBigAbove))
-        hipLaunchKernelGGL(scan_emit<kEmitChunksBig>, dim3((unsigned)((chunks + kEmitChunksBig - 1) / kEmitChunksBig)),
+    if (big)
+        hipLaunchKernelGGL(scan_emit<kBlkChunksBig>, dim3((unsigned)((chunks + kBlkChunksBig - 1) / kBlkChunksBig)),
                            dim3(kScanT), 0, stream, a, tiles);
     else
         hipLaunchKernelGGL(scan_emit<kEmitChunks>, dim3((unsigned)((chunks + kEmitChunks - 1) / kEmitChunks)), dim3(kScanT),

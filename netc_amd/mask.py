@@ -111,7 +111,7 @@ def tune(unroll: int = 1, max_blocks: int = 0, flags: int = NETC_GPU_TUNE_AUTO) 
 
 KNOBS = {"ENC_DENSE_BYTES": 1, "ENC_SCAN_PER": 2, "SCAN_FAST_RANK": 3, "SCAN_ANCHOR_SLOTS": 4, "VAL_STEPS": 5, "SCAN_FUSE": 6,
          "MASK_TAPER": 7, "ENC_SRC": 8, "ENC_FIX": 9, "INJECT_FAULT": 10,
-         "ENC_PROBE": 11, "ENC_PF": 12, "SCAN_EMIT_CHUNKS": 13}
+         "ENC_PROBE": 11, "ENC_PF": 12, "SCAN_BLOCK_CHUNKS": 13}
 
 
 def set_knob(name: str, value: int) -> None:

@@ -280,7 +280,7 @@ def test_dense_chunks_parallel_walks(torch_cuda, gpu_knob, masked, strict, slots
     # K2' anchor slots (None: one per chunk, K4b' emits from them; "0": none, every
     # dense chunk goes through the LDS emit; "3": both paths in one call)
     gpu_knob("SCAN_ANCHOR_SLOTS", slots)
-    gpu_knob("SCAN_EMIT_CHUNKS", emit)   # "64": the emit blocks of streams over 128 MiB
+    gpu_knob("SCAN_BLOCK_CHUNKS", emit)   # "64": the link and emit blocks of streams over 128 MiB
     rng = np.random.default_rng(41 + masked)
     sizes = np.concatenate([np.full(3000, 16), np.full(2500, 8), np.zeros(3000, dtype=np.int64),
                             rng.integers(0, 20, 3000), [70000], np.full(1000, 1)])
@@ -355,10 +355,10 @@ def test_fused_and_separate_launches(torch_cuda, gpu_knob, fuse):
 
 @pytest.mark.parametrize("emit", ["64", "32"])
 def test_emit_block_sizes(torch_cuda, gpu_knob, emit):
-    """K4 (scan_emit) takes 32 chunks per block up to 128 MiB of stream and 64 above (knob
-    SCAN_EMIT_CHUNKS forces either): the C2 and C4 shapes, tiny frames, mixed sizes with 64-bit
+    """K2 (scan_links) and K4 (scan_emit) take 32 chunks per block up to 128 MiB of stream and 64
+    above (knob SCAN_BLOCK_CHUNKS forces either): the C2 and C4 shapes, tiny frames, mixed sizes with 64-bit
     lengths, non-strict streams, truncations, start offsets and the serial fallback, both ways"""
-    gpu_knob("SCAN_EMIT_CHUNKS", emit)
+    gpu_knob("SCAN_BLOCK_CHUNKS", emit)
     rng = np.random.default_rng(77)
     wire, _ = _stream(rng, np.full(65536, 1024))
     assert run_scan(torch_cuda, wire, parallel=True) == 65536

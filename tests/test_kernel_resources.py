@@ -32,7 +32,7 @@ HOT = [
     "void netc_gpu::encode_frames_kernel<4, false, 4, true>",
     "void netc_gpu::wire_offsets_chained<4, false>",
     "void netc_gpu::wire_offsets_chained<16, false>",
-    "netc_gpu::scan_links(",
+    "void netc_gpu::scan_links<",
     "netc_gpu::scan_tiles_resolve(",
     "netc_gpu::scan_tiles(",
     "netc_gpu::scan_resolve(",
