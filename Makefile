@@ -25,14 +25,16 @@ GPU_HDRS   := netc_amd/csrc/ws_mask_gpu.h netc_amd/csrc/gpu_util.h include/ws/ma
 
 .PHONY: all host gpu oracle diag clean asan mock
 all: host gpu oracle mock
-mock: tests/bin/libnetc_ingest_mock.so
+mock: tests/bin/libnetc_ingest_mock.so tests/bin/ws_close_track_mock tests/bin/libnetc_hub_cpu.so tests/bin/ws_hub_server_cpu \
+      tests/bin/ws_egress_hub_server_cpu tests/bin/ws_echo_server_cpu
 host: $(LIBDIR)/libnetc.so
 gpu: $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc_ceiling.so tests/bin/ws_gpu_epoll tests/bin/ws_egress_bench \
-     tests/bin/ws_route_bench tests/bin/ws_hub_server tests/bin/ws_egress_hub_server tests/bin/ws_echo_server
+     tests/bin/ws_route_bench tests/bin/ws_hub_server tests/bin/ws_egress_hub_server tests/bin/ws_echo_server \
+     tests/bin/ws_close_track
 
 $(LIBDIR)/libnetc.so: $(HOST_SRCS) $(HOST_HDRS)
 	@mkdir -p $(LIBDIR)
-	$(CC) $(CFLAGS) -shared -o $@ $(HOST_SRCS) -lpthread
+	$(CC) $(CFLAGS) -shared -o $@ $(HOST_SRCS) -lpthread -ldl
 
 # one object per source (make -j compiles them in parallel), linked into one library
 GPU_OBJS   := $(patsubst netc_amd/csrc/%.hip,build/%.o,$(GPU_SRCS))
@@ -96,12 +98,36 @@ tests/bin/ws_egress_hub_server: tests/drivers/ws_egress_hub_server.c $(LIBDIR)/l
 	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -L$(LIBDIR) -lnetc_ws_gpu -lnetc -L/opt/rocm/lib -lamdhip64 \
 	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib -lpthread -ldl
 
+# close() on routed sockets in a process linked as netc links libnetc.so (tests/test_close_track.py):
+# against the GPU library, and against the mock (CPU suite)
+tests/bin/ws_close_track: tests/drivers/ws_close_track.c $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc.so $(HOST_HDRS)
+	@mkdir -p tests/bin
+	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -L$(LIBDIR) -lnetc_ws_gpu -lnetc -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib -lpthread -ldl
+tests/bin/ws_close_track_mock: tests/drivers/ws_close_track.c tests/bin/libnetc_ingest_mock.so $(LIBDIR)/libnetc.so $(HOST_HDRS)
+	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -Ltests/bin -lnetc_ingest_mock -L$(LIBDIR) -lnetc \
+	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -lpthread -ldl
+
+# MEASUREMENT CONTROL ONLY ("hubcpu" legs of tools/bench_hub.py): the hubs' and rings' host code with
+# the device work done on the host (tests/mockhip; netc_ws_mask for the XOR, libnetc's header walk),
+# at -O3, and the server drivers linked to it -- the same batching and syscalls as the GPU legs, so
+# the difference between "hub" and "hubcpu" is what the GPU itself adds or costs.  Never the product.
+tests/bin/libnetc_hub_cpu.so: netc_amd/csrc/ws_ingest.hip netc_amd/csrc/ws_hub.hip netc_amd/csrc/ws_egress_hub.hip tests/mockhip/mock_gpu.cc \
+                              tests/mockhip/hip/hip_runtime.h netc_amd/csrc/ws_mask_gpu.h $(LIBDIR)/libnetc.so $(HOST_HDRS)
+	@mkdir -p tests/bin
+	g++ -O3 -g -std=c++17 -fPIC -shared -Wall -Wno-unused-result -Itests/mockhip -x c++ netc_amd/csrc/ws_ingest.hip netc_amd/csrc/ws_hub.hip netc_amd/csrc/ws_egress_hub.hip \
+	    -x none tests/mockhip/mock_gpu.cc -L$(LIBDIR) -lnetc -Wl,-Bsymbolic -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -o $@
+tests/bin/%_cpu: tests/drivers/%.c tests/bin/libnetc_hub_cpu.so $(LIBDIR)/libnetc.so $(HOST_HDRS)
+	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -Ltests/bin -lnetc_hub_cpu -L$(LIBDIR) -lnetc \
+	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -lpthread -ldl
+
 oracle:
 	$(MAKE) -C oracle
 
 clean:
 	rm -f $(LIBDIR)/*.so build/*.o tests/bin/ws_gpu_epoll tests/bin/ws_egress_bench tests/bin/ws_route_bench \
-	    tests/bin/libnetc_ingest_mock.so tests/bin/ws_hub_server
+	    tests/bin/libnetc_ingest_mock.so tests/bin/ws_hub_server tests/bin/ws_egress_hub_server tests/bin/ws_echo_server \
+	    tests/bin/ws_close_track tests/bin/ws_close_track_mock tests/bin/libnetc_hub_cpu.so tests/bin/*_cpu
 	$(MAKE) -C oracle clean
 
 # diagnostics (tools/, not part of the product)
@@ -127,7 +153,7 @@ ASAN_TESTS := tests/test_host_framing.py tests/test_mask_cpu.py tests/test_oracl
               tests/test_utf8_oracle.py tests/test_route.py
 build/asan/libnetc.so: $(HOST_SRCS) $(HOST_HDRS)
 	@mkdir -p build/asan
-	$(CC) $(ASAN_FLAGS) -Wall -fPIC -std=gnu11 -shared -o $@ $(HOST_SRCS) -lpthread
+	$(CC) $(ASAN_FLAGS) -Wall -fPIC -std=gnu11 -shared -o $@ $(HOST_SRCS) -lpthread -ldl
 build/asan/liboracle.so: oracle/ws_oracle.c
 	@mkdir -p build/asan
 	$(CC) $(ASAN_FLAGS) -Wall -fPIC -shared -o $@ $<

@@ -30,10 +30,18 @@
  * order they were queued (include/ws/egress.h lists the rules: the reference's split, header
  * forms, one key per message, each frame masked from its own first byte).
  *
- * Sends block, as ws_send_message's do: a socket whose buffer is full is waited for (POLLOUT),
- * so one slow client delays the flush.  A connection whose send() fails (the peer went away)
- * drops its remaining bytes; its next ws_send_message returns -1 (netc_errno_reason BADSEND) and
- * the failure is counted in the stats.  A message larger than slot_bytes, or in more frames than
+ * Sends never wait (round 6): each connection's bytes leave with sendmsg(MSG_DONTWAIT), and what
+ * its socket does not take moves to the connection's send backlog (include/ws/route.h), so the
+ * slot is free at once and a client that stops reading delays nobody else.  The backlog goes
+ * out ahead of the connection's later bytes at the next flush (or ws_send_message /
+ * ws_parse_frame / netc_ws_send_flush on it); netc_ws_egress_hub_pending says how much is
+ * held.  A backlog past its bound (netc_ws_send_backlog_limit) fails that connection alone.  A
+ * connection whose send() fails (the peer went away) drops its remaining bytes; its next
+ * ws_send_message returns -1 (netc_errno_reason BADSEND) and the failure is counted in the
+ * stats.  A close frame (WS_OPCODE_CLOSE) is flushed as soon as it is queued, with everything
+ * before it: netc closes the socket right after sending one (src/ws/server.c:123-124); with
+ * close tracking (include/ws/route.h) a close() on an attached socket flushes and detaches it
+ * first, so nothing queued for it is lost.  A message larger than slot_bytes, or in more frames than
  * a slot's table holds, is refused (-1, NETC_WS_EGRESS_TOO_BIG in netc_gpu_strerror).
  *
  * Threading: a hub is driven by one thread, the event loop's.  Errors as in include/ws/mask.h.
@@ -67,20 +75,26 @@ void netc_ws_egress_hub_destroy(struct netc_ws_egress_hub *hub);
 int netc_ws_gpu_attach_send_hub(int sockfd, struct netc_ws_egress_hub *hub);
 
 /**
- * Sends every message the hub holds (ws_send_message returned 1 for them), then drops the
- * socket's route.  0, or the flush's negative code (the route is dropped either way).
+ * Sends every message the hub holds for the socket (ws_send_message returned 1 for them; what its
+ * socket does not take now stays in its backlog, ahead of its later CPU-path bytes), then drops
+ * the socket's route.  0, or the flush's negative code (the route is dropped either way).
  */
 int netc_ws_gpu_detach_send_hub(int sockfd);
 
 /**
  * Every queued message framed on the GPU and sent: the filling slot is submitted, then each
- * slot in queue order is waited for and its connections' bytes are sent.  Bytes sent (>= 0), or
+ * slot in queue order is waited for and its connections' bytes are sent, never waiting for a
+ * socket (what one does not take is held in its backlog), then the backlogs are written as far
+ * as their sockets take them.  Bytes handed to the sockets or their backlogs (>= 0), or
  * a negative code for a device failure.  Per-connection send failures do not fail the flush.
  * A slot whose wire the device does not vouch for (its wire length is not the host's) fails
  * each of its connections as a failed send does, and the flush returns NETC_GPU_ERUNTIME after
  * sending the later slots; the hub goes on serving the other connections.
  */
 long netc_ws_egress_hub_flush(struct netc_ws_egress_hub *hub);
+
+/** Bytes the hub's connections hold in their send backlogs (0: everything is on the sockets). */
+long netc_ws_egress_hub_pending(const struct netc_ws_egress_hub *hub);
 
 /** Counters since creation. */
 struct netc_ws_egress_hub_stats
@@ -94,6 +108,8 @@ struct netc_ws_egress_hub_stats
     uint64_t sendmsg_calls;     /* sendmsg() calls that put those bytes on the sockets */
     uint64_t send_errors;       /* connections whose send() failed */
     uint64_t connections;       /* connections attached now */
+    uint64_t deferred_sends;    /* times a connection's socket left bytes for its send backlog */
+    uint64_t pending_bytes;     /* bytes its connections' backlogs hold now */
 };
 int netc_ws_egress_hub_stats(const struct netc_ws_egress_hub *hub, struct netc_ws_egress_hub_stats *out);
 

@@ -12,7 +12,8 @@
  * slice (B2); masked binary payloads of any length (B1) and TEXT payloads with
  * embedded NULs (B3) are sent from payload_length, not strlen / the header
  * byte; frames are assembled on the heap, not a stack VLA (B4); short writes
- * are completed (B5); a masked empty payload still carries its key (RFC 6455
+ * are completed without waiting for the peer: what a non-blocking socket does not
+ * take is kept in the connection's send backlog (include/ws/route.h) (B5); a masked empty payload still carries its key (RFC 6455
  * §5.2); a recv() error no longer corrupts the buffer bookkeeping (B6); split
  * masking keys / extended lengths are resumed by byte count, not by a zero-byte
  * heuristic (B7, B8).
@@ -24,15 +25,10 @@
 #include "../../../include/utils/error.h"
 
 #include <errno.h>
-#include <poll.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/socket.h>
 #include <sys/uio.h>
-
-#ifndef MSG_NOSIGNAL
-#define MSG_NOSIGNAL 0
-#endif
 
 /*
  * struct web_client (reference include/web/client.h:12-100) begins with
@@ -68,44 +64,6 @@ void ws_build_message(struct ws_message *message, uint8_t opcode, uint64_t paylo
 }
 
 /* ------------------------------------------------------------------ send -- */
-
-/* writes every byte of the iovec list; returns 1, or the failing send result (<= 0) */
-static int send_all(socket_t fd, struct iovec *iov, int iovcnt)
-{
-    while (iovcnt > 0)
-    {
-        struct msghdr msg;
-        memset(&msg, 0, sizeof(msg));
-        msg.msg_iov = iov;
-        msg.msg_iovlen = (size_t)iovcnt;
-        const ssize_t r = sendmsg(fd, &msg, MSG_NOSIGNAL);
-        if (r < 0)
-        {
-            if (errno == EINTR) continue;
-            if (errno == EAGAIN || errno == EWOULDBLOCK)
-            {
-                struct pollfd p = {.fd = fd, .events = POLLOUT};
-                if (poll(&p, 1, -1) >= 0 || errno == EINTR) continue;
-            }
-            (void)netc_error(BADSEND);
-            return -1;
-        }
-        if (r == 0) return 0;
-        size_t left = (size_t)r;
-        while (iovcnt > 0 && left >= iov->iov_len)
-        {
-            left -= iov->iov_len;
-            ++iov;
-            --iovcnt;
-        }
-        if (iovcnt > 0)
-        {
-            iov->iov_base = (char *)iov->iov_base + left;
-            iov->iov_len -= left;
-        }
-    }
-    return 1;
-}
 
 /* header of one frame into out (<= 14 bytes); returns its length */
 static size_t encode_header(uint8_t *out, int fin, uint8_t opcode, const uint8_t *key, uint64_t len)
@@ -172,13 +130,13 @@ int ws_send_message(struct web_client *client, struct ws_message *message, uint8
             memcpy(frame, hdr, hlen);
             netc_ws_mask(frame + hlen, payload + passed, (size_t)flen, masking_key, 0);
             struct iovec iov[1] = {{frame, hlen + flen}};
-            r = send_all(fd, iov, 1);
+            r = netc_ws_send_nb((int)fd, iov, 1, 0);
             free(frame);
         }
         else
         {
             struct iovec iov[2] = {{hdr, hlen}, {(void *)(payload + passed), (size_t)flen}};
-            r = send_all(fd, iov, flen ? 2 : 1);
+            r = netc_ws_send_nb((int)fd, iov, flen ? 2 : 1, 0);
         }
         if (r <= 0) return r;
         passed += flen;
@@ -217,6 +175,8 @@ int ws_parse_frame(struct web_client *client, struct ws_frame_parsing_state *st,
        netc_ws_gpu_attach) is served by it, with this function's contract */
     void *route_ctx = NULL;
     const netc_ws_route_fn route = netc_ws_route_get((int)fd, &route_ctx);
+    /* the connection is readable: a send backlog it holds goes out first, without waiting */
+    if (netc_ws_send_pending((int)fd) > 0) (void)netc_ws_send_flush((int)fd);
     if (route) return route(route_ctx, (int)fd, st, MAX_PAYLOAD_LENGTH);
 
     for (;;)

@@ -20,7 +20,6 @@
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
-#include <poll.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -209,27 +208,16 @@ int acquire(netc_ws_egress* g) {
     return 0;
 }
 
-// every byte of [p, p + n) on fd; a send that would block waits for POLLOUT (as ws_send_message)
+// [p, p + n) on fd without waiting for the peer: what the socket does not take joins the
+// connection's send backlog (include/ws/route.h), ahead of its later bytes
 int send_all(int fd, const uint8_t* p, uint64_t n) {
-    while (n) {
-        const ssize_t r = send(fd, p, n, MSG_NOSIGNAL);
-        if (r < 0) {
-            if (errno == EINTR) continue;
-            if (errno == EAGAIN || errno == EWOULDBLOCK) {
-                struct pollfd q = {fd, POLLOUT, 0};
-                if (poll(&q, 1, -1) >= 0 || errno == EINTR) continue;
-            }
-            const int saved = errno;
-            api_fail(NETC_WS_EGRESS_ESEND, "egress: send: %s", strerror(saved));
-            netc_errno_reason = kBadSend;
-            errno = saved;
-            return NETC_WS_EGRESS_ESEND;
-        }
-        if (r == 0) return api_fail(NETC_WS_EGRESS_ESEND, "egress: send() wrote nothing");
-        p += r;
-        n -= (uint64_t)r;
-    }
-    return 0;
+    struct iovec v = {(void*)p, (size_t)n};
+    if (netc_ws_send_nb(fd, &v, 1, 1) == 1) return 0;
+    const int saved = errno;
+    api_fail(NETC_WS_EGRESS_ESEND, "egress: send: %s", strerror(saved));
+    netc_errno_reason = kBadSend;
+    errno = saved;
+    return NETC_WS_EGRESS_ESEND;
 }
 
 }  // namespace
@@ -411,10 +399,15 @@ static int gpu_send_route(void* ctx, int sockfd, struct ws_message* message, uin
                                  num_frames);
     }
     if (r) return -1;
-    const long s = (g->flags & NETC_WS_EGRESS_DEFER) ? netc_ws_egress_send(g, sockfd, 0)
-                                                     : netc_ws_egress_flush(g, sockfd);
+    // a DEFER ring sends what has finished; a close frame goes out at once, with everything
+    // queued before it (netc closes the socket right after sending one, src/ws/server.c:123-124)
+    const bool now = !(g->flags & NETC_WS_EGRESS_DEFER) || message->opcode == WS_OPCODE_CLOSE;
+    const long s = now ? netc_ws_egress_flush(g, sockfd) : netc_ws_egress_send(g, sockfd, 0);
     return s < 0 ? -1 : 1;
 }
+
+// close() on the attached socket (close tracking, include/ws/route.h): what it queued goes out first
+static void ring_close_hook(void* ctx, int sockfd) { (void)netc_ws_gpu_detach_send(sockfd); }
 
 static bool sock_identity(int fd, uint64_t* dev, uint64_t* ino) {
     struct stat st;
@@ -453,6 +446,7 @@ int netc_ws_gpu_attach_send(int sockfd, struct netc_ws_egress* ring) {
     ring->owner_fd = sockfd;
     ring->owner_dev = dev;
     ring->owner_ino = ino;
+    (void)netc_ws_send_route_on_close(sockfd, ring_close_hook);
     return 0;
 }
 

@@ -11,15 +11,16 @@
 //            assembly (launch_encode_frames: ONE launch when every frame of the slot is in one
 //            length class -- the host saw each length -- else the wire-offsets scan first), D2H
 //            of the wire into the slot's pinned wire buffer and of the device's wire length
-//   send     once its event is done: per connection, one sendmsg() over iovecs of its messages'
-//            runs in the wire (a connection's consecutive messages are one run), then the slot
-//            is free.  Slots go out in the order they were filled, so a connection's bytes keep
-//            its queue order.
+//   send     once its event is done: per connection, one sendmsg(MSG_DONTWAIT) over iovecs of its
+//            messages' runs in the wire (a connection's consecutive messages are one run); what
+//            the socket does not take moves to the connection's send backlog (libnetc.so,
+//            include/ws/route.h), which goes out ahead of its later bytes; then the slot is
+//            free.  Slots go out in the order they were filled, so a connection's bytes keep its
+//            queue order, and a peer that stops reading holds up nobody but itself.
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
 #include <limits.h>
-#include <poll.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -57,7 +58,9 @@ struct EhConn {
     int fd = -1;
     uint64_t dev = 0, ino = 0;
     int failed = 0;             // send() failed: its bytes are dropped, its calls return -1
+    bool deferred = false;      // its send backlog holds bytes (on the hub's deferred list)
     uint64_t last_gen = 0;      // the slot filling this connection last queued into
+    uint64_t queued = 0;        // its messages in slots not yet sent
     std::vector<struct iovec> iov;   // flush scratch: its runs in the slot being sent
 };
 
@@ -105,6 +108,14 @@ inline uint64_t header_len(uint64_t payload, bool masked) {   // src/ws/common.c
     return 2 + (payload <= 125 ? 0 : (payload <= 0xFFFF ? 2 : 8)) + (masked ? 4 : 0);
 }
 
+bool sock_identity(int fd, uint64_t* dev, uint64_t* ino) {
+    struct stat st;
+    if (fstat(fd, &st) != 0 || !S_ISSOCK(st.st_mode)) return false;
+    *dev = (uint64_t)st.st_dev;
+    *ino = (uint64_t)st.st_ino;
+    return true;
+}
+
 }  // namespace
 
 struct netc_ws_egress_hub {
@@ -116,6 +127,7 @@ struct netc_ws_egress_hub {
     std::deque<int> fifo;        // submitted slots, oldest first
     uint64_t gens = 0;
     std::unordered_map<int, EhConn*> conns;
+    std::vector<EhConn*> deferred;   // connections whose send backlog holds bytes
     struct netc_ws_egress_hub_stats st{};
 };
 
@@ -208,39 +220,37 @@ int submit(netc_ws_egress_hub* h) {
     return 0;
 }
 
-// every byte of the iovecs on fd; a send that would block waits for POLLOUT (as ws_send_message)
-int send_iov(netc_ws_egress_hub* h, int fd, struct iovec* iov, size_t cnt) {
-    while (cnt) {
-        struct msghdr mh;
-        memset(&mh, 0, sizeof mh);
-        mh.msg_iov = iov;
-        mh.msg_iovlen = cnt < (size_t)IOV_MAX ? cnt : (size_t)IOV_MAX;
-        const ssize_t r = sendmsg(fd, &mh, MSG_NOSIGNAL);
-        if (r < 0) {
-            if (errno == EINTR) continue;
-            if (errno == EAGAIN || errno == EWOULDBLOCK) {
-                struct pollfd q = {fd, POLLOUT, 0};
-                if (poll(&q, 1, -1) >= 0 || errno == EINTR) continue;
-            }
-            return -1;
-        }
-        if (r == 0) {
-            errno = EPIPE;
-            return -1;
-        }
-        h->st.sendmsg_calls++;
-        size_t left = (size_t)r;
-        while (cnt && left >= iov->iov_len) {
-            left -= iov->iov_len;
-            ++iov;
-            --cnt;
-        }
-        if (cnt && left) {
-            iov->iov_base = (uint8_t*)iov->iov_base + left;
-            iov->iov_len -= left;
-        }
+// the connection's send backlog after a send: still holding bytes (kept on the deferred list), or
+// failed past its bound
+void note_backlog(netc_ws_egress_hub* h, EhConn* c) {
+    const long p = netc_ws_send_pending(c->fd);
+    if (p < 0) {
+        c->failed = errno ? errno : ENOBUFS;
+        h->st.send_errors++;
+    } else if (p > 0 && !c->deferred) {
+        c->deferred = true;
+        h->deferred.push_back(c);
+        h->st.deferred_sends++;
     }
-    return 0;
+}
+
+// the deferred connections' backlogs, written as far as their sockets take them now
+void drain_deferred(netc_ws_egress_hub* h) {
+    size_t keep = 0;
+    for (size_t i = 0; i < h->deferred.size(); ++i) {
+        EhConn* c = h->deferred[i];
+        const long r = c->failed ? -1 : netc_ws_send_flush(c->fd);
+        if (r > 0) {
+            h->deferred[keep++] = c;
+            continue;
+        }
+        if (r < 0 && !c->failed) {
+            c->failed = errno ? errno : EPIPE;
+            h->st.send_errors++;
+        }
+        c->deferred = false;
+    }
+    h->deferred.resize(keep);
 }
 
 // wait for the oldest submitted slot and put its connections' bytes on their sockets; bytes sent.
@@ -273,6 +283,7 @@ long send_oldest(netc_ws_egress_hub* h, bool* dropped) {
     for (const Span& sp : s.spans) {
         EhConn* c = sp.conn;
         if (!c) continue;   // detached since
+        if (c->queued) --c->queued;
         if (c->iov.empty()) order.push_back(c);
         struct iovec* last = c->iov.empty() ? nullptr : &c->iov.back();
         if (last && (uint8_t*)last->iov_base + last->iov_len == s.h_wire + sp.w0) last->iov_len += sp.w1 - sp.w0;
@@ -280,11 +291,21 @@ long send_oldest(netc_ws_egress_hub* h, bool* dropped) {
     }
     long sent = 0;
     for (EhConn* c : order) {
+        // a connection closed without a detach that close tracking did not see (a raw close, a
+        // process where close() does not reach libnetc.so): its descriptor may name another
+        // connection by now, which must not get these bytes.  One fstat per connection per slot.
+        uint64_t d = 0, ino = 0;
+        if (!c->failed && !(sock_identity(c->fd, &d, &ino) && d == c->dev && ino == c->ino)) {
+            c->failed = EBADF;
+            h->st.send_errors++;
+        }
         if (!c->failed) {
             uint64_t n = 0;
             for (const struct iovec& v : c->iov) n += v.iov_len;
-            if (send_iov(h, c->fd, c->iov.data(), c->iov.size()) == 0) {
+            if (netc_ws_send_nb(c->fd, c->iov.data(), (int)c->iov.size(), 1) == 1) {
                 sent += (long)n;
+                h->st.sendmsg_calls++;
+                note_backlog(h, c);
             } else {
                 c->failed = errno ? errno : EPIPE;
                 h->st.send_errors++;
@@ -333,7 +354,10 @@ int queue(netc_ws_egress_hub* h, EhConn* c, const void* payload, size_t len, uin
     if (int r = acquire(h)) return r;
     {
         const EhSlot& s = h->slots[h->cur];
-        if (s.frames && (s.masked != masked || s.fill + len > h->slot_bytes || s.frames + nf > h->max_frames)) {
+        // a slot past its full mark is one whose submission failed: tried again (and reported)
+        // before anything more is queued; a message that does not fit starts the next slot
+        const bool full = s.fill + 4096 > h->slot_bytes || s.frames + 64 > h->max_frames;
+        if (s.frames && (full || s.masked != masked || s.fill + len > h->slot_bytes || s.frames + nf > h->max_frames)) {
             if (int e = submit(h)) return e;
             if (int r = acquire(h)) return r;
         }
@@ -360,6 +384,7 @@ int queue(netc_ws_egress_hub* h, EhConn* c, const void* payload, size_t len, uin
         s.ext = s.ext == -2 || s.ext == ext ? ext : -1;
     }
     s.spans.push_back(Span{c, s.wire, s.wire + wire});
+    ++c->queued;
     if (c->last_gen != s.gen) {
         c->last_gen = s.gen;
         ++s.nconn;
@@ -368,7 +393,7 @@ int queue(netc_ws_egress_hub* h, EhConn* c, const void* payload, size_t len, uin
     s.frames += nf;
     s.wire += wire;
     // full: on its way now.  The message is queued either way; a failed submission leaves the slot
-    // filling, and the next queue or flush tries again and reports it (before queueing anything).
+    // filling, and the next queue or flush tries it again and reports it (before queueing anything).
     if (s.fill + 4096 > h->slot_bytes || s.frames + 64 > h->max_frames) (void)submit(h);
     return 0;
 }
@@ -384,15 +409,8 @@ long flush(netc_ws_egress_hub* h) {
         if (r < 0) err = r;
         else sent += r;
     }
+    drain_deferred(h);
     return err ? err : sent;
-}
-
-bool sock_identity(int fd, uint64_t* dev, uint64_t* ino) {
-    struct stat st;
-    if (fstat(fd, &st) != 0 || !S_ISSOCK(st.st_mode)) return false;
-    *dev = (uint64_t)st.st_dev;
-    *ino = (uint64_t)st.st_ino;
-    return true;
 }
 
 // ws_send_message on a socket attached to an egress hub (include/ws/egress_hub.h)
@@ -410,14 +428,36 @@ int hub_send_route(void* ctx, int sockfd, struct ws_message* message, uint8_t ma
         errno = c->failed;
         return -1;
     }
+    if (c->deferred && netc_ws_send_pending(sockfd) < 0) {   // its backlog passed the bound
+        c->failed = errno ? errno : ENOBUFS;
+        h->st.send_errors++;
+        api_fail(NETC_WS_EGRESS_ESEND, "egress hub: socket %d: %s", sockfd, strerror(c->failed));
+        netc_errno_reason = kBadSend;
+        errno = c->failed;
+        return -1;
+    }
     if (queue(h, c, message->buffer, message->payload_length, message->opcode, masking_key, num_frames)) return -1;
+    // a close frame goes out now: netc closes the socket right after sending it
+    // (src/ws/server.c:123-124), and everything queued before it must precede it on the wire
+    if (message->opcode == WS_OPCODE_CLOSE) {
+        DeviceGuard dg(h->device);
+        if (flush(h) < 0) return -1;
+    }
     return 1;
 }
+
+// close() on an attached socket (close tracking, include/ws/route.h): what was queued for it goes out
+void hub_close_hook(void* ctx, int sockfd) { (void)netc_ws_gpu_detach_send_hub(sockfd); }
 
 void forget(netc_ws_egress_hub* h, EhConn* c) {   // spans queued for it are skipped when sent
     for (int i = 0; i < h->nslots; ++i)
         for (Span& sp : h->slots[i].spans)
             if (sp.conn == c) sp.conn = nullptr;
+    for (size_t i = 0; i < h->deferred.size(); ++i)
+        if (h->deferred[i] == c) {
+            h->deferred.erase(h->deferred.begin() + (long)i);
+            break;
+        }
     delete c;
 }
 
@@ -506,6 +546,7 @@ int netc_ws_gpu_attach_send_hub(int sockfd, struct netc_ws_egress_hub* h) {
     }
     h->conns[sockfd] = c;
     h->st.connections = h->conns.size();
+    (void)netc_ws_send_route_on_close(sockfd, hub_close_hook);
     return 0;
 }
 
@@ -522,7 +563,7 @@ int netc_ws_gpu_detach_send_hub(int sockfd) {
             uint64_t d = 0, i = 0;
             if (!(sock_identity(sockfd, &d, &i) && d == it->second->dev && i == it->second->ino))
                 it->second->failed = EBADF;   // closed without a detach: its bytes have nowhere to go
-            flushed = flush(h);
+            if (it->second->queued || it->second->deferred) flushed = flush(h);
             forget(h, it->second);
             h->conns.erase(it);
             h->st.connections = h->conns.size();
@@ -540,9 +581,20 @@ long netc_ws_egress_hub_flush(struct netc_ws_egress_hub* h) {
     return flush(h);
 }
 
+long netc_ws_egress_hub_pending(const struct netc_ws_egress_hub* h) {
+    if (!h) return api_fail(NETC_GPU_EINVAL, "egress hub: null hub");
+    long n = 0;
+    for (EhConn* c : h->deferred) {
+        const long p = c->failed ? 0 : netc_ws_send_pending(c->fd);
+        if (p > 0) n += p;
+    }
+    return n;
+}
+
 int netc_ws_egress_hub_stats(const struct netc_ws_egress_hub* h, struct netc_ws_egress_hub_stats* out) {
     if (!h || !out) return NETC_GPU_EINVAL;
     *out = h->st;
+    out->pending_bytes = (uint64_t)netc_ws_egress_hub_pending(h);
     return 0;
 }
 

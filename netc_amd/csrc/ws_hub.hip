@@ -122,6 +122,7 @@ struct netc_ws_hub {
     HubSlot* slots = nullptr;
     int cur = -1;                // the filling slot
     uint64_t gens = 0;
+    uint64_t swept_gen = ~0ull;  // the generation a full pool last looked for closed holders at
     std::unordered_map<int, HubConn*> conns;
     struct netc_ws_hub_stats st{};
 };
@@ -163,19 +164,50 @@ void maybe_free(HubSlot& s) {
     if (s.refs == 0 && s.state == kDone) s.state = kFree;
 }
 
+void drop_conn(netc_ws_hub* h, HubConn* c);
+bool sock_identity(int fd, uint64_t* dev, uint64_t* ino);
+int hub_route(void* ctx, int sockfd, struct ws_frame_parsing_state* state, size_t max_payload_length);
+
+// Connections closed without a detach that close tracking did not see (include/ws/route.h): their
+// undelivered frames pin slots nobody will drain.  Dropped, with their routes; how many.
+size_t sweep_closed(netc_ws_hub* h) {
+    size_t n = 0;
+    for (auto it = h->conns.begin(); it != h->conns.end();) {
+        uint64_t d = 0, i = 0;
+        HubConn* c = it->second;
+        if (!c->ranges.empty() && !(sock_identity(c->fd, &d, &i) && d == c->dev && i == c->ino)) {
+            void* ctx = nullptr;
+            if (netc_ws_route_get_raw(c->fd, &ctx) == hub_route && ctx == h) (void)netc_ws_route_detach(c->fd);
+            drop_conn(h, c);
+            it = h->conns.erase(it);
+            ++n;
+        } else {
+            ++it;
+        }
+    }
+    h->st.connections = h->conns.size();
+    return n;
+}
+
 // the filling slot, a new one if there is none; -1 (FULL) when every slot holds undelivered frames
 int acquire(netc_ws_hub* h) {
     if (h->cur >= 0) return h->cur;
-    for (int i = 0; i < h->nslots; ++i) {
-        HubSlot& s = h->slots[i];
-        if (s.state == kInflight && s.refs == 0 && hipEventQuery(s.done) == hipSuccess) s.state = kDone;
-        maybe_free(s);
-        if (s.state != kFree) continue;
-        s.state = kFilling;
-        s.fill = s.nframes = 0;
-        s.refs = s.nconn = 0;
-        s.gen = ++h->gens;
-        return h->cur = i;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int i = 0; i < h->nslots; ++i) {
+            HubSlot& s = h->slots[i];
+            if (s.state == kInflight && s.refs == 0 && hipEventQuery(s.done) == hipSuccess) s.state = kDone;
+            maybe_free(s);
+            if (s.state != kFree) continue;
+            s.state = kFilling;
+            s.fill = s.nframes = 0;
+            s.refs = s.nconn = 0;
+            s.gen = ++h->gens;
+            return h->cur = i;
+        }
+        // every slot is held: once per filling generation, look for holders that are gone
+        if (pass || h->swept_gen == h->gens) break;
+        h->swept_gen = h->gens;
+        if (!sweep_closed(h)) break;
     }
     return -1;
 }
@@ -493,6 +525,9 @@ bool sock_identity(int fd, uint64_t* dev, uint64_t* ino) {
     return true;
 }
 
+// close() on an attached socket (close tracking, include/ws/route.h): its frames stop holding slots
+void hub_close_hook(void* ctx, int sockfd) { (void)netc_ws_gpu_detach_hub(sockfd); }
+
 // ws_parse_frame on a socket attached to a hub (include/ws/hub.h)
 int hub_route(void* ctx, int sockfd, struct ws_frame_parsing_state* state, size_t max_payload_length) {
     netc_ws_hub* h = (netc_ws_hub*)ctx;
@@ -631,6 +666,7 @@ int netc_ws_gpu_attach_hub(int sockfd, struct netc_ws_hub* h) {
     }
     h->conns[sockfd] = c;
     h->st.connections = h->conns.size();
+    (void)netc_ws_route_on_close(sockfd, hub_close_hook);
     return 0;
 }
 

@@ -802,6 +802,9 @@ static bool sock_identity(int fd, uint64_t* dev, uint64_t* ino) {
     return true;
 }
 
+// close() on the attached socket (close tracking, include/ws/route.h): the ring lets go of it
+static void ingest_close_hook(void* ctx, int sockfd) { (void)netc_ws_gpu_detach(sockfd); }
+
 int netc_ws_gpu_attach(int sockfd, struct netc_ws_ingest* ring) {
     if (!ring) return api_fail(NETC_GPU_EINVAL, "attach: null ring");
     uint64_t dev = 0, ino = 0;
@@ -836,6 +839,7 @@ int netc_ws_gpu_attach(int sockfd, struct netc_ws_ingest* ring) {
     rs.ino = ino;
     rs.tcp = domain == AF_INET || domain == AF_INET6;
     rs.sock_pos = 0;
+    (void)netc_ws_route_on_close(sockfd, ingest_close_hook);
     return 0;
 }
 

@@ -102,7 +102,8 @@ class EgressHubStats(ctypes.Structure):
     _fields_ = [("launches", ctypes.c_uint64), ("messages", ctypes.c_uint64), ("frames", ctypes.c_uint64),
                 ("wire_bytes", ctypes.c_uint64), ("max_connections", ctypes.c_uint64),
                 ("connection_slots", ctypes.c_uint64), ("sendmsg_calls", ctypes.c_uint64),
-                ("send_errors", ctypes.c_uint64), ("connections", ctypes.c_uint64)]
+                ("send_errors", ctypes.c_uint64), ("connections", ctypes.c_uint64),
+                ("deferred_sends", ctypes.c_uint64), ("pending_bytes", ctypes.c_uint64)]
 
 
 def _bind_send(lib):
@@ -121,6 +122,8 @@ def _bind_send(lib):
     lib.netc_ws_egress_hub_flush.restype = ctypes.c_long
     lib.netc_ws_egress_hub_stats.argtypes = [vp, ctypes.POINTER(EgressHubStats)]
     lib.netc_ws_egress_hub_stats.restype = ctypes.c_int
+    lib.netc_ws_egress_hub_pending.argtypes = [vp]
+    lib.netc_ws_egress_hub_pending.restype = ctypes.c_long
     lib.netc_gpu_strerror.restype = ctypes.c_char_p
     lib._egress_hub_bound = True
     return lib
@@ -153,6 +156,23 @@ class EgressHub:
         if r < 0:
             Hub._raise(int(r), self._lib)
         return int(r)
+
+    def pending(self) -> int:
+        """bytes the hub's connections hold in their send backlogs (sockets that were full)"""
+        return int(self._lib.netc_ws_egress_hub_pending(self._h))
+
+    def drain(self, timeout: float = 30.0) -> int:
+        """flush, then keep flushing until every backlog is on its socket (the peers must be reading);
+        bytes flushed by the first call"""
+        import time
+        sent = self.flush()
+        deadline = time.monotonic() + timeout
+        while self.pending() > 0:
+            if time.monotonic() > deadline:
+                raise TimeoutError(f"egress hub: {self.pending()} bytes still held after {timeout} s")
+            time.sleep(0.001)
+            self.flush()
+        return sent
 
     def stats(self) -> dict:
         st = EgressHubStats()

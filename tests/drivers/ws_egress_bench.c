@@ -29,6 +29,7 @@
 #include <dlfcn.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -41,6 +42,7 @@
 #include "tcp/server.h"
 #include "ws/common.h"
 #include "ws/egress.h"
+#include "ws/route.h"
 #include "ws/mask.h"
 
 struct web_client_head {
@@ -101,7 +103,20 @@ static void sp_open(struct sockpair *s) {
     pthread_create(&s->th, NULL, drain_reader, &s->fd[1]);
 }
 
+/* sends never wait (include/ws/route.h): the bench's own flow control waits for the socket while
+   its backlog holds more than `keep` bytes */
+static int wait_sent(int fd, long keep) {
+    long p;
+    while ((p = netc_ws_send_pending(fd)) > keep) {
+        struct pollfd q = {fd, POLLOUT, 0};
+        (void)poll(&q, 1, 100);
+        if (netc_ws_send_flush(fd) < 0) return -1;
+    }
+    return p < 0 ? -1 : 0;
+}
+
 static uint64_t sp_close(struct sockpair *s) {
+    (void)wait_sent(s->fd[0], 0);
     shutdown(s->fd[0], SHUT_WR);
     void *ret = NULL;
     pthread_join(s->th, &ret);
@@ -198,11 +213,12 @@ int main(int argc, char **argv) {
             if (rc == NETC_WS_EGRESS_FULL) {
                 /* the oldest slot onto the socket (waits for it), the rest when finished */
                 if (netc_ws_egress_send(eg, sp.fd[0], 0) == 0 && netc_ws_egress_send(eg, sp.fd[0], 1) < 0) return 1;
+                if (wait_sent(sp.fd[0], 16 << 20)) return 1;
                 rc = netc_ws_egress_queue(eg, src + j * msg, msg, WS_OPCODE_BINARY, masked ? keys + 4 * j : NULL, 1);
             }
             if (rc) return 1;
         }
-        if (netc_ws_egress_flush(eg, sp.fd[0]) < 0) return 1;
+        if (netc_ws_egress_flush(eg, sp.fd[0]) < 0 || wait_sent(sp.fd[0], 0)) return 1;
         const double secs = now() - t0;
         report("ring_socket", msg, nmsg, masked, wire_total, secs, sp_close(&sp));
     }
@@ -222,8 +238,9 @@ int main(int argc, char **argv) {
             const uint64_t j = i % per_src;
             ws_build_message(&m, WS_OPCODE_BINARY, msg, src + j * msg);
             if (ws_send_message((struct web_client *)&head, &m, masked ? keys + 4 * j : NULL, 1) != 1) return 1;
+            if ((i & 255) == 255 && wait_sent(sp.fd[0], 16 << 20)) return 1;
         }
-        if (netc_ws_egress_flush(dg, sp.fd[0]) < 0) return 1;
+        if (netc_ws_egress_flush(dg, sp.fd[0]) < 0 || wait_sent(sp.fd[0], 0)) return 1;
         const double secs = now() - t0;
         netc_ws_gpu_detach_send(sp.fd[0]);
         report("route_socket", msg, nmsg, masked, wire_total, secs, sp_close(&sp));

@@ -187,7 +187,7 @@ int main(int argc, char **argv) {
     const char *ref_lib = argc > 7 && strcmp(argv[7], "-") ? argv[7] : "oracle/_ref/libref_ws.so";
     const size_t burst = argc > 8 && atoi(argv[8]) > 0 ? (size_t)atoi(argv[8]) : 1;
     const size_t nmsg = rounds * burst;   /* messages per connection */
-    const int is_hub = !strcmp(leg, "hub"), is_ref = !strcmp(leg, "ref");
+    const int is_hub = !strcmp(leg, "hub") || !strcmp(leg, "hubcpu"), is_ref = !strcmp(leg, "ref");
     if (!is_hub && !is_ref && strcmp(leg, "cpu")) return 2;
     if (g_conns < 4 || g_conns % 4) {
         fprintf(stderr, "CONNS must be a multiple of 4\n");
@@ -284,6 +284,14 @@ int main(int argc, char **argv) {
             }
         }
         if (hub && netc_ws_egress_hub_flush(hub) < 0) {
+            fprintf(stderr, "server: flush: %s\n", netc_gpu_strerror());
+            return 3;
+        }
+    }
+    /* what the sockets did not take yet (sends never wait): written as the clients read it */
+    while (hub && netc_ws_egress_hub_pending(hub) > 0) {
+        usleep(100);
+        if (netc_ws_egress_hub_flush(hub) < 0) {
             fprintf(stderr, "server: flush: %s\n", netc_gpu_strerror());
             return 3;
         }

@@ -266,7 +266,7 @@ int main(int argc, char **argv) {
     g_verify = argc > 6 && atoi(argv[6]);
     const char *ref_lib = argc > 7 && strcmp(argv[7], "-") ? argv[7] : "oracle/_ref/libref_ws.so";
     g_chunk = argc > 8 ? (size_t)strtoull(argv[8], NULL, 10) : 0;
-    const int is_hub = !strcmp(leg, "hub"), is_ref = !strcmp(leg, "ref");
+    const int is_hub = !strcmp(leg, "hub") || !strcmp(leg, "hubcpu"), is_ref = !strcmp(leg, "ref");
     if (!is_hub && !is_ref && strcmp(leg, "cpu")) return 2;
     if (g_conns < 4 || g_conns % 4) {
         fprintf(stderr, "CONNS must be a multiple of 4\n");

@@ -1,7 +1,9 @@
 // TEST INFRASTRUCTURE ONLY: host stand-ins for the netc_gpu:: kernel launches and C-ABI helpers
 // that ws_ingest.hip calls (see hip/hip_runtime.h here).  The frame scan is libnetc's host header
-// walk (netc_ws_scan_frames_host, pinned against the oracle in tests/test_scan_host.py); the
-// unmask is the reference's scalar loop (src/ws/common.c:317-323) over the frames it found.
+// walk (netc_ws_scan_frames_host, pinned against the oracle in tests/test_scan_host.py); the XOR of
+// the unmask and of the frame assembly is libnetc's netc_ws_mask (pinned against the oracle in
+// tests/test_mask_cpu.py), so the same build serves as the "hubcpu" measurement control
+// (tests/bin/libnetc_hub_cpu.so): the hubs' host code with their device work done on the host.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -10,6 +12,7 @@
 #include "../../netc_amd/csrc/ws_mask_gpu.h"
 extern "C" {
 #include "../../include/ws/frame.h"
+#include "../../include/ws/mask.h"
 extern __thread int netc_errno_reason;
 }
 
@@ -41,8 +44,9 @@ hipError_t launch_unmask_scanned(uint8_t* wire, uint64_t, const uint64_t* hdr, c
         const uint64_t code = second & 0x7F;
         if (!(second & 0x80)) continue;
         const uint64_t p = h + 2 + (code == 126 ? 2 : code == 127 ? 8 : 0) + 4;
-        const uint8_t* key = wire + p - 4;
-        for (uint64_t i = p; i < hdr[k + 1]; ++i) wire[i] ^= key[(i - p) & 3];
+        uint8_t key[4];
+        memcpy(key, wire + p - 4, 4);
+        netc_ws_mask(wire + p, wire + p, (size_t)(hdr[k + 1] - p), key, 0);
     }
     return hipSuccess;
 }
@@ -77,7 +81,7 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t, const uint8_t* src, uin
             memcpy(p, key, 4);
             p += 4;
         }
-        for (uint64_t i = 0; i < len; ++i) p[i] = src[off[k] + i] ^ key[i & 3];
+        netc_ws_mask(p, src + off[k], (size_t)len, key, 0);
         w = (uint64_t)(p + len - wire);
     }
     if (g_bad_wire >= 0 && g_bad_wire-- == 0) broken = true;
@@ -104,6 +108,7 @@ bool inject_fault() {
 }  // namespace netc_gpu
 
 extern "C" const char* netc_gpu_strerror(void) { return netc_gpu::g_err; }
+extern "C" int netc_gpu_init(int) { return 0; }
 extern "C" int netc_mock_inject_fault(int countdown) {
     netc_gpu::g_fault = countdown;
     return 0;

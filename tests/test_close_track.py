@@ -1,0 +1,46 @@
+"""close() on routed sockets (include/ws/route.h "close tracking").
+
+tests/drivers/ws_close_track.c runs in a process linked the way netc links libnetc.so, so its
+close() -- like netc's own at src/tcp/server.c:267 and src/ws/server.c:124 -- reaches libnetc.so's
+close(): queued egress-hub bytes go out before the descriptor closes, a receive hub releases the
+slots a closed connection held, and nothing of a closed connection (route, send backlog) is left
+for the next socket to get its number.  MODE raw closes with syscall(SYS_close), which the hooks
+never see: the egress hub's per-send identity check still keeps the old connection's frames from a
+new, unattached socket with the same number, and a full receive hub finds and drops the closed
+holders.  NETC_WS_ROUTE_VERIFY=1 forces the per-call identity checks (close() not "tracked").
+
+The CPU suite runs the driver linked against the mock build of the same host code
+(tests/bin/ws_close_track_mock); the GPU suite against libnetc_ws_gpu.so.
+"""
+
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(exe, mode, verify=False):
+    path = os.path.join(ROOT, "tests", "bin", exe)
+    assert os.path.exists(path), f"tests/bin/{exe} missing: run make"
+    env = dict(os.environ)
+    env.pop("NETC_WS_ROUTE_VERIFY", None)
+    if verify:
+        env["NETC_WS_ROUTE_VERIFY"] = "1"
+    r = subprocess.run([path, mode], capture_output=True, text=True, timeout=100, env=env, cwd=ROOT)
+    assert r.returncode == 0, f"{exe} {mode}: rc {r.returncode}\n{r.stdout}\n{r.stderr}"
+    assert r.stdout.startswith(f"ok {mode} tracked={0 if verify else 1}"), r.stdout
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("mode,verify", [("close", False), ("raw", False), ("close", True)])
+def test_close_tracking_mock(mode, verify):
+    run("ws_close_track_mock", mode, verify)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("mode,verify", [("close", False), ("raw", False), ("close", True)])
+def test_close_tracking_gpu(mode, verify):
+    run("ws_close_track", mode, verify)

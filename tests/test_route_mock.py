@@ -240,3 +240,17 @@ def test_egress_hub_echo_server_both_hubs(egress_hub_mock):
 
 def test_egress_hub_bad_wire_fails_only_its_slot(egress_hub_mock, mock):
     egress_hub_mock.bad_wire_fails_only_its_slot(lambda: mock.netc_mock_bad_wire(0), lambda: mock.netc_mock_bad_wire(-1))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("bounded", [False, True])
+def test_egress_hub_one_stalled_reader_of_256(egress_hub_mock, bounded):
+    egress_hub_mock.test_one_stalled_reader_of_256(bounded)
+
+
+def test_egress_hub_reused_descriptor_not_attached_gets_nothing(egress_hub_mock):
+    egress_hub_mock.test_reused_descriptor_not_attached_gets_nothing()
+
+
+def test_egress_hub_close_frame_goes_out_with_what_was_queued_before_it(egress_hub_mock):
+    egress_hub_mock.test_close_frame_goes_out_with_what_was_queued_before_it()

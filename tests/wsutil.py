@@ -61,6 +61,24 @@ def pending(sock: socket.socket) -> int:
     return struct.unpack("i", fcntl.ioctl(sock.fileno(), termios.FIONREAD, b"\0\0\0\0"))[0]
 
 
+def settle(*socks, timeout: float = 30.0):
+    """writes what each socket's send backlog holds (include/ws/route.h: sends never wait, so bytes a
+    full socket did not take wait there), waiting for the peers to read it"""
+    import time
+    lib = _lib.host()
+    lib.netc_ws_send_flush.argtypes = [ctypes.c_int]
+    lib.netc_ws_send_flush.restype = ctypes.c_long
+    deadline = time.monotonic() + timeout
+    for s in socks:
+        while True:
+            r = lib.netc_ws_send_flush(s.fileno())
+            if r <= 0:
+                break
+            if time.monotonic() > deadline:
+                raise TimeoutError(f"socket {s.fileno()}: {r} bytes still held")
+            time.sleep(0.001)
+
+
 def pair():
     a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
     for s in (a, b):

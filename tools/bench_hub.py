@@ -15,6 +15,11 @@ set the pace.
 
     python tools/bench_hub.py [--configs 256x400x1024,1024x100x1024,64x200x16384] [--chunks 0] [--out FILE]
 
+Legs: hub (the GPU hub), hubcpu (the SAME hub host code -- slots, peeks, sendmsg batching -- with its
+device work done on the host: tests/bin/*_cpu linked to tests/bin/libnetc_hub_cpu.so, netc_ws_mask
+for the XOR; the control that isolates what the GPU itself adds), cpu (libnetc's per-connection CPU
+path), ref (the reference's own code).  --repeat N interleaves N passes of every leg.
+
 --send runs the send side instead (tests/bin/ws_egress_hub_server, include/ws/egress_hub.h): CONNS
 connections answered ROUNDS times each from one loop with netc's ws_send_message -- through one
 GPU egress hub (flushed once per loop iteration), libnetc's CPU path, or the reference's own
@@ -37,7 +42,8 @@ REF = os.path.join(ROOT, "oracle", "_ref", "libref_ws.so")
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="256x400x1024,1024x100x1024,64x200x16384,16x100x262144")
-    ap.add_argument("--legs", default="hub,cpu,ref")
+    ap.add_argument("--legs", default="hub,hubcpu,cpu,ref")
+    ap.add_argument("--repeat", type=int, default=1, help="passes over every leg, interleaved")
     ap.add_argument("--chunks", default="0,65536", help="client send chunk sizes (0: live ws_send_message)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--send", action="store_true", help="the send side (egress hub) instead")
@@ -56,11 +62,12 @@ def main():
     out = open(args.out, "a") if args.out else None
     for cfg in args.configs.split(","):
         conns, msgs, mx = cfg.split("x")
-        for chunk, leg in [(c, l) for c in args.chunks.split(",") for l in args.legs.split(",")]:
+        for _, chunk, leg in [(i, c, l) for c in args.chunks.split(",") for i in range(args.repeat)
+                              for l in args.legs.split(",")]:
             if leg == "ref" and not os.path.exists(REF):
                 continue
-            r = subprocess.run([EXE, leg, conns, msgs, mx, "0", "0", "-", chunk], capture_output=True, text=True,
-                               timeout=600, cwd=ROOT)
+            r = subprocess.run([exe_of(EXE, leg), leg, conns, msgs, mx, "0", "0", "-", chunk], capture_output=True,
+                               text=True, timeout=600, cwd=ROOT)
             if r.returncode:
                 sys.exit(f"{cfg} {leg}: rc {r.returncode}: {r.stderr[-2000:]}")
             rec = json.loads(r.stdout.strip().splitlines()[-1])
@@ -72,13 +79,19 @@ def main():
                 out.flush()
 
 
+def exe_of(exe, leg):
+    """the hubcpu leg runs the driver built against the host-backend hub library"""
+    return exe + "_cpu" if leg == "hubcpu" else exe
+
+
 def echo(args):
     exe = os.path.join(ROOT, "tests", "bin", "ws_echo_server")
     out = open(args.out, "a") if args.out else None
     for cfg in args.echo_configs.split(","):
         conns, msgs, mx, chunk = cfg.split("x")
-        for leg in ("hub", "cpu"):
-            r = subprocess.run([exe, leg, conns, msgs, mx, chunk], capture_output=True, text=True, timeout=600, cwd=ROOT)
+        for _, leg in [(i, l) for i in range(args.repeat) for l in args.legs.split(",") if l != "ref"]:
+            r = subprocess.run([exe_of(exe, leg), leg, conns, msgs, mx, chunk], capture_output=True, text=True,
+                               timeout=600, cwd=ROOT)
             if r.returncode:
                 sys.exit(f"echo {cfg} {leg}: rc {r.returncode}: {r.stderr[-2000:]}")
             line = r.stdout.strip().splitlines()[-1]
@@ -94,10 +107,11 @@ def send_side(args):
     out = open(args.out, "a") if args.out else None
     for cfg in args.send_configs.split(","):
         conns, rounds, mx = cfg.split("x")
-        for burst, leg in [(b, l) for b in args.bursts.split(",") for l in args.legs.split(",")]:
+        for _, burst, leg in [(i, b, l) for b in args.bursts.split(",") for i in range(args.repeat)
+                              for l in args.legs.split(",")]:
             if leg == "ref" and (args.masked or not os.path.exists(REF)):
                 continue
-            r = subprocess.run([SEND_EXE, leg, conns, str(max(1, int(rounds) // int(burst))), mx, str(args.masked), "0",
+            r = subprocess.run([exe_of(SEND_EXE, leg), leg, conns, str(max(1, int(rounds) // int(burst))), mx, str(args.masked), "0",
                                 "-", burst], capture_output=True, text=True, timeout=600, cwd=ROOT)
             if r.returncode:
                 sys.exit(f"send {cfg} {leg}: rc {r.returncode}: {r.stderr[-2000:]}")

@@ -77,6 +77,12 @@ for s in ${STEPS:-tests smoke bench}; do
     mkdir -p $D
     (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- $R/tests/bin/ws_hub_server hub 256 400 1024 > $D/trace.log 2>&1) || { echo HUBTRACEFAIL; tail -20 $D/trace.log; exit 1; }
     tail -1 $D/trace.log | cut -c1-300 ;;
+  hubs)
+    # round 6: hub / hubcpu / cpu / ref at 256 and 1,024 connections, 0-1 KiB and 0-16 KiB, both sides and the echo
+    timeout -k 10 600 python3 -u tools/bench_hub.py --configs ${RX_CFGS:-256x400x1024,1024x100x1024,256x100x16384,1024x25x16384} --chunks 65536 --repeat ${REPEAT:-2} --out $OUT/hub_rx.jsonl > $OUT/hub_rx.log 2>&1 || { echo HUBRXFAIL; tail -20 $OUT/hub_rx.log; exit 1; }
+    timeout -k 10 600 python3 -u tools/bench_hub.py --send --send-configs ${TX_CFGS:-256x100x1024,1024x40x1024,256x40x16384,1024x10x16384} --bursts 1 --repeat ${REPEAT:-2} --out $OUT/hub_tx.jsonl > $OUT/hub_tx.log 2>&1 || { echo HUBTXFAIL; tail -20 $OUT/hub_tx.log; exit 1; }
+    timeout -k 10 600 python3 -u tools/bench_hub.py --echo --echo-configs ${ECHO_CFGS:-256x200x1024x65536,1024x50x1024x65536,256x50x16384x65536,1024x12x16384x65536} --repeat ${REPEAT:-2} --out $OUT/hub_echo.jsonl > $OUT/hub_echo.log 2>&1 || { echo HUBECHOFAIL; tail -20 $OUT/hub_echo.log; exit 1; }
+    wc -l $OUT/hub_*.jsonl ;;
   *)
     echo "unknown step $s"; exit 2 ;;
   esac
