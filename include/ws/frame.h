@@ -147,7 +147,9 @@ int netc_gpu_scan_release(int device, void *stream);
  * parallel pass with the strict checks except MASK, speculatively -- met a header
  * those checks reject and walked on serially from it), -1 when no scan ran on that
  * stream, or a negative code.  The results are the same either way; only the
- * speed differs.
+ * speed differs.  Bit 32 is set when the call finished on its one-pass path (the
+ * chunks resolved their entries and frame indexes inside the first launch; knob
+ * SCAN_ONEPASS), clear when the graph kernels resolved it.
  */
 int64_t netc_gpu_scan_diag(int device, void *stream);
 

@@ -156,6 +156,10 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *                      else 0]                                      (NETC_ENC_PF)
  *   SCAN_BLOCK_CHUNKS  chunks per block of the frame scan's link and emit phases: 32 or 64
  *                      [32 up to 128 MiB of stream, 64 above]       (NETC_SCAN_BLOCK_CHUNKS)
+ *   SCAN_ONEPASS       the frame scan's one-pass path (the chunks resolve their entries and
+ *                      frame indexes by decoupled look-back inside the first launch; the
+ *                      graph kernels then only check a flag): 0 never, 1 at every size
+ *                      [on up to 256 MiB of stream]                 (NETC_SCAN_ONEPASS)
  *   INJECT_FAULT       fault injection for tests: the ingest / egress ring submission this
  *                      countdown reaches (0 = the next one) fails as NETC_GPU_ELAUNCH
  *                      without launching, then the knob disarms itself [off]
@@ -174,6 +178,7 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
 #define NETC_GPU_KNOB_ENC_PROBE        11
 #define NETC_GPU_KNOB_ENC_PF           12
 #define NETC_GPU_KNOB_SCAN_BLOCK_CHUNKS 13
+#define NETC_GPU_KNOB_SCAN_ONEPASS     14
 int netc_gpu_knob(int knob, int64_t value);
 
 /**

@@ -47,14 +47,15 @@ netc_gpu::LaunchCfg cfg_now() {
 // Measurement / test knobs (netc_gpu_knob).  Seeded once per process from the environment
 // (tools/ sweeps set NETC_ENC_SCAN_PER=...), then changed only through netc_gpu_knob; the
 // launch paths read one atomic word, never getenv.
-constexpr int kKnobs = 14;   // knobs 1 .. 13 (include/ws/mask.h NETC_GPU_KNOB_*)
+constexpr int kKnobs = 15;   // knobs 1 .. 14 (include/ws/mask.h NETC_GPU_KNOB_*)
 std::atomic<int64_t> g_knob[kKnobs];
 std::once_flag g_knob_once;
 void knobs_init() {
     static const char* const env[kKnobs] = {nullptr, "NETC_ENC_DENSE_BYTES", "NETC_ENC_SCAN_PER", "NETC_SCAN_FAST_RANK",
                                             "NETC_SCAN_ANCHOR_SLOTS", "NETC_VAL_STEPS", "NETC_SCAN_FUSE", "NETC_MASK_TAPER",
                                             "NETC_ENC_SRC", "NETC_ENC_FIX", "NETC_INJECT_FAULT",
-                                            "NETC_ENC_PROBE", "NETC_ENC_PF", "NETC_SCAN_BLOCK_CHUNKS"};
+                                            "NETC_ENC_PROBE", "NETC_ENC_PF", "NETC_SCAN_BLOCK_CHUNKS",
+                                            "NETC_SCAN_ONEPASS"};
     for (int k = 0; k < kKnobs; ++k) {
         const char* e = env[k] ? getenv(env[k]) : nullptr;
         g_knob[k].store(e && *e ? (int64_t)strtoll(e, nullptr, 10) : -1, std::memory_order_relaxed);

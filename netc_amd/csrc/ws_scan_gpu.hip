@@ -246,6 +246,14 @@ struct ScanArgs {
     uint64_t* result;      // [0] frames, [1] consumed, [2] error offset or ~0
     int fast_rank;         // K3a / K3b may take their one-barrier-per-round ranking (0: the generic
                            // loop always; NETC_SCAN_FAST_RANK=0, tests)
+    // the one-pass path (scan_exits<_, true>; see "One pass" below)
+    int onepass;           // this call runs it (the host's choice: knob SCAN_ONEPASS, stream size)
+    uint32_t* opfail;      // this call's one-pass failure word (flags[4] / flags[5] on alternate calls;
+    uint32_t* opfail_prev; // ... K4 zeroes the previous call's, as for ovf)
+    uint64_t* st_t;        // per chunk: its exit prediction T      [63:40] epoch | [39:0] value
+    uint64_t* st_x;        // per chunk: X, the chain's first header at or past its end
+    uint64_t* st_f;        // per chunk: its frame count (aggregate) or the frames before its end (inclusive)
+    uint64_t epoch;        // 1 .. 2^24 - 1, one per call on the scratch (words of other calls do not match)
 };
 
 // RSV bits the header filter rejects: all three in strict mode; in the speculative pass
@@ -456,6 +464,7 @@ __device__ __forceinline__ void append_cand(const ScanArgs& a, uint64_t x, bool 
     }
 }
 
+__device__ __forceinline__ void put_frame(const ScanArgs& a, uint64_t k, uint64_t p, uint32_t key, uint8_t b0);
 // a lane of the last vector of a chunk whose 16 positions can exit the chunk with a
 // 7-bit length: p + 2 + 4 + 125 >= chunk end  <=>  offset >= 3965 (lane 55 holds 3952-3967)
 static constexpr int kNearLane = 55;
@@ -471,6 +480,239 @@ static constexpr int kStageWords = NETC_K1_SLIM ? (int)((kChunk + 16) / 4) : kWo
 static_assert(!NETC_K1_SLIM || 4 * (4 * kStageWords + 8 * kSet + 2 * kQCap) <= 20480,
               "K1: a 4-wave block must stay within 20,480 B of LDS (8 blocks per CU)");
 static constexpr int kCheapMax = 64;   // K1: more from the cheap selection: the full quick check instead
+
+// ------------------------------------------------------------------ one pass --
+// The one-pass path: the chunks of K1 resolve the chain themselves, by
+// decoupled look-back, so the graph kernels (K2-K4) only read a flag.
+//
+// Per chunk c, K1 already has the distinct exits of its exit-capable candidates, and which of
+// them land on a position that can start a header (the nodes it appends).  T(c), published
+// right after the parse, predicts where a chain that visits c leaves it: the one such exit
+// when there is exactly one (Single E), none (None: a chain that visits c ends in it, or dies at
+// an exit onto a position that cannot start a header), or Multi.  Garbage chains (payload bytes
+// parsed as headers) land on such positions with ~2 % odds, so nearly every chunk is Single or
+// None.  X(c) is the chain's first header at or past c's end, or END.  Then, per chunk:
+//
+//   X(c-1)   look back at the 64 predecessors at once (one load per lane of st_x and st_t): the
+//            nearest published X, carried forward through the chunks after it -- a chunk the
+//            carried X does not reach (X >= its end: a frame covers it) passes X on; one it
+//            does reach maps X to T (END for None; a Multi chunk's own X is waited for)
+//   walk     a visited chunk (X(c-1) inside it) walks its frames from there in LDS (its bytes are
+//            staged for the parse anyway) to its exit; a covered one does nothing
+//   check    the walk's exit against T(c): a chunk whose prediction was wrong (a stream that ends
+//            or dies in it with a garbage exit beside) sets the failure word -- the earliest
+//            wrong chunk always walks from a right entry, so every wrong prediction is seen
+//   F(c)     the frames before c's end: the count published at once (aggregate), then the look-
+//            back's sum back to the nearest inclusive prefix (inclusive)
+//   emit     the chunk's frames at F(c-1) .. F(c) - 1 from its LDS copy; the chunk where the chain
+//            ends writes the results
+//
+// A wait that outlasts kOnePassWait (an adversarial run of Multi chunks, a predecessor that
+// failed), a full candidate queue or exit set, or a speculative (non-strict) stop at a header
+// the filter rejects also set the failure word.  Then K2-K4 run as before, from the nodes K1
+// appended all the same, and overwrite everything this path wrote: the results are the same
+// either way.  Words carry the call's epoch, so no clearing launch is needed.
+static constexpr uint64_t kOpBits = 40;
+static constexpr uint64_t kOpMask = (1ull << kOpBits) - 1;
+static constexpr uint64_t kTNone = kOpMask, kTMulti = kOpMask - 1;   // T values; else the exit
+static constexpr uint64_t kXEnd = kOpMask;                              // X: the chain has ended
+static constexpr uint64_t kFIncl = 1ull << 39;                          // F: inclusive (else aggregate)
+static constexpr uint64_t kOnePassWait = 2000000;                       // 20 ms at 100 MHz
+static constexpr uint64_t kOnePassMax = 256ull << 20;                   // default: streams up to 256 MiB
+
+__device__ __forceinline__ void op_put(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t op_get(const uint64_t* p) {
+    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool op_failed(const ScanArgs& a) {
+    return __hip_atomic_load(a.opfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+__device__ __forceinline__ void op_fail(const ScanArgs& a, int lane) {
+    if (lane == 0) __hip_atomic_fetch_or(a.opfail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the graph kernels: the one-pass path finished this call (every chunk resolved, none failed)
+__device__ __forceinline__ bool onepass_done(const ScanArgs& a) { return a.onepass && !op_failed(a); }
+
+// a poll that found a predecessor not published yet: false once the wait is over (failure set)
+__device__ __forceinline__ bool op_wait(const ScanArgs& a, uint64_t t0, int lane) {
+    if (op_failed(a)) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > kOnePassWait) {
+        op_fail(a, lane);
+        return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+    return true;
+}
+
+// X(c - 1): where the chain stands when it reaches chunk c (a position >= c's start, or kXEnd)
+__device__ bool op_x_before(const ScanArgs& a, uint64_t c, uint64_t c0, int lane, uint64_t* out) {
+    if (c <= c0) {
+        *out = a.start;
+        return true;
+    }
+    const uint64_t ep = a.epoch;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const int64_t j = (int64_t)c - 1 - lane;
+        const bool below = j < (int64_t)c0;   // before the start chunk: X = the start
+        uint64_t wx = 0, wt = 0;
+        if (!below) {
+            wx = op_get(a.st_x + j);
+            wt = op_get(a.st_t + j);
+        }
+        const bool hx = below || (wx >> kOpBits) == ep;
+        const bool ht = !below && (wt >> kOpBits) == ep;
+        const uint64_t bx = __ballot(hx), bt = __ballot(ht);
+        const uint64_t xv = below ? a.start : (wx & kOpMask), tv = wt & kOpMask;
+        if (bx) {
+            const int L = __builtin_ctzll(bx);   // the nearest published X
+            uint64_t X = readlane64(xv, L);
+            bool ok = true;
+            for (int l = L - 1; l >= 0 && X != kXEnd; --l) {   // carried forward to chunk c
+                const uint64_t k = c - 1 - (uint64_t)l;
+                if (X >= (k + 1) * kChunk) continue;   // a frame covers chunk k
+                if (!((bt >> l) & 1)) {
+                    ok = false;   // its T is not published yet
+                    break;
+                }
+                const uint64_t t = readlane64(tv, l);
+                if (t == kTMulti) {
+                    ok = false;   // its own X is needed
+                    break;
+                }
+                X = t == kTNone ? kXEnd : t;
+            }
+            if (ok) {
+                *out = X;
+                return true;
+            }
+        }
+        if (!op_wait(a, t0, lane)) return false;
+    }
+}
+
+// F(c - 1): the chain's frames before chunk c
+__device__ bool op_f_before(const ScanArgs& a, uint64_t c, uint64_t c0, int lane, uint64_t* out) {
+    const uint64_t ep = a.epoch;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t acc = 0;
+    for (int64_t top = (int64_t)c - 1; top >= (int64_t)c0;) {
+        const int64_t j = top - lane;
+        const bool below = j < (int64_t)c0;   // an inclusive 0
+        const uint64_t w = below ? 0 : op_get(a.st_f + j);
+        const bool has = below || (w >> kOpBits) == ep;
+        const bool incl = below || (has && (w & kFIncl));
+        const uint64_t bi = __ballot(incl), bh = __ballot(has);
+        const int L = bi ? __builtin_ctzll(bi) : kWave;
+        const uint64_t need = L >= kWave - 1 ? ~0ull : ((2ull << L) - 1);
+        if ((bh & need) != need) {
+            if (!op_wait(a, t0, lane)) return false;
+            continue;
+        }
+        acc += wave_sum(lane <= L && !below ? (w & (kFIncl - 1)) : 0);
+        if (L < kWave) break;
+        top -= kWave;
+    }
+    *out = acc;
+    return true;
+}
+
+// The one-pass path for chunk c (every lane of its wavefront).  st: the chunk's bytes in LDS
+// (unused for the virtual chunk); q: the wave's candidate queue, free again (frame offsets);
+// tval: T(c), or ~0 when the parse overflowed (the call fails).
+__device__ void op_chunk(const ScanArgs& a, uint64_t c, const uint32_t* st, uint16_t* q, uint64_t tval, int lane) {
+    const uint64_t c0 = a.start / kChunk;
+    if (c < c0) return;   // before the stream start: no one looks here
+    const uint64_t ep = a.epoch << kOpBits;
+    if (tval == ~0ull) {
+        op_fail(a, lane);
+        return;
+    }
+    if (lane == 0) op_put(a.st_t + c, ep | tval);
+    uint64_t X;
+    if (!op_x_before(a, c, c0, lane, &X)) return;
+    const uint64_t B = c * kChunk, Bend = B + kChunk;
+    uint64_t Xc = X, cnt = 0, endpos = 0;
+    int ended = 0;   // 1: the chain ends here (END), 2: it dies here (an error at endpos)
+    if (X != kXEnd && X < Bend) {   // the chain visits chunk c: walk it from X
+        uint64_t p = X;
+        for (;;) {
+            if (p >= Bend) {   // its exit
+                if (quick_reject(a, p)) {   // onto a position that cannot start a header: dies there
+                    if (a.spec) {
+                        op_fail(a, lane);   // (the speculative pass walks on serially in K4)
+                        return;
+                    }
+                    ended = 2;
+                    endpos = p;
+                    Xc = kXEnd;
+                } else {
+                    Xc = p;
+                }
+                break;
+            }
+            uint32_t key;
+            uint8_t b0;
+            const uint64_t v = B >= a.len ? term(kEnd, p) : parse_at(a, p, window_at(st, (int)(p - B)), &key, &b0);
+            if (v & kTerm) {
+                if (term_type(v) == kDead && a.spec) {
+                    op_fail(a, lane);
+                    return;
+                }
+                ended = term_type(v) == kDead ? 2 : 1;
+                endpos = term_pos(v);
+                Xc = kXEnd;
+                break;
+            }
+            if (lane == 0 && cnt < (uint64_t)kQCap) q[cnt] = (uint16_t)(p - B);
+            ++cnt;
+            p = v;
+        }
+        // the prediction the successors may have used
+        if (tval != kTMulti && (tval == kTNone ? Xc != kXEnd : Xc != tval)) {
+            op_fail(a, lane);
+            return;
+        }
+    }
+    if (lane == 0) {
+        op_put(a.st_x + c, ep | Xc);
+        op_put(a.st_f + c, ep | cnt);
+    }
+    uint64_t F;
+    if (!op_f_before(a, c, c0, lane, &F)) return;
+    if (lane == 0) op_put(a.st_f + c, ep | kFIncl | (F + cnt));
+    // the frames: recorded offsets by all lanes, the rest (a chunk of more than kQCap frames) by lane 0
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t rec = cnt < (uint64_t)kQCap ? cnt : (uint64_t)kQCap;
+    for (uint64_t i = lane; i < rec; i += kWave) {
+        const uint32_t off = q[i];
+        uint32_t key;
+        uint8_t b0;
+        (void)parse_at(a, B + off, window_at(st, (int)off), &key, &b0);
+        put_frame(a, F + i, B + off, key, b0);
+    }
+    if (lane == 0) {
+        if (cnt > rec) {
+            uint64_t p = B + q[rec - 1];
+            for (uint64_t i = rec - 1; i < cnt; ++i) {
+                uint32_t key;
+                uint8_t b0;
+                const uint64_t v = parse_at(a, p, window_at(st, (int)(p - B)), &key, &b0);
+                if (i >= rec) put_frame(a, F + i, p, key, b0);
+                p = v;
+            }
+        }
+        if (ended) {   // the chain ends in this chunk: the results
+            const uint64_t total = F + cnt;
+            a.result[0] = total;
+            a.result[1] = endpos;
+            a.result[2] = ended == 2 ? endpos : ~0ull;
+            if (total <= a.max_frames) a.hdr[total] = endpos;
+        }
+    }
+}
 
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
 
@@ -523,7 +765,8 @@ __device__ __forceinline__ u32x4 k1_load(const uint8_t* p) {
     return *(const NETC_GLOBAL u32x4u*)p;
 }
 
-template <bool NT>
+// ONE: the one-pass path after the parse (op_chunk).
+template <bool NT, bool ONE>
 __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     __shared__ uint32_t stage[4][kStageWords];   // per wave: its chunk's bytes (+ 16 after)
     __shared__ unsigned long long set[4][kSet];
@@ -540,7 +783,10 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     if (c > a.nc) return;
     const uint64_t B = c * kChunk, Bend = B + kChunk;
     if (lane == 0 && a.start / kChunk == c) append_cand(a, a.start, true);   // the root node
-    if (B >= a.len) return;   // the virtual chunk: no bytes
+    if (B >= a.len) {   // the virtual chunk: no bytes
+        if constexpr (ONE) op_chunk(a, c, nullptr, queue[wv], kTNone, lane);
+        return;
+    }
     uint32_t d[4][4], nx[4];
     if (Bend <= a.pf_lim) {   // wave-uniform: every load in place, no clamps (scalar base + lane offset)
         const uint8_t* base = a.pf_base + B;
@@ -716,6 +962,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     }
     if (total > (uint32_t)kQCap) {   // wave-uniform (adversarial payloads, non-strict mode)
         if (lane == 0) atomicOr(a.ovf, kOvfQueue);
+        if constexpr (ONE) op_chunk(a, c, st, queue[wv], ~0ull, lane);
         return;
     }
     uint32_t at = incl - mine;
@@ -730,6 +977,8 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     SCAN_STAMP(0, 2);   // quick check done, candidates queued
     bool ovf = false;
+    uint32_t nodes = 0;   // (one pass) exits this lane appended as nodes, and the last of them
+    uint64_t ex = 0;
     for (uint32_t e = lane; e < total; e += kWave) {
         const uint32_t off = queue[wv][e];
         const uint64_t v = parse_at(a, B + off, window_at(st, (int)off), nullptr, nullptr);
@@ -744,12 +993,22 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
             if (k < (uint32_t)kCand) a.cand[c * kCand + k] = v;
         }
 #else
-        if (!(v & kTerm) && v >= Bend && set_insert(set[wv], v, &ovf) && !quick_reject(a, v))
+        if (!(v & kTerm) && v >= Bend && set_insert(set[wv], v, &ovf) && !quick_reject(a, v)) {
             append_cand(a, v, v / kChunk / kTileChunks != c / kTileChunks);
+            ++nodes;
+            ex = v;
+        }
 #endif
     }
     SCAN_STAMP(0, 3);   // parsed, exits checked and appended
     if (ovf) atomicOr(a.ovf, kOvfSet);
+    if constexpr (ONE) {
+        // T(c) from the distinct exits onto header-capable positions (a full set: unknown)
+        const uint64_t bn = __ballot(nodes != 0);
+        const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(nodes), kWave - 1);
+        const uint64_t t = __ballot(ovf) ? ~0ull : (n == 0 ? kTNone : (n > 1 ? kTMulti : readlane64(ex, __builtin_ctzll(bn))));
+        op_chunk(a, c, st, queue[wv], t, lane);
+    }
 }
 
 // K2 -> K3a words: plain, or (SC1: scan_links_fused, K3a in the same launch, maybe on another XCD)
@@ -1201,6 +1460,7 @@ template <int BC>
 __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
     __shared__ LinksLdsT<BC> sl;
     SCAN_SCOPE(1);
+    if (onepass_done(a)) return;   // K1 resolved the chain (block-uniform: one word)
     links_body<false, BC>(a, sl);
 }
 
@@ -1448,6 +1708,7 @@ __device__ __forceinline__ void tiles_body(const ScanArgs& a, uint64_t tile, Til
 __global__ __launch_bounds__(kScanT) void scan_tiles(ScanArgs a) {
     __shared__ TilesLds st;
     SCAN_SCOPE(2);
+    if (onepass_done(a)) return;
     tiles_body<false>(a, blockIdx.x, st);
 }
 
@@ -1738,6 +1999,7 @@ __device__ __forceinline__ void resolve_body(const ScanArgs& a, uint64_t tiles, 
 __global__ __launch_bounds__(kResolveT) void scan_resolve(ScanArgs a, uint64_t tiles) {
     __shared__ ResolveLds<kMaxTiles, kExtCap> sm;
     SCAN_SCOPE(3);
+    if (onepass_done(a)) return;
     resolve_body<kResolveT, 1>(a, tiles, sm);
 }
 
@@ -1781,6 +2043,7 @@ __global__ __launch_bounds__(kScanT) void scan_links_fused(ScanArgs a, uint64_t 
     __shared__ FusedLds sm;
     __shared__ int flag;
     SCAN_SCOPE(1);
+    if (onepass_done(a)) return;
     links_body<true, kBlkChunks>(a, sm.k2);
     constexpr uint32_t kPerTile = (uint32_t)(kTileChunks / kBlkChunks);
     const uint32_t tile = blockIdx.x / kPerTile;
@@ -1815,6 +2078,7 @@ __global__ __launch_bounds__(kScanT) void scan_tiles_resolve(ScanArgs a, uint64_
     __shared__ MergedLds sm;
     __shared__ int last;
     SCAN_SCOPE(2);
+    if (onepass_done(a)) return;
     tiles_body<false>(a, blockIdx.x, sm.k3a);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 stores have completed
     __syncthreads();
@@ -1934,6 +2198,27 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
     (void)tiles;
     const int tid = threadIdx.x;
     const uint64_t tile = (uint64_t)blockIdx.x * EC / kTileChunks;   // EC divides kTileChunks
+    if (onepass_done(a)) {   // K1 wrote the frames and results: only the clearing for the next call
+        if (tid < EC) {
+            const uint64_t c = (uint64_t)blockIdx.x * EC + tid;
+            if (c <= a.nc) {
+                a.ccount[c] = 0;
+                *(uint64_t*)(a.ext + c * kCand) = 0;
+            }
+        }
+        if (blockIdx.x == 0 && tid == 0) {
+            *a.ovf_prev = 0;
+            *a.opfail_prev = 0;
+            a.flags[8] = 0;
+            a.flags[9] = 0;    // no serial walk
+            a.flags[10] = 1;   // the one-pass path (netc_gpu_scan_diag bit 32)
+        }
+        return;
+    }
+    if (blockIdx.x == 0 && tid == 0) {
+        *a.opfail_prev = 0;
+        a.flags[10] = 0;
+    }
     if (tid == 0) {
         fbs = __hip_atomic_load(&a.flags[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
         bti = a.tinfo[tile];
@@ -2121,6 +2406,7 @@ struct ScanScratch {
     uint64_t cap = 0;      // chunks the layout is sized for
     bool dirty = false;    // a call did not launch all its kernels: clear before the next
     uint64_t calls = 0;    // the overflow word alternates per call
+    uint64_t epoch = 0;    // the one-pass status words' epoch of the last call (1 .. 2^24 - 1)
     std::vector<void*> retired;   // outgrown allocations (queued work may still use them)
 };
 
@@ -2150,7 +2436,7 @@ std::mutex& stream_scratch_mu() {
 // regions; flags, ccount and ext first -- the region every call leaves zeroed.
 struct Layout {
     uint64_t flags, ccount, ext, tarr, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, flist, text, tcount, tinfo,
-        total;
+        st_t, st_x, st_f, total;
 };
 Layout layout_for(uint64_t cap) {
     auto align = [](uint64_t x) { return (x + 63) & ~63ull; };
@@ -2175,6 +2461,9 @@ Layout layout_for(uint64_t cap) {
     l.text = o;    o = align(o + tiles * kExt * sizeof(TileExt));
     l.tcount = o;  o = align(o + tiles * 4);
     l.tinfo = o;   o = align(o + tiles * sizeof(TileInfo));
+    l.st_t = o;    o = align(o + cap * 8);   // one-pass status words (epochs: never cleared per call)
+    l.st_x = o;    o = align(o + cap * 8);
+    l.st_f = o;    o = align(o + cap * 8);
     l.total = o;
     return l;
 }
@@ -2229,11 +2518,11 @@ int64_t scan_diag(int device, hipStream_t stream) {
         if (!keep->mem) return -1;
         word = (const uint8_t*)keep->mem + 9 * sizeof(uint32_t);
     }
-    uint32_t why = 0;
-    if (hipMemcpyAsync(&why, word, sizeof(why), hipMemcpyDeviceToHost, stream) != hipSuccess ||
+    uint32_t w[2] = {0, 0};   // flags[9]: why the serial walk; flags[10]: 1 = the one-pass path
+    if (hipMemcpyAsync(w, word, sizeof(w), hipMemcpyDeviceToHost, stream) != hipSuccess ||
         hipStreamSynchronize(stream) != hipSuccess)
         return -1;
-    return why;
+    return (int64_t)w[0] | (int64_t)(w[1] & 1) << 32;
 }
 
 int release_stream_scratch(int device, hipStream_t stream) {
@@ -2294,7 +2583,22 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.flags = (uint32_t*)(m + l.flags);
     a.ovf = a.flags + ((s.calls & 1) ? 2 : 0);
     a.ovf_prev = a.flags + ((s.calls & 1) ? 0 : 2);
+    a.opfail = a.flags + ((s.calls & 1) ? 5 : 4);
+    a.opfail_prev = a.flags + ((s.calls & 1) ? 4 : 5);
     ++s.calls;
+    // the one-pass path: knob SCAN_ONEPASS (0 never, 1 always), by default up to kOnePassMax of
+    // stream; positions must fit its 40-bit words.  Each call has its own epoch; when the 24-bit
+    // epoch wraps, the status words are cleared once, so a word left from 2^24 calls ago cannot match.
+    const int64_t op = knob(NETC_GPU_KNOB_SCAN_ONEPASS);
+    a.onepass = op == 0 ? 0 : ((op == 1 || len <= kOnePassMax) && len < (1ull << 38) ? 1 : 0);
+    if (++s.epoch >= (1ull << 24)) {
+        if ((e = hipMemsetAsync(m + l.st_t, 0, l.total - l.st_t, stream)) != hipSuccess) return e;
+        s.epoch = 1;
+    }
+    a.epoch = s.epoch;
+    a.st_t = (uint64_t*)(m + l.st_t);
+    a.st_x = (uint64_t*)(m + l.st_x);
+    a.st_f = (uint64_t*)(m + l.st_f);
     a.ccount = (uint32_t*)(m + l.ccount);
     a.ext = m + l.ext;
     a.tarr = (uint32_t*)(m + l.tarr);
@@ -2320,8 +2624,14 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.pf_base = len >= 16 ? wire : m + l.flags;
     a.pf_lim = len >= 16 ? len - 16 : 0;
     const unsigned blk = (unsigned)((chunks + kBlkChunks - 1) / kBlkChunks);
-    if (len <= (128ull << 20)) hipLaunchKernelGGL(scan_exits<false>, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL(scan_exits<true>, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, stream, a);
+    const dim3 g1((unsigned)((chunks + 3) / 4));
+    if (len <= (128ull << 20)) {
+        if (a.onepass) hipLaunchKernelGGL((scan_exits<false, true>), g1, dim3(256), 0, stream, a);
+        else hipLaunchKernelGGL((scan_exits<false, false>), g1, dim3(256), 0, stream, a);
+    } else {
+        if (a.onepass) hipLaunchKernelGGL((scan_exits<true, true>), g1, dim3(256), 0, stream, a);
+        else hipLaunchKernelGGL((scan_exits<true, false>), g1, dim3(256), 0, stream, a);
+    }
 #if defined(NETC_SCAN_K1_ONLY) || defined(NETC_SCAN_K1_EXP)
     return hipGetLastError();   // diagnostic builds only (tools/): K1 timed alone
 #endif

@@ -111,7 +111,7 @@ def tune(unroll: int = 1, max_blocks: int = 0, flags: int = NETC_GPU_TUNE_AUTO) 
 
 KNOBS = {"ENC_DENSE_BYTES": 1, "ENC_SCAN_PER": 2, "SCAN_FAST_RANK": 3, "SCAN_ANCHOR_SLOTS": 4, "VAL_STEPS": 5, "SCAN_FUSE": 6,
          "MASK_TAPER": 7, "ENC_SRC": 8, "ENC_FIX": 9, "INJECT_FAULT": 10,
-         "ENC_PROBE": 11, "ENC_PF": 12, "SCAN_BLOCK_CHUNKS": 13}
+         "ENC_PROBE": 11, "ENC_PF": 12, "SCAN_BLOCK_CHUNKS": 13, "SCAN_ONEPASS": 14}
 
 
 def set_knob(name: str, value: int) -> None:
@@ -330,7 +330,15 @@ def scan_diag(stream=None, device: int = 0) -> int:
     r = int(_lib.gpu().netc_gpu_scan_diag(device, _stream_handle(stream)))
     if r < -1:
         _check(r)
-    return r
+    return r if r < 0 else r & 0xFFFFFFFF
+
+
+def scan_onepass(stream=None, device: int = 0) -> bool:
+    """bit 32 of netc_gpu_scan_diag: the last scan on `stream` finished on its one-pass path"""
+    r = int(_lib.gpu().netc_gpu_scan_diag(device, _stream_handle(stream)))
+    if r < -1:
+        _check(r)
+    return r >= 0 and bool((r >> 32) & 1)
 
 
 def unmask_frames(wire, hdr, keys, result, length: Optional[int] = None, stream=None,

@@ -382,3 +382,47 @@ def test_emit_block_sizes(torch_cuda, gpu_knob, emit):
     payload = np.concatenate([inner, rng.integers(0, 256, 10, dtype=np.uint8)])
     wire, _ = orc.encode_batch(payload, off, np.array([0, 0x01020304], dtype=np.uint32), None, True)
     assert run_scan(torch_cuda, wire) == 2   # capacity overflow: the serial walk in K4
+
+
+@pytest.mark.parametrize("onepass", ["1", "0"])
+def test_onepass_and_graph_paths(torch_cuda, gpu_knob, onepass):
+    """the one-pass path (K1's chunks resolve the chain by decoupled look-back; K2-K4 only read a
+    flag) and the graph path (knob SCAN_ONEPASS = 0) on the same streams: identical results, and
+    on clean strict streams the one-pass path finishes the call (netc_gpu_scan_diag bit 32)"""
+    gpu_knob("SCAN_ONEPASS", onepass)
+    rng = np.random.default_rng(97)
+    want = onepass == "1"
+    c2, _ = _stream(rng, np.full(65536, 1024))
+    assert run_scan(torch_cuda, c2, parallel=True) == 65536
+    assert nm.scan_onepass() == want
+    c4, _ = _stream(rng, rng.integers(256, 65537, 2000))
+    assert run_scan(torch_cuda, c4, parallel=True) == 2000
+    assert nm.scan_onepass() == want
+    sizes = np.concatenate([rng.integers(0, 5000, 2000), rng.integers(0, 130, 2000), [65535, 65536, 300000]])
+    rng.shuffle(sizes)
+    mixed, wo = _stream(rng, sizes)
+    assert run_scan(torch_cuda, mixed, parallel=True) == sizes.size
+    assert nm.scan_onepass() == want
+    # start offsets, truncations, a frame cap, an error mid-stream, non-strict, tiny frames,
+    # unmasked non-strict, the adversarial overflow: parity whichever path finishes
+    for s in (int(wo[1]), int(wo[3999]), mixed.size):
+        run_scan(torch_cuda, mixed, start=s, parallel=True)
+    for cut in (0, 1, 7, int(wo[2000]) + 3, int(wo[2000]), mixed.size - 1):
+        run_scan(torch_cuda, mixed[:cut], parallel=True)
+    run_scan(torch_cuda, mixed, max_frames=1234, parallel=True)
+    bad = np.concatenate([mixed[:int(wo[1000])], np.frombuffer(bytes.fromhex("c185") + bytes(9), dtype=np.uint8),
+                          mixed[int(wo[1000]):]])
+    run_scan(torch_cuda, bad, strict=True)
+    run_scan(torch_cuda, mixed, strict=False, parallel=True)
+    tiny, _ = _stream(rng, rng.integers(0, 4, 20000))
+    assert run_scan(torch_cuda, tiny, parallel=True) == 20000
+    unm, _ = _stream(rng, rng.integers(0, 3000, 300), masked=False)
+    assert run_scan(torch_cuda, unm, strict=False, parallel=True) == 300
+    rec = b"".join(bytes.fromhex("82fe") + (5000 + i % 997).to_bytes(2, "big") + bytes(4) for i in range(997))
+    inner = np.tile(np.frombuffer(rec, dtype=np.uint8), 20)
+    adv, _ = orc.encode_batch(inner, np.array([0, inner.size], dtype=np.uint64), np.array([0], dtype=np.uint32),
+                              None, True)
+    run_scan(torch_cuda, adv)
+    for _ in range(3):   # epochs: one call after another on the same scratch
+        assert run_scan(torch_cuda, c2[:4096 * 300 + 11], parallel=True) > 0
+        assert run_scan(torch_cuda, c4, parallel=True) == 2000

@@ -29,6 +29,7 @@ def main():
                     help="every frame with RSV1 set (as permessage-deflate sends them): strict rejects the stream; "
                          "non-strict keeps the speculative parallel pass (it filters RSV2 / RSV3 only since round 3; "
                          "ADVICE r2 measured the serial-walk cliff it replaced)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU walks (A/B runs)")
     args = ap.parse_args()
     flags = 0 if args.non_strict else 1
 
@@ -89,7 +90,7 @@ def main():
         cb = np.zeros(n + 1, dtype=np.uint8)
         cons, err = ctypes.c_uint64(0), ctypes.c_uint64(0)
         reps, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < 2.0:
+        while time.perf_counter() - t0 < (0.0 if args.no_cpu else 2.0) or reps == 0:
             orc.lib().oracle_scan_frames(wire.ctypes.data, wire.size, 0, flags, ch.ctypes.data, ck.ctypes.data,
                                          cb.ctypes.data, n + 1, ctypes.addressof(cons), ctypes.addressof(err))
             reps += 1
@@ -98,7 +99,7 @@ def main():
         hres = np.zeros(3, dtype=np.uint64)
         hl = _lib.host().netc_ws_scan_frames_host
         reps, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < 2.0:
+        while time.perf_counter() - t0 < (0.0 if args.no_cpu else 2.0) or reps == 0:
             hl(wire.ctypes.data, wire.size, 0, flags, ch.ctypes.data, ck.ctypes.data, cb.ctypes.data, n + 1,
                hres.ctypes.data)
             reps += 1
@@ -106,7 +107,7 @@ def main():
         print(json.dumps({"workload": wl, "strict": bool(flags), "masked": not args.unmasked, "rsv1": args.rsv1, "frames": int(n), "wire_bytes": int(wire.size), "us_per_scan": round(us, 2),
                           "wire_GBps": round(wire.size / (us * 1e-6) / 1e9, 1),
                           "frames_per_s": round(n / (us * 1e-6), 1), "matches_oracle": bool(ok),
-                          "serial_fallback": hex(nm.scan_diag(s)),
+                          "serial_fallback": hex(nm.scan_diag(s)), "onepass": nm.scan_onepass(s),
                           "cpu_serial_us": round(cpu_s * 1e6, 1),
                           "cpu_serial_frames_per_s": round(n / cpu_s, 1),
                           "host_walk_us": round(host_s * 1e6, 1), "host_walk_ok": int(hres[0]) == n}), flush=True)
