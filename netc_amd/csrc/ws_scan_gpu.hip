@@ -546,6 +546,12 @@ __device__ __forceinline__ bool op_wait(const ScanArgs& a, uint64_t t0, int lane
     return true;
 }
 
+// 16 stream bytes at p of chunk B: K1's LDS copy, which holds the stream's bytes below len once the
+// stream has 16 (a shorter one was loaded from a scratch word: its bytes come from global memory)
+__device__ __forceinline__ Win op_window(const ScanArgs& a, const uint32_t* st, uint64_t B, uint64_t p) {
+    return a.len >= 16 ? window_at(st, (int)(p - B)) : window_global(a, p);
+}
+
 // X(c - 1): where the chain stands when it reaches chunk c (a position >= c's start, or kXEnd)
 __device__ bool op_x_before(const ScanArgs& a, uint64_t c, uint64_t c0, int lane, uint64_t* out) {
     if (c <= c0) {
@@ -655,7 +661,7 @@ __device__ void op_chunk(const ScanArgs& a, uint64_t c, const uint32_t* st, uint
             }
             uint32_t key;
             uint8_t b0;
-            const uint64_t v = B >= a.len ? term(kEnd, p) : parse_at(a, p, window_at(st, (int)(p - B)), &key, &b0);
+            const uint64_t v = B >= a.len ? term(kEnd, p) : parse_at(a, p, op_window(a, st, B, p), &key, &b0);
             if (v & kTerm) {
                 if (term_type(v) == kDead && a.spec) {
                     op_fail(a, lane);
@@ -690,7 +696,7 @@ __device__ void op_chunk(const ScanArgs& a, uint64_t c, const uint32_t* st, uint
         const uint32_t off = q[i];
         uint32_t key;
         uint8_t b0;
-        (void)parse_at(a, B + off, window_at(st, (int)off), &key, &b0);
+        (void)parse_at(a, B + off, op_window(a, st, B, B + off), &key, &b0);
         put_frame(a, F + i, B + off, key, b0);
     }
     if (lane == 0) {
@@ -699,7 +705,7 @@ __device__ void op_chunk(const ScanArgs& a, uint64_t c, const uint32_t* st, uint
             for (uint64_t i = rec - 1; i < cnt; ++i) {
                 uint32_t key;
                 uint8_t b0;
-                const uint64_t v = parse_at(a, p, window_at(st, (int)(p - B)), &key, &b0);
+                const uint64_t v = parse_at(a, p, op_window(a, st, B, p), &key, &b0);
                 if (i >= rec) put_frame(a, F + i, p, key, b0);
                 p = v;
             }
