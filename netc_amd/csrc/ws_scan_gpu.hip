@@ -251,8 +251,10 @@ struct ScanArgs {
     uint32_t* opfail;      // this call's one-pass failure word (flags[4] / flags[5] on alternate calls;
     uint32_t* opfail_prev; // ... K4 zeroes the previous call's, as for ovf)
     uint64_t* st_t;        // per chunk: its exit prediction T      [63:40] epoch | [39:0] value
-    uint64_t* st_x;        // per chunk: X, the chain's first header at or past its end
-    uint64_t* st_f;        // per chunk: its frame count (aggregate) or the frames before its end (inclusive)
+    uint64_t* st_x;        // per chunk: W, where its walk left it (or END)
+    uint32_t* opcnt;       // per chunk: its frames (plain stores, read by the next launch)
+    uint32_t* opbsum;      // per 4 chunks: their frames (atomic adds; zero when a call starts, K4 re-zeroes)
+    uint64_t* opend;       // [0] chunk + 1 where the chain ends, [1] where | dead << 63
     uint64_t epoch;        // 1 .. 2^24 - 1, one per call on the scratch (words of other calls do not match)
 };
 
@@ -482,43 +484,40 @@ static_assert(!NETC_K1_SLIM || 4 * (4 * kStageWords + 8 * kSet + 2 * kQCap) <= 2
 static constexpr int kCheapMax = 64;   // K1: more from the cheap selection: the full quick check instead
 
 // ------------------------------------------------------------------ one pass --
-// The one-pass path: the chunks of K1 resolve the chain themselves, by
-// decoupled look-back, so the graph kernels (K2-K4) only read a flag.
+// The one-pass path: dense streams -- frames shorter than a chunk, so the chain
+// visits every chunk from the start on (the C2 shape) -- are resolved by K1 itself and one
+// prefix-and-emit pass in K2's launch; K3 and K4 then only read a flag.
 //
-// Per chunk c, K1 already has the distinct exits of its exit-capable candidates, and which of
+// K1 already has, per chunk c, the distinct exits of its exit-capable candidates and which of
 // them land on a position that can start a header (the nodes it appends).  T(c), published
-// right after the parse, predicts where a chain that visits c leaves it: the one such exit
-// when there is exactly one (Single E), none (None: a chain that visits c ends in it, or dies at
-// an exit onto a position that cannot start a header), or Multi.  Garbage chains (payload bytes
-// parsed as headers) land on such positions with ~2 % odds, so nearly every chunk is Single or
-// None.  X(c) is the chain's first header at or past c's end, or END.  Then, per chunk:
-//
-//   X(c-1)   look back at the 64 predecessors at once (one load per lane of st_x and st_t): the
-//            nearest published X, carried forward through the chunks after it -- a chunk the
-//            carried X does not reach (X >= its end: a frame covers it) passes X on; one it
-//            does reach maps X to T (END for None; a Multi chunk's own X is waited for)
-//   walk     a visited chunk (X(c-1) inside it) walks its frames from there in LDS (its bytes are
-//            staged for the parse anyway) to its exit; a covered one does nothing
-//   check    the walk's exit against T(c): a chunk whose prediction was wrong (a stream that ends
-//            or dies in it with a garbage exit beside) sets the failure word -- the earliest
-//            wrong chunk always walks from a right entry, so every wrong prediction is seen
-//   F(c)     the frames before c's end: the count published at once (aggregate), then the look-
-//            back's sum back to the nearest inclusive prefix (inclusive)
-//   emit     the chunk's frames at F(c-1) .. F(c) - 1 from its LDS copy; the chunk where the chain
-//            ends writes the results
-//
-// A wait that outlasts kOnePassWait (an adversarial run of Multi chunks, a predecessor that
-// failed), a full candidate queue or exit set, or a speculative (non-strict) stop at a header
-// the filter rejects also set the failure word.  Then K2-K4 run as before, from the nodes K1
-// appended all the same, and overwrite everything this path wrote: the results are the same
-// either way.  Words carry the call's epoch, so no clearing launch is needed.
+// right after the parse, predicts where the chain leaves c: that exit when there is exactly one
+// (Single), None (no such exit: a chain that visits c ends in it, or dies at an exit onto a
+// position that cannot start a header), or Multi.  Garbage chains (payload bytes parsed as
+// headers) land on header-capable positions with ~2 % odds, so nearly every chunk is Single.
+// Each chunk then SPECULATES its entry from its predecessor alone -- T(c-1) if Single, END if
+// None, the predecessor's own walk exit W(c-1) if Multi (the only wait longer than a hop) --
+// walks its frames from there in LDS to its exit W(c), and checks:
+//   * a chunk whose entry lies past its end (a frame covers it: not dense) fails;
+//   * a visited chunk's W(c) must equal T(c) when T(c) is Single, or END when None (the
+//     successor speculated from it);
+//   * a chunk not visited (entry END) must not be Single (its successor would walk from it).
+// By induction from the start chunk (entry = the start, exact), if no chunk fails every
+// speculated entry is the true one.  Each chunk writes its frame count (opcnt), its frames
+// {offset, header byte 0, key} (flist, up to kOpRec; more fails) and adds its count to its
+// 4-chunk block's total (opbsum); the chunk where the chain ends records where (opend).  K2's
+// launch (links_onepass) turns the block totals into each chunk's first frame index and writes
+// the descriptors and results.  A failure (any check, a full queue or exit set, a speculative
+// stop at a header the filter rejects, a wait past kOnePassWait) sets the call's failure word,
+// and K2-K4 run as before from the nodes K1 appended all the same, overwriting what this path
+// wrote: the results are the same either way.  T and W words carry the call's epoch, so they are
+// never cleared per call.
 static constexpr uint64_t kOpBits = 40;
 static constexpr uint64_t kOpMask = (1ull << kOpBits) - 1;
 static constexpr uint64_t kTNone = kOpMask, kTMulti = kOpMask - 1;   // T values; else the exit
-static constexpr uint64_t kXEnd = kOpMask;                              // X: the chain has ended
-static constexpr uint64_t kFIncl = 1ull << 39;                          // F: inclusive (else aggregate)
+static constexpr uint64_t kXEnd = kOpMask;                              // W / entry: no chain here
 static constexpr uint64_t kOnePassWait = 2000000;                       // 20 ms at 100 MHz
 static constexpr uint64_t kOnePassMax = 256ull << 20;                   // default: streams up to 256 MiB
+static constexpr int kOpRec = 32;                                       // frames recorded per chunk (flist)
 
 __device__ __forceinline__ void op_put(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -532,18 +531,25 @@ __device__ __forceinline__ bool op_failed(const ScanArgs& a) {
 __device__ __forceinline__ void op_fail(const ScanArgs& a, int lane) {
     if (lane == 0) __hip_atomic_fetch_or(a.opfail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// the graph kernels: the one-pass path finished this call (every chunk resolved, none failed)
+// the graph kernels: the one-pass path holds this call (every chunk checked, none failed)
 __device__ __forceinline__ bool onepass_done(const ScanArgs& a) { return a.onepass && !op_failed(a); }
 
-// a poll that found a predecessor not published yet: false once the wait is over (failure set)
-__device__ __forceinline__ bool op_wait(const ScanArgs& a, uint64_t t0, int lane) {
-    if (op_failed(a)) return false;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > kOnePassWait) {
-        op_fail(a, lane);
-        return false;
+// the predecessor's word (epoch-checked), waited for; false once the call has failed
+__device__ bool op_await(const ScanArgs& a, const uint64_t* p, int lane, uint64_t* out) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const uint64_t w = op_get(p);
+        if ((w >> kOpBits) == a.epoch) {
+            *out = w & kOpMask;
+            return true;
+        }
+        if (op_failed(a)) return false;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kOnePassWait) {
+            op_fail(a, lane);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
     }
-    __builtin_amdgcn_s_sleep(2);
-    return true;
 }
 
 // 16 stream bytes at p of chunk B: K1's LDS copy, which holds the stream's bytes below len once the
@@ -552,98 +558,38 @@ __device__ __forceinline__ Win op_window(const ScanArgs& a, const uint32_t* st, 
     return a.len >= 16 ? window_at(st, (int)(p - B)) : window_global(a, p);
 }
 
-// X(c - 1): where the chain stands when it reaches chunk c (a position >= c's start, or kXEnd)
-__device__ bool op_x_before(const ScanArgs& a, uint64_t c, uint64_t c0, int lane, uint64_t* out) {
-    if (c <= c0) {
-        *out = a.start;
-        return true;
-    }
-    const uint64_t ep = a.epoch;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        const int64_t j = (int64_t)c - 1 - lane;
-        const bool below = j < (int64_t)c0;   // before the start chunk: X = the start
-        uint64_t wx = 0, wt = 0;
-        if (!below) {
-            wx = op_get(a.st_x + j);
-            wt = op_get(a.st_t + j);
-        }
-        const bool hx = below || (wx >> kOpBits) == ep;
-        const bool ht = !below && (wt >> kOpBits) == ep;
-        const uint64_t bx = __ballot(hx), bt = __ballot(ht);
-        const uint64_t xv = below ? a.start : (wx & kOpMask), tv = wt & kOpMask;
-        if (bx) {
-            const int L = __builtin_ctzll(bx);   // the nearest published X
-            uint64_t X = readlane64(xv, L);
-            bool ok = true;
-            for (int l = L - 1; l >= 0 && X != kXEnd; --l) {   // carried forward to chunk c
-                const uint64_t k = c - 1 - (uint64_t)l;
-                if (X >= (k + 1) * kChunk) continue;   // a frame covers chunk k
-                if (!((bt >> l) & 1)) {
-                    ok = false;   // its T is not published yet
-                    break;
-                }
-                const uint64_t t = readlane64(tv, l);
-                if (t == kTMulti) {
-                    ok = false;   // its own X is needed
-                    break;
-                }
-                X = t == kTNone ? kXEnd : t;
-            }
-            if (ok) {
-                *out = X;
-                return true;
-            }
-        }
-        if (!op_wait(a, t0, lane)) return false;
-    }
-}
-
-// F(c - 1): the chain's frames before chunk c
-__device__ bool op_f_before(const ScanArgs& a, uint64_t c, uint64_t c0, int lane, uint64_t* out) {
-    const uint64_t ep = a.epoch;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    uint64_t acc = 0;
-    for (int64_t top = (int64_t)c - 1; top >= (int64_t)c0;) {
-        const int64_t j = top - lane;
-        const bool below = j < (int64_t)c0;   // an inclusive 0
-        const uint64_t w = below ? 0 : op_get(a.st_f + j);
-        const bool has = below || (w >> kOpBits) == ep;
-        const bool incl = below || (has && (w & kFIncl));
-        const uint64_t bi = __ballot(incl), bh = __ballot(has);
-        const int L = bi ? __builtin_ctzll(bi) : kWave;
-        const uint64_t need = L >= kWave - 1 ? ~0ull : ((2ull << L) - 1);
-        if ((bh & need) != need) {
-            if (!op_wait(a, t0, lane)) return false;
-            continue;
-        }
-        acc += wave_sum(lane <= L && !below ? (w & (kFIncl - 1)) : 0);
-        if (L < kWave) break;
-        top -= kWave;
-    }
-    *out = acc;
-    return true;
-}
-
-// The one-pass path for chunk c (every lane of its wavefront).  st: the chunk's bytes in LDS
-// (unused for the virtual chunk); q: the wave's candidate queue, free again (frame offsets);
-// tval: T(c), or ~0 when the parse overflowed (the call fails).
-__device__ void op_chunk(const ScanArgs& a, uint64_t c, const uint32_t* st, uint16_t* q, uint64_t tval, int lane) {
+// The one-pass tail of K1 for chunk c (every lane of its wavefront).  st: the chunk's bytes in
+// LDS (unused for the virtual chunk); tval: T(c), or ~0 when the parse overflowed.
+__device__ void op_chunk(const ScanArgs& a, uint64_t c, const uint32_t* st, uint64_t tval, int lane) {
     const uint64_t c0 = a.start / kChunk;
-    if (c < c0) return;   // before the stream start: no one looks here
+    if (c < c0) return;   // before the stream start: nothing, no one looks here
     const uint64_t ep = a.epoch << kOpBits;
-    if (tval == ~0ull) {
+    if (tval == ~0ull || op_failed(a)) {
         op_fail(a, lane);
         return;
     }
     if (lane == 0) op_put(a.st_t + c, ep | tval);
-    uint64_t X;
-    if (!op_x_before(a, c, c0, lane, &X)) return;
+    // the entry, speculated from the predecessor alone
+    uint64_t e = a.start;
+    if (c > c0) {
+        uint64_t t;
+        if (!op_await(a, a.st_t + c - 1, lane, &t)) return;
+        if (t == kTMulti && !op_await(a, a.st_x + c - 1, lane, &t)) return;
+        e = t == kTNone ? kXEnd : t;
+    }
     const uint64_t B = c * kChunk, Bend = B + kChunk;
-    uint64_t Xc = X, cnt = 0, endpos = 0;
+    uint64_t W = kXEnd, cnt = 0, endpos = 0;
     int ended = 0;   // 1: the chain ends here (END), 2: it dies here (an error at endpos)
-    if (X != kXEnd && X < Bend) {   // the chain visits chunk c: walk it from X
-        uint64_t p = X;
+    if (e == kXEnd) {
+        if (tval != kTNone && tval != kTMulti) {   // not visited, yet a successor would walk from T
+            op_fail(a, lane);
+            return;
+        }
+    } else if (e >= Bend) {   // a frame covers this chunk: not a dense stream
+        op_fail(a, lane);
+        return;
+    } else {
+        uint64_t p = e;
         for (;;) {
             if (p >= Bend) {   // its exit
                 if (quick_reject(a, p)) {   // onto a position that cannot start a header: dies there
@@ -653,14 +599,13 @@ __device__ void op_chunk(const ScanArgs& a, uint64_t c, const uint32_t* st, uint
                     }
                     ended = 2;
                     endpos = p;
-                    Xc = kXEnd;
                 } else {
-                    Xc = p;
+                    W = p;
                 }
                 break;
             }
-            uint32_t key;
-            uint8_t b0;
+            uint32_t key = 0;
+            uint8_t b0 = 0;
             const uint64_t v = B >= a.len ? term(kEnd, p) : parse_at(a, p, op_window(a, st, B, p), &key, &b0);
             if (v & kTerm) {
                 if (term_type(v) == kDead && a.spec) {
@@ -669,53 +614,25 @@ __device__ void op_chunk(const ScanArgs& a, uint64_t c, const uint32_t* st, uint
                 }
                 ended = term_type(v) == kDead ? 2 : 1;
                 endpos = term_pos(v);
-                Xc = kXEnd;
                 break;
             }
-            if (lane == 0 && cnt < (uint64_t)kQCap) q[cnt] = (uint16_t)(p - B);
+            if (cnt < (uint64_t)kOpRec && lane == 0)
+                a.flist[c * kOpRec + cnt] = (p - B) | (uint64_t)b0 << 16 | (uint64_t)key << 32;
             ++cnt;
             p = v;
         }
-        // the prediction the successors may have used
-        if (tval != kTMulti && (tval == kTNone ? Xc != kXEnd : Xc != tval)) {
-            op_fail(a, lane);
+        if (cnt > (uint64_t)kOpRec || (tval != kTMulti && (tval == kTNone ? W != kXEnd : W != tval))) {
+            op_fail(a, lane);   // more frames than recorded, or a wrong prediction
             return;
         }
     }
     if (lane == 0) {
-        op_put(a.st_x + c, ep | Xc);
-        op_put(a.st_f + c, ep | cnt);
-    }
-    uint64_t F;
-    if (!op_f_before(a, c, c0, lane, &F)) return;
-    if (lane == 0) op_put(a.st_f + c, ep | kFIncl | (F + cnt));
-    // the frames: recorded offsets by all lanes, the rest (a chunk of more than kQCap frames) by lane 0
-    __builtin_amdgcn_wave_barrier();
-    const uint64_t rec = cnt < (uint64_t)kQCap ? cnt : (uint64_t)kQCap;
-    for (uint64_t i = lane; i < rec; i += kWave) {
-        const uint32_t off = q[i];
-        uint32_t key;
-        uint8_t b0;
-        (void)parse_at(a, B + off, op_window(a, st, B, B + off), &key, &b0);
-        put_frame(a, F + i, B + off, key, b0);
-    }
-    if (lane == 0) {
-        if (cnt > rec) {
-            uint64_t p = B + q[rec - 1];
-            for (uint64_t i = rec - 1; i < cnt; ++i) {
-                uint32_t key;
-                uint8_t b0;
-                const uint64_t v = parse_at(a, p, op_window(a, st, B, p), &key, &b0);
-                if (i >= rec) put_frame(a, F + i, p, key, b0);
-                p = v;
-            }
-        }
-        if (ended) {   // the chain ends in this chunk: the results
-            const uint64_t total = F + cnt;
-            a.result[0] = total;
-            a.result[1] = endpos;
-            a.result[2] = ended == 2 ? endpos : ~0ull;
-            if (total <= a.max_frames) a.hdr[total] = endpos;
+        op_put(a.st_x + c, ep | W);
+        a.opcnt[c] = (uint32_t)cnt;
+        if (cnt) atomicAdd(a.opbsum + c / 4, (uint32_t)cnt);
+        if (ended) {   // the chain ends in this chunk: K2's pass writes the results
+            a.opend[0] = c + 1;
+            a.opend[1] = endpos | (ended == 2 ? (1ull << 63) : 0);
         }
     }
 }
@@ -790,7 +707,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     const uint64_t B = c * kChunk, Bend = B + kChunk;
     if (lane == 0 && a.start / kChunk == c) append_cand(a, a.start, true);   // the root node
     if (B >= a.len) {   // the virtual chunk: no bytes
-        if constexpr (ONE) op_chunk(a, c, nullptr, queue[wv], kTNone, lane);
+        if constexpr (ONE) op_chunk(a, c, nullptr, kTNone, lane);
         return;
     }
     uint32_t d[4][4], nx[4];
@@ -968,7 +885,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     }
     if (total > (uint32_t)kQCap) {   // wave-uniform (adversarial payloads, non-strict mode)
         if (lane == 0) atomicOr(a.ovf, kOvfQueue);
-        if constexpr (ONE) op_chunk(a, c, st, queue[wv], ~0ull, lane);
+        if constexpr (ONE) op_chunk(a, c, st, ~0ull, lane);
         return;
     }
     uint32_t at = incl - mine;
@@ -1013,7 +930,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         const uint64_t bn = __ballot(nodes != 0);
         const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(nodes), kWave - 1);
         const uint64_t t = __ballot(ovf) ? ~0ull : (n == 0 ? kTNone : (n > 1 ? kTMulti : readlane64(ex, __builtin_ctzll(bn))));
-        op_chunk(a, c, st, queue[wv], t, lane);
+        op_chunk(a, c, st, t, lane);
     }
 }
 
@@ -1462,11 +1379,71 @@ __device__ __forceinline__ void links_body(const ScanArgs& a, LinksLdsT<BC>& sl)
     }
 }
 
+// K2's launch on the one-pass path: chunks [cb, cb + BC) of the block.  Their first frame indexes
+// (the frames of every chunk before cb, from K1's per-4-chunk totals, then a scan over the block's
+// counts), their descriptors from the frames K1 recorded, and the results where the chain ends.
+static_assert(kOpRec <= kListSlots * kList, "one pass: a chunk's recorded frames fit its flist slots");
+struct OnePassLds {
+    uint64_t red[kScanT / kWave];
+    uint64_t base[kWave];
+    uint32_t cnt[kWave];
+};
+template <int BC>
+__device__ void links_onepass(const ScanArgs& a, void* lds) {   // lds: the launch's own LDS, unused otherwise
+    uint64_t* const red = ((OnePassLds*)lds)->red;
+    uint64_t* const base = ((OnePassLds*)lds)->base;
+    uint32_t* const cnt = ((OnePassLds*)lds)->cnt;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    const uint64_t cb = (uint64_t)blockIdx.x * BC, c0 = a.start / kChunk;
+    uint64_t part = 0;
+    for (uint64_t k = tid; k < cb / 4; k += kScanT) part += a.opbsum[k];
+    part = wave_sum(part);
+    if (lane == 0) red[wv] = part;
+    if (tid < BC) {
+        const uint64_t c = cb + tid;
+        cnt[tid] = c >= c0 && c <= a.nc ? a.opcnt[c] : 0u;
+    }
+    __syncthreads();
+    if (wv == 0) {   // the block's exclusive scan over its chunks (BC <= 64: one wavefront)
+        static_assert(BC <= kWave, "one pass: one wavefront scans the block's chunks");
+        uint64_t pre = 0;
+#pragma unroll
+        for (int w = 0; w < kScanT / kWave; ++w) pre += red[w];
+        const uint32_t v = lane < BC ? cnt[lane] : 0u;
+        const uint32_t incl = wave_incl_sum(v);
+        if (lane < BC) base[lane] = pre + incl - v;
+    }
+    __syncthreads();
+    for (int i = tid; i < BC * kOpRec; i += kScanT) {
+        const int t = i / kOpRec, j = i % kOpRec;
+        if ((uint32_t)j < cnt[t]) {
+            const uint64_t c = cb + t;
+            const uint64_t f = a.flist[c * kOpRec + j];
+            put_frame(a, base[t] + j, c * kChunk + (f & 0xFFFFu), (uint32_t)(f >> 32), (uint8_t)(f >> 16));
+        }
+    }
+    if (tid == 0) {
+        const uint64_t e = a.opend[0] - 1;   // the chunk where the chain ends
+        if (e >= cb && e < cb + BC) {
+            const uint64_t total = base[e - cb] + cnt[e - cb], w = a.opend[1];
+            const uint64_t pos = w & ~(1ull << 63);
+            a.result[0] = total;
+            a.result[1] = pos;
+            a.result[2] = (w >> 63) ? pos : ~0ull;
+            if (total <= a.max_frames) a.hdr[total] = pos;
+        }
+    }
+}
+
 template <int BC>
 __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
     __shared__ LinksLdsT<BC> sl;
     SCAN_SCOPE(1);
-    if (onepass_done(a)) return;   // K1 resolved the chain (block-uniform: one word)
+    if (onepass_done(a)) {   // K1 resolved the chain (block-uniform: one word): the frames' indexes
+        static_assert(sizeof(LinksLdsT<BC>) >= sizeof(OnePassLds), "one pass: its LDS overlays K2's");
+        links_onepass<BC>(a, &sl);
+        return;
+    }
     links_body<false, BC>(a, sl);
 }
 
@@ -2049,7 +2026,10 @@ __global__ __launch_bounds__(kScanT) void scan_links_fused(ScanArgs a, uint64_t 
     __shared__ FusedLds sm;
     __shared__ int flag;
     SCAN_SCOPE(1);
-    if (onepass_done(a)) return;
+    if (onepass_done(a)) {
+        links_onepass<kBlkChunks>(a, &sm);
+        return;
+    }
     links_body<true, kBlkChunks>(a, sm.k2);
     constexpr uint32_t kPerTile = (uint32_t)(kTileChunks / kBlkChunks);
     const uint32_t tile = blockIdx.x / kPerTile;
@@ -2210,6 +2190,7 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
             if (c <= a.nc) {
                 a.ccount[c] = 0;
                 *(uint64_t*)(a.ext + c * kCand) = 0;
+                if ((c & 3) == 0) a.opbsum[c / 4] = 0;
             }
         }
         if (blockIdx.x == 0 && tid == 0) {
@@ -2298,6 +2279,7 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
             }
             a.ccount[c] = 0;
             *(uint64_t*)(a.ext + c * kCand) = 0;   // kCand == 8 flag bytes, 8-aligned
+            if ((c & 3) == 0) a.opbsum[c / 4] = 0;   // the one-pass path's per-4-chunk totals
         }
     }
     if (fb) {   // block-uniform
@@ -2441,8 +2423,8 @@ std::mutex& stream_scratch_mu() {
 // The scratch layout for `cap` chunks (cap a multiple of kTileChunks): offsets of the
 // regions; flags, ccount and ext first -- the region every call leaves zeroed.
 struct Layout {
-    uint64_t flags, ccount, ext, tarr, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, flist, text, tcount, tinfo,
-        st_t, st_x, st_f, total;
+    uint64_t flags, ccount, ext, tarr, opbsum, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, flist, text,
+        tcount, tinfo, st_t, st_x, opcnt, opend, total;
 };
 Layout layout_for(uint64_t cap) {
     auto align = [](uint64_t x) { return (x + 63) & ~63ull; };
@@ -2453,6 +2435,7 @@ Layout layout_for(uint64_t cap) {
     l.ccount = o;  o = align(o + cap * 4);
     l.ext = o;     o = align(o + slots);
     l.tarr = o;    o = align(o + tiles * 4);
+    l.opbsum = o;  o = align(o + cap);            // one pass: per 4 chunks, u32 (K4 re-zeroes)
     l.cleared = o;
     l.cand = o;    o = align(o + slots * 8);
     l.link = o;    o = align(o + slots * 4);
@@ -2463,13 +2446,14 @@ Layout layout_for(uint64_t cap) {
     l.anq = o;     o = align(o + slots * 4);
     l.anc = o;     o = align(o + cap * kAncSlot * 2);
     l.anc_n = o;   o = align(o + cap * 4);
-    l.flist = o;   o = align(o + cap * kListSlots * kList * 8);
+    l.flist = o;   o = align(o + cap * kListSlots * kList * 8);   // (one pass: kOpRec frames per chunk)
     l.text = o;    o = align(o + tiles * kExt * sizeof(TileExt));
     l.tcount = o;  o = align(o + tiles * 4);
     l.tinfo = o;   o = align(o + tiles * sizeof(TileInfo));
     l.st_t = o;    o = align(o + cap * 8);   // one-pass status words (epochs: never cleared per call)
     l.st_x = o;    o = align(o + cap * 8);
-    l.st_f = o;    o = align(o + cap * 8);
+    l.opcnt = o;   o = align(o + cap * 4);
+    l.opend = o;   o = align(o + 16);
     l.total = o;
     return l;
 }
@@ -2598,13 +2582,15 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     const int64_t op = knob(NETC_GPU_KNOB_SCAN_ONEPASS);
     a.onepass = op == 0 ? 0 : ((op == 1 || len <= kOnePassMax) && len < (1ull << 38) ? 1 : 0);
     if (++s.epoch >= (1ull << 24)) {
-        if ((e = hipMemsetAsync(m + l.st_t, 0, l.total - l.st_t, stream)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(m + l.st_t, 0, l.opcnt - l.st_t, stream)) != hipSuccess) return e;
         s.epoch = 1;
     }
     a.epoch = s.epoch;
     a.st_t = (uint64_t*)(m + l.st_t);
     a.st_x = (uint64_t*)(m + l.st_x);
-    a.st_f = (uint64_t*)(m + l.st_f);
+    a.opcnt = (uint32_t*)(m + l.opcnt);
+    a.opbsum = (uint32_t*)(m + l.opbsum);
+    a.opend = (uint64_t*)(m + l.opend);
     a.ccount = (uint32_t*)(m + l.ccount);
     a.ext = m + l.ext;
     a.tarr = (uint32_t*)(m + l.tarr);
