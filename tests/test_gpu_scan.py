@@ -386,23 +386,27 @@ def test_emit_block_sizes(torch_cuda, gpu_knob, emit):
 
 @pytest.mark.parametrize("onepass", ["1", "0"])
 def test_onepass_and_graph_paths(torch_cuda, gpu_knob, onepass):
-    """the one-pass path (K1's chunks resolve the chain by decoupled look-back; K2-K4 only read a
-    flag) and the graph path (knob SCAN_ONEPASS = 0) on the same streams: identical results, and
-    on clean strict streams the one-pass path finishes the call (netc_gpu_scan_diag bit 32)"""
+    """the one-pass path (dense streams: K1's chunks speculate their entries from their
+    predecessors and check them; K2's launch writes the frames; K3 and K4 only read a flag) and the
+    graph path (knob SCAN_ONEPASS = 0) on the same streams: identical results; dense strict streams
+    finish on the one-pass path (netc_gpu_scan_diag bit 32), streams with chunk-covering frames on
+    the graph kernels"""
     gpu_knob("SCAN_ONEPASS", onepass)
     rng = np.random.default_rng(97)
     want = onepass == "1"
     c2, _ = _stream(rng, np.full(65536, 1024))
     assert run_scan(torch_cuda, c2, parallel=True) == 65536
     assert nm.scan_onepass() == want
-    c4, _ = _stream(rng, rng.integers(256, 65537, 2000))
-    assert run_scan(torch_cuda, c4, parallel=True) == 2000
+    dense, _ = _stream(rng, rng.integers(0, 3500, 20000))   # frames shorter than a chunk: every chunk visited
+    assert run_scan(torch_cuda, dense, parallel=True) == 20000
     assert nm.scan_onepass() == want
+    c4, _ = _stream(rng, rng.integers(256, 65537, 2000))   # frames that cover chunks: the graph kernels
+    assert run_scan(torch_cuda, c4, parallel=True) == 2000
+    assert not nm.scan_onepass()
     sizes = np.concatenate([rng.integers(0, 5000, 2000), rng.integers(0, 130, 2000), [65535, 65536, 300000]])
     rng.shuffle(sizes)
     mixed, wo = _stream(rng, sizes)
     assert run_scan(torch_cuda, mixed, parallel=True) == sizes.size
-    assert nm.scan_onepass() == want
     # start offsets, truncations, a frame cap, an error mid-stream, non-strict, tiny frames,
     # unmasked non-strict, the adversarial overflow: parity whichever path finishes
     for s in (int(wo[1]), int(wo[3999]), mixed.size):
