@@ -534,19 +534,27 @@ __device__ __forceinline__ void op_fail(const ScanArgs& a, int lane) {
 // the graph kernels: the one-pass path holds this call (every chunk checked, none failed)
 __device__ __forceinline__ bool onepass_done(const ScanArgs& a) { return a.onepass && !op_failed(a); }
 
-// the predecessor's word (epoch-checked), waited for; false once the call has failed
-__device__ bool op_await(const ScanArgs& a, const uint64_t* p, int lane, uint64_t* out) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        const uint64_t w = op_get(p);
-        if ((w >> kOpBits) == a.epoch) {
+// the predecessor's word, waited for: from global memory (epoch-tagged; the previous block's
+// last chunk) or from this block's LDS (tagged with the chunk index + 1: another block's word left
+// in the same LDS, or the exit-set entry it overlays, never matches); false once the call failed.
+// The time limit and the failure word are looked at every 32 polls.
+template <bool LDS>
+__device__ bool op_await(const ScanArgs& a, const uint64_t* p, uint64_t tag, int lane, uint64_t* out) {
+    uint64_t t0 = 0;
+    for (uint32_t n = 0;; ++n) {
+        const uint64_t w = LDS ? __atomic_load_n((const volatile uint64_t*)p, __ATOMIC_RELAXED) : op_get(p);
+        if ((w >> kOpBits) == tag) {
             *out = w & kOpMask;
             return true;
         }
-        if (op_failed(a)) return false;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kOnePassWait) {
-            op_fail(a, lane);
-            return false;
+        if ((n & 31) == 0) {
+            if (op_failed(a)) return false;
+            const uint64_t t = __builtin_amdgcn_s_memrealtime();
+            if (n == 0) t0 = t;
+            else if (t - t0 > kOnePassWait) {
+                op_fail(a, lane);
+                return false;
+            }
         }
         __builtin_amdgcn_s_sleep(1);
     }
@@ -559,22 +567,32 @@ __device__ __forceinline__ Win op_window(const ScanArgs& a, const uint32_t* st, 
 }
 
 // The one-pass tail of K1 for chunk c (every lane of its wavefront).  st: the chunk's bytes in
-// LDS (unused for the virtual chunk); tval: T(c), or ~0 when the parse overflowed.
-__device__ void op_chunk(const ScanArgs& a, uint64_t c, const uint32_t* st, uint64_t tval, int lane) {
+// LDS (unused for the virtual chunk); tval: T(c), or ~0 when the parse overflowed; pub: the
+// block's exit sets, whose entries 0 and 1 of wave wv carry its T and W to wave wv + 1 once its
+// parse is done.
+__device__ void op_chunk(const ScanArgs& a, uint64_t c, const uint32_t* st, uint64_t tval, int lane,
+                         unsigned long long (*pub)[kSet], int wv) {
     const uint64_t c0 = a.start / kChunk;
     if (c < c0) return;   // before the stream start: nothing, no one looks here
-    const uint64_t ep = a.epoch << kOpBits;
-    if (tval == ~0ull || op_failed(a)) {
+    const uint64_t ep = a.epoch << kOpBits, me = (c + 1) << kOpBits;
+    if (tval == ~0ull) {
         op_fail(a, lane);
         return;
     }
-    if (lane == 0) op_put(a.st_t + c, ep | tval);
+    if (lane == 0) {
+        op_put(a.st_t + c, ep | tval);                              // for the next block's wave 0
+        __atomic_store_n((volatile uint64_t*)&pub[wv][0], me | tval, __ATOMIC_RELAXED);   // for wave wv + 1
+    }
     // the entry, speculated from the predecessor alone
     uint64_t e = a.start;
     if (c > c0) {
         uint64_t t;
-        if (!op_await(a, a.st_t + c - 1, lane, &t)) return;
-        if (t == kTMulti && !op_await(a, a.st_x + c - 1, lane, &t)) return;
+        const bool ok = wv ? op_await<true>(a, (const uint64_t*)&pub[wv - 1][0], c, lane, &t)
+                           : op_await<false>(a, a.st_t + c - 1, a.epoch, lane, &t);
+        if (!ok) return;
+        if (t == kTMulti && !(wv ? op_await<true>(a, (const uint64_t*)&pub[wv - 1][1], c, lane, &t)
+                                 : op_await<false>(a, a.st_x + c - 1, a.epoch, lane, &t)))
+            return;
         e = t == kTNone ? kXEnd : t;
     }
     const uint64_t B = c * kChunk, Bend = B + kChunk;
@@ -591,8 +609,9 @@ __device__ void op_chunk(const ScanArgs& a, uint64_t c, const uint32_t* st, uint
     } else {
         uint64_t p = e;
         for (;;) {
-            if (p >= Bend) {   // its exit
-                if (quick_reject(a, p)) {   // onto a position that cannot start a header: dies there
+            if (p >= Bend) {   // its exit (onto a header-capable position: in T's set, so T None
+                               // means it dies there, and T Single is checked below)
+                if (tval == kTNone || (tval == kTMulti && quick_reject(a, p))) {
                     if (a.spec) {
                         op_fail(a, lane);   // (the speculative pass walks on serially in K4)
                         return;
@@ -628,6 +647,7 @@ __device__ void op_chunk(const ScanArgs& a, uint64_t c, const uint32_t* st, uint
     }
     if (lane == 0) {
         op_put(a.st_x + c, ep | W);
+        if (tval == kTMulti) __atomic_store_n((volatile uint64_t*)&pub[wv][1], me | W, __ATOMIC_RELAXED);
         a.opcnt[c] = (uint32_t)cnt;
         if (cnt) atomicAdd(a.opbsum + c / 4, (uint32_t)cnt);
         if (ended) {   // the chain ends in this chunk: K2's pass writes the results
@@ -703,11 +723,15 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     // then scalar (SGPR arithmetic, scalar branches) instead of per-lane VALU
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(tid / kWave);
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
+    if constexpr (ONE) {   // the waves' T / W hand-off slots (op_chunk) cleared before any wave looks
+        if (lane < 2) set[wv][lane] = 0;
+        __syncthreads();
+    }
     if (c > a.nc) return;
     const uint64_t B = c * kChunk, Bend = B + kChunk;
     if (lane == 0 && a.start / kChunk == c) append_cand(a, a.start, true);   // the root node
     if (B >= a.len) {   // the virtual chunk: no bytes
-        if constexpr (ONE) op_chunk(a, c, nullptr, kTNone, lane);
+        if constexpr (ONE) op_chunk(a, c, nullptr, kTNone, lane, set, wv);
         return;
     }
     uint32_t d[4][4], nx[4];
@@ -885,7 +909,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     }
     if (total > (uint32_t)kQCap) {   // wave-uniform (adversarial payloads, non-strict mode)
         if (lane == 0) atomicOr(a.ovf, kOvfQueue);
-        if constexpr (ONE) op_chunk(a, c, st, ~0ull, lane);
+        if constexpr (ONE) op_chunk(a, c, st, ~0ull, lane, set, wv);
         return;
     }
     uint32_t at = incl - mine;
@@ -930,7 +954,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         const uint64_t bn = __ballot(nodes != 0);
         const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(nodes), kWave - 1);
         const uint64_t t = __ballot(ovf) ? ~0ull : (n == 0 ? kTNone : (n > 1 ? kTMulti : readlane64(ex, __builtin_ctzll(bn))));
-        op_chunk(a, c, st, t, lane);
+        op_chunk(a, c, st, t, lane, set, wv);
     }
 }
 
@@ -2581,7 +2605,7 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     // epoch wraps, the status words are cleared once, so a word left from 2^24 calls ago cannot match.
     const int64_t op = knob(NETC_GPU_KNOB_SCAN_ONEPASS);
     a.onepass = op == 0 ? 0 : ((op == 1 || len <= kOnePassMax) && len < (1ull << 38) ? 1 : 0);
-    if (++s.epoch >= (1ull << 24)) {
+    if (++s.epoch >= (1ull << 24) - 1) {   // (all-ones never: an exit-set entry's ~0 must not match)
         if ((e = hipMemsetAsync(m + l.st_t, 0, l.opcnt - l.st_t, stream)) != hipSuccess) return e;
         s.epoch = 1;
     }
