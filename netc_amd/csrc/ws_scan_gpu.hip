@@ -250,11 +250,10 @@ struct ScanArgs {
     int onepass;           // this call runs it (the host's choice: knob SCAN_ONEPASS, stream size)
     uint32_t* opfail;      // this call's one-pass failure word (flags[4] / flags[5] on alternate calls;
     uint32_t* opfail_prev; // ... K4 zeroes the previous call's, as for ovf)
-    uint64_t* st_t;        // per chunk: its exit prediction T      [63:40] epoch | [39:0] value
-    uint64_t* st_x;        // per chunk: W, where its walk left it (or END)
-    uint32_t* opcnt;       // per chunk: its frames (plain stores, read by the next launch)
-    uint32_t* opbsum;      // per 4 chunks: their frames (atomic adds; zero when a call starts, K4 re-zeroes)
-    uint64_t* opend;       // [0] chunk + 1 where the chain ends, [1] where | dead << 63
+    uint64_t* st_t;        // per chunk: its exit prediction T (K1, plain stores)
+    uint64_t* st_x;        // per chunk: W, where its walk left it (or END), for the next group
+    uint64_t* st_g;        // per group of kPG chunks: its look-back status word
+    uint64_t* opfl;        // per chunk: kOpRec frames {offset, byte 0, key} (the group's own)
     uint64_t epoch;        // 1 .. 2^24 - 1, one per call on the scratch (words of other calls do not match)
 };
 
@@ -483,41 +482,44 @@ static_assert(!NETC_K1_SLIM || 4 * (4 * kStageWords + 8 * kSet + 2 * kQCap) <= 2
               "K1: a 4-wave block must stay within 20,480 B of LDS (8 blocks per CU)");
 static constexpr int kCheapMax = 64;   // K1: more from the cheap selection: the full quick check instead
 
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v);
 // ------------------------------------------------------------------ one pass --
-// The one-pass path: dense streams -- frames shorter than a chunk, so the chain
-// visits every chunk from the start on (the C2 shape) -- are resolved by K1 itself and one
-// prefix-and-emit pass in K2's launch; K3 and K4 then only read a flag.
+// The one-pass path for dense streams -- frames shorter than a chunk, so the chain
+// visits every chunk from the start on (the C2 shape).  K1 publishes, per chunk c, T(c): where
+// the chain leaves c if it visits it, from the distinct exits of c's exit-capable candidates that
+// land on a position able to start a header (the nodes K1 appends): that exit when there is
+// exactly one (Single), None (no such exit: a chain that visits c ends in it, or dies at an exit
+// onto a position that cannot start a header), Multi, or Fail (K1's queue or set overflowed).
+// Garbage chains (payload bytes parsed as headers) land on header-capable positions with ~2 %
+// odds, so nearly every chunk is Single.
 //
-// K1 already has, per chunk c, the distinct exits of its exit-capable candidates and which of
-// them land on a position that can start a header (the nodes it appends).  T(c), published
-// right after the parse, predicts where the chain leaves c: that exit when there is exactly one
-// (Single), None (no such exit: a chain that visits c ends in it, or dies at an exit onto a
-// position that cannot start a header), or Multi.  Garbage chains (payload bytes parsed as
-// headers) land on header-capable positions with ~2 % odds, so nearly every chunk is Single.
-// Each chunk then SPECULATES its entry from its predecessor alone -- T(c-1) if Single, END if
-// None, the predecessor's own walk exit W(c-1) if Multi (the only wait longer than a hop) --
-// walks its frames from there in LDS to its exit W(c), and checks:
-//   * a chunk whose entry lies past its end (a frame covers it: not dense) fails;
-//   * a visited chunk's W(c) must equal T(c) when T(c) is Single, or END when None (the
-//     successor speculated from it);
-//   * a chunk not visited (entry END) must not be Single (its successor would walk from it).
-// By induction from the start chunk (entry = the start, exact), if no chunk fails every
-// speculated entry is the true one.  Each chunk writes its frame count (opcnt), its frames
-// {offset, header byte 0, key} (flist, up to kOpRec; more fails) and adds its count to its
-// 4-chunk block's total (opbsum); the chunk where the chain ends records where (opend).  K2's
-// launch (links_onepass) turns the block totals into each chunk's first frame index and writes
-// the descriptors and results.  A failure (any check, a full queue or exit set, a speculative
-// stop at a header the filter rejects, a wait past kOnePassWait) sets the call's failure word,
-// and K2-K4 run as before from the nodes K1 appended all the same, overwriting what this path
-// wrote: the results are the same either way.  T and W words carry the call's epoch, so they are
-// never cleared per call.
+// K2's launch then runs groups of kPG chunks, claimed in order (one thread per chunk).  Each chunk
+// SPECULATES its entry from its predecessor alone -- T(c-1) if Single, END if None, the
+// predecessor's own walk exit W(c-1) if Multi (handed over in LDS, or across groups in global
+// memory) -- walks its frames from there (header bytes from global memory) to its exit W(c), and
+// checks:
+//   * an entry past the chunk's end (a frame covers it: not a dense stream) fails;
+//   * a visited chunk's W(c) must equal T(c) when T(c) is Single (its successor used T(c));
+//   * a chunk not visited (entry END) must not be Single (its successor would walk from T(c)).
+// By induction from the start chunk (entry = the start), if no chunk fails every speculated entry
+// is the true one.  The group's frame counts are summed, the groups' totals chained by a
+// decoupled look-back (status words tagged with the call's epoch: never cleared per call), and
+// each chunk writes its descriptors; the chunk where the chain ends writes the results.  Once
+// every group is done the blocks read the failure word: on a failure (any check, Fail, a
+// speculative stop at a header the filter rejects, a wait past kOnePassWait) they run K2's own
+// work (claimed, as the groups were) and K3 / K4 follow as before, overwriting everything this
+// path wrote; without one, K3 and K4 only read the word.  The results are the same either way.
 static constexpr uint64_t kOpBits = 40;
 static constexpr uint64_t kOpMask = (1ull << kOpBits) - 1;
-static constexpr uint64_t kTNone = kOpMask, kTMulti = kOpMask - 1;   // T values; else the exit
+static constexpr uint64_t kTNone = kOpMask, kTMulti = kOpMask - 1, kTFail = kOpMask - 2;   // T values; else the exit
 static constexpr uint64_t kXEnd = kOpMask;                              // W / entry: no chain here
+static constexpr uint64_t kWPend = ~0ull;                               // (LDS) W not known yet
 static constexpr uint64_t kOnePassWait = 2000000;                       // 20 ms at 100 MHz
-static constexpr uint64_t kOnePassMax = 256ull << 20;                   // default: streams up to 256 MiB
-static constexpr int kOpRec = 32;                                       // frames recorded per chunk (flist)
+static constexpr uint64_t kOnePassMax = 128ull << 20;                   // default: streams up to 128 MiB
+static constexpr int kOpRec = 32;                                       // frames one chunk may hold
+static constexpr int kPG = kScanT;                                      // chunks per group (a thread each)
+// K2's claim counters in the flags word array (the last block to leave re-zeroes them)
+enum : int { kFPClaim = 6, kFPDone = 7, kFLClaim = 11, kFExit = 14 };
 
 __device__ __forceinline__ void op_put(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -528,22 +530,18 @@ __device__ __forceinline__ uint64_t op_get(const uint64_t* p) {
 __device__ __forceinline__ bool op_failed(const ScanArgs& a) {
     return __hip_atomic_load(a.opfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 }
-__device__ __forceinline__ void op_fail(const ScanArgs& a, int lane) {
-    if (lane == 0) __hip_atomic_fetch_or(a.opfail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void op_fail(const ScanArgs& a) {
+    __hip_atomic_fetch_or(a.opfail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// the graph kernels: the one-pass path holds this call (every chunk checked, none failed)
+// K3 / K4: the one-pass path holds this call (every group checked, none failed)
 __device__ __forceinline__ bool onepass_done(const ScanArgs& a) { return a.onepass && !op_failed(a); }
 
-// the predecessor's word, waited for: from global memory (epoch-tagged; the previous block's
-// last chunk) or from this block's LDS (tagged with the chunk index + 1: another block's word left
-// in the same LDS, or the exit-set entry it overlays, never matches); false once the call failed.
-// The time limit and the failure word are looked at every 32 polls.
-template <bool LDS>
-__device__ bool op_await(const ScanArgs& a, const uint64_t* p, uint64_t tag, int lane, uint64_t* out) {
+// a global word tagged with the call's epoch, waited for (one thread); false once the call failed
+__device__ bool op_await(const ScanArgs& a, const uint64_t* p, uint64_t* out) {
     uint64_t t0 = 0;
     for (uint32_t n = 0;; ++n) {
-        const uint64_t w = LDS ? __atomic_load_n((const volatile uint64_t*)p, __ATOMIC_RELAXED) : op_get(p);
-        if ((w >> kOpBits) == tag) {
+        const uint64_t w = op_get(p);
+        if ((w >> kOpBits) == a.epoch) {
             *out = w & kOpMask;
             return true;
         }
@@ -552,7 +550,7 @@ __device__ bool op_await(const ScanArgs& a, const uint64_t* p, uint64_t tag, int
             const uint64_t t = __builtin_amdgcn_s_memrealtime();
             if (n == 0) t0 = t;
             else if (t - t0 > kOnePassWait) {
-                op_fail(a, lane);
+                op_fail(a);
                 return false;
             }
         }
@@ -560,100 +558,180 @@ __device__ bool op_await(const ScanArgs& a, const uint64_t* p, uint64_t tag, int
     }
 }
 
-// 16 stream bytes at p of chunk B: K1's LDS copy, which holds the stream's bytes below len once the
-// stream has 16 (a shorter one was loaded from a scratch word: its bytes come from global memory)
-__device__ __forceinline__ Win op_window(const ScanArgs& a, const uint32_t* st, uint64_t B, uint64_t p) {
-    return a.len >= 16 ? window_at(st, (int)(p - B)) : window_global(a, p);
+// K1: T(c) for K2's launch (a plain store: the next launch reads it)
+__device__ __forceinline__ void op_publish_t(const ScanArgs& a, uint64_t c, uint64_t tval, int lane) {
+    if (lane == 0 && c >= a.start / kChunk) a.st_t[c] = tval;
 }
 
-// The one-pass tail of K1 for chunk c (every lane of its wavefront).  st: the chunk's bytes in
-// LDS (unused for the virtual chunk); tval: T(c), or ~0 when the parse overflowed; pub: the
-// block's exit sets, whose entries 0 and 1 of wave wv carry its T and W to wave wv + 1 once its
-// parse is done.
-__device__ void op_chunk(const ScanArgs& a, uint64_t c, const uint32_t* st, uint64_t tval, int lane,
-                         unsigned long long (*pub)[kSet], int wv) {
-    const uint64_t c0 = a.start / kChunk;
-    if (c < c0) return;   // before the stream start: nothing, no one looks here
-    const uint64_t ep = a.epoch << kOpBits, me = (c + 1) << kOpBits;
-    if (tval == ~0ull) {
-        op_fail(a, lane);
-        return;
+struct OpGroupLds {
+    uint64_t w[kPG];            // W per chunk, kWPend until its walk is done
+    uint32_t wsum[kScanT / kWave];
+    uint64_t base;              // the group's first frame index
+    uint32_t item;
+    int flag;
+};
+
+// the group's status word: [63:62] 1 aggregate / 2 inclusive | [61:38] epoch | [37:0] frames
+static constexpr int kGValBits = 38;
+__device__ __forceinline__ uint64_t op_gword(uint64_t flag, uint64_t epoch, uint64_t v) {
+    return flag << 62 | (epoch & 0xFFFFFF) << kGValBits | (v & ((1ull << kGValBits) - 1));
+}
+
+// the frames before group g (wave 0; its aggregate `agg` published first); false once the call failed
+__device__ bool op_group_prefix(const ScanArgs& a, uint64_t g, uint64_t agg, int lane, uint64_t* out) {
+    if (lane == 0) op_put(a.st_g + g, op_gword(1, a.epoch, agg));
+    uint64_t acc = 0, t0 = 0;
+    uint32_t n = 0;
+    for (int64_t top = (int64_t)g - 1; top >= 0; ++n) {
+        const int64_t idx = top - lane;
+        uint64_t v = 0;
+        bool ok = true, incl = idx < 0;   // before group 0: an inclusive 0
+        if (idx >= 0) {
+            const uint64_t w = op_get(a.st_g + idx);
+            ok = (w >> 62) != 0 && ((w >> kGValBits) & 0xFFFFFF) == (a.epoch & 0xFFFFFF);
+            incl = ok && (w >> 62) == 2;
+            v = w & ((1ull << kGValBits) - 1);
+        }
+        const uint64_t im = __ballot(incl);
+        const int stop = im ? __builtin_ctzll(im) : kWave;   // the nearest inclusive prefix
+        const uint64_t need = stop >= kWave - 1 ? ~0ull : ((2ull << stop) - 1);
+        if ((__ballot(ok) & need) != need) {   // a predecessor has not published yet
+            if ((n & 31) == 0) {
+                if (op_failed(a)) return false;
+                const uint64_t t = __builtin_amdgcn_s_memrealtime();
+                if (n == 0) t0 = t;
+                else if (t - t0 > kOnePassWait) {
+                    if (lane == 0) op_fail(a);
+                    return false;
+                }
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        acc += wave_sum(lane <= stop && idx >= 0 ? v : 0);
+        if (stop < kWave) break;
+        top -= kWave;
     }
-    if (lane == 0) {
-        op_put(a.st_t + c, ep | tval);                              // for the next block's wave 0
-        __atomic_store_n((volatile uint64_t*)&pub[wv][0], me | tval, __ATOMIC_RELAXED);   // for wave wv + 1
-    }
-    // the entry, speculated from the predecessor alone
-    uint64_t e = a.start;
-    if (c > c0) {
-        uint64_t t;
-        const bool ok = wv ? op_await<true>(a, (const uint64_t*)&pub[wv - 1][0], c, lane, &t)
-                           : op_await<false>(a, a.st_t + c - 1, a.epoch, lane, &t);
-        if (!ok) return;
-        if (t == kTMulti && !(wv ? op_await<true>(a, (const uint64_t*)&pub[wv - 1][1], c, lane, &t)
-                                 : op_await<false>(a, a.st_x + c - 1, a.epoch, lane, &t)))
-            return;
-        e = t == kTNone ? kXEnd : t;
-    }
+    if (lane == 0) op_put(a.st_g + g, op_gword(2, a.epoch, acc + agg));
+    *out = acc;
+    return true;
+}
+
+// One group: chunks [g kPG, (g + 1) kPG), thread t the chunk g kPG + t (every thread of the block).
+__device__ __forceinline__ void op_group(const ScanArgs& a, uint64_t g, OpGroupLds& L) {
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    const uint64_t c0 = a.start / kChunk, c = g * kPG + tid;
+    const bool mine = c >= c0 && c <= a.nc;
     const uint64_t B = c * kChunk, Bend = B + kChunk;
-    uint64_t W = kXEnd, cnt = 0, endpos = 0;
-    int ended = 0;   // 1: the chain ends here (END), 2: it dies here (an error at endpos)
-    if (e == kXEnd) {
-        if (tval != kTNone && tval != kTMulti) {   // not visited, yet a successor would walk from T
-            op_fail(a, lane);
-            return;
-        }
-    } else if (e >= Bend) {   // a frame covers this chunk: not a dense stream
-        op_fail(a, lane);
-        return;
-    } else {
-        uint64_t p = e;
-        for (;;) {
-            if (p >= Bend) {   // its exit (onto a header-capable position: in T's set, so T None
-                               // means it dies there, and T Single is checked below)
-                if (tval == kTNone || (tval == kTMulti && quick_reject(a, p))) {
-                    if (a.spec) {
-                        op_fail(a, lane);   // (the speculative pass walks on serially in K4)
-                        return;
-                    }
-                    ended = 2;
-                    endpos = p;
+    const uint64_t tval = mine ? a.st_t[c] : kTNone;
+    bool bad = mine && tval == kTFail;
+    // the entry: from T(c - 1), or W(c - 1) when T(c - 1) is Multi (known later: rounds below)
+    uint64_t e = kXEnd;
+    bool known = true;
+    if (mine && c == c0) {
+        e = a.start;
+    } else if (mine) {
+        const uint64_t tp = a.st_t[c - 1];
+        if (tp == kTFail) bad = true;
+        else if (tp == kTMulti) known = false;
+        else e = tp == kTNone ? kXEnd : tp;
+    }
+    L.w[tid] = mine ? kWPend : kXEnd;
+    uint64_t cnt = 0, endpos = 0, W = kXEnd;
+    int ended = 0;   // 1: the chain ends in this chunk (END), 2: it dies here (an error at endpos)
+    bool done = !mine;
+    for (;;) {
+        __syncthreads();
+        if (!done && !known) {   // W(c - 1): the previous thread's, or the previous group's last
+            if (tid > 0) {
+                const uint64_t w = L.w[tid - 1];
+                if (w != kWPend) {
+                    e = w;
+                    known = true;
+                }
+            } else {
+                uint64_t w;
+                if (op_await(a, a.st_x + c - 1, &w)) {
+                    e = w;
+                    known = true;
                 } else {
-                    W = p;
+                    bad = true;
                 }
-                break;
             }
-            uint32_t key = 0;
-            uint8_t b0 = 0;
-            const uint64_t v = B >= a.len ? term(kEnd, p) : parse_at(a, p, op_window(a, st, B, p), &key, &b0);
-            if (v & kTerm) {
-                if (term_type(v) == kDead && a.spec) {
-                    op_fail(a, lane);
-                    return;
-                }
-                ended = term_type(v) == kDead ? 2 : 1;
-                endpos = term_pos(v);
-                break;
-            }
-            if (cnt < (uint64_t)kOpRec && lane == 0)
-                a.flist[c * kOpRec + cnt] = (p - B) | (uint64_t)b0 << 16 | (uint64_t)key << 32;
-            ++cnt;
-            p = v;
         }
-        if (cnt > (uint64_t)kOpRec || (tval != kTMulti && (tval == kTNone ? W != kXEnd : W != tval))) {
-            op_fail(a, lane);   // more frames than recorded, or a wrong prediction
-            return;
+        if (!done && (known || bad)) {
+            done = true;
+            if (!bad && e == kXEnd) {
+                if (tval != kTNone && tval != kTMulti) bad = true;   // not visited, yet Single
+            } else if (!bad && e >= Bend) {
+                bad = true;   // a frame covers this chunk: not dense
+            } else if (!bad) {
+                uint64_t p = e;
+                for (;;) {
+                    if (p >= Bend) {   // its exit (onto a header-capable position it would be in T's set)
+                        if (tval == kTNone || (tval == kTMulti && quick_reject(a, p))) {
+                            if (a.spec) bad = true;   // (the speculative pass walks on serially in K4)
+                            ended = 2;
+                            endpos = p;
+                        } else {
+                            W = p;
+                        }
+                        break;
+                    }
+                    uint32_t key = 0;
+                    uint8_t b0 = 0;
+                    const uint64_t v = parse_at(a, p, window_global(a, p), &key, &b0);
+                    if (v & kTerm) {
+                        if (term_type(v) == kDead && a.spec) bad = true;
+                        ended = term_type(v) == kDead ? 2 : 1;
+                        endpos = term_pos(v);
+                        break;
+                    }
+                    if (cnt < (uint64_t)kOpRec) a.opfl[c * kOpRec + cnt] = (p - B) | (uint64_t)b0 << 16 | (uint64_t)key << 32;
+                    ++cnt;
+                    p = v;
+                }
+                if (cnt > (uint64_t)kOpRec || (tval != kTMulti && tval != kTNone && W != tval)) bad = true;
+            }
+            L.w[tid] = W;
+            if (tid == kPG - 1 && mine) op_put(a.st_x + c, a.epoch << kOpBits | W);   // for the next group
+        }
+        if (!__syncthreads_or(!done)) break;
+    }
+    if (__syncthreads_or(bad)) {
+        if (tid == 0) op_fail(a);
+        return;
+    }
+    // the frames before each chunk: the group's scan, then the groups' look-back
+    const uint32_t incl = wave_incl_sum((uint32_t)cnt);
+    if (lane == kWave - 1) L.wsum[wv] = incl;
+    __syncthreads();
+    uint64_t before = incl - (uint32_t)cnt;
+    for (int k = 0; k < wv; ++k) before += L.wsum[k];
+    if (wv == 0) {
+        uint64_t agg = 0;
+#pragma unroll
+        for (int k = 0; k < kScanT / kWave; ++k) agg += L.wsum[k];
+        uint64_t pre = 0;
+        const bool ok = op_group_prefix(a, g, agg, lane, &pre);
+        if (lane == 0) {
+            L.base = pre;
+            L.flag = ok;
         }
     }
-    if (lane == 0) {
-        op_put(a.st_x + c, ep | W);
-        if (tval == kTMulti) __atomic_store_n((volatile uint64_t*)&pub[wv][1], me | W, __ATOMIC_RELAXED);
-        a.opcnt[c] = (uint32_t)cnt;
-        if (cnt) atomicAdd(a.opbsum + c / 4, (uint32_t)cnt);
-        if (ended) {   // the chain ends in this chunk: K2's pass writes the results
-            a.opend[0] = c + 1;
-            a.opend[1] = endpos | (ended == 2 ? (1ull << 63) : 0);
-        }
+    __syncthreads();
+    if (!L.flag) return;   // (the call failed meanwhile)
+    const uint64_t k0 = L.base + before;
+    for (uint64_t i = 0; i < cnt; ++i) {
+        const uint64_t f = a.opfl[c * kOpRec + i];
+        put_frame(a, k0 + i, B + (f & 0xFFFFu), (uint32_t)(f >> 32), (uint8_t)(f >> 16));
+    }
+    if (ended) {   // the chain ends in this chunk: the results
+        const uint64_t total = k0 + cnt;
+        a.result[0] = total;
+        a.result[1] = endpos;
+        a.result[2] = ended == 2 ? endpos : ~0ull;
+        if (total <= a.max_frames) a.hdr[total] = endpos;
     }
 }
 
@@ -708,7 +786,7 @@ __device__ __forceinline__ u32x4 k1_load(const uint8_t* p) {
     return *(const NETC_GLOBAL u32x4u*)p;
 }
 
-// ONE: the one-pass path after the parse (op_chunk).
+// ONE: the one-pass path's prediction T(c) after the parse (op_publish_t).
 template <bool NT, bool ONE>
 __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     __shared__ uint32_t stage[4][kStageWords];   // per wave: its chunk's bytes (+ 16 after)
@@ -723,15 +801,11 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     // then scalar (SGPR arithmetic, scalar branches) instead of per-lane VALU
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(tid / kWave);
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
-    if constexpr (ONE) {   // the waves' T / W hand-off slots (op_chunk) cleared before any wave looks
-        if (lane < 2) set[wv][lane] = 0;
-        __syncthreads();
-    }
     if (c > a.nc) return;
     const uint64_t B = c * kChunk, Bend = B + kChunk;
     if (lane == 0 && a.start / kChunk == c) append_cand(a, a.start, true);   // the root node
     if (B >= a.len) {   // the virtual chunk: no bytes
-        if constexpr (ONE) op_chunk(a, c, nullptr, kTNone, lane, set, wv);
+        if constexpr (ONE) op_publish_t(a, c, kTNone, lane);
         return;
     }
     uint32_t d[4][4], nx[4];
@@ -909,7 +983,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     }
     if (total > (uint32_t)kQCap) {   // wave-uniform (adversarial payloads, non-strict mode)
         if (lane == 0) atomicOr(a.ovf, kOvfQueue);
-        if constexpr (ONE) op_chunk(a, c, st, ~0ull, lane, set, wv);
+        if constexpr (ONE) op_publish_t(a, c, kTFail, lane);
         return;
     }
     uint32_t at = incl - mine;
@@ -953,8 +1027,8 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         // T(c) from the distinct exits onto header-capable positions (a full set: unknown)
         const uint64_t bn = __ballot(nodes != 0);
         const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(nodes), kWave - 1);
-        const uint64_t t = __ballot(ovf) ? ~0ull : (n == 0 ? kTNone : (n > 1 ? kTMulti : readlane64(ex, __builtin_ctzll(bn))));
-        op_chunk(a, c, st, t, lane, set, wv);
+        const uint64_t t = __ballot(ovf) ? kTFail : (n == 0 ? kTNone : (n > 1 ? kTMulti : readlane64(ex, __builtin_ctzll(bn))));
+        op_publish_t(a, c, t, lane);
     }
 }
 
@@ -1095,6 +1169,7 @@ struct LinksLdsT {
     };
     uint16_t queue[BC * kCand];   // queued nodes (slot in the block); kQTaken once the wavefront path took one
     int nq;
+    uint32_t item;                // (one pass) the block of K2's work this block claimed
 };
 using LinksLds = LinksLdsT<kBlkChunks>;
 static constexpr uint16_t kQTaken = 0xFFFF;
@@ -1165,7 +1240,7 @@ __device__ __forceinline__ void chunk_regs_store(uint32_t* words, const ChunkReg
 // false (wave-uniform, nothing written) leaves it to the block path.  qi: its queue index
 // (anchor slot as the block path).  x: the node's position (a.cand[node]).
 template <bool SC1, int BC>
-__device__ __forceinline__ bool dense_node(const ScanArgs& a, DenseLds& d, uint64_t node, uint64_t x, uint32_t qi DENSE_ARG) {
+__device__ __forceinline__ bool dense_node(const ScanArgs& a, DenseLds& d, uint64_t node, uint64_t x, uint32_t qi, uint32_t bid DENSE_ARG) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;
     DENSE_T(1);
@@ -1216,7 +1291,7 @@ __device__ __forceinline__ bool dense_node(const ScanArgs& a, DenseLds& d, uint6
     DENSE_T(4);
     if (__builtin_amdgcn_readfirstlane((int)e) == (int)kNoLink) return false;   // wave-uniform (not listed)
     // anchor j (every 8 frames from the entry) by lane j mod 64: s64^(j/8), then s8^(j%8)
-    const uint64_t q = (uint64_t)blockIdx.x * BC + qi;
+    const uint64_t q = (uint64_t)bid * BC + qi;
     const bool keep = qi < (uint32_t)BC && q < a.anc_cap;
     uint16_t* anc = a.anc + (keep ? q : 0) * kAncSlot;
     uint32_t na = 0;   // anchors (wave-uniform)
@@ -1271,13 +1346,13 @@ __device__ __forceinline__ bool dense_node(const ScanArgs& a, DenseLds& d, uint6
 }
 
 template <bool SC1, int BC>
-__device__ __forceinline__ void links_body(const ScanArgs& a, LinksLdsT<BC>& sl) {
+__device__ __forceinline__ void links_body(const ScanArgs& a, LinksLdsT<BC>& sl, uint32_t bid) {
     uint32_t* words = sl.b.words;
     uint16_t* l1 = sl.b.l1;
     uint16_t* lj = sl.b.lj;
     uint16_t* lk16 = sl.b.lk16;
     uint16_t* queue = sl.queue;
-    const uint64_t blk0 = (uint64_t)blockIdx.x * (BC * kCand);   // the block's first node slot
+    const uint64_t blk0 = (uint64_t)bid * (BC * kCand);   // the block's first node slot
     int& nq = sl.nq;
     const int tid = threadIdx.x;
     if (tid == 0) nq = 0;
@@ -1358,7 +1433,7 @@ __device__ __forceinline__ void links_body(const ScanArgs& a, LinksLdsT<BC>& sl)
             const int qn = qi + kScanT / kWave;
             rfast = qn < n && chunk_regs_load(a, (blk0 + queue[qn]) / kCand * kChunk, lane, R);
             wave_lds_sync();
-            if (dense_node<SC1, BC>(a, d, node, x, (uint32_t)qi DENSE_PASS) && lane == 0) queue[qi] = kQTaken;
+            if (dense_node<SC1, BC>(a, d, node, x, (uint32_t)qi, bid DENSE_PASS) && lane == 0) queue[qi] = kQTaken;
             wave_lds_sync();   // (the next chunk overwrites d)
         }
         DENSE_FLUSH();
@@ -1376,7 +1451,7 @@ __device__ __forceinline__ void links_body(const ScanArgs& a, LinksLdsT<BC>& sl)
             uint32_t p = (uint32_t)(x - B), hops = 0;
             // the walk's positions every 8 frames are K4's anchors if this node turns out
             // to be its chunk's true entry: kept in the block's slots while they last
-            const uint64_t q = (uint64_t)blockIdx.x * BC + qi;
+            const uint64_t q = (uint64_t)bid * BC + qi;
             const bool keep = qi < BC && q < a.anc_cap;
             uint16_t* anc = a.anc + (keep ? q : 0) * kAncSlot;
             int na = 0;
@@ -1403,72 +1478,80 @@ __device__ __forceinline__ void links_body(const ScanArgs& a, LinksLdsT<BC>& sl)
     }
 }
 
-// K2's launch on the one-pass path: chunks [cb, cb + BC) of the block.  Their first frame indexes
-// (the frames of every chunk before cb, from K1's per-4-chunk totals, then a scan over the block's
-// counts), their descriptors from the frames K1 recorded, and the results where the chain ends.
-static_assert(kOpRec <= kListSlots * kList, "one pass: a chunk's recorded frames fit its flist slots");
-struct OnePassLds {
-    uint64_t red[kScanT / kWave];
-    uint64_t base[kWave];
-    uint32_t cnt[kWave];
-};
+// K2's launch on the one-pass path: the groups (op_group), claimed in order; once every group is
+// done, the failure word decides whether K2's own work runs (then its blocks' worth is claimed the
+// same way).  Claims make any number of resident blocks enough: a block never waits on one that
+// has not started.  True: the graph path goes on.
 template <int BC>
-__device__ void links_onepass(const ScanArgs& a, void* lds) {   // lds: the launch's own LDS, unused otherwise
-    uint64_t* const red = ((OnePassLds*)lds)->red;
-    uint64_t* const base = ((OnePassLds*)lds)->base;
-    uint32_t* const cnt = ((OnePassLds*)lds)->cnt;
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
-    const uint64_t cb = (uint64_t)blockIdx.x * BC, c0 = a.start / kChunk;
-    uint64_t part = 0;
-    for (uint64_t k = tid; k < cb / 4; k += kScanT) part += a.opbsum[k];
-    part = wave_sum(part);
-    if (lane == 0) red[wv] = part;
-    if (tid < BC) {
-        const uint64_t c = cb + tid;
-        cnt[tid] = c >= c0 && c <= a.nc ? a.opcnt[c] : 0u;
+__device__ bool onepass_groups(const ScanArgs& a, LinksLdsT<BC>& sl) {
+    static_assert(sizeof(LinksLdsT<BC>) >= sizeof(OpGroupLds), "one pass: its LDS overlays K2's");
+    OpGroupLds& L = *reinterpret_cast<OpGroupLds*>(&sl);
+    uint32_t* const f = a.flags;
+    const int tid = threadIdx.x;
+    const uint32_t groups = (uint32_t)(a.nc / kPG + 1);
+    for (;;) {
+        if (tid == 0) L.item = __hip_atomic_fetch_add(f + kFPClaim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const uint32_t g = L.item;
+        if (g >= groups) break;   // block-uniform
+        op_group(a, g, L);
+        __syncthreads();   // (every thread's failure atomic before the group counts as done)
+        if (tid == 0) __hip_atomic_fetch_add(f + kFPDone, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid == 0) {   // every group claimed: wait for the last ones, then the verdict
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(f + kFPDone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < groups) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 5 * kOnePassWait) {   // (cannot happen: a safety valve)
+                op_fail(a);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        L.flag = op_failed(a);
     }
     __syncthreads();
-    if (wv == 0) {   // the block's exclusive scan over its chunks (BC <= 64: one wavefront)
-        static_assert(BC <= kWave, "one pass: one wavefront scans the block's chunks");
-        uint64_t pre = 0;
-#pragma unroll
-        for (int w = 0; w < kScanT / kWave; ++w) pre += red[w];
-        const uint32_t v = lane < BC ? cnt[lane] : 0u;
-        const uint32_t incl = wave_incl_sum(v);
-        if (lane < BC) base[lane] = pre + incl - v;
-    }
+    const bool graph = L.flag != 0;
     __syncthreads();
-    for (int i = tid; i < BC * kOpRec; i += kScanT) {
-        const int t = i / kOpRec, j = i % kOpRec;
-        if ((uint32_t)j < cnt[t]) {
-            const uint64_t c = cb + t;
-            const uint64_t f = a.flist[c * kOpRec + j];
-            put_frame(a, base[t] + j, c * kChunk + (f & 0xFFFFu), (uint32_t)(f >> 32), (uint8_t)(f >> 16));
-        }
-    }
-    if (tid == 0) {
-        const uint64_t e = a.opend[0] - 1;   // the chunk where the chain ends
-        if (e >= cb && e < cb + BC) {
-            const uint64_t total = base[e - cb] + cnt[e - cb], w = a.opend[1];
-            const uint64_t pos = w & ~(1ull << 63);
-            a.result[0] = total;
-            a.result[1] = pos;
-            a.result[2] = (w >> 63) ? pos : ~0ull;
-            if (total <= a.max_frames) a.hdr[total] = pos;
-        }
+    return graph;
+}
+
+// the last block to leave re-zeroes the claim counters for the next call
+__device__ __forceinline__ void onepass_leave(const ScanArgs& a) {
+    uint32_t* const f = a.flags;
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(f + kFExit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+        __hip_atomic_store(f + kFPClaim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(f + kFPDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(f + kFLClaim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(f + kFExit, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-template <int BC>
+// OP: the one-pass groups first (a separate instance: their registers would cost the plain K2
+// occupancy); K2's own work only if they failed, its blocks' worth claimed.
+template <int BC, bool OP>
 __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
     __shared__ LinksLdsT<BC> sl;
     SCAN_SCOPE(1);
-    if (onepass_done(a)) {   // K1 resolved the chain (block-uniform: one word): the frames' indexes
-        static_assert(sizeof(LinksLdsT<BC>) >= sizeof(OnePassLds), "one pass: its LDS overlays K2's");
-        links_onepass<BC>(a, &sl);
+    constexpr bool claim = OP;
+    if (claim && !onepass_groups<BC>(a, sl)) {
+        onepass_leave(a);
         return;
     }
-    links_body<false, BC>(a, sl);
+    uint32_t* const item = &sl.item;
+    for (uint32_t it = blockIdx.x;;) {
+        if (claim) {
+            __syncthreads();
+            if (threadIdx.x == 0)
+                *item = __hip_atomic_fetch_add(a.flags + kFLClaim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            it = *item;
+            if (it >= gridDim.x) break;
+        }
+        links_body<false, BC>(a, sl, it);
+        if (!claim) break;
+    }
+    if (claim) onepass_leave(a);
 }
 
 // exclusive prefix sum over a block of NT threads; the block total in *total
@@ -2050,11 +2133,7 @@ __global__ __launch_bounds__(kScanT) void scan_links_fused(ScanArgs a, uint64_t 
     __shared__ FusedLds sm;
     __shared__ int flag;
     SCAN_SCOPE(1);
-    if (onepass_done(a)) {
-        links_onepass<kBlkChunks>(a, &sm);
-        return;
-    }
-    links_body<true, kBlkChunks>(a, sm.k2);
+    links_body<true, kBlkChunks>(a, sm.k2, blockIdx.x);
     constexpr uint32_t kPerTile = (uint32_t)(kTileChunks / kBlkChunks);
     const uint32_t tile = blockIdx.x / kPerTile;
     const uint32_t in_tile = min(blocks - tile * kPerTile, kPerTile);
@@ -2214,7 +2293,6 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
             if (c <= a.nc) {
                 a.ccount[c] = 0;
                 *(uint64_t*)(a.ext + c * kCand) = 0;
-                if ((c & 3) == 0) a.opbsum[c / 4] = 0;
             }
         }
         if (blockIdx.x == 0 && tid == 0) {
@@ -2303,7 +2381,6 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
             }
             a.ccount[c] = 0;
             *(uint64_t*)(a.ext + c * kCand) = 0;   // kCand == 8 flag bytes, 8-aligned
-            if ((c & 3) == 0) a.opbsum[c / 4] = 0;   // the one-pass path's per-4-chunk totals
         }
     }
     if (fb) {   // block-uniform
@@ -2447,8 +2524,8 @@ std::mutex& stream_scratch_mu() {
 // The scratch layout for `cap` chunks (cap a multiple of kTileChunks): offsets of the
 // regions; flags, ccount and ext first -- the region every call leaves zeroed.
 struct Layout {
-    uint64_t flags, ccount, ext, tarr, opbsum, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, flist, text,
-        tcount, tinfo, st_t, st_x, opcnt, opend, total;
+    uint64_t flags, ccount, ext, tarr, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, flist, text,
+        tcount, tinfo, st_t, st_x, st_g, opfl, total;
 };
 Layout layout_for(uint64_t cap) {
     auto align = [](uint64_t x) { return (x + 63) & ~63ull; };
@@ -2459,7 +2536,6 @@ Layout layout_for(uint64_t cap) {
     l.ccount = o;  o = align(o + cap * 4);
     l.ext = o;     o = align(o + slots);
     l.tarr = o;    o = align(o + tiles * 4);
-    l.opbsum = o;  o = align(o + cap);            // one pass: per 4 chunks, u32 (K4 re-zeroes)
     l.cleared = o;
     l.cand = o;    o = align(o + slots * 8);
     l.link = o;    o = align(o + slots * 4);
@@ -2476,8 +2552,8 @@ Layout layout_for(uint64_t cap) {
     l.tinfo = o;   o = align(o + tiles * sizeof(TileInfo));
     l.st_t = o;    o = align(o + cap * 8);   // one-pass status words (epochs: never cleared per call)
     l.st_x = o;    o = align(o + cap * 8);
-    l.opcnt = o;   o = align(o + cap * 4);
-    l.opend = o;   o = align(o + 16);
+    l.st_g = o;    o = align(o + (cap / kPG + 1) * 8);
+    l.opfl = o;    o = align(o + cap * kOpRec * 8);
     l.total = o;
     return l;
 }
@@ -2604,17 +2680,20 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     // stream; positions must fit its 40-bit words.  Each call has its own epoch; when the 24-bit
     // epoch wraps, the status words are cleared once, so a word left from 2^24 calls ago cannot match.
     const int64_t op = knob(NETC_GPU_KNOB_SCAN_ONEPASS);
-    a.onepass = op == 0 ? 0 : ((op == 1 || len <= kOnePassMax) && len < (1ull << 38) ? 1 : 0);
+    const int64_t fuse = knob(NETC_GPU_KNOB_SCAN_FUSE);
+    // (the one-pass groups run in scan_links: not with K2 + K3 fused into one launch)
+    a.onepass = op == 0 || (fuse == 1 && tiles <= (uint64_t)kFuseTiles)
+                    ? 0
+                    : ((op == 1 || len <= kOnePassMax) && len < (1ull << 38) ? 1 : 0);
     if (++s.epoch >= (1ull << 24) - 1) {   // (all-ones never: an exit-set entry's ~0 must not match)
-        if ((e = hipMemsetAsync(m + l.st_t, 0, l.opcnt - l.st_t, stream)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(m + l.st_t, 0, l.opfl - l.st_t, stream)) != hipSuccess) return e;
         s.epoch = 1;
     }
     a.epoch = s.epoch;
     a.st_t = (uint64_t*)(m + l.st_t);
     a.st_x = (uint64_t*)(m + l.st_x);
-    a.opcnt = (uint32_t*)(m + l.opcnt);
-    a.opbsum = (uint32_t*)(m + l.opbsum);
-    a.opend = (uint64_t*)(m + l.opend);
+    a.st_g = (uint64_t*)(m + l.st_g);
+    a.opfl = (uint64_t*)(m + l.opfl);
     a.ccount = (uint32_t*)(m + l.ccount);
     a.ext = m + l.ext;
     a.tarr = (uint32_t*)(m + l.tarr);
@@ -2663,15 +2742,15 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     // profiles/r04ii_scan_fuse.json -- the tiles' K3a still waits for each tile's slowest K2
     // block and K3b for the last tile, so the overlap saves little, while the launch runs at the
     // fused LDS footprint (4 blocks per CU against K2's 5).  Not the default.)
-    const int64_t fuse = knob(NETC_GPU_KNOB_SCAN_FUSE);
     const int64_t bk = knob(NETC_GPU_KNOB_SCAN_BLOCK_CHUNKS);
     const bool big = bk == kBlkChunksBig || (bk != kBlkChunks && chunks > kBigBlocksAbove);
     auto links = [&]() {
         if (big)
-            hipLaunchKernelGGL(scan_links<kBlkChunksBig>, dim3((unsigned)((chunks + kBlkChunksBig - 1) / kBlkChunksBig)),
-                               dim3(kScanT), 0, stream, a);
+            hipLaunchKernelGGL((a.onepass ? scan_links<kBlkChunksBig, true> : scan_links<kBlkChunksBig, false>),
+                               dim3((unsigned)((chunks + kBlkChunksBig - 1) / kBlkChunksBig)), dim3(kScanT), 0, stream, a);
         else
-            hipLaunchKernelGGL(scan_links<kBlkChunks>, dim3(blk), dim3(kScanT), 0, stream, a);
+            hipLaunchKernelGGL((a.onepass ? scan_links<kBlkChunks, true> : scan_links<kBlkChunks, false>), dim3(blk),
+                               dim3(kScanT), 0, stream, a);
     };
     if (fuse == 1 && tiles <= (uint64_t)kFuseTiles) {   // (32 chunks per K2 block: the tiles' arrival counts)
         hipLaunchKernelGGL(scan_links_fused, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
