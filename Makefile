@@ -132,7 +132,7 @@ clean:
 
 # diagnostics (tools/, not part of the product)
 diag: tools/libdiag_stream.so tools/libnetc_ws_gpu_stamps.so tools/libnetc_ws_gpu_checks.so tools/libscan_k1only.so \
-      tools/libscan_k1exp.so
+      tools/libscan_k1exp.so diag/libnetc_ws_gpu_trace.so
 tools/libdiag_stream.so: tools/diag_stream.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 tools/libnetc_ws_gpu_stamps.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
@@ -141,6 +141,10 @@ tools/libnetc_ws_gpu_checks.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
 	$(HIPCC) $(HIPFLAGS) -DNETC_ENC_CHECKS -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 tools/libscan_k1only.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
 	$(HIPCC) $(HIPFLAGS) -DNETC_SCAN_K1_ONLY -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
+# one-pass scan progress words in host-mapped memory (tools/scan_probe.py); diag/ travels to the GPU box
+diag/libnetc_ws_gpu_trace.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
+	@mkdir -p diag
+	$(HIPCC) $(HIPFLAGS) -DNETC_SCAN_TRACE -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 tools/libscan_k1exp.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
 	$(HIPCC) $(HIPFLAGS) -DNETC_SCAN_K1_EXP -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 

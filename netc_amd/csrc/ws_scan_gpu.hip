@@ -162,6 +162,21 @@ extern "C" int netc_gpu_debug_dense_phases(unsigned long long* out8, int reset) 
 #define DENSE_FLUSH() ((void)0)
 #endif
 
+#ifdef NETC_SCAN_TRACE
+// diagnostic build only (tools/scan_probe.py): progress words in host-mapped memory, readable
+// while a kernel still runs
+__device__ uint32_t* g_op_trace;
+extern "C" int netc_gpu_debug_scan_trace(void* host_mapped) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_op_trace), &host_mapped, sizeof(host_mapped));
+}
+#define OP_TRACE(i, v) \
+    do { \
+        if (g_op_trace) __hip_atomic_store(g_op_trace + (i), (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+    } while (0)
+#else
+#define OP_TRACE(i, v) ((void)0)
+#endif
+
 __device__ __forceinline__ uint64_t term(uint64_t type, uint64_t pos) { return kTerm | type << 61 | pos; }
 __device__ __forceinline__ uint64_t term_type(uint64_t v) { return (v >> 61) & 3; }
 __device__ __forceinline__ uint64_t term_pos(uint64_t v) { return v & kPosMask; }
@@ -507,7 +522,7 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v);
 // each chunk writes its descriptors; the chunk where the chain ends writes the results.  Once
 // every group is done the blocks read the failure word: on a failure (any check, Fail, a
 // speculative stop at a header the filter rejects, a wait past kOnePassWait) they run K2's own
-// work (claimed, as the groups were) and K3 / K4 follow as before, overwriting everything this
+// work (a block each) and K3 / K4 follow as before, overwriting everything this
 // path wrote; without one, K3 and K4 only read the word.  The results are the same either way.
 static constexpr uint64_t kOpBits = 40;
 static constexpr uint64_t kOpMask = (1ull << kOpBits) - 1;
@@ -516,10 +531,11 @@ static constexpr uint64_t kXEnd = kOpMask;                              // W / e
 static constexpr uint64_t kWPend = ~0ull;                               // (LDS) W not known yet
 static constexpr uint64_t kOnePassWait = 2000000;                       // 20 ms at 100 MHz
 static constexpr uint64_t kOnePassMax = 128ull << 20;                   // default: streams up to 128 MiB
+static constexpr uint64_t kOnePassCap = 256ull << 20;                   // knob 1: up to 256 MiB (256 groups)
 static constexpr int kOpRec = 32;                                       // frames one chunk may hold
 static constexpr int kPG = kScanT;                                      // chunks per group (a thread each)
 // K2's claim counters in the flags word array (the last block to leave re-zeroes them)
-enum : int { kFPClaim = 6, kFPDone = 7, kFLClaim = 11, kFExit = 14 };
+enum : int { kFPClaim = 6, kFPDone = 7, kFExit = 14 };
 
 __device__ __forceinline__ void op_put(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -582,6 +598,7 @@ __device__ bool op_group_prefix(const ScanArgs& a, uint64_t g, uint64_t agg, int
     if (lane == 0) op_put(a.st_g + g, op_gword(1, a.epoch, agg));
     uint64_t acc = 0, t0 = 0;
     uint32_t n = 0;
+    if (lane == 0) OP_TRACE(5, g + 1);   // prefix of group g started
     for (int64_t top = (int64_t)g - 1; top >= 0; ++n) {
         const int64_t idx = top - lane;
         uint64_t v = 0;
@@ -613,6 +630,7 @@ __device__ bool op_group_prefix(const ScanArgs& a, uint64_t g, uint64_t agg, int
         top -= kWave;
     }
     if (lane == 0) op_put(a.st_g + g, op_gword(2, a.epoch, acc + agg));
+    if (lane == 0) OP_TRACE(6, g + 1);   // prefix of group g done
     *out = acc;
     return true;
 }
@@ -637,14 +655,17 @@ __device__ __forceinline__ void op_group(const ScanArgs& a, uint64_t g, OpGroupL
         else e = tp == kTNone ? kXEnd : tp;
     }
     L.w[tid] = mine ? kWPend : kXEnd;
+    __syncthreads();   // every chunk's W slot set before any thread reads its neighbour's
     uint64_t cnt = 0, endpos = 0, W = kXEnd;
     int ended = 0;   // 1: the chain ends in this chunk (END), 2: it dies here (an error at endpos)
+    // per thread, no barrier inside (a chunk after a Multi one spins on its neighbour's W in LDS;
+    // the group's first chunk on the previous group's, in global memory)
     bool done = !mine;
-    for (;;) {
-        __syncthreads();
-        if (!done && !known) {   // W(c - 1): the previous thread's, or the previous group's last
+    uint64_t t0 = 0;
+    for (uint32_t n = 0; !done; ++n) {
+        if (!known && !bad) {
             if (tid > 0) {
-                const uint64_t w = L.w[tid - 1];
+                const uint64_t w = __atomic_load_n((volatile uint64_t*)&L.w[tid - 1], __ATOMIC_RELAXED);
                 if (w != kWPend) {
                     e = w;
                     known = true;
@@ -659,46 +680,52 @@ __device__ __forceinline__ void op_group(const ScanArgs& a, uint64_t g, OpGroupL
                 }
             }
         }
-        if (!done && (known || bad)) {
-            done = true;
-            if (!bad && e == kXEnd) {
-                if (tval != kTNone && tval != kTMulti) bad = true;   // not visited, yet Single
-            } else if (!bad && e >= Bend) {
-                bad = true;   // a frame covers this chunk: not dense
-            } else if (!bad) {
-                uint64_t p = e;
-                for (;;) {
-                    if (p >= Bend) {   // its exit (onto a header-capable position it would be in T's set)
-                        if (tval == kTNone || (tval == kTMulti && quick_reject(a, p))) {
-                            if (a.spec) bad = true;   // (the speculative pass walks on serially in K4)
-                            ended = 2;
-                            endpos = p;
-                        } else {
-                            W = p;
-                        }
-                        break;
-                    }
-                    uint32_t key = 0;
-                    uint8_t b0 = 0;
-                    const uint64_t v = parse_at(a, p, window_global(a, p), &key, &b0);
-                    if (v & kTerm) {
-                        if (term_type(v) == kDead && a.spec) bad = true;
-                        ended = term_type(v) == kDead ? 2 : 1;
-                        endpos = term_pos(v);
-                        break;
-                    }
-                    if (cnt < (uint64_t)kOpRec) a.opfl[c * kOpRec + cnt] = (p - B) | (uint64_t)b0 << 16 | (uint64_t)key << 32;
-                    ++cnt;
-                    p = v;
-                }
-                if (cnt > (uint64_t)kOpRec || (tval != kTMulti && tval != kTNone && W != tval)) bad = true;
+        if (!known && !bad) {   // the neighbour is not done yet
+            if ((n & 31) == 0) {
+                const uint64_t t = __builtin_amdgcn_s_memrealtime();
+                if (n == 0) t0 = t;
+                else if (t - t0 > kOnePassWait) bad = true;
             }
-            L.w[tid] = W;
-            if (tid == kPG - 1 && mine) op_put(a.st_x + c, a.epoch << kOpBits | W);   // for the next group
+            __builtin_amdgcn_s_sleep(1);
+            continue;
         }
-        if (!__syncthreads_or(!done)) break;
+        done = true;
+        if (!bad && e == kXEnd) {
+            if (tval != kTNone && tval != kTMulti) bad = true;   // not visited, yet Single
+        } else if (!bad && e >= Bend) {
+            bad = true;   // a frame covers this chunk: not dense
+        } else if (!bad) {
+            uint64_t p = e;
+            for (;;) {
+                if (p >= Bend) {   // its exit (onto a header-capable position it would be in T's set)
+                    if (tval == kTNone || (tval == kTMulti && quick_reject(a, p))) {
+                        if (a.spec) bad = true;   // (the speculative pass walks on serially in K4)
+                        ended = 2;
+                        endpos = p;
+                    } else {
+                        W = p;
+                    }
+                    break;
+                }
+                uint32_t key = 0;
+                uint8_t b0 = 0;
+                const uint64_t v = parse_at(a, p, window_global(a, p), &key, &b0);
+                if (v & kTerm) {
+                    if (term_type(v) == kDead && a.spec) bad = true;
+                    ended = term_type(v) == kDead ? 2 : 1;
+                    endpos = term_pos(v);
+                    break;
+                }
+                if (cnt < (uint64_t)kOpRec) a.opfl[c * kOpRec + cnt] = (p - B) | (uint64_t)b0 << 16 | (uint64_t)key << 32;
+                ++cnt;
+                p = v;
+            }
+            if (cnt > (uint64_t)kOpRec || (tval != kTMulti && tval != kTNone && W != tval)) bad = true;
+        }
+        __atomic_store_n((volatile uint64_t*)&L.w[tid], W, __ATOMIC_RELAXED);
+        if (tid == kPG - 1) op_put(a.st_x + c, a.epoch << kOpBits | W);   // for the next group
     }
-    if (__syncthreads_or(bad)) {
+    if (__builtin_amdgcn_readfirstlane(__syncthreads_or(bad))) {
         if (tid == 0) op_fail(a);
         return;
     }
@@ -720,7 +747,7 @@ __device__ __forceinline__ void op_group(const ScanArgs& a, uint64_t g, OpGroupL
         }
     }
     __syncthreads();
-    if (!L.flag) return;   // (the call failed meanwhile)
+    if (!__builtin_amdgcn_readfirstlane(L.flag)) return;   // (the call failed meanwhile)
     const uint64_t k0 = L.base + before;
     for (uint64_t i = 0; i < cnt; ++i) {
         const uint64_t f = a.opfl[c * kOpRec + i];
@@ -789,6 +816,7 @@ __device__ __forceinline__ u32x4 k1_load(const uint8_t* p) {
 // ONE: the one-pass path's prediction T(c) after the parse (op_publish_t).
 template <bool NT, bool ONE>
 __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) OP_TRACE(0, 1);
     __shared__ uint32_t stage[4][kStageWords];   // per wave: its chunk's bytes (+ 16 after)
     __shared__ unsigned long long set[4][kSet];
     __shared__ uint16_t queue[4][kQCap];
@@ -1478,39 +1506,44 @@ __device__ __forceinline__ void links_body(const ScanArgs& a, LinksLdsT<BC>& sl,
     }
 }
 
-// K2's launch on the one-pass path: the groups (op_group), claimed in order; once every group is
-// done, the failure word decides whether K2's own work runs (then its blocks' worth is claimed the
-// same way).  Claims make any number of resident blocks enough: a block never waits on one that
-// has not started.  True: the graph path goes on.
+// K2's launch on the one-pass path: the groups (op_group), claimed in order (a block's look-back
+// waits only on groups claimed before its own, by blocks already running); once every group is
+// done, the failure word decides whether K2's own work runs.  True: the graph path goes on.
 template <int BC>
 __device__ bool onepass_groups(const ScanArgs& a, LinksLdsT<BC>& sl) {
     static_assert(sizeof(LinksLdsT<BC>) >= sizeof(OpGroupLds), "one pass: its LDS overlays K2's");
     OpGroupLds& L = *reinterpret_cast<OpGroupLds*>(&sl);
     uint32_t* const f = a.flags;
     const int tid = threadIdx.x;
-    const uint32_t groups = (uint32_t)(a.nc / kPG + 1);
-    for (;;) {
-        if (tid == 0) L.item = __hip_atomic_fetch_add(f + kFPClaim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const uint32_t g = L.item;
-        if (g >= groups) break;   // block-uniform
+    const uint32_t groups = (uint32_t)(a.nc / kPG + 1);   // (<= the launch's blocks: one claim each)
+    // No loop with a barrier in it here: every branch around a barrier goes on a value made
+    // wave-uniform with readfirstlane, and each block claims at most one group.  (A first build
+    // looped over claims; the compiler, taking the loop's exit as divergent, restructured it per
+    // lane and the barriers paired up with the wrong ones: group 0 ran for ever.)
+    if (tid == 0) L.item = __hip_atomic_fetch_add(f + kFPClaim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t g = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.item);
+    if (tid == 0) OP_TRACE(1, g + 1);   // last group claimed
+    if (g < groups) {
         op_group(a, g, L);
         __syncthreads();   // (every thread's failure atomic before the group counts as done)
         if (tid == 0) __hip_atomic_fetch_add(f + kFPDone, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) OP_TRACE(2, g + 1);   // last group done
     }
-    if (tid == 0) {   // every group claimed: wait for the last ones, then the verdict
+    if (tid == 0) {   // every group claimed or being claimed: wait for them, then the verdict
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__hip_atomic_load(f + kFPDone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < groups) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 5 * kOnePassWait) {   // (cannot happen: a safety valve)
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 5 * kOnePassWait) {   // (a safety valve)
                 op_fail(a);
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
         }
         L.flag = op_failed(a);
+        OP_TRACE(3, 1 + L.flag);   // the verdict
     }
     __syncthreads();
-    const bool graph = L.flag != 0;
+    const bool graph = __builtin_amdgcn_readfirstlane(L.flag) != 0;
     __syncthreads();
     return graph;
 }
@@ -1522,36 +1555,19 @@ __device__ __forceinline__ void onepass_leave(const ScanArgs& a) {
         __hip_atomic_fetch_add(f + kFExit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
         __hip_atomic_store(f + kFPClaim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(f + kFPDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(f + kFLClaim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(f + kFExit, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 // OP: the one-pass groups first (a separate instance: their registers would cost the plain K2
-// occupancy); K2's own work only if they failed, its blocks' worth claimed.
+// occupancy); K2's own work only if they failed.
 template <int BC, bool OP>
 __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
     __shared__ LinksLdsT<BC> sl;
     SCAN_SCOPE(1);
-    constexpr bool claim = OP;
-    if (claim && !onepass_groups<BC>(a, sl)) {
-        onepass_leave(a);
-        return;
-    }
-    uint32_t* const item = &sl.item;
-    for (uint32_t it = blockIdx.x;;) {
-        if (claim) {
-            __syncthreads();
-            if (threadIdx.x == 0)
-                *item = __hip_atomic_fetch_add(a.flags + kFLClaim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __syncthreads();
-            it = *item;
-            if (it >= gridDim.x) break;
-        }
-        links_body<false, BC>(a, sl, it);
-        if (!claim) break;
-    }
-    if (claim) onepass_leave(a);
+    // (a block goes on to its own K2 work only after every group is done: nothing waits there)
+    if (!OP || onepass_groups<BC>(a, sl)) links_body<false, BC>(a, sl, blockIdx.x);
+    if (OP) onepass_leave(a);
 }
 
 // exclusive prefix sum over a block of NT threads; the block total in *total
@@ -2167,6 +2183,7 @@ __global__ __launch_bounds__(kScanT) void scan_tiles_resolve(ScanArgs a, uint64_
     __shared__ MergedLds sm;
     __shared__ int last;
     SCAN_SCOPE(2);
+    if (threadIdx.x == 0 && blockIdx.x == 0) OP_TRACE(7, 1);
     if (onepass_done(a)) return;
     tiles_body<false>(a, blockIdx.x, sm.k3a);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 stores have completed
@@ -2287,6 +2304,7 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
     (void)tiles;
     const int tid = threadIdx.x;
     const uint64_t tile = (uint64_t)blockIdx.x * EC / kTileChunks;   // EC divides kTileChunks
+    if (tid == 0 && blockIdx.x == 0) OP_TRACE(8, 1);
     if (onepass_done(a)) {   // K1 wrote the frames and results: only the clearing for the next call
         if (tid < EC) {
             const uint64_t c = (uint64_t)blockIdx.x * EC + tid;
@@ -2676,15 +2694,16 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.opfail = a.flags + ((s.calls & 1) ? 5 : 4);
     a.opfail_prev = a.flags + ((s.calls & 1) ? 4 : 5);
     ++s.calls;
-    // the one-pass path: knob SCAN_ONEPASS (0 never, 1 always), by default up to kOnePassMax of
-    // stream; positions must fit its 40-bit words.  Each call has its own epoch; when the 24-bit
+    // the one-pass path: knob SCAN_ONEPASS (0 never, 1 up to 256 MiB), by default up to
+    // kOnePassMax of stream.  (Each of K2's blocks claims at most one group and waits for all of
+    // them: 256 MiB is 256 groups, a block per CU -- resident whatever else the CU holds.)  Each call has its own epoch; when the 24-bit
     // epoch wraps, the status words are cleared once, so a word left from 2^24 calls ago cannot match.
     const int64_t op = knob(NETC_GPU_KNOB_SCAN_ONEPASS);
     const int64_t fuse = knob(NETC_GPU_KNOB_SCAN_FUSE);
     // (the one-pass groups run in scan_links: not with K2 + K3 fused into one launch)
     a.onepass = op == 0 || (fuse == 1 && tiles <= (uint64_t)kFuseTiles)
                     ? 0
-                    : ((op == 1 || len <= kOnePassMax) && len < (1ull << 38) ? 1 : 0);
+                    : (len <= (op == 1 ? kOnePassCap : kOnePassMax) ? 1 : 0);
     if (++s.epoch >= (1ull << 24) - 1) {   // (all-ones never: an exit-set entry's ~0 must not match)
         if ((e = hipMemsetAsync(m + l.st_t, 0, l.opfl - l.st_t, stream)) != hipSuccess) return e;
         s.epoch = 1;
