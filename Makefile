@@ -27,7 +27,7 @@ GPU_HDRS   := netc_amd/csrc/ws_mask_gpu.h netc_amd/csrc/gpu_util.h include/ws/ma
 all: host gpu oracle mock
 mock: tests/bin/libnetc_ingest_mock.so tests/bin/ws_close_track_mock tests/bin/libnetc_hub_cpu.so tests/bin/ws_hub_server_cpu \
       tests/bin/ws_egress_hub_server_cpu tests/bin/ws_echo_server_cpu
-host: $(LIBDIR)/libnetc.so
+host: $(LIBDIR)/libnetc.so tests/bin/ws_route_lookup
 gpu: $(LIBDIR)/libnetc_ws_gpu.so $(LIBDIR)/libnetc_ceiling.so tests/bin/ws_gpu_epoll tests/bin/ws_egress_bench \
      tests/bin/ws_route_bench tests/bin/ws_hub_server tests/bin/ws_egress_hub_server tests/bin/ws_echo_server \
      tests/bin/ws_close_track
@@ -121,13 +121,19 @@ tests/bin/%_cpu: tests/drivers/%.c tests/bin/libnetc_hub_cpu.so $(LIBDIR)/libnet
 	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -Ltests/bin -lnetc_hub_cpu -L$(LIBDIR) -lnetc \
 	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -lpthread -ldl
 
+# the per-call cost of an attached socket's route lookups, close-tracked or fstat-checked (host only)
+tests/bin/ws_route_lookup: tests/drivers/ws_route_lookup.c $(LIBDIR)/libnetc.so $(HOST_HDRS)
+	@mkdir -p tests/bin
+	$(CC) -O2 -g -Wall -std=gnu11 -Iinclude -o $@ $< -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -lpthread -ldl
+
 oracle:
 	$(MAKE) -C oracle
 
 clean:
 	rm -f $(LIBDIR)/*.so build/*.o tests/bin/ws_gpu_epoll tests/bin/ws_egress_bench tests/bin/ws_route_bench \
 	    tests/bin/libnetc_ingest_mock.so tests/bin/ws_hub_server tests/bin/ws_egress_hub_server tests/bin/ws_echo_server \
-	    tests/bin/ws_close_track tests/bin/ws_close_track_mock tests/bin/libnetc_hub_cpu.so tests/bin/*_cpu
+	    tests/bin/ws_close_track tests/bin/ws_close_track_mock tests/bin/libnetc_hub_cpu.so tests/bin/*_cpu \
+	    tests/bin/ws_route_lookup
 	$(MAKE) -C oracle clean
 
 # diagnostics (tools/, not part of the product)

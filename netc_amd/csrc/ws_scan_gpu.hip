@@ -665,7 +665,7 @@ __device__ __forceinline__ void op_group(const ScanArgs& a, uint64_t g, OpGroupL
     for (uint32_t n = 0; !done; ++n) {
         if (!known && !bad) {
             if (tid > 0) {
-                const uint64_t w = __atomic_load_n((volatile uint64_t*)&L.w[tid - 1], __ATOMIC_RELAXED);
+                const uint64_t w = __atomic_load_n((volatile NETC_LDS uint64_t*)&L.w[tid - 1], __ATOMIC_RELAXED);
                 if (w != kWPend) {
                     e = w;
                     known = true;
@@ -722,7 +722,7 @@ __device__ __forceinline__ void op_group(const ScanArgs& a, uint64_t g, OpGroupL
             }
             if (cnt > (uint64_t)kOpRec || (tval != kTMulti && tval != kTNone && W != tval)) bad = true;
         }
-        __atomic_store_n((volatile uint64_t*)&L.w[tid], W, __ATOMIC_RELAXED);
+        __atomic_store_n((volatile NETC_LDS uint64_t*)&L.w[tid], W, __ATOMIC_RELAXED);
         if (tid == kPG - 1) op_put(a.st_x + c, a.epoch << kOpBits | W);   // for the next group
     }
     if (__builtin_amdgcn_readfirstlane(__syncthreads_or(bad))) {
@@ -1527,12 +1527,17 @@ __device__ bool onepass_groups(const ScanArgs& a, LinksLdsT<BC>& sl) {
     if (g < groups) {
         op_group(a, g, L);
         __syncthreads();   // (every thread's failure atomic before the group counts as done)
-        if (tid == 0) __hip_atomic_fetch_add(f + kFPDone, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) __hip_atomic_fetch_add(f + kFPDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (tid == 0) OP_TRACE(2, g + 1);   // last group done
     }
+    // Relaxed (sc1) polls: an acquire or release at agent scope writes back or invalidates the
+    // whole L2 of the XCD (buffer_wbl2 / buffer_inv sc1) -- hundreds of waiting blocks doing that
+    // cost this launch 150 us at config 2 (r06l).  Only the failure word is read after the wait,
+    // itself an atomic, and every failure atomic of a group is done (vmcnt, the barrier above)
+    // before its count goes up.
     if (tid == 0) {   // every group claimed or being claimed: wait for them, then the verdict
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(f + kFPDone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < groups) {
+        while (__hip_atomic_load(f + kFPDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < groups) {
             if (__builtin_amdgcn_s_memrealtime() - t0 > 5 * kOnePassWait) {   // (a safety valve)
                 op_fail(a);
                 break;
@@ -2409,7 +2414,7 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
     SCAN_STAMP(4, 1);
     // anchored chunks: one wavefront each, the chunk's bytes staged in the wavefront's LDS (one
     // coalesced 4-KiB read; the 8-frame runs from the anchors then parse from LDS instead of a
-    // dependent global read per frame: K4 117 -> see DESIGN §14 at 64 MiB of 16-B frames)
+    // dependent global read per frame: K4 117 -> see DESIGN_ROUNDS.md §14 at 64 MiB of 16-B frames)
     const int lane = tid & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(tid / kWave);
     for (int q = wv; q < nqa; q += kScanT / kWave) {
         const uint64_t node = qa_node[q], chunk = node / kCand, B = chunk * kChunk, Bend = B + kChunk;

@@ -44,3 +44,21 @@ def test_close_tracking_mock(mode, verify):
 @pytest.mark.parametrize("mode,verify", [("close", False), ("raw", False), ("close", True)])
 def test_close_tracking_gpu(mode, verify):
     run("ws_close_track", mode, verify)
+
+
+@pytest.mark.parametrize("verify", [False, True])
+def test_route_lookup_identity(verify):
+    """tests/drivers/ws_route_lookup.c: the lookups of every ws_parse_frame / ws_send_message call on
+    an attached socket resolve; close-tracked (netc's link) unless NETC_WS_ROUTE_VERIFY forces the
+    per-call fstat.  (The timing it prints is DESIGN.md §16.1's; not asserted here.)"""
+    import json
+    exe = os.path.join(ROOT, "tests", "bin", "ws_route_lookup")
+    env = dict(os.environ)
+    env.pop("NETC_WS_ROUTE_VERIFY", None)
+    if verify:
+        env["NETC_WS_ROUTE_VERIFY"] = "1"
+    r = subprocess.run([exe, "20000"], capture_output=True, text=True, env=env, timeout=60)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["ok"] is True
+    assert d["tracked"] == (0 if verify else 1)

@@ -126,7 +126,7 @@ def test_hot_kernels_do_not_spill(resources):
 
 def test_scan_k1_fits_eight_blocks_per_cu():
     """K1 (scan_exits) at 20,480 B of LDS per 4-wave block: 8 blocks, the SIMDs' 32 waves, fit a
-    CU's 160 KiB (C4 scan 81.2 -> 80.1 us against the 20,608-B layout)"""
+    CU's 160 KiB (C4 scan 81.2 -> 80.1 us against the 20,608-B layout; DESIGN_ROUNDS.md §15.5)"""
     if not os.path.exists(LIB) or not os.path.exists(READELF):
         pytest.skip("libnetc_ws_gpu.so or llvm-readelf missing")
     lds = {}

@@ -1,4 +1,4 @@
-"""Prints tools/bench_routes.py's JSON lines as a table."""
+"""Prints tools/bench_routes.py's JSON lines as a table (DESIGN_ROUNDS.md §15)."""
 import json
 import sys
 
