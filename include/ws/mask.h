@@ -133,9 +133,10 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *   VAL_STEPS          netc_gpu_unmask_validate's 4 KiB window as 1, 2 or 4 steps
  *                      [2 up to 256 MiB, 1 above]                  (NETC_VAL_STEPS)
  *   SCAN_FUSE          the frame scan's links / tiles / resolve phases: 0 three launches;
- *                      1 one launch up to 512 MiB (arrival counters; slower on MI355X:
- *                      each block's release writes back its XCD's L2) [links, then
- *                      tiles + resolve as one launch up to 256 MiB]
+ *                      1 one launch up to 512 MiB (arrival counters; sc1 hand-offs);
+ *                      2 links, then tiles + resolve as one launch up to 256 MiB
+ *                      [one launch on the one-pass path (SCAN_ONEPASS) up to 128 MiB,
+ *                      else as 2]
  *                                                                  (NETC_SCAN_FUSE)
  *   ENC_SRC            1 selects the source-driven frame assembly (one pass over the payload
  *                      buffer, headers written in it; measured slower than the default

@@ -173,9 +173,38 @@ extern "C" int netc_gpu_debug_scan_trace(void* host_mapped) {
     do { \
         if (g_op_trace) __hip_atomic_store(g_op_trace + (i), (uint32_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
     } while (0)
+// ... and a device buffer of 64-bit words (timestamps, counts) the probe copies after the call
+__device__ uint64_t* g_op_stamp;
+extern "C" int netc_gpu_debug_scan_stamps(void* device_buffer) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_op_stamp), &device_buffer, sizeof(device_buffer));
+}
+#define OP_STAMP(i, v) \
+    do { \
+        if (g_op_stamp) g_op_stamp[i] = (uint64_t)(v); \
+    } while (0)
+#define OP_STAMP_MAX(i, v) \
+    do { \
+        if (g_op_stamp) __hip_atomic_fetch_max(g_op_stamp + (i), (uint64_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+    } while (0)
+#define OP_STAMP_MIN(i, v) \
+    do { \
+        if (g_op_stamp) __hip_atomic_fetch_min(g_op_stamp + (i), (uint64_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+    } while (0)
+#define OP_STAMP_ADD(i, v) \
+    do { \
+        if (g_op_stamp) __hip_atomic_fetch_add(g_op_stamp + (i), (uint64_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+    } while (0)
 #else
 #define OP_TRACE(i, v) ((void)0)
+#define OP_STAMP(i, v) ((void)0)
+#define OP_STAMP_MAX(i, v) ((void)0)
+#define OP_STAMP_MIN(i, v) ((void)0)
+#define OP_STAMP_ADD(i, v) ((void)0)
 #endif
+// OP_STAMP layout (trace build): [0] K1 first start (min), [1] K1 last end (max), [2] K2 first
+// start (min), [3] K2 verdict seen (max), [4] K2 last end (max), [5] [6] [7] [8] chunks whose T is
+// None, Single, Multi, Fail; group g at 16 + 8 g: start,
+// walks done, prefix done, emitted, Multi chunks, longest neighbour wait (loop trips), bad
 
 __device__ __forceinline__ uint64_t term(uint64_t type, uint64_t pos) { return kTerm | type << 61 | pos; }
 __device__ __forceinline__ uint64_t term_type(uint64_t v) { return (v >> 61) & 3; }
@@ -268,6 +297,7 @@ struct ScanArgs {
     uint64_t* st_t;        // per chunk: its exit prediction T (K1, plain stores)
     uint64_t* st_x;        // per chunk: W, where its walk left it (or END), for the next group
     uint64_t* st_g;        // per group of kPG chunks: its look-back status word
+    uint64_t* st_v;        // kVerdicts copies of the call's verdict (epoch << 1 | failed), kVStride apart
     uint64_t* opfl;        // per chunk: kOpRec frames {offset, byte 0, key} (the group's own)
     uint64_t epoch;        // 1 .. 2^24 - 1, one per call on the scratch (words of other calls do not match)
 };
@@ -534,6 +564,10 @@ static constexpr uint64_t kOnePassMax = 128ull << 20;                   // defau
 static constexpr uint64_t kOnePassCap = 256ull << 20;                   // knob 1: up to 256 MiB (256 groups)
 static constexpr int kOpRec = 32;                                       // frames one chunk may hold
 static constexpr int kPG = kScanT;                                      // chunks per group (a thread each)
+// The verdict, in kVerdicts words 256 B apart: K2's blocks wait on it, each on the copy blockIdx picks.
+// (One word polled by every waiting block -- ~450 at config 2 -- held one memory channel busy and
+// stretched every other trip through it: the groups' walks took 15-25 us, r06o.)
+static constexpr int kVerdicts = 64, kVStride = 32;
 // K2's claim counters in the flags word array (the last block to leave re-zeroes them)
 enum : int { kFPClaim = 6, kFPDone = 7, kFExit = 14 };
 
@@ -549,8 +583,22 @@ __device__ __forceinline__ bool op_failed(const ScanArgs& a) {
 __device__ __forceinline__ void op_fail(const ScanArgs& a) {
     __hip_atomic_fetch_or(a.opfail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The call's verdict (epoch << 1 | failed), decided once in st_v[0]: by the last group to finish
+// (failed = the failure word then), or failed by a block whose wait ran out first -- whichever
+// swaps it in first; every block and K3 / K4 follow the word, never the failure word alone.
+__device__ __forceinline__ uint64_t op_decide(const ScanArgs& a, uint64_t failed) {
+    uint64_t w = op_get(a.st_v);
+    while ((w >> 1) != a.epoch) {
+        if (__hip_atomic_compare_exchange_strong(a.st_v, &w, a.epoch << 1 | failed, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            return a.epoch << 1 | failed;
+    }
+    return w;
+}
 // K3 / K4: the one-pass path holds this call (every group checked, none failed)
-__device__ __forceinline__ bool onepass_done(const ScanArgs& a) { return a.onepass && !op_failed(a); }
+__device__ __forceinline__ bool onepass_done(const ScanArgs& a) {
+    return a.onepass && op_get(a.st_v) == a.epoch << 1;
+}
 
 // a global word tagged with the call's epoch, waited for (one thread); false once the call failed
 __device__ bool op_await(const ScanArgs& a, const uint64_t* p, uint64_t* out) {
@@ -643,6 +691,7 @@ __device__ __forceinline__ void op_group(const ScanArgs& a, uint64_t g, OpGroupL
     const uint64_t B = c * kChunk, Bend = B + kChunk;
     const uint64_t tval = mine ? a.st_t[c] : kTNone;
     bool bad = mine && tval == kTFail;
+    if (tid == 0) OP_STAMP(16 + 8 * g, __builtin_amdgcn_s_memrealtime());
     // the entry: from T(c - 1), or W(c - 1) when T(c - 1) is Multi (known later: rounds below)
     uint64_t e = kXEnd;
     bool known = true;
@@ -724,7 +773,19 @@ __device__ __forceinline__ void op_group(const ScanArgs& a, uint64_t g, OpGroupL
         }
         __atomic_store_n((volatile NETC_LDS uint64_t*)&L.w[tid], W, __ATOMIC_RELAXED);
         if (tid == kPG - 1) op_put(a.st_x + c, a.epoch << kOpBits | W);   // for the next group
+#ifdef NETC_SCAN_TRACE
+        OP_STAMP_MAX(16 + 8 * g + 5, n);
+#endif
     }
+#ifdef NETC_SCAN_TRACE
+    {
+        const int multi = __syncthreads_count(mine && a.st_t[c - (c > 0)] == kTMulti && c > c0);
+        if (tid == 0) {
+            OP_STAMP(16 + 8 * g + 1, __builtin_amdgcn_s_memrealtime());
+            OP_STAMP(16 + 8 * g + 4, multi);
+        }
+    }
+#endif
     if (__builtin_amdgcn_readfirstlane(__syncthreads_or(bad))) {
         if (tid == 0) op_fail(a);
         return;
@@ -747,6 +808,7 @@ __device__ __forceinline__ void op_group(const ScanArgs& a, uint64_t g, OpGroupL
         }
     }
     __syncthreads();
+    if (tid == 0) OP_STAMP(16 + 8 * g + 2, __builtin_amdgcn_s_memrealtime());
     if (!__builtin_amdgcn_readfirstlane(L.flag)) return;   // (the call failed meanwhile)
     const uint64_t k0 = L.base + before;
     for (uint64_t i = 0; i < cnt; ++i) {
@@ -760,6 +822,10 @@ __device__ __forceinline__ void op_group(const ScanArgs& a, uint64_t g, OpGroupL
         a.result[2] = ended == 2 ? endpos : ~0ull;
         if (total <= a.max_frames) a.hdr[total] = endpos;
     }
+#ifdef NETC_SCAN_TRACE
+    __syncthreads();
+    if (tid == 0) OP_STAMP(16 + 8 * g + 3, __builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
@@ -817,6 +883,7 @@ __device__ __forceinline__ u32x4 k1_load(const uint8_t* p) {
 template <bool NT, bool ONE>
 __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     if (threadIdx.x == 0 && blockIdx.x == 0) OP_TRACE(0, 1);
+    if (threadIdx.x == 0) OP_STAMP_MIN(0, __builtin_amdgcn_s_memrealtime());
     __shared__ uint32_t stage[4][kStageWords];   // per wave: its chunk's bytes (+ 16 after)
     __shared__ unsigned long long set[4][kSet];
     __shared__ uint16_t queue[4][kQCap];
@@ -1057,6 +1124,10 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(nodes), kWave - 1);
         const uint64_t t = __ballot(ovf) ? kTFail : (n == 0 ? kTNone : (n > 1 ? kTMulti : readlane64(ex, __builtin_ctzll(bn))));
         op_publish_t(a, c, t, lane);
+        if (lane == 0) {
+            OP_STAMP_ADD(t == kTNone ? 5 : t == kTMulti ? 7 : t == kTFail ? 8 : 6, 1);
+            OP_STAMP_MAX(1, __builtin_amdgcn_s_memrealtime());
+        }
     }
 }
 
@@ -1510,7 +1581,7 @@ __device__ __forceinline__ void links_body(const ScanArgs& a, LinksLdsT<BC>& sl,
 // waits only on groups claimed before its own, by blocks already running); once every group is
 // done, the failure word decides whether K2's own work runs.  True: the graph path goes on.
 template <int BC>
-__device__ bool onepass_groups(const ScanArgs& a, LinksLdsT<BC>& sl) {
+__device__ __forceinline__ bool onepass_groups(const ScanArgs& a, LinksLdsT<BC>& sl) {
     static_assert(sizeof(LinksLdsT<BC>) >= sizeof(OpGroupLds), "one pass: its LDS overlays K2's");
     OpGroupLds& L = *reinterpret_cast<OpGroupLds*>(&sl);
     uint32_t* const f = a.flags;
@@ -1520,6 +1591,7 @@ __device__ bool onepass_groups(const ScanArgs& a, LinksLdsT<BC>& sl) {
     // wave-uniform with readfirstlane, and each block claims at most one group.  (A first build
     // looped over claims; the compiler, taking the loop's exit as divergent, restructured it per
     // lane and the barriers paired up with the wrong ones: group 0 ran for ever.)
+    if (tid == 0) OP_STAMP_MIN(2, __builtin_amdgcn_s_memrealtime());
     if (tid == 0) L.item = __hip_atomic_fetch_add(f + kFPClaim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     const uint32_t g = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.item);
@@ -1527,25 +1599,36 @@ __device__ bool onepass_groups(const ScanArgs& a, LinksLdsT<BC>& sl) {
     if (g < groups) {
         op_group(a, g, L);
         __syncthreads();   // (every thread's failure atomic before the group counts as done)
-        if (tid == 0) __hip_atomic_fetch_add(f + kFPDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) L.item = __hip_atomic_fetch_add(f + kFPDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (tid == 0) OP_TRACE(2, g + 1);   // last group done
+        __syncthreads();
+        if (__builtin_amdgcn_readfirstlane((int)L.item) == (int)groups - 1) {   // the last group: decide
+            if (tid == 0) L.base = op_decide(a, op_failed(a) ? 1 : 0);
+            __syncthreads();
+            if (tid > 0 && tid < kVerdicts) op_put(a.st_v + tid * kVStride, L.base);   // the copies
+        }
     }
     // Relaxed (sc1) polls: an acquire or release at agent scope writes back or invalidates the
     // whole L2 of the XCD (buffer_wbl2 / buffer_inv sc1) -- hundreds of waiting blocks doing that
     // cost this launch 150 us at config 2 (r06l).  Only the failure word is read after the wait,
     // itself an atomic, and every failure atomic of a group is done (vmcnt, the barrier above)
     // before its count goes up.
-    if (tid == 0) {   // every group claimed or being claimed: wait for them, then the verdict
+    if (tid == 0) {   // every group claimed or being claimed: wait for the verdict
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(f + kFPDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < groups) {
+        const uint64_t* vw = a.st_v + (blockIdx.x % kVerdicts) * kVStride;
+        uint64_t v;
+        for (;;) {
+            v = op_get(vw);
+            if ((v >> 1) == a.epoch) break;
             if (__builtin_amdgcn_s_memrealtime() - t0 > 5 * kOnePassWait) {   // (a safety valve)
-                op_fail(a);
+                v = op_decide(a, 1);
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(8);
         }
-        L.flag = op_failed(a);
+        L.flag = (int)(v & 1);
         OP_TRACE(3, 1 + L.flag);   // the verdict
+        OP_STAMP_MAX(3, __builtin_amdgcn_s_memrealtime());
     }
     __syncthreads();
     const bool graph = __builtin_amdgcn_readfirstlane(L.flag) != 0;
@@ -1556,6 +1639,7 @@ __device__ bool onepass_groups(const ScanArgs& a, LinksLdsT<BC>& sl) {
 // the last block to leave re-zeroes the claim counters for the next call
 __device__ __forceinline__ void onepass_leave(const ScanArgs& a) {
     uint32_t* const f = a.flags;
+    if (threadIdx.x == 0) OP_STAMP_MAX(4, __builtin_amdgcn_s_memrealtime());
     if (threadIdx.x == 0 &&
         __hip_atomic_fetch_add(f + kFExit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
         __hip_atomic_store(f + kFPClaim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2150,10 +2234,19 @@ __device__ __forceinline__ bool arrive_last(uint32_t* counter, uint32_t expect, 
     return *flag != 0;
 }
 
+// OP: the one-pass groups first (onepass_groups); the graph phases only if they failed.  On the
+// one-pass path this launch and K4 (a flag read) follow K1: one launch boundary fewer than
+// scan_links<OP> + scan_tiles_resolve.
+template <bool OP>
 __global__ __launch_bounds__(kScanT) void scan_links_fused(ScanArgs a, uint64_t tiles, uint32_t blocks) {
     __shared__ FusedLds sm;
     __shared__ int flag;
     SCAN_SCOPE(1);
+    if (OP) {
+        const bool graph = onepass_groups<kBlkChunks>(a, sm.k2);
+        onepass_leave(a);
+        if (!graph) return;
+    }
     links_body<true, kBlkChunks>(a, sm.k2, blockIdx.x);
     constexpr uint32_t kPerTile = (uint32_t)(kTileChunks / kBlkChunks);
     const uint32_t tile = blockIdx.x / kPerTile;
@@ -2548,7 +2641,7 @@ std::mutex& stream_scratch_mu() {
 // regions; flags, ccount and ext first -- the region every call leaves zeroed.
 struct Layout {
     uint64_t flags, ccount, ext, tarr, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, flist, text,
-        tcount, tinfo, st_t, st_x, st_g, opfl, total;
+        tcount, tinfo, st_t, st_x, st_g, st_v, opfl, total;
 };
 Layout layout_for(uint64_t cap) {
     auto align = [](uint64_t x) { return (x + 63) & ~63ull; };
@@ -2576,6 +2669,7 @@ Layout layout_for(uint64_t cap) {
     l.st_t = o;    o = align(o + cap * 8);   // one-pass status words (epochs: never cleared per call)
     l.st_x = o;    o = align(o + cap * 8);
     l.st_g = o;    o = align(o + (cap / kPG + 1) * 8);
+    l.st_v = o;    o = align(o + kVerdicts * kVStride * 8);
     l.opfl = o;    o = align(o + cap * kOpRec * 8);
     l.total = o;
     return l;
@@ -2706,9 +2800,7 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     const int64_t op = knob(NETC_GPU_KNOB_SCAN_ONEPASS);
     const int64_t fuse = knob(NETC_GPU_KNOB_SCAN_FUSE);
     // (the one-pass groups run in scan_links: not with K2 + K3 fused into one launch)
-    a.onepass = op == 0 || (fuse == 1 && tiles <= (uint64_t)kFuseTiles)
-                    ? 0
-                    : (len <= (op == 1 ? kOnePassCap : kOnePassMax) ? 1 : 0);
+    a.onepass = op != 0 && len <= (op == 1 ? kOnePassCap : kOnePassMax) ? 1 : 0;
     if (++s.epoch >= (1ull << 24) - 1) {   // (all-ones never: an exit-set entry's ~0 must not match)
         if ((e = hipMemsetAsync(m + l.st_t, 0, l.opfl - l.st_t, stream)) != hipSuccess) return e;
         s.epoch = 1;
@@ -2717,6 +2809,7 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.st_t = (uint64_t*)(m + l.st_t);
     a.st_x = (uint64_t*)(m + l.st_x);
     a.st_g = (uint64_t*)(m + l.st_g);
+    a.st_v = (uint64_t*)(m + l.st_v);
     a.opfl = (uint64_t*)(m + l.opfl);
     a.ccount = (uint32_t*)(m + l.ccount);
     a.ext = m + l.ext;
@@ -2776,8 +2869,11 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
             hipLaunchKernelGGL((a.onepass ? scan_links<kBlkChunks, true> : scan_links<kBlkChunks, false>), dim3(blk),
                                dim3(kScanT), 0, stream, a);
     };
-    if (fuse == 1 && tiles <= (uint64_t)kFuseTiles) {   // (32 chunks per K2 block: the tiles' arrival counts)
-        hipLaunchKernelGGL(scan_links_fused, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
+    // the one-pass path: K2 + K3 fused behind the groups by default (SCAN_FUSE 2: the split launches)
+    const bool fused = tiles <= (uint64_t)kFuseTiles && (fuse == 1 || (a.onepass && fuse < 0 && !big));
+    if (fused) {   // (32 chunks per K2 block: the tiles' arrival counts)
+        if (a.onepass) hipLaunchKernelGGL(scan_links_fused<true>, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
+        else hipLaunchKernelGGL(scan_links_fused<false>, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
     } else if (fuse != 0 && tiles <= (uint64_t)kMergeTiles) {
         links();
         hipLaunchKernelGGL(scan_tiles_resolve, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a, tiles);

@@ -323,15 +323,18 @@ def test_far_exits(torch_cuda, strict):
     run_scan(torch_cuda, wire[:int(wo[-3]) + 100], strict=strict, parallel=True)
 
 
-@pytest.mark.parametrize("fuse", ["1", "0", "-1"])
-def test_fused_and_separate_launches(torch_cuda, gpu_knob, fuse):
+@pytest.mark.parametrize("onepass", ["0", "-1"])
+@pytest.mark.parametrize("fuse", ["1", "0", "2", "-1"])
+def test_fused_and_separate_launches(torch_cuda, gpu_knob, fuse, onepass):
     # K2 + K3a + K3b as one launch (knob SCAN_FUSE = 1: arrival counters per tile and per
     # stream, the last arrival runs the next phase and re-zeroes its counter), as three
     # (SCAN_FUSE = 0, as for streams over 512 MiB), or the default, K3a + K3b as one launch
     # (the last tile block to arrive resolves; sc1 hand-off): the same results over
     # alternating stream sizes, the serial fallback, non-strict streams and truncations, one
     # call after another on one stream (a counter left non-zero would break the next call)
+    # (with the one-pass path on, its groups run first in whichever K2 launch this is)
     gpu_knob("SCAN_FUSE", fuse)
+    gpu_knob("SCAN_ONEPASS", onepass)
     rng = np.random.default_rng(51)
     big, _ = _stream(rng, np.full(16384, 1024))                      # 16 tiles
     mixed_sizes = np.concatenate([rng.integers(0, 5000, 2000), rng.integers(0, 130, 2000), [65535, 300000]])
@@ -384,14 +387,16 @@ def test_emit_block_sizes(torch_cuda, gpu_knob, emit):
     assert run_scan(torch_cuda, wire) == 2   # capacity overflow: the serial walk in K4
 
 
-@pytest.mark.parametrize("onepass", ["1", "0"])
-def test_onepass_and_graph_paths(torch_cuda, gpu_knob, onepass):
+@pytest.mark.parametrize("onepass,fuse", [("1", "-1"), ("1", "2"), ("0", "-1")])
+def test_onepass_and_graph_paths(torch_cuda, gpu_knob, onepass, fuse):
     """the one-pass path (dense streams: K1's chunks speculate their entries from their
     predecessors and check them; K2's launch writes the frames; K3 and K4 only read a flag) and the
     graph path (knob SCAN_ONEPASS = 0) on the same streams: identical results; dense strict streams
     finish on the one-pass path (netc_gpu_scan_diag bit 32), streams with chunk-covering frames on
-    the graph kernels"""
+    the graph kernels.  The one-pass groups run in K2 + K3's fused launch by default, in K2's own
+    with SCAN_FUSE = 2."""
     gpu_knob("SCAN_ONEPASS", onepass)
+    gpu_knob("SCAN_FUSE", fuse)
     rng = np.random.default_rng(97)
     want = onepass == "1"
     c2, _ = _stream(rng, np.full(65536, 1024))

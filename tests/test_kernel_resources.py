@@ -33,6 +33,7 @@ HOT = [
     "void netc_gpu::wire_offsets_chained<4, false>",
     "void netc_gpu::wire_offsets_chained<16, false>",
     "void netc_gpu::scan_links<",
+    "void netc_gpu::scan_links_fused<true>",    # the one-pass path's launch
     "netc_gpu::scan_tiles_resolve(",
     "netc_gpu::scan_tiles(",
     "netc_gpu::scan_resolve(",
@@ -46,7 +47,8 @@ KNOB_ONLY = [
     "void netc_gpu::encode_frames_kernel<2,",  # 2 KiB chunks (netc_gpu_tune unroll 2 / 4; ENC_PF = 1)
     "void netc_gpu::wire_offsets_chained<16, true>",   # fixups in the scan (ENC_FIX = 1)
     "void netc_gpu::wire_offsets_chained<1, true>",
-    "netc_gpu::scan_links_fused(",             # NETC_GPU_KNOB_SCAN_FUSE = 1
+    "void netc_gpu::scan_links_fused<false>",   # NETC_GPU_KNOB_SCAN_FUSE = 1 without the one-pass path
+    "void netc_gpu::scan_links<64, true>",      # the one-pass path above 128 MiB (SCAN_ONEPASS = 1)
 ]
 
 
