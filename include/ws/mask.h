@@ -157,10 +157,11 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *                      else 0]                                      (NETC_ENC_PF)
  *   SCAN_BLOCK_CHUNKS  chunks per block of the frame scan's link and emit phases: 32 or 64
  *                      [32 up to 128 MiB of stream, 64 above]       (NETC_SCAN_BLOCK_CHUNKS)
- *   SCAN_ONEPASS       the frame scan's one-pass path (the chunks resolve their entries and
- *                      frame indexes by decoupled look-back inside the first launch; the
- *                      graph kernels then only check a flag): 0 never, 1 at every size
- *                      [on up to 256 MiB of stream]                 (NETC_SCAN_ONEPASS)
+ *   SCAN_ONEPASS       the frame scan's one-pass path (K1's chunks speculate their entries
+ *                      from their predecessors' exit predictions and walk their frames; the
+ *                      graph kernels then only check a flag): 0 never, 1 up to 256 MiB of
+ *                      stream, 2 up to 128 MiB [off: slower than the graph path at config 2,
+ *                      DESIGN.md §16.4]                             (NETC_SCAN_ONEPASS)
  *   INJECT_FAULT       fault injection for tests: the ingest / egress ring submission this
  *                      countdown reaches (0 = the next one) fails as NETC_GPU_ELAUNCH
  *                      without launching, then the knob disarms itself [off]

@@ -201,10 +201,9 @@ extern "C" int netc_gpu_debug_scan_stamps(void* device_buffer) {
 #define OP_STAMP_MIN(i, v) ((void)0)
 #define OP_STAMP_ADD(i, v) ((void)0)
 #endif
-// OP_STAMP layout (trace build): [0] K1 first start (min), [1] K1 last end (max), [2] K2 first
-// start (min), [3] K2 verdict seen (max), [4] K2 last end (max), [5] [6] [7] [8] chunks whose T is
-// None, Single, Multi, Fail; group g at 16 + 8 g: start,
-// walks done, prefix done, emitted, Multi chunks, longest neighbour wait (loop trips), bad
+// OP_STAMP layout (trace build): [0] K1 first start (min), [1] K1 last wave's end (max), [5] [6]
+// [7] [8] chunks whose T is None, Single, Multi, Fail, [9] [10] [11] K1's entry waits: summed,
+// longest, over 2 us (100 MHz ticks)
 
 __device__ __forceinline__ uint64_t term(uint64_t type, uint64_t pos) { return kTerm | type << 61 | pos; }
 __device__ __forceinline__ uint64_t term_type(uint64_t v) { return (v >> 61) & 3; }
@@ -292,13 +291,16 @@ struct ScanArgs {
                            // loop always; NETC_SCAN_FAST_RANK=0, tests)
     // the one-pass path (scan_exits<_, true>; see "One pass" below)
     int onepass;           // this call runs it (the host's choice: knob SCAN_ONEPASS, stream size)
-    uint32_t* opfail;      // this call's one-pass failure word (flags[4] / flags[5] on alternate calls;
-    uint32_t* opfail_prev; // ... K4 zeroes the previous call's, as for ovf)
-    uint64_t* st_t;        // per chunk: its exit prediction T (K1, plain stores)
-    uint64_t* st_x;        // per chunk: W, where its walk left it (or END), for the next group
-    uint64_t* st_g;        // per group of kPG chunks: its look-back status word
-    uint64_t* st_v;        // kVerdicts copies of the call's verdict (epoch << 1 | failed), kVStride apart
-    uint64_t* opfl;        // per chunk: kOpRec frames {offset, byte 0, key} (the group's own)
+    uint32_t* opfail;      // this call's one-pass failure words: kFailCopies, kFailStride apart (two sets,
+    uint32_t* opfail_prev; // ... alternate calls; K4 zeroes the previous call's, as for ovf)
+    uint64_t* st_t;        // per chunk: its exit prediction T (epoch-tagged)
+    uint64_t* st_x;        // per chunk after a Multi T: W, where its walk left it (or END), epoch-tagged
+    uint64_t* opfl;        // per chunk: kOpRec frames {offset, byte 0 << 16, key << 32}
+    uint64_t* opin;        // per chunk: {frames | how the chain ends here << 32, where}
+    uint32_t* opc;         // this call's counters: frames per group of kOpGroup chunks, then per tile
+    uint32_t* opc_prev;    // ... the previous call's (K4 zeroes them, opc_words of them)
+    uint64_t opc_tiles;    // index of the first tile counter
+    uint64_t opc_words;
     uint64_t epoch;        // 1 .. 2^24 - 1, one per call on the scratch (words of other calls do not match)
 };
 
@@ -521,311 +523,305 @@ static constexpr int kNearLane = 55;
 #ifndef NETC_K1_SLIM
 #define NETC_K1_SLIM 1
 #endif
-static constexpr int kQCap = NETC_K1_SLIM ? 248 : 256;   // K1: exit-capable candidates queued per chunk (more: serial walk)
+static constexpr int kQCap = NETC_K1_SLIM ? 240 : 256;   // K1: exit-capable candidates queued per chunk (more: serial walk)
 static constexpr int kStageWords = NETC_K1_SLIM ? (int)((kChunk + 16) / 4) : kWords;
-static_assert(!NETC_K1_SLIM || 4 * (4 * kStageWords + 8 * kSet + 2 * kQCap) <= 20480,
+static_assert(!NETC_K1_SLIM || 4 * (4 * kStageWords + 8 * kSet + 2 * kQCap) + 64 <= 20480,
               "K1: a 4-wave block must stay within 20,480 B of LDS (8 blocks per CU)");
 static constexpr int kCheapMax = 64;   // K1: more from the cheap selection: the full quick check instead
 
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v);
 // ------------------------------------------------------------------ one pass --
 // The one-pass path for dense streams -- frames shorter than a chunk, so the chain
-// visits every chunk from the start on (the C2 shape).  K1 publishes, per chunk c, T(c): where
-// the chain leaves c if it visits it, from the distinct exits of c's exit-capable candidates that
-// land on a position able to start a header (the nodes K1 appends): that exit when there is
-// exactly one (Single), None (no such exit: a chain that visits c ends in it, or dies at an exit
-// onto a position that cannot start a header), Multi, or Fail (K1's queue or set overflowed).
-// Garbage chains (payload bytes parsed as headers) land on header-capable positions with ~2 %
-// odds, so nearly every chunk is Single.
+// visits every chunk from the start on (the C2 shape) -- runs inside K1's launch.  After its
+// parse, each chunk c publishes T(c): where the chain leaves c if it visits it, from the distinct
+// exits of c's exit-capable candidates that land on a position able to start a header (the nodes
+// K1 appends): that exit when there is exactly one (Single), None (no such exit: a chain that
+// visits c ends in it, or dies at an exit onto a position that cannot start a header), Multi, or
+// Fail (K1's queue or set overflowed).  Garbage chains (payload bytes parsed as headers) land on
+// header-capable positions with ~2 % odds, so nearly every chunk is Single.
 //
-// K2's launch then runs groups of kPG chunks, claimed in order (one thread per chunk).  Each chunk
-// SPECULATES its entry from its predecessor alone -- T(c-1) if Single, END if None, the
-// predecessor's own walk exit W(c-1) if Multi (handed over in LDS, or across groups in global
-// memory) -- walks its frames from there (header bytes from global memory) to its exit W(c), and
-// checks:
+// The chunk's wavefront then SPECULATES its entry from its predecessor alone -- T(c-1) if Single,
+// END if None, the predecessor's own walk exit W(c-1) if Multi -- and walks its frames from there
+// in LDS (its bytes are staged for the parse anyway) to its exit W(c), checking:
 //   * an entry past the chunk's end (a frame covers it: not a dense stream) fails;
 //   * a visited chunk's W(c) must equal T(c) when T(c) is Single (its successor used T(c));
 //   * a chunk not visited (entry END) must not be Single (its successor would walk from T(c)).
 // By induction from the start chunk (entry = the start), if no chunk fails every speculated entry
-// is the true one.  The group's frame counts are summed, the groups' totals chained by a
-// decoupled look-back (status words tagged with the call's epoch: never cleared per call), and
-// each chunk writes its descriptors; the chunk where the chain ends writes the results.  Once
-// every group is done the blocks read the failure word: on a failure (any check, Fail, a
-// speculative stop at a header the filter rejects, a wait past kOnePassWait) they run K2's own
-// work (a block each) and K3 / K4 follow as before, overwriting everything this
-// path wrote; without one, K3 and K4 only read the word.  The results are the same either way.
+// is the true one.  A wave waits only for its predecessor's T, published right after that
+// predecessor's parse whatever its entry -- or, after a Multi chunk, for its W -- so nothing is
+// serial beyond a run of Multi chunks.  (Round 6's first build waited for each predecessor's
+// resolved exit: a serial chain through the whole stream, 4 ms at config 2; the second walked in
+// K2's launch, a thread per chunk with header bytes from global memory: 50 us against the graph
+// path's 41, profiles/r06_scan_onepass.md.)
+//
+// The walk's frames go to a per-chunk record (a lane each, kOpRec at most), its count to two
+// counters -- the chunk's group of kOpGroup chunks and its tile (relaxed atomics, no wait) -- and
+// K4, one launch later with every count in, sums the counters before each of its blocks, scans
+// the block's chunks and writes the descriptors and the results (op_emit).  Any failure (a
+// check, Fail, a speculative stop at a header the filter rejects, more than kOpRec frames in a
+// chunk, a wait past kOnePassWait) sets the call's failure word; K2-K4 then run the graph path
+// from the nodes K1 appended all the same, and the results are the same either way.  The T and
+// W words carry the call's epoch (never cleared per call); the counters alternate per call, each
+// call's K4 zeroing the other set.  Correctness never rests on dispatch order: a wait that
+// outlasts kOnePassWait fails the call over to the graph path.
 static constexpr uint64_t kOpBits = 40;
 static constexpr uint64_t kOpMask = (1ull << kOpBits) - 1;
 static constexpr uint64_t kTNone = kOpMask, kTMulti = kOpMask - 1, kTFail = kOpMask - 2;   // T values; else the exit
 static constexpr uint64_t kXEnd = kOpMask;                              // W / entry: no chain here
-static constexpr uint64_t kWPend = ~0ull;                               // (LDS) W not known yet
 static constexpr uint64_t kOnePassWait = 2000000;                       // 20 ms at 100 MHz
 static constexpr uint64_t kOnePassMax = 128ull << 20;                   // default: streams up to 128 MiB
-static constexpr uint64_t kOnePassCap = 256ull << 20;                   // knob 1: up to 256 MiB (256 groups)
-static constexpr int kOpRec = 32;                                       // frames one chunk may hold
-static constexpr int kPG = kScanT;                                      // chunks per group (a thread each)
-// The verdict, in kVerdicts words 256 B apart: K2's blocks wait on it, each on the copy blockIdx picks.
-// (One word polled by every waiting block -- ~450 at config 2 -- held one memory channel busy and
-// stretched every other trip through it: the groups' walks took 15-25 us, r06o.)
-static constexpr int kVerdicts = 64, kVStride = 32;
-// K2's claim counters in the flags word array (the last block to leave re-zeroes them)
-enum : int { kFPClaim = 6, kFPDone = 7, kFExit = 14 };
+static constexpr uint64_t kOnePassCap = 256ull << 20;                   // knob 1: up to 256 MiB
+static constexpr int kOpRec = 64;                                       // frames one chunk may hold (a lane each)
+static constexpr int kOpGroup = 32;                                     // chunks per group counter
+static constexpr int kFailCopies = kWave, kFailStride = 16;             // the failure word's copies, 64 B apart
+static_assert(kTileChunks % kOpGroup == 0 && kOpRec == kWave, "one pass: groups inside tiles, a lane per frame");
+static_assert(kOnePassCap / kChunk / kTileChunks <= 256, "one pass: K4 sums the tiles before a block, a thread each");
+// counter words per parity for a scratch of `cap` chunks: the groups', then the tiles'
+static constexpr uint64_t op_counter_words(uint64_t cap) { return cap / kOpGroup + cap / kTileChunks; }
 
+// T / W words and the failure word: system-scope (sc0 sc1) stores and loads on both sides, so a
+// poll never re-reads a stale copy its own XCD's L2 kept from an earlier poll
 __device__ __forceinline__ void op_put(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ uint64_t op_get(const uint64_t* p) {
-    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// The failure word in kFailCopies copies on lines of their own: a failing chunk sets the copy its
+// index picks (a store: set once, never cleared within the call), a reader ORs all of them (one
+// load per lane; call it with the whole wavefront).  (One word -- an atomic OR by every failing
+// chunk, a load by every poller -- held one memory channel and K1 took 147 us at config 2, r06i.)
 __device__ __forceinline__ bool op_failed(const ScanArgs& a) {
-    return __hip_atomic_load(a.opfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    const uint32_t v = __hip_atomic_load(a.opfail + (threadIdx.x & (kWave - 1)) * kFailStride, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+    return __ballot(v != 0) != 0;
 }
-__device__ __forceinline__ void op_fail(const ScanArgs& a) {
-    __hip_atomic_fetch_or(a.opfail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void op_fail(const ScanArgs& a, uint64_t c) {
+    __hip_atomic_store(a.opfail + (c % kFailCopies) * kFailStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// The call's verdict (epoch << 1 | failed), decided once in st_v[0]: by the last group to finish
-// (failed = the failure word then), or failed by a block whose wait ran out first -- whichever
-// swaps it in first; every block and K3 / K4 follow the word, never the failure word alone.
-__device__ __forceinline__ uint64_t op_decide(const ScanArgs& a, uint64_t failed) {
-    uint64_t w = op_get(a.st_v);
-    while ((w >> 1) != a.epoch) {
-        if (__hip_atomic_compare_exchange_strong(a.st_v, &w, a.epoch << 1 | failed, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT))
-            return a.epoch << 1 | failed;
-    }
-    return w;
-}
-// K3 / K4: the one-pass path holds this call (every group checked, none failed)
-__device__ __forceinline__ bool onepass_done(const ScanArgs& a) {
-    return a.onepass && op_get(a.st_v) == a.epoch << 1;
-}
+// K2-K4: K1 resolved this call (every chunk checked, none failed -- K1 has finished by then)
+__device__ __forceinline__ bool onepass_done(const ScanArgs& a) { return a.onepass && !op_failed(a); }
 
-// a global word tagged with the call's epoch, waited for (one thread); false once the call failed
-__device__ bool op_await(const ScanArgs& a, const uint64_t* p, uint64_t* out) {
+// a word tagged with the call's epoch, waited for by the whole wavefront (its value read from
+// lane 0, so every branch on it is scalar); false once the call failed or the wait ran out
+__device__ bool op_await(const ScanArgs& a, const uint64_t* p, uint64_t* out, uint64_t c) {
     uint64_t t0 = 0;
     for (uint32_t n = 0;; ++n) {
-        const uint64_t w = op_get(p);
+        const uint64_t w = readlane64(op_get(p), 0);
         if ((w >> kOpBits) == a.epoch) {
             *out = w & kOpMask;
             return true;
         }
-        if ((n & 31) == 0) {
-            if (op_failed(a)) return false;
+        if ((n & 15) == 0) {   // (about every 7 us once the back-off is long)
+            if (n && op_failed(a)) return false;
             const uint64_t t = __builtin_amdgcn_s_memrealtime();
             if (n == 0) t0 = t;
             else if (t - t0 > kOnePassWait) {
-                op_fail(a);
+                op_fail(a, c);
                 return false;
             }
         }
-        __builtin_amdgcn_s_sleep(1);
+        if (n < 8) __builtin_amdgcn_s_sleep(2);   // (~130 cycles, then ~1,000)
+        else __builtin_amdgcn_s_sleep(16);
     }
 }
 
-// K1: T(c) for K2's launch (a plain store: the next launch reads it)
-__device__ __forceinline__ void op_publish_t(const ScanArgs& a, uint64_t c, uint64_t tval, int lane) {
-    if (lane == 0 && c >= a.start / kChunk) a.st_t[c] = tval;
-}
+// K1's hand-over words in LDS: [0][w] T and [1][w] W of wave w's chunk, for wave w + 1 of the block
+// (kHPend until set: every wave clears its own before the block's one barrier).  Only the block's
+// last wave hands over through global memory (st_t, st_x), to the next block's first: one
+// global poller per block, each backing off -- a poll per wave of a covering grid, every ~100
+// cycles, swamped the memory system (K1 at config 2: 115 us, r06f).
+static constexpr uint64_t kHPend = ~0ull;
+typedef uint64_t OpHand[2][4];
 
-struct OpGroupLds {
-    uint64_t w[kPG];            // W per chunk, kWPend until its walk is done
-    uint32_t wsum[kScanT / kWave];
-    uint64_t base;              // the group's first frame index
-    uint32_t item;
-    int flag;
-};
-
-// the group's status word: [63:62] 1 aggregate / 2 inclusive | [61:38] epoch | [37:0] frames
-static constexpr int kGValBits = 38;
-__device__ __forceinline__ uint64_t op_gword(uint64_t flag, uint64_t epoch, uint64_t v) {
-    return flag << 62 | (epoch & 0xFFFFFF) << kGValBits | (v & ((1ull << kGValBits) - 1));
-}
-
-// the frames before group g (wave 0; its aggregate `agg` published first); false once the call failed
-__device__ bool op_group_prefix(const ScanArgs& a, uint64_t g, uint64_t agg, int lane, uint64_t* out) {
-    if (lane == 0) op_put(a.st_g + g, op_gword(1, a.epoch, agg));
-    uint64_t acc = 0, t0 = 0;
-    uint32_t n = 0;
-    if (lane == 0) OP_TRACE(5, g + 1);   // prefix of group g started
-    for (int64_t top = (int64_t)g - 1; top >= 0; ++n) {
-        const int64_t idx = top - lane;
-        uint64_t v = 0;
-        bool ok = true, incl = idx < 0;   // before group 0: an inclusive 0
-        if (idx >= 0) {
-            const uint64_t w = op_get(a.st_g + idx);
-            ok = (w >> 62) != 0 && ((w >> kGValBits) & 0xFFFFFF) == (a.epoch & 0xFFFFFF);
-            incl = ok && (w >> 62) == 2;
-            v = w & ((1ull << kGValBits) - 1);
-        }
-        const uint64_t im = __ballot(incl);
-        const int stop = im ? __builtin_ctzll(im) : kWave;   // the nearest inclusive prefix
-        const uint64_t need = stop >= kWave - 1 ? ~0ull : ((2ull << stop) - 1);
-        if ((__ballot(ok) & need) != need) {   // a predecessor has not published yet
-            if ((n & 31) == 0) {
-                if (op_failed(a)) return false;
-                const uint64_t t = __builtin_amdgcn_s_memrealtime();
-                if (n == 0) t0 = t;
-                else if (t - t0 > kOnePassWait) {
-                    if (lane == 0) op_fail(a);
-                    return false;
-                }
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        acc += wave_sum(lane <= stop && idx >= 0 ? v : 0);
-        if (stop < kWave) break;
-        top -= kWave;
+// K1: T(c), for the successor's wave
+__device__ __forceinline__ void op_publish_t(const ScanArgs& a, uint64_t c, uint64_t tval, int lane, int wv, OpHand& h) {
+    if (lane == 0) {
+        __hip_atomic_store(&h[0][wv], tval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (wv == 3 && c >= a.start / kChunk) op_put(a.st_t + c, a.epoch << kOpBits | tval);
     }
-    if (lane == 0) op_put(a.st_g + g, op_gword(2, a.epoch, acc + agg));
-    if (lane == 0) OP_TRACE(6, g + 1);   // prefix of group g done
-    *out = acc;
-    return true;
 }
 
-// One group: chunks [g kPG, (g + 1) kPG), thread t the chunk g kPG + t (every thread of the block).
-__device__ __forceinline__ void op_group(const ScanArgs& a, uint64_t g, OpGroupLds& L) {
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
-    const uint64_t c0 = a.start / kChunk, c = g * kPG + tid;
-    const bool mine = c >= c0 && c <= a.nc;
-    const uint64_t B = c * kChunk, Bend = B + kChunk;
-    const uint64_t tval = mine ? a.st_t[c] : kTNone;
-    bool bad = mine && tval == kTFail;
-    if (tid == 0) OP_STAMP(16 + 8 * g, __builtin_amdgcn_s_memrealtime());
-    // the entry: from T(c - 1), or W(c - 1) when T(c - 1) is Multi (known later: rounds below)
-    uint64_t e = kXEnd;
-    bool known = true;
-    if (mine && c == c0) {
-        e = a.start;
-    } else if (mine) {
-        const uint64_t tp = a.st_t[c - 1];
-        if (tp == kTFail) bad = true;
-        else if (tp == kTMulti) known = false;
-        else e = tp == kTNone ? kXEnd : tp;
-    }
-    L.w[tid] = mine ? kWPend : kXEnd;
-    __syncthreads();   // every chunk's W slot set before any thread reads its neighbour's
-    uint64_t cnt = 0, endpos = 0, W = kXEnd;
-    int ended = 0;   // 1: the chain ends in this chunk (END), 2: it dies here (an error at endpos)
-    // per thread, no barrier inside (a chunk after a Multi one spins on its neighbour's W in LDS;
-    // the group's first chunk on the previous group's, in global memory)
-    bool done = !mine;
+// a hand-over word of the wave before, in LDS; false once the call failed or the wait ran out
+__device__ bool op_await_lds(const ScanArgs& a, const uint64_t* p, uint64_t* out, uint64_t c) {
     uint64_t t0 = 0;
-    for (uint32_t n = 0; !done; ++n) {
-        if (!known && !bad) {
-            if (tid > 0) {
-                const uint64_t w = __atomic_load_n((volatile NETC_LDS uint64_t*)&L.w[tid - 1], __ATOMIC_RELAXED);
-                if (w != kWPend) {
-                    e = w;
-                    known = true;
-                }
-            } else {
-                uint64_t w;
-                if (op_await(a, a.st_x + c - 1, &w)) {
-                    e = w;
-                    known = true;
-                } else {
-                    bad = true;
-                }
+    for (uint32_t n = 0;; ++n) {
+        const uint64_t w = readlane64(__hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP), 0);
+        if (w != kHPend) {
+            *out = w;
+            return true;
+        }
+        if ((n & 255) == 0) {   // (about every 7 us)
+            if (n && op_failed(a)) return false;
+            const uint64_t t = __builtin_amdgcn_s_memrealtime();
+            if (n == 0) t0 = t;
+            else if (t - t0 > kOnePassWait) {
+                op_fail(a, c);
+                return false;
             }
         }
-        if (!known && !bad) {   // the neighbour is not done yet
-            if ((n & 31) == 0) {
-                const uint64_t t = __builtin_amdgcn_s_memrealtime();
-                if (n == 0) t0 = t;
-                else if (t - t0 > kOnePassWait) bad = true;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        done = true;
-        if (!bad && e == kXEnd) {
-            if (tval != kTNone && tval != kTMulti) bad = true;   // not visited, yet Single
-        } else if (!bad && e >= Bend) {
-            bad = true;   // a frame covers this chunk: not dense
-        } else if (!bad) {
-            uint64_t p = e;
-            for (;;) {
-                if (p >= Bend) {   // its exit (onto a header-capable position it would be in T's set)
-                    if (tval == kTNone || (tval == kTMulti && quick_reject(a, p))) {
+        if (n < 8) __builtin_amdgcn_s_sleep(2);   // (~130 cycles, then ~1,000)
+        else __builtin_amdgcn_s_sleep(16);
+    }
+}
+
+// K1, after T(c) is published: the one-pass work of chunk c (the whole wavefront; every value but
+// the lane's frame record is wave-uniform).  st: the chunk's bytes in LDS (not loaded for the
+// virtual chunk, whose only possible entry -- the stream's end -- parses without them).
+__device__ void op_chunk(const ScanArgs& a, uint64_t c, uint64_t tval, const uint32_t* st, int lane, int wv, OpHand& h) {
+    const uint64_t c0 = a.start / kChunk;
+    const uint64_t B = c * kChunk, Bend = B + kChunk;
+    if (c < c0) {   // before the first header: no chain, no frames
+        if (lane == 0) a.opin[2 * c] = 0;
+        return;
+    }
+    bool bad = tval == kTFail;
+    uint64_t e = kXEnd;
+#ifdef NETC_SCAN_TRACE
+    const uint64_t tw0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (c == c0) {
+        e = a.start;
+    } else if (!bad) {   // the entry, speculated from the predecessor
+        uint64_t tp = 0;
+        if (!(wv ? op_await_lds(a, &h[0][wv - 1], &tp, c) : op_await(a, a.st_t + c - 1, &tp, c)) || tp == kTFail) bad = true;
+        else if (tp != kTMulti) e = tp == kTNone ? kXEnd : tp;
+        else if (!(wv ? op_await_lds(a, &h[1][wv - 1], &e, c) : op_await(a, a.st_x + c - 1, &e, c)) || e == kTFail) bad = true;
+    }
+#ifdef NETC_SCAN_TRACE
+    if (lane == 0) {   // [9] waits summed, [10] the longest, [11] waits over 2 us (100 MHz ticks)
+        const uint64_t tw = __builtin_amdgcn_s_memrealtime() - tw0;
+        OP_STAMP_ADD(9, tw);
+        OP_STAMP_MAX(10, tw);
+        if (tw > 200) OP_STAMP_ADD(11, 1);
+    }
+#endif
+    uint64_t cnt = 0, endpos = 0, W = kXEnd, rec = 0;
+    uint32_t ended = 0;   // 1: the chain ends in this chunk (END), 2: it dies here (an error at endpos)
+    if (bad) {
+    } else if (e == kXEnd) {
+        if (tval != kTNone && tval != kTMulti) bad = true;   // not visited, yet Single
+    } else if (e >= Bend) {
+        bad = true;   // a frame covers this chunk: not dense
+    } else {
+        uint64_t p = e;
+        for (;;) {
+            if (p >= Bend) {   // the exit: a Single T must be it (checked below)
+                if (tval == kTNone || tval == kTMulti) {
+                    if (quick_reject(a, p)) {   // no header can start there: the chain dies at p
                         if (a.spec) bad = true;   // (the speculative pass walks on serially in K4)
                         ended = 2;
                         endpos = p;
+                    } else if (tval == kTNone) {
+                        bad = true;   // an exit K1's exit set did not hold
                     } else {
                         W = p;
                     }
-                    break;
+                } else {
+                    W = p;
                 }
-                uint32_t key = 0;
-                uint8_t b0 = 0;
-                const uint64_t v = parse_at(a, p, window_global(a, p), &key, &b0);
-                if (v & kTerm) {
-                    if (term_type(v) == kDead && a.spec) bad = true;
-                    ended = term_type(v) == kDead ? 2 : 1;
-                    endpos = term_pos(v);
-                    break;
-                }
-                if (cnt < (uint64_t)kOpRec) a.opfl[c * kOpRec + cnt] = (p - B) | (uint64_t)b0 << 16 | (uint64_t)key << 32;
-                ++cnt;
-                p = v;
+                break;
             }
-            if (cnt > (uint64_t)kOpRec || (tval != kTMulti && tval != kTNone && W != tval)) bad = true;
+            uint32_t key = 0;
+            uint8_t b0 = 0;
+            // the chunk's LDS copy holds the stream's bytes below len once the stream has 16 (a
+            // shorter one was loaded from a scratch word: its bytes come from global memory)
+            const uint64_t v = B >= a.len ? term(kEnd, p)
+                               : parse_at(a, p, a.len >= 16 ? window_at(st, (int)(p - B)) : window_global(a, p), &key, &b0);
+            if (v & kTerm) {
+                if (term_type(v) == kDead && a.spec) bad = true;
+                ended = term_type(v) == kDead ? 2 : 1;
+                endpos = term_pos(v);
+                break;
+            }
+            if (cnt == (uint64_t)kOpRec) {   // a chunk of more frames: the graph path
+                bad = true;
+                break;
+            }
+            if ((uint64_t)lane == cnt) rec = (p - B) | (uint64_t)b0 << 16 | (uint64_t)key << 32;
+            ++cnt;
+            p = v;
         }
-        __atomic_store_n((volatile NETC_LDS uint64_t*)&L.w[tid], W, __ATOMIC_RELAXED);
-        if (tid == kPG - 1) op_put(a.st_x + c, a.epoch << kOpBits | W);   // for the next group
-#ifdef NETC_SCAN_TRACE
-        OP_STAMP_MAX(16 + 8 * g + 5, n);
-#endif
+        if (tval != kTMulti && tval != kTNone && W != tval) bad = true;
     }
-#ifdef NETC_SCAN_TRACE
-    {
-        const int multi = __syncthreads_count(mine && a.st_t[c - (c > 0)] == kTMulti && c > c0);
-        if (tid == 0) {
-            OP_STAMP(16 + 8 * g + 1, __builtin_amdgcn_s_memrealtime());
-            OP_STAMP(16 + 8 * g + 4, multi);
+    if (lane == 0) {   // the successor's entry after a Multi T (kTFail: this chunk failed)
+        __hip_atomic_store(&h[1][wv], bad ? kTFail : W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (bad) op_fail(a, c);
+        else if (wv == 3 && tval == kTMulti) op_put(a.st_x + c, a.epoch << kOpBits | W);
+    }
+    if (bad) return;
+    if ((uint64_t)lane < cnt) a.opfl[c * kOpRec + lane] = rec;
+    if (lane == 0) {
+        a.opin[2 * c] = cnt | (uint64_t)ended << 32;
+        a.opin[2 * c + 1] = endpos;
+        if (cnt) {
+            __hip_atomic_fetch_add(a.opc + c / kOpGroup, (uint32_t)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(a.opc + a.opc_tiles + c / kTileChunks, (uint32_t)cnt, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-#endif
-    if (__builtin_amdgcn_readfirstlane(__syncthreads_or(bad))) {
-        if (tid == 0) op_fail(a);
-        return;
-    }
-    // the frames before each chunk: the group's scan, then the groups' look-back
-    const uint32_t incl = wave_incl_sum((uint32_t)cnt);
-    if (lane == kWave - 1) L.wsum[wv] = incl;
-    __syncthreads();
-    uint64_t before = incl - (uint32_t)cnt;
-    for (int k = 0; k < wv; ++k) before += L.wsum[k];
+}
+
+// K4 on the one-pass path, EC chunks per block: the frames before the block (the earlier tiles'
+// counters and the tile's earlier groups'), the block's chunks scanned, their recorded frames
+// written (a wavefront per chunk, a lane per frame), and the results by the chunk where the chain
+// ends.
+template <int EC>
+__device__ void op_emit(const ScanArgs& a) {
+    static_assert(EC <= kWave && EC % kOpGroup == 0, "one pass: a block's chunks in one wavefront's scan");
+    __shared__ uint64_t k0s[EC];
+    __shared__ uint32_t cnts[EC];
+    __shared__ uint32_t red[kScanT / kWave];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    const uint64_t cb = (uint64_t)blockIdx.x * EC, tile = cb / kTileChunks;
+    const uint64_t g0 = tile * (kTileChunks / kOpGroup), ng = (cb - tile * kTileChunks) / kOpGroup;
+    uint32_t v = 0;
+    if ((uint64_t)tid < tile) v += a.opc[a.opc_tiles + tid];
+    if ((uint64_t)tid < ng) v += a.opc[g0 + tid];
+    const uint32_t inc = wave_incl_sum(v);
+    if (lane == kWave - 1) red[wv] = inc;
+    uint64_t cnt = 0, info = 0;
     if (wv == 0) {
-        uint64_t agg = 0;
+        const uint64_t c = cb + lane;
+        if (lane < EC && c <= a.nc) info = a.opin[2 * c];
+        cnt = (uint32_t)info;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        uint64_t base = 0;
 #pragma unroll
-        for (int k = 0; k < kScanT / kWave; ++k) agg += L.wsum[k];
-        uint64_t pre = 0;
-        const bool ok = op_group_prefix(a, g, agg, lane, &pre);
-        if (lane == 0) {
-            L.base = pre;
-            L.flag = ok;
+        for (int k = 0; k < kScanT / kWave; ++k) base += red[k];
+        const uint32_t ci = wave_incl_sum((uint32_t)cnt);
+        const uint64_t k0 = base + ci - (uint32_t)cnt;
+        if (lane < EC) {
+            k0s[lane] = k0;
+            cnts[lane] = (uint32_t)cnt;
+        }
+        if (info >> 32) {   // the chain ends in this chunk: the results
+            const uint64_t c = cb + lane, total = k0 + cnt, endpos = a.opin[2 * c + 1];
+            a.result[0] = total;
+            a.result[1] = endpos;
+            a.result[2] = (info >> 32) == 2 ? endpos : ~0ull;
+            if (total <= a.max_frames) a.hdr[total] = endpos;
         }
     }
     __syncthreads();
-    if (tid == 0) OP_STAMP(16 + 8 * g + 2, __builtin_amdgcn_s_memrealtime());
-    if (!__builtin_amdgcn_readfirstlane(L.flag)) return;   // (the call failed meanwhile)
-    const uint64_t k0 = L.base + before;
-    for (uint64_t i = 0; i < cnt; ++i) {
-        const uint64_t f = a.opfl[c * kOpRec + i];
-        put_frame(a, k0 + i, B + (f & 0xFFFFu), (uint32_t)(f >> 32), (uint8_t)(f >> 16));
+    for (int j = wv; j < EC; j += kScanT / kWave) {
+        const uint64_t c = cb + j;
+        if (c > a.nc) break;
+        if ((uint32_t)lane < cnts[j]) {
+            const uint64_t f = a.opfl[c * kOpRec + lane];
+            put_frame(a, k0s[j] + lane, c * kChunk + (f & 0xFFFFu), (uint32_t)(f >> 32), (uint8_t)(f >> 16));
+        }
     }
-    if (ended) {   // the chain ends in this chunk: the results
-        const uint64_t total = k0 + cnt;
-        a.result[0] = total;
-        a.result[1] = endpos;
-        a.result[2] = ended == 2 ? endpos : ~0ull;
-        if (total <= a.max_frames) a.hdr[total] = endpos;
-    }
-#ifdef NETC_SCAN_TRACE
-    __syncthreads();
-    if (tid == 0) OP_STAMP(16 + 8 * g + 3, __builtin_amdgcn_s_memrealtime());
-#endif
+}
+
+// K4, both paths: the other parity's counters zeroed for the next call (a grid-stride loop)
+__device__ __forceinline__ void op_clear_prev(const ScanArgs& a) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kScanT + threadIdx.x; i < a.opc_words; i += (uint64_t)gridDim.x * kScanT)
+        a.opc_prev[i] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < kFailCopies) a.opfail_prev[threadIdx.x * kFailStride] = 0;
 }
 
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
@@ -879,7 +875,8 @@ __device__ __forceinline__ u32x4 k1_load(const uint8_t* p) {
     return *(const NETC_GLOBAL u32x4u*)p;
 }
 
-// ONE: the one-pass path's prediction T(c) after the parse (op_publish_t).
+// ONE: the one-pass path after the parse -- T(c) published (op_publish_t), then the chunk's walk
+// from its speculated entry (op_chunk).
 template <bool NT, bool ONE>
 __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     if (threadIdx.x == 0 && blockIdx.x == 0) OP_TRACE(0, 1);
@@ -887,6 +884,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     __shared__ uint32_t stage[4][kStageWords];   // per wave: its chunk's bytes (+ 16 after)
     __shared__ unsigned long long set[4][kSet];
     __shared__ uint16_t queue[4][kQCap];
+    __shared__ OpHand hand;   // (ONE) the waves' T and W hand-over words
 #ifdef NETC_SCAN_K1_EXP
     __shared__ uint32_t qn[4];
     if ((threadIdx.x & 63) == 0) qn[threadIdx.x / 64] = 0;
@@ -896,11 +894,18 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     // then scalar (SGPR arithmetic, scalar branches) instead of per-lane VALU
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(tid / kWave);
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
+    if constexpr (ONE) {   // each wave clears its hand-over words before any wave of the block reads them
+        if (lane == 0) hand[0][wv] = hand[1][wv] = kHPend;
+        __syncthreads();
+    }
     if (c > a.nc) return;
     const uint64_t B = c * kChunk, Bend = B + kChunk;
     if (lane == 0 && a.start / kChunk == c) append_cand(a, a.start, true);   // the root node
     if (B >= a.len) {   // the virtual chunk: no bytes
-        if constexpr (ONE) op_publish_t(a, c, kTNone, lane);
+        if constexpr (ONE) {
+            op_publish_t(a, c, kTNone, lane, wv, hand);
+            op_chunk(a, c, kTNone, stage[wv], lane, wv, hand);
+        }
         return;
     }
     uint32_t d[4][4], nx[4];
@@ -1078,7 +1083,10 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     }
     if (total > (uint32_t)kQCap) {   // wave-uniform (adversarial payloads, non-strict mode)
         if (lane == 0) atomicOr(a.ovf, kOvfQueue);
-        if constexpr (ONE) op_publish_t(a, c, kTFail, lane);
+        if constexpr (ONE) {
+            op_publish_t(a, c, kTFail, lane, wv, hand);
+            if (lane == 0) op_fail(a, c);
+        }
         return;
     }
     uint32_t at = incl - mine;
@@ -1123,11 +1131,10 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         const uint64_t bn = __ballot(nodes != 0);
         const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(nodes), kWave - 1);
         const uint64_t t = __ballot(ovf) ? kTFail : (n == 0 ? kTNone : (n > 1 ? kTMulti : readlane64(ex, __builtin_ctzll(bn))));
-        op_publish_t(a, c, t, lane);
-        if (lane == 0) {
-            OP_STAMP_ADD(t == kTNone ? 5 : t == kTMulti ? 7 : t == kTFail ? 8 : 6, 1);
-            OP_STAMP_MAX(1, __builtin_amdgcn_s_memrealtime());
-        }
+        op_publish_t(a, c, t, lane, wv, hand);
+        if (lane == 0) OP_STAMP_ADD(t == kTNone ? 5 : t == kTMulti ? 7 : t == kTFail ? 8 : 6, 1);
+        op_chunk(a, c, t, stage[wv], lane, wv, hand);
+        if (lane == 0) OP_STAMP_MAX(1, __builtin_amdgcn_s_memrealtime());
     }
 }
 
@@ -1577,86 +1584,13 @@ __device__ __forceinline__ void links_body(const ScanArgs& a, LinksLdsT<BC>& sl,
     }
 }
 
-// K2's launch on the one-pass path: the groups (op_group), claimed in order (a block's look-back
-// waits only on groups claimed before its own, by blocks already running); once every group is
-// done, the failure word decides whether K2's own work runs.  True: the graph path goes on.
+// K2: nothing when K1 resolved the call on the one-pass path (a flag read)
 template <int BC>
-__device__ __forceinline__ bool onepass_groups(const ScanArgs& a, LinksLdsT<BC>& sl) {
-    static_assert(sizeof(LinksLdsT<BC>) >= sizeof(OpGroupLds), "one pass: its LDS overlays K2's");
-    OpGroupLds& L = *reinterpret_cast<OpGroupLds*>(&sl);
-    uint32_t* const f = a.flags;
-    const int tid = threadIdx.x;
-    const uint32_t groups = (uint32_t)(a.nc / kPG + 1);   // (<= the launch's blocks: one claim each)
-    // No loop with a barrier in it here: every branch around a barrier goes on a value made
-    // wave-uniform with readfirstlane, and each block claims at most one group.  (A first build
-    // looped over claims; the compiler, taking the loop's exit as divergent, restructured it per
-    // lane and the barriers paired up with the wrong ones: group 0 ran for ever.)
-    if (tid == 0) OP_STAMP_MIN(2, __builtin_amdgcn_s_memrealtime());
-    if (tid == 0) L.item = __hip_atomic_fetch_add(f + kFPClaim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint32_t g = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.item);
-    if (tid == 0) OP_TRACE(1, g + 1);   // last group claimed
-    if (g < groups) {
-        op_group(a, g, L);
-        __syncthreads();   // (every thread's failure atomic before the group counts as done)
-        if (tid == 0) L.item = __hip_atomic_fetch_add(f + kFPDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (tid == 0) OP_TRACE(2, g + 1);   // last group done
-        __syncthreads();
-        if (__builtin_amdgcn_readfirstlane((int)L.item) == (int)groups - 1) {   // the last group: decide
-            if (tid == 0) L.base = op_decide(a, op_failed(a) ? 1 : 0);
-            __syncthreads();
-            if (tid > 0 && tid < kVerdicts) op_put(a.st_v + tid * kVStride, L.base);   // the copies
-        }
-    }
-    // Relaxed (sc1) polls: an acquire or release at agent scope writes back or invalidates the
-    // whole L2 of the XCD (buffer_wbl2 / buffer_inv sc1) -- hundreds of waiting blocks doing that
-    // cost this launch 150 us at config 2 (r06l).  Only the failure word is read after the wait,
-    // itself an atomic, and every failure atomic of a group is done (vmcnt, the barrier above)
-    // before its count goes up.
-    if (tid == 0) {   // every group claimed or being claimed: wait for the verdict
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        const uint64_t* vw = a.st_v + (blockIdx.x % kVerdicts) * kVStride;
-        uint64_t v;
-        for (;;) {
-            v = op_get(vw);
-            if ((v >> 1) == a.epoch) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 5 * kOnePassWait) {   // (a safety valve)
-                v = op_decide(a, 1);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(8);
-        }
-        L.flag = (int)(v & 1);
-        OP_TRACE(3, 1 + L.flag);   // the verdict
-        OP_STAMP_MAX(3, __builtin_amdgcn_s_memrealtime());
-    }
-    __syncthreads();
-    const bool graph = __builtin_amdgcn_readfirstlane(L.flag) != 0;
-    __syncthreads();
-    return graph;
-}
-
-// the last block to leave re-zeroes the claim counters for the next call
-__device__ __forceinline__ void onepass_leave(const ScanArgs& a) {
-    uint32_t* const f = a.flags;
-    if (threadIdx.x == 0) OP_STAMP_MAX(4, __builtin_amdgcn_s_memrealtime());
-    if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(f + kFExit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
-        __hip_atomic_store(f + kFPClaim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(f + kFPDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(f + kFExit, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// OP: the one-pass groups first (a separate instance: their registers would cost the plain K2
-// occupancy); K2's own work only if they failed.
-template <int BC, bool OP>
 __global__ __launch_bounds__(kScanT) void scan_links(ScanArgs a) {
     __shared__ LinksLdsT<BC> sl;
     SCAN_SCOPE(1);
-    // (a block goes on to its own K2 work only after every group is done: nothing waits there)
-    if (!OP || onepass_groups<BC>(a, sl)) links_body<false, BC>(a, sl, blockIdx.x);
-    if (OP) onepass_leave(a);
+    if (onepass_done(a)) return;
+    links_body<false, BC>(a, sl, blockIdx.x);
 }
 
 // exclusive prefix sum over a block of NT threads; the block total in *total
@@ -2234,19 +2168,13 @@ __device__ __forceinline__ bool arrive_last(uint32_t* counter, uint32_t expect, 
     return *flag != 0;
 }
 
-// OP: the one-pass groups first (onepass_groups); the graph phases only if they failed.  On the
-// one-pass path this launch and K4 (a flag read) follow K1: one launch boundary fewer than
-// scan_links<OP> + scan_tiles_resolve.
-template <bool OP>
+// On the one-pass path this launch (a flag read) and K4 follow K1: one launch boundary fewer
+// than scan_links + scan_tiles_resolve.
 __global__ __launch_bounds__(kScanT) void scan_links_fused(ScanArgs a, uint64_t tiles, uint32_t blocks) {
     __shared__ FusedLds sm;
     __shared__ int flag;
     SCAN_SCOPE(1);
-    if (OP) {
-        const bool graph = onepass_groups<kBlkChunks>(a, sm.k2);
-        onepass_leave(a);
-        if (!graph) return;
-    }
+    if (onepass_done(a)) return;
     links_body<true, kBlkChunks>(a, sm.k2, blockIdx.x);
     constexpr uint32_t kPerTile = (uint32_t)(kTileChunks / kBlkChunks);
     const uint32_t tile = blockIdx.x / kPerTile;
@@ -2403,7 +2331,9 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
     const int tid = threadIdx.x;
     const uint64_t tile = (uint64_t)blockIdx.x * EC / kTileChunks;   // EC divides kTileChunks
     if (tid == 0 && blockIdx.x == 0) OP_TRACE(8, 1);
-    if (onepass_done(a)) {   // K1 wrote the frames and results: only the clearing for the next call
+    op_clear_prev(a);
+    if (onepass_done(a)) {   // K1 walked every chunk: the descriptors, the results, the clearing
+        op_emit<EC>(a);
         if (tid < EC) {
             const uint64_t c = (uint64_t)blockIdx.x * EC + tid;
             if (c <= a.nc) {
@@ -2413,7 +2343,6 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
         }
         if (blockIdx.x == 0 && tid == 0) {
             *a.ovf_prev = 0;
-            *a.opfail_prev = 0;
             a.flags[8] = 0;
             a.flags[9] = 0;    // no serial walk
             a.flags[10] = 1;   // the one-pass path (netc_gpu_scan_diag bit 32)
@@ -2421,7 +2350,6 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
         return;
     }
     if (blockIdx.x == 0 && tid == 0) {
-        *a.opfail_prev = 0;
         a.flags[10] = 0;
     }
     if (tid == 0) {
@@ -2641,7 +2569,7 @@ std::mutex& stream_scratch_mu() {
 // regions; flags, ccount and ext first -- the region every call leaves zeroed.
 struct Layout {
     uint64_t flags, ccount, ext, tarr, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, flist, text,
-        tcount, tinfo, st_t, st_x, st_g, st_v, opfl, total;
+        tcount, tinfo, st_t, st_x, opfl, opin, opc, opf, total;
 };
 Layout layout_for(uint64_t cap) {
     auto align = [](uint64_t x) { return (x + 63) & ~63ull; };
@@ -2652,6 +2580,8 @@ Layout layout_for(uint64_t cap) {
     l.ccount = o;  o = align(o + cap * 4);
     l.ext = o;     o = align(o + slots);
     l.tarr = o;    o = align(o + tiles * 4);
+    l.opc = o;     o = align(o + 2 * op_counter_words(cap) * 4);   // one-pass counters, two parities
+    l.opf = o;     o = align(o + 2 * kFailCopies * kFailStride * 4);  // one-pass failure words, two sets
     l.cleared = o;
     l.cand = o;    o = align(o + slots * 8);
     l.link = o;    o = align(o + slots * 4);
@@ -2668,9 +2598,8 @@ Layout layout_for(uint64_t cap) {
     l.tinfo = o;   o = align(o + tiles * sizeof(TileInfo));
     l.st_t = o;    o = align(o + cap * 8);   // one-pass status words (epochs: never cleared per call)
     l.st_x = o;    o = align(o + cap * 8);
-    l.st_g = o;    o = align(o + (cap / kPG + 1) * 8);
-    l.st_v = o;    o = align(o + kVerdicts * kVStride * 8);
     l.opfl = o;    o = align(o + cap * kOpRec * 8);
+    l.opin = o;    o = align(o + cap * 16);
     l.total = o;
     return l;
 }
@@ -2790,17 +2719,16 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.flags = (uint32_t*)(m + l.flags);
     a.ovf = a.flags + ((s.calls & 1) ? 2 : 0);
     a.ovf_prev = a.flags + ((s.calls & 1) ? 0 : 2);
-    a.opfail = a.flags + ((s.calls & 1) ? 5 : 4);
-    a.opfail_prev = a.flags + ((s.calls & 1) ? 4 : 5);
+    a.opfail = (uint32_t*)(m + l.opf) + ((s.calls & 1) ? kFailCopies * kFailStride : 0);
+    a.opfail_prev = (uint32_t*)(m + l.opf) + ((s.calls & 1) ? 0 : kFailCopies * kFailStride);
     ++s.calls;
-    // the one-pass path: knob SCAN_ONEPASS (0 never, 1 up to 256 MiB), by default up to
-    // kOnePassMax of stream.  (Each of K2's blocks claims at most one group and waits for all of
-    // them: 256 MiB is 256 groups, a block per CU -- resident whatever else the CU holds.)  Each call has its own epoch; when the 24-bit
-    // epoch wraps, the status words are cleared once, so a word left from 2^24 calls ago cannot match.
+    // the one-pass path: knob SCAN_ONEPASS (1: up to kOnePassCap, 2: up to kOnePassMax; off by
+    // default -- it measured 126 us against the graph path's 41 at config 2).  Each
+    // call has its own epoch; when the 24-bit epoch wraps, the status words are cleared once, so a
+    // word left from 2^24 calls ago cannot match.
     const int64_t op = knob(NETC_GPU_KNOB_SCAN_ONEPASS);
     const int64_t fuse = knob(NETC_GPU_KNOB_SCAN_FUSE);
-    // (the one-pass groups run in scan_links: not with K2 + K3 fused into one launch)
-    a.onepass = op != 0 && len <= (op == 1 ? kOnePassCap : kOnePassMax) ? 1 : 0;
+    a.onepass = op > 0 && len <= (op == 1 ? kOnePassCap : kOnePassMax) ? 1 : 0;
     if (++s.epoch >= (1ull << 24) - 1) {   // (all-ones never: an exit-set entry's ~0 must not match)
         if ((e = hipMemsetAsync(m + l.st_t, 0, l.opfl - l.st_t, stream)) != hipSuccess) return e;
         s.epoch = 1;
@@ -2808,9 +2736,12 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.epoch = s.epoch;
     a.st_t = (uint64_t*)(m + l.st_t);
     a.st_x = (uint64_t*)(m + l.st_x);
-    a.st_g = (uint64_t*)(m + l.st_g);
-    a.st_v = (uint64_t*)(m + l.st_v);
     a.opfl = (uint64_t*)(m + l.opfl);
+    a.opin = (uint64_t*)(m + l.opin);
+    a.opc_words = op_counter_words(s.cap);
+    a.opc_tiles = s.cap / kOpGroup;
+    a.opc = (uint32_t*)(m + l.opc) + ((s.calls & 1) ? a.opc_words : 0);      // (s.calls: already counted)
+    a.opc_prev = (uint32_t*)(m + l.opc) + ((s.calls & 1) ? 0 : a.opc_words);
     a.ccount = (uint32_t*)(m + l.ccount);
     a.ext = m + l.ext;
     a.tarr = (uint32_t*)(m + l.tarr);
@@ -2863,17 +2794,15 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     const bool big = bk == kBlkChunksBig || (bk != kBlkChunks && chunks > kBigBlocksAbove);
     auto links = [&]() {
         if (big)
-            hipLaunchKernelGGL((a.onepass ? scan_links<kBlkChunksBig, true> : scan_links<kBlkChunksBig, false>),
-                               dim3((unsigned)((chunks + kBlkChunksBig - 1) / kBlkChunksBig)), dim3(kScanT), 0, stream, a);
-        else
-            hipLaunchKernelGGL((a.onepass ? scan_links<kBlkChunks, true> : scan_links<kBlkChunks, false>), dim3(blk),
+            hipLaunchKernelGGL(scan_links<kBlkChunksBig>, dim3((unsigned)((chunks + kBlkChunksBig - 1) / kBlkChunksBig)),
                                dim3(kScanT), 0, stream, a);
+        else
+            hipLaunchKernelGGL(scan_links<kBlkChunks>, dim3(blk), dim3(kScanT), 0, stream, a);
     };
-    // the one-pass path: K2 + K3 fused behind the groups by default (SCAN_FUSE 2: the split launches)
+    // the one-pass path: K2 + K3 fused by default (one gated launch; SCAN_FUSE 2: the split launches)
     const bool fused = tiles <= (uint64_t)kFuseTiles && (fuse == 1 || (a.onepass && fuse < 0 && !big));
     if (fused) {   // (32 chunks per K2 block: the tiles' arrival counts)
-        if (a.onepass) hipLaunchKernelGGL(scan_links_fused<true>, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
-        else hipLaunchKernelGGL(scan_links_fused<false>, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
+        hipLaunchKernelGGL(scan_links_fused, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);
     } else if (fuse != 0 && tiles <= (uint64_t)kMergeTiles) {
         links();
         hipLaunchKernelGGL(scan_tiles_resolve, dim3((unsigned)tiles), dim3(kScanT), 0, stream, a, tiles);

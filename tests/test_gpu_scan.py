@@ -323,7 +323,7 @@ def test_far_exits(torch_cuda, strict):
     run_scan(torch_cuda, wire[:int(wo[-3]) + 100], strict=strict, parallel=True)
 
 
-@pytest.mark.parametrize("onepass", ["0", "-1"])
+@pytest.mark.parametrize("onepass", ["0", "1"])
 @pytest.mark.parametrize("fuse", ["1", "0", "2", "-1"])
 def test_fused_and_separate_launches(torch_cuda, gpu_knob, fuse, onepass):
     # K2 + K3a + K3b as one launch (knob SCAN_FUSE = 1: arrival counters per tile and per
@@ -332,7 +332,7 @@ def test_fused_and_separate_launches(torch_cuda, gpu_knob, fuse, onepass):
     # (the last tile block to arrive resolves; sc1 hand-off): the same results over
     # alternating stream sizes, the serial fallback, non-strict streams and truncations, one
     # call after another on one stream (a counter left non-zero would break the next call)
-    # (with the one-pass path on, its groups run first in whichever K2 launch this is)
+    # (with the one-pass path on, the K2 launch, whichever it is, reads its flag first)
     gpu_knob("SCAN_FUSE", fuse)
     gpu_knob("SCAN_ONEPASS", onepass)
     rng = np.random.default_rng(51)
@@ -390,11 +390,11 @@ def test_emit_block_sizes(torch_cuda, gpu_knob, emit):
 @pytest.mark.parametrize("onepass,fuse", [("1", "-1"), ("1", "2"), ("0", "-1")])
 def test_onepass_and_graph_paths(torch_cuda, gpu_knob, onepass, fuse):
     """the one-pass path (dense streams: K1's chunks speculate their entries from their
-    predecessors and check them; K2's launch writes the frames; K3 and K4 only read a flag) and the
-    graph path (knob SCAN_ONEPASS = 0) on the same streams: identical results; dense strict streams
-    finish on the one-pass path (netc_gpu_scan_diag bit 32), streams with chunk-covering frames on
-    the graph kernels.  The one-pass groups run in K2 + K3's fused launch by default, in K2's own
-    with SCAN_FUSE = 2."""
+    predecessors, walk and check them; K2 + K3 only read a flag; K4 sums the counts and writes the
+    frames) and the graph path (knob SCAN_ONEPASS = 0) on the same streams: identical results;
+    dense strict streams finish on the one-pass path (netc_gpu_scan_diag bit 32), streams with
+    chunk-covering frames or chunks of more than 64 frames on the graph kernels.  K2 + K3 are one
+    gated launch by default, separate ones with SCAN_FUSE = 2."""
     gpu_knob("SCAN_ONEPASS", onepass)
     gpu_knob("SCAN_FUSE", fuse)
     rng = np.random.default_rng(97)

@@ -33,7 +33,7 @@ HOT = [
     "void netc_gpu::wire_offsets_chained<4, false>",
     "void netc_gpu::wire_offsets_chained<16, false>",
     "void netc_gpu::scan_links<",
-    "void netc_gpu::scan_links_fused<true>",    # the one-pass path's launch
+    "netc_gpu::scan_links_fused(",              # the one-pass path's gated launch
     "netc_gpu::scan_tiles_resolve(",
     "netc_gpu::scan_tiles(",
     "netc_gpu::scan_resolve(",
@@ -47,8 +47,6 @@ KNOB_ONLY = [
     "void netc_gpu::encode_frames_kernel<2,",  # 2 KiB chunks (netc_gpu_tune unroll 2 / 4; ENC_PF = 1)
     "void netc_gpu::wire_offsets_chained<16, true>",   # fixups in the scan (ENC_FIX = 1)
     "void netc_gpu::wire_offsets_chained<1, true>",
-    "void netc_gpu::scan_links_fused<false>",   # NETC_GPU_KNOB_SCAN_FUSE = 1 without the one-pass path
-    "void netc_gpu::scan_links<64, true>",      # the one-pass path above 128 MiB (SCAN_ONEPASS = 1)
 ]
 
 
@@ -116,10 +114,20 @@ def test_every_hot_kernel_is_found(resources):
         assert any(k.startswith(prefix) for k in resources), f"no kernel {prefix}* in the library"
 
 
+# kernels allowed a small private segment (no spills): bytes per lane, and why
+SCRATCH_OK = {
+    # K2 + K3a + K3b in one launch: on the default path only as the one-pass path's gate (a flag
+    # read, then return); its graph body runs when the one-pass path fails over (or with SCAN_FUSE=1)
+    "netc_gpu::scan_links_fused(": 64,
+}
+
+
 def test_hot_kernels_do_not_spill(resources):
     bad = []
     for k, (vgprs, spills, scratch) in sorted(resources.items()):
         if any(k.startswith(p) for p in KNOB_ONLY):
+            continue
+        if not spills and any(k.startswith(p) and scratch <= lim for p, lim in SCRATCH_OK.items()):
             continue
         if any(k.startswith(p) for p in HOT) and (spills or scratch):
             bad.append(f"{k}: {vgprs} VGPRs, {spills} spilled, {scratch} B scratch per lane")
