@@ -15,7 +15,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // out of order and forces s_waitcnt vmcnt(0) lgkmcnt(0) at every use, which
 // drains prefetched loads and kills a software pipeline.
 #define NETC_GLOBAL __attribute__((address_space(1)))
-#define NETC_LDS __attribute__((address_space(3)))   // (the same for LDS: ds_* rather than flat_*)
 template <typename T>
 __device__ __forceinline__ const NETC_GLOBAL T* gptr(const T* p) {
     return (const NETC_GLOBAL T*)p;
