@@ -1572,7 +1572,11 @@ hipError_t launch_encode_frames(uint8_t* wire, uint64_t wire_bound, const uint8_
     // in the assembly's tail, where they fill the CUs its last waves leave (r04kk)
     const bool fix_in_scan = !all_spans && !src_walk && knob(NETC_GPU_KNOB_ENC_FIX) == 1;
     const bool fix_tail = !all_spans && !src_walk && knob(NETC_GPU_KNOB_ENC_FIX) == 2;
+#ifdef NETC_ENC_DIAG_NOFIX   // diagnostic build only (tools/pmc_encode.sh): no header fixups -- wrong
+    const bool fix_blocks = false;   // wire bytes, for attributing the assembly's counter traffic
+#else
     const bool fix_blocks = !all_spans && !src_walk && !fix_in_scan && !fix_tail;
+#endif
     // (the scan with the fixups holds 8 frames per thread at most: 16 spilled)
     const int per0 = scan_per(n), per = fix_in_scan && per0 > 8 ? 8 : per0;
     const uint64_t tiles = scan_tiles_for(n, per);
