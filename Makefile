@@ -138,7 +138,7 @@ clean:
 
 # diagnostics (tools/, not part of the product)
 diag: tools/libdiag_stream.so tools/libnetc_ws_gpu_stamps.so tools/libnetc_ws_gpu_checks.so tools/libscan_k1only.so \
-      tools/libscan_k1exp.so diag/libnetc_ws_gpu_trace.so
+      tools/libscan_k1exp.so diag/libnetc_ws_gpu_trace.so diag/libnetc_ws_gpu_nofix.so
 tools/libdiag_stream.so: tools/diag_stream.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 tools/libnetc_ws_gpu_stamps.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
@@ -151,6 +151,11 @@ tools/libscan_k1only.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
 diag/libnetc_ws_gpu_trace.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
 	@mkdir -p diag
 	$(HIPCC) $(HIPFLAGS) -DNETC_SCAN_TRACE -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
+# the frame assembly without its header fixups (wrong wire bytes: counter attribution only,
+# tools/pmc_encode_fixups.sh)
+diag/libnetc_ws_gpu_nofix.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
+	@mkdir -p diag
+	$(HIPCC) $(HIPFLAGS) -DNETC_ENC_DIAG_NOFIX -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 tools/libscan_k1exp.so: $(GPU_SRCS) $(GPU_HDRS) $(LIBDIR)/libnetc.so
 	$(HIPCC) $(HIPFLAGS) -DNETC_SCAN_K1_EXP -shared -o $@ $(GPU_SRCS) -L$(LIBDIR) -lnetc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 
