@@ -236,3 +236,38 @@ def test_large_text_batch(torch_cuda):
         frames.append((0x81, p))
     exp = run_validate(torch_cuda, frames)
     assert (exp == 0).sum() > 300
+
+
+def edge_text(rng, n, bad):
+    """n bytes of text whose first and last 3 bytes are multi-byte sequences (or, bad: a stray
+    continuation first / a truncated sequence last)"""
+    if n < 8:
+        return corrupt(rng, text_bytes(rng, n)) if bad else text_bytes(rng, n)
+    head, tail = "\u20ac".encode(), "\U0001F600".encode()
+    mid = bytearray(text_bytes(rng, max(0, n - 7)))
+    body = head + bytes(mid) + tail
+    if bad:
+        body = (b"\x80" + body[1:]) if rng.random() < 0.5 else body[:-1]
+    return body
+
+
+@pytest.mark.parametrize("steps", [None, 1, 2, 4])
+@pytest.mark.parametrize("place", sorted(PLACES))
+def test_message_edges(torch_cuda, gpu_knob, steps, place):
+    """single-frame TEXT messages starting and ending at every offset around span (1 KiB) and
+    window (4 KiB) edges, with multi-byte first and last bytes, half of them broken at the start
+    or end (the bytes the per-message launch checks), short ones among them"""
+    gpu_knob("VAL_STEPS", steps)
+    rng = np.random.default_rng(171)
+    frames = []
+    for _ in range(600):
+        r = rng.random()
+        n = int(rng.integers(0, 12)) if r < 0.2 else (int(rng.integers(1015, 1034)) if r < 0.7 else int(rng.integers(30, 3000)))
+        bad = rng.random() < 0.5
+        frames.append((0x81, edge_text(rng, n, bad)))
+        if rng.random() < 0.05:
+            frames.append((0x82, rng.integers(0, 256, int(rng.integers(0, 50)), dtype=np.uint8).tobytes()))
+    shift = PLACES[place]
+    exp = run_validate(torch_cuda, frames, shift=0 if shift is None else 0, inplace=shift is None,
+                       dshift=shift or 3)
+    assert 100 < (exp == 0).sum() < len(frames)
