@@ -1,5 +1,6 @@
 #!/bin/bash
-# netc_gpu_unmask_validate with and without the in-pass verdicts (NETC_VAL_INPASS=0), config 2 and
+# netc_gpu_unmask_validate with and without the in-pass verdicts (NETC_VAL_INPASS=0: a knob of the
+# measured build, removed since -- DESIGN §16.6), config 2 and
 # 4 shapes, three interleaved rounds, then a kernel trace of each (through gpurun, repo root)
 set -o pipefail
 R=$PWD
