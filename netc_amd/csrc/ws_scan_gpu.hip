@@ -202,8 +202,7 @@ extern "C" int netc_gpu_debug_scan_stamps(void* device_buffer) {
 #define OP_STAMP_ADD(i, v) ((void)0)
 #endif
 // OP_STAMP layout (trace build): [0] K1 first start (min), [1] K1 last wave's end (max), [5] [6]
-// [7] [8] chunks whose T is None, Single, Multi, Fail, [9] [10] [11] K1's entry waits: summed,
-// longest, over 2 us (100 MHz ticks)
+// [7] [8] chunks whose T is None, Single, Multi, Fail
 
 __device__ __forceinline__ uint64_t term(uint64_t type, uint64_t pos) { return kTerm | type << 61 | pos; }
 __device__ __forceinline__ uint64_t term_type(uint64_t v) { return (v >> 61) & 3; }
@@ -293,14 +292,9 @@ struct ScanArgs {
     int onepass;           // this call runs it (the host's choice: knob SCAN_ONEPASS, stream size)
     uint32_t* opfail;      // this call's one-pass failure words: kFailCopies, kFailStride apart (two sets,
     uint32_t* opfail_prev; // ... alternate calls; K4 zeroes the previous call's, as for ovf)
-    uint64_t* st_t;        // per chunk: its exit prediction T (epoch-tagged)
-    uint64_t* st_x;        // per chunk after a Multi T: W, where its walk left it (or END), epoch-tagged
+    uint64_t* st_t;        // per chunk: its exit prediction T (epoch-tagged; K1)
+    uint64_t* st_g;        // per block of kOpT chunks: its look-back status word
     uint64_t* opfl;        // per chunk: kOpRec frames {offset, byte 0 << 16, key << 32}
-    uint64_t* opin;        // per chunk: {frames | how the chain ends here << 32, where}
-    uint32_t* opc;         // this call's counters: frames per group of kOpGroup chunks, then per tile
-    uint32_t* opc_prev;    // ... the previous call's (K4 zeroes them, opc_words of them)
-    uint64_t opc_tiles;    // index of the first tile counter
-    uint64_t opc_words;
     uint64_t epoch;        // 1 .. 2^24 - 1, one per call on the scratch (words of other calls do not match)
 };
 
@@ -523,183 +517,171 @@ static constexpr int kNearLane = 55;
 #ifndef NETC_K1_SLIM
 #define NETC_K1_SLIM 1
 #endif
-static constexpr int kQCap = NETC_K1_SLIM ? 240 : 256;   // K1: exit-capable candidates queued per chunk (more: serial walk)
+static constexpr int kQCap = NETC_K1_SLIM ? 248 : 256;   // K1: exit-capable candidates queued per chunk (more: serial walk)
 static constexpr int kStageWords = NETC_K1_SLIM ? (int)((kChunk + 16) / 4) : kWords;
-static_assert(!NETC_K1_SLIM || 4 * (4 * kStageWords + 8 * kSet + 2 * kQCap) + 64 <= 20480,
+static_assert(!NETC_K1_SLIM || 4 * (4 * kStageWords + 8 * kSet + 2 * kQCap) <= 20480,
               "K1: a 4-wave block must stay within 20,480 B of LDS (8 blocks per CU)");
 static constexpr int kCheapMax = 64;   // K1: more from the cheap selection: the full quick check instead
 
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v);
 // ------------------------------------------------------------------ one pass --
 // The one-pass path for dense streams -- frames shorter than a chunk, so the chain
-// visits every chunk from the start on (the C2 shape) -- runs inside K1's launch.  After its
-// parse, each chunk c publishes T(c): where the chain leaves c if it visits it, from the distinct
-// exits of c's exit-capable candidates that land on a position able to start a header (the nodes
-// K1 appends): that exit when there is exactly one (Single), None (no such exit: a chain that
-// visits c ends in it, or dies at an exit onto a position that cannot start a header), Multi, or
-// Fail (K1's queue or set overflowed).  Garbage chains (payload bytes parsed as headers) land on
-// header-capable positions with ~2 % odds, so nearly every chunk is Single.
+// visits every chunk from the start on (the C2 shape).  K1 publishes, per chunk c, T(c): where the
+// chain leaves c if it visits it, from the distinct exits of c's exit-capable candidates that land
+// on a position able to start a header (the nodes K1 appends): that exit when there is exactly one
+// (Single), None (no such exit: a chain that visits c ends in it, or dies at an exit onto a
+// position that cannot start a header), Multi, or Fail (K1's queue or set overflowed).  Garbage
+// chains (payload bytes parsed as headers) land on header-capable positions with ~2 % odds, so
+// nearly every chunk is Single.
 //
-// The chunk's wavefront then SPECULATES its entry from its predecessor alone -- T(c-1) if Single,
-// END if None, the predecessor's own walk exit W(c-1) if Multi -- and walks its frames from there
-// in LDS (its bytes are staged for the parse anyway) to its exit W(c), checking:
+// The next launch (scan_op_walk, a thread per chunk) SPECULATES each chunk's entry from its
+// predecessor alone -- T(c-1) if Single, END if None, the predecessor's own walk exit W(c-1) if
+// Multi, which it walks to itself from the nearest predecessor with a known T -- walks its frames
+// from there (header bytes from global memory) to its exit W(c), and checks:
 //   * an entry past the chunk's end (a frame covers it: not a dense stream) fails;
 //   * a visited chunk's W(c) must equal T(c) when T(c) is Single (its successor used T(c));
 //   * a chunk not visited (entry END) must not be Single (its successor would walk from T(c)).
 // By induction from the start chunk (entry = the start), if no chunk fails every speculated entry
-// is the true one.  A wave waits only for its predecessor's T, published right after that
-// predecessor's parse whatever its entry -- or, after a Multi chunk, for its W -- so nothing is
-// serial beyond a run of Multi chunks.  (Round 6's first build waited for each predecessor's
-// resolved exit: a serial chain through the whole stream, 4 ms at config 2; the second walked in
-// K2's launch, a thread per chunk with header bytes from global memory: 50 us against the graph
-// path's 41, profiles/r06_scan_onepass.md.)
-//
-// The walk's frames go to a per-chunk record (a lane each, kOpRec at most), its count to two
-// counters -- the chunk's group of kOpGroup chunks and its tile (relaxed atomics, no wait) -- and
-// K4, one launch later with every count in, sums the counters before each of its blocks, scans
-// the block's chunks and writes the descriptors and the results (op_emit).  Any failure (a
-// check, Fail, a speculative stop at a header the filter rejects, more than kOpRec frames in a
-// chunk, a wait past kOnePassWait) sets the call's failure word; K2-K4 then run the graph path
-// from the nodes K1 appended all the same, and the results are the same either way.  The T and
-// W words carry the call's epoch (never cleared per call); the counters alternate per call, each
-// call's K4 zeroing the other set.  Correctness never rests on dispatch order: a wait that
-// outlasts kOnePassWait fails the call over to the graph path.
+// is the true one.  Nothing waits but the blocks' decoupled look-back over their frame counts;
+// then every chunk writes its descriptors and
+// the chunk where the chain ends the results.  Any failure (a check, Fail, a speculative stop at a
+// header the filter rejects, more than kOpRec frames in a chunk) sets the call's failure word, and
+// K2-K4 then run the graph path from the nodes K1 appended all the same, overwriting everything;
+// the results are the same either way.  T and the look-back words carry the call's epoch (never
+// cleared per call).  (Round 6 first resolved the chunks inside K1 itself: with a frame counter
+// per group and tile bumped by device-scope atomics, 126 us at config 2 -- hot-address atomics
+// under K1's stream; without them still 34 us for K1 alone, the entry waits holding K1's waves.
+// DESIGN.md §16.4.)
 static constexpr uint64_t kOpBits = 40;
 static constexpr uint64_t kOpMask = (1ull << kOpBits) - 1;
 static constexpr uint64_t kTNone = kOpMask, kTMulti = kOpMask - 1, kTFail = kOpMask - 2;   // T values; else the exit
 static constexpr uint64_t kXEnd = kOpMask;                              // W / entry: no chain here
-static constexpr uint64_t kOnePassWait = 2000000;                       // 20 ms at 100 MHz
-static constexpr uint64_t kOnePassMax = 128ull << 20;                   // default: streams up to 128 MiB
+static constexpr uint64_t kOnePassWait = 200000;                        // 2 ms at 100 MHz
+static constexpr uint64_t kOnePassMax = 128ull << 20;                   // knob 2: streams up to 128 MiB
 static constexpr uint64_t kOnePassCap = 256ull << 20;                   // knob 1: up to 256 MiB
-static constexpr int kOpRec = 64;                                       // frames one chunk may hold (a lane each)
-static constexpr int kOpGroup = 32;                                     // chunks per group counter
+static constexpr int kOpRec = 64;                                       // frames one chunk may hold
+static constexpr int kOpT = 256;                                        // chunks per scan_op_walk block
+static constexpr int kOpReg = 6;                                        // ... frames of a chunk held in registers
 static constexpr int kFailCopies = kWave, kFailStride = 16;             // the failure word's copies, 64 B apart
-static_assert(kTileChunks % kOpGroup == 0 && kOpRec == kWave, "one pass: groups inside tiles, a lane per frame");
-static_assert(kOnePassCap / kChunk / kTileChunks <= 256, "one pass: K4 sums the tiles before a block, a thread each");
-// counter words per parity for a scratch of `cap` chunks: the groups', then the tiles'
-static constexpr uint64_t op_counter_words(uint64_t cap) { return cap / kOpGroup + cap / kTileChunks; }
 
-// T / W words and the failure word: system-scope (sc0 sc1) stores and loads on both sides, so a
-// poll never re-reads a stale copy its own XCD's L2 kept from an earlier poll
 __device__ __forceinline__ void op_put(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint64_t op_get(const uint64_t* p) {
-    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // The failure word in kFailCopies copies on lines of their own: a failing chunk sets the copy its
 // index picks (a store: set once, never cleared within the call), a reader ORs all of them (one
 // load per lane; call it with the whole wavefront).  (One word -- an atomic OR by every failing
-// chunk, a load by every poller -- held one memory channel and K1 took 147 us at config 2, r06i.)
+// chunk, a load by every poller -- held one memory channel busy, r06i.)
 __device__ __forceinline__ bool op_failed(const ScanArgs& a) {
     const uint32_t v = __hip_atomic_load(a.opfail + (threadIdx.x & (kWave - 1)) * kFailStride, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_SYSTEM);
+                                         __HIP_MEMORY_SCOPE_AGENT);
     return __ballot(v != 0) != 0;
 }
 __device__ __forceinline__ void op_fail(const ScanArgs& a, uint64_t c) {
-    __hip_atomic_store(a.opfail + (c % kFailCopies) * kFailStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.opfail + (c % kFailCopies) * kFailStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// K2-K4: K1 resolved this call (every chunk checked, none failed -- K1 has finished by then)
+// K2-K4: the one-pass launch resolved this call (every chunk checked, none failed -- it has
+// finished by then)
 __device__ __forceinline__ bool onepass_done(const ScanArgs& a) { return a.onepass && !op_failed(a); }
 
-// a word tagged with the call's epoch, waited for by the whole wavefront (its value read from
-// lane 0, so every branch on it is scalar); false once the call failed or the wait ran out
-__device__ bool op_await(const ScanArgs& a, const uint64_t* p, uint64_t* out, uint64_t c) {
-    uint64_t t0 = 0;
-    for (uint32_t n = 0;; ++n) {
-        const uint64_t w = readlane64(op_get(p), 0);
-        if ((w >> kOpBits) == a.epoch) {
-            *out = w & kOpMask;
-            return true;
+// K1: T(c), for the next launch (a plain store)
+__device__ __forceinline__ void op_publish_t(const ScanArgs& a, uint64_t c, uint64_t tval, int lane) {
+    if (lane == 0 && c >= a.start / kChunk) a.st_t[c] = a.epoch << kOpBits | tval;
+}
+// T(c) as K1 published it (kTFail when this call's K1 did not: never on a finished K1)
+__device__ __forceinline__ uint64_t op_t(const ScanArgs& a, uint64_t c) {
+    const uint64_t w = a.st_t[c];
+    return (w >> kOpBits) == a.epoch ? (w & kOpMask) : kTFail;
+}
+
+// a look-back status word: [63:62] 1 aggregate / 2 inclusive | [61:38] epoch | [37:0] frames
+static constexpr int kGValBits = 38;
+__device__ __forceinline__ uint64_t op_gword(uint64_t flag, uint64_t epoch, uint64_t v) {
+    return flag << 62 | (epoch & 0xFFFFFF) << kGValBits | (v & ((1ull << kGValBits) - 1));
+}
+
+// the frames before block g (wave 0, every lane; its aggregate published first).  Every block
+// publishes, failed or not, so no wait outlives its predecessors' work; false past kOnePassWait.
+__device__ bool op_prefix(const ScanArgs& a, uint64_t g, uint64_t agg, int lane, uint64_t* out) {
+    if (lane == 0) op_put(a.st_g + g, op_gword(1, a.epoch, agg));
+    uint64_t acc = 0, t0 = 0;
+    for (int64_t top = (int64_t)g - 1, n = 0; top >= 0; ++n) {
+        const int64_t idx = top - lane;
+        uint64_t v = 0;
+        bool ok = true, incl = idx < 0;   // before block 0: an inclusive 0
+        if (idx >= 0) {
+            const uint64_t w = op_get(a.st_g + idx);
+            ok = (w >> 62) != 0 && ((w >> kGValBits) & 0xFFFFFF) == (a.epoch & 0xFFFFFF);
+            incl = ok && (w >> 62) == 2;
+            v = w & ((1ull << kGValBits) - 1);
         }
-        if ((n & 15) == 0) {   // (about every 7 us once the back-off is long)
-            if (n && op_failed(a)) return false;
+        const uint64_t im = __ballot(incl);
+        const int stop = im ? __builtin_ctzll(im) : kWave;   // the nearest inclusive prefix
+        const uint64_t need = stop >= kWave - 1 ? ~0ull : ((2ull << stop) - 1);
+        if ((__ballot(ok) & need) != need) {   // a predecessor has not published yet
             const uint64_t t = __builtin_amdgcn_s_memrealtime();
             if (n == 0) t0 = t;
-            else if (t - t0 > kOnePassWait) {
-                op_fail(a, c);
-                return false;
-            }
+            else if (t - t0 > kOnePassWait) return false;
+            __builtin_amdgcn_s_sleep(1);
+            continue;
         }
-        if (n < 8) __builtin_amdgcn_s_sleep(2);   // (~130 cycles, then ~1,000)
-        else __builtin_amdgcn_s_sleep(16);
+        acc += wave_sum(lane <= stop && idx >= 0 ? v : 0);
+        if (stop < kWave) break;
+        top -= kWave;
     }
+    if (lane == 0) op_put(a.st_g + g, op_gword(2, a.epoch, acc + agg));
+    *out = acc;
+    return true;
 }
 
-// K1's hand-over words in LDS: [0][w] T and [1][w] W of wave w's chunk, for wave w + 1 of the block
-// (kHPend until set: every wave clears its own before the block's one barrier).  Only the block's
-// last wave hands over through global memory (st_t, st_x), to the next block's first: one
-// global poller per block, each backing off -- a poll per wave of a covering grid, every ~100
-// cycles, swamped the memory system (K1 at config 2: 115 us, r06f).
-static constexpr uint64_t kHPend = ~0ull;
-typedef uint64_t OpHand[2][4];
-
-// K1: T(c), for the successor's wave
-__device__ __forceinline__ void op_publish_t(const ScanArgs& a, uint64_t c, uint64_t tval, int lane, int wv, OpHand& h) {
-    if (lane == 0) {
-        __hip_atomic_store(&h[0][wv], tval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (wv == 3 && c >= a.start / kChunk) op_put(a.st_t + c, a.epoch << kOpBits | tval);
-    }
-}
-
-// a hand-over word of the wave before, in LDS; false once the call failed or the wait ran out
-__device__ bool op_await_lds(const ScanArgs& a, const uint64_t* p, uint64_t* out, uint64_t c) {
-    uint64_t t0 = 0;
-    for (uint32_t n = 0;; ++n) {
-        const uint64_t w = readlane64(__hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_WORKGROUP), 0);
-        if (w != kHPend) {
-            *out = w;
-            return true;
-        }
-        if ((n & 255) == 0) {   // (about every 7 us)
-            if (n && op_failed(a)) return false;
-            const uint64_t t = __builtin_amdgcn_s_memrealtime();
-            if (n == 0) t0 = t;
-            else if (t - t0 > kOnePassWait) {
-                op_fail(a, c);
-                return false;
-            }
-        }
-        if (n < 8) __builtin_amdgcn_s_sleep(2);   // (~130 cycles, then ~1,000)
-        else __builtin_amdgcn_s_sleep(16);
-    }
-}
-
-// K1, after T(c) is published: the one-pass work of chunk c (the whole wavefront; every value but
-// the lane's frame record is wave-uniform).  st: the chunk's bytes in LDS (not loaded for the
-// virtual chunk, whose only possible entry -- the stream's end -- parses without them).
-__device__ void op_chunk(const ScanArgs& a, uint64_t c, uint64_t tval, const uint32_t* st, int lane, int wv, OpHand& h) {
-    const uint64_t c0 = a.start / kChunk;
+// The one-pass launch: chunks [b kOpT, (b + 1) kOpT), thread t the chunk b kOpT + t.  A chunk after
+// Multi ones walks on from the nearest predecessor whose T is known (Single or None) through them
+// to its own start, so no thread waits for another's walk (a wave waiting on its own lanes' walks
+// took one walk round per Multi chunk in it: 19.6 us for this launch at config 2, r06_onepass).
+static constexpr int kOpBack = 8;   // Multi predecessors walked through at most (more: the graph path)
+__global__ __launch_bounds__(kOpT) void scan_op_walk(ScanArgs a) {
+    __shared__ uint32_t wsum[kOpT / kWave];
+    __shared__ uint64_t base;
+    __shared__ int lb_ok;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    const uint64_t g = blockIdx.x, c = g * kOpT + tid, c0 = a.start / kChunk;
+    const bool mine = c >= c0 && c <= a.nc;
     const uint64_t B = c * kChunk, Bend = B + kChunk;
-    if (c < c0) {   // before the first header: no chain, no frames
-        if (lane == 0) a.opin[2 * c] = 0;
-        return;
-    }
-    bool bad = tval == kTFail;
+    const uint64_t tval = mine ? op_t(a, c) : kTNone;
+    bool bad = mine && tval == kTFail;
+    // the entry: the chain's position at or past B (kXEnd: it ended before)
     uint64_t e = kXEnd;
-#ifdef NETC_SCAN_TRACE
-    const uint64_t tw0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    if (c == c0) {
-        e = a.start;
-    } else if (!bad) {   // the entry, speculated from the predecessor
-        uint64_t tp = 0;
-        if (!(wv ? op_await_lds(a, &h[0][wv - 1], &tp, c) : op_await(a, a.st_t + c - 1, &tp, c)) || tp == kTFail) bad = true;
-        else if (tp != kTMulti) e = tp == kTNone ? kXEnd : tp;
-        else if (!(wv ? op_await_lds(a, &h[1][wv - 1], &e, c) : op_await(a, a.st_x + c - 1, &e, c)) || e == kTFail) bad = true;
+    if (mine && !bad) {
+        if (c == c0) {
+            e = a.start;
+        } else {
+            uint64_t k = 1, tp = op_t(a, c - 1);
+            while (tp == kTMulti && c - k > c0 && k < (uint64_t)kOpBack) tp = op_t(a, c - ++k);
+            if (tp == kTFail || (tp == kTMulti && c - k > c0)) {
+                bad = true;   // (a failed prediction, or a run of more than kOpBack Multi chunks)
+            } else {
+                // p: where the chain enters chunk c - k + 1 (c - k == c0 with a Multi T: the start)
+                uint64_t p = tp == kTMulti ? a.start : (tp == kTNone ? kXEnd : tp);
+                for (uint32_t hops = 0; p < B && !bad; ++hops) {   // through the Multi chunks to B
+                    if (hops == (uint32_t)(kOpRec * kOpBack)) {
+                        bad = true;
+                        break;
+                    }
+                    const uint64_t v = parse_at(a, p, window_global(a, p), nullptr, nullptr);
+                    p = (v & kTerm) ? kXEnd : v;   // (the chunk where it ends reports it)
+                }
+                e = p;
+            }
+        }
     }
-#ifdef NETC_SCAN_TRACE
-    if (lane == 0) {   // [9] waits summed, [10] the longest, [11] waits over 2 us (100 MHz ticks)
-        const uint64_t tw = __builtin_amdgcn_s_memrealtime() - tw0;
-        OP_STAMP_ADD(9, tw);
-        OP_STAMP_MAX(10, tw);
-        if (tw > 200) OP_STAMP_ADD(11, 1);
-    }
-#endif
-    uint64_t cnt = 0, endpos = 0, W = kXEnd, rec = 0;
+    uint64_t cnt = 0, endpos = 0, Wx = kXEnd;
     uint32_t ended = 0;   // 1: the chain ends in this chunk (END), 2: it dies here (an error at endpos)
-    if (bad) {
+    uint64_t reg[kOpReg];
+#pragma unroll
+    for (int r = 0; r < kOpReg; ++r) reg[r] = 0;
+    if (!mine || bad) {
     } else if (e == kXEnd) {
         if (tval != kTNone && tval != kTMulti) bad = true;   // not visited, yet Single
     } else if (e >= Bend) {
@@ -716,19 +698,16 @@ __device__ void op_chunk(const ScanArgs& a, uint64_t c, uint64_t tval, const uin
                     } else if (tval == kTNone) {
                         bad = true;   // an exit K1's exit set did not hold
                     } else {
-                        W = p;
+                        Wx = p;
                     }
                 } else {
-                    W = p;
+                    Wx = p;
                 }
                 break;
             }
             uint32_t key = 0;
             uint8_t b0 = 0;
-            // the chunk's LDS copy holds the stream's bytes below len once the stream has 16 (a
-            // shorter one was loaded from a scratch word: its bytes come from global memory)
-            const uint64_t v = B >= a.len ? term(kEnd, p)
-                               : parse_at(a, p, a.len >= 16 ? window_at(st, (int)(p - B)) : window_global(a, p), &key, &b0);
+            const uint64_t v = parse_at(a, p, window_global(a, p), &key, &b0);
             if (v & kTerm) {
                 if (term_type(v) == kDead && a.spec) bad = true;
                 ended = term_type(v) == kDead ? 2 : 1;
@@ -739,88 +718,64 @@ __device__ void op_chunk(const ScanArgs& a, uint64_t c, uint64_t tval, const uin
                 bad = true;
                 break;
             }
-            if ((uint64_t)lane == cnt) rec = (p - B) | (uint64_t)b0 << 16 | (uint64_t)key << 32;
+            const uint64_t fr = (p - B) | (uint64_t)b0 << 16 | (uint64_t)key << 32;
+            // the first kOpReg frames stay in registers (constant indices: selects, no scratch)
+#pragma unroll
+            for (int r = 0; r < kOpReg; ++r) reg[r] = cnt == (uint64_t)r ? fr : reg[r];
+            if (cnt >= (uint64_t)kOpReg) a.opfl[c * kOpRec + cnt] = fr;
             ++cnt;
             p = v;
         }
-        if (tval != kTMulti && tval != kTNone && W != tval) bad = true;
+        if (tval != kTMulti && tval != kTNone && Wx != tval) bad = true;
     }
-    if (lane == 0) {   // the successor's entry after a Multi T (kTFail: this chunk failed)
-        __hip_atomic_store(&h[1][wv], bad ? kTFail : W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (bad) op_fail(a, c);
-        else if (wv == 3 && tval == kTMulti) op_put(a.st_x + c, a.epoch << kOpBits | W);
+    // one store per wavefront that failed (a store per failing chunk -- most chunks of a stream of
+    // large frames -- queued on the 64 copies' lines)
+    if (const uint64_t bm = __ballot(bad)) {
+        if (lane == __builtin_ctzll(bm)) op_fail(a, c);
     }
-    if (bad) return;
-    if ((uint64_t)lane < cnt) a.opfl[c * kOpRec + lane] = rec;
-    if (lane == 0) {
-        a.opin[2 * c] = cnt | (uint64_t)ended << 32;
-        a.opin[2 * c + 1] = endpos;
-        if (cnt) {
-            __hip_atomic_fetch_add(a.opc + c / kOpGroup, (uint32_t)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(a.opc + a.opc_tiles + c / kTileChunks, (uint32_t)cnt, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-// K4 on the one-pass path, EC chunks per block: the frames before the block (the earlier tiles'
-// counters and the tile's earlier groups'), the block's chunks scanned, their recorded frames
-// written (a wavefront per chunk, a lane per frame), and the results by the chunk where the chain
-// ends.
-template <int EC>
-__device__ void op_emit(const ScanArgs& a) {
-    static_assert(EC <= kWave && EC % kOpGroup == 0, "one pass: a block's chunks in one wavefront's scan");
-    __shared__ uint64_t k0s[EC];
-    __shared__ uint32_t cnts[EC];
-    __shared__ uint32_t red[kScanT / kWave];
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
-    const uint64_t cb = (uint64_t)blockIdx.x * EC, tile = cb / kTileChunks;
-    const uint64_t g0 = tile * (kTileChunks / kOpGroup), ng = (cb - tile * kTileChunks) / kOpGroup;
-    uint32_t v = 0;
-    if ((uint64_t)tid < tile) v += a.opc[a.opc_tiles + tid];
-    if ((uint64_t)tid < ng) v += a.opc[g0 + tid];
-    const uint32_t inc = wave_incl_sum(v);
-    if (lane == kWave - 1) red[wv] = inc;
-    uint64_t cnt = 0, info = 0;
-    if (wv == 0) {
-        const uint64_t c = cb + lane;
-        if (lane < EC && c <= a.nc) info = a.opin[2 * c];
-        cnt = (uint32_t)info;
-    }
+    // the frames before each chunk: the block's scan, then the blocks' look-back (every block
+    // publishes, failed or not, so no look-back waits on a block that gave up)
+    const uint32_t incl = wave_incl_sum((uint32_t)cnt);
+    if (lane == kWave - 1) wsum[wv] = incl;
     __syncthreads();
+    uint64_t before = incl - (uint32_t)cnt;
+    for (int k = 0; k < wv; ++k) before += wsum[k];
     if (wv == 0) {
-        uint64_t base = 0;
+        uint64_t agg = 0;
 #pragma unroll
-        for (int k = 0; k < kScanT / kWave; ++k) base += red[k];
-        const uint32_t ci = wave_incl_sum((uint32_t)cnt);
-        const uint64_t k0 = base + ci - (uint32_t)cnt;
-        if (lane < EC) {
-            k0s[lane] = k0;
-            cnts[lane] = (uint32_t)cnt;
-        }
-        if (info >> 32) {   // the chain ends in this chunk: the results
-            const uint64_t c = cb + lane, total = k0 + cnt, endpos = a.opin[2 * c + 1];
-            a.result[0] = total;
-            a.result[1] = endpos;
-            a.result[2] = (info >> 32) == 2 ? endpos : ~0ull;
-            if (total <= a.max_frames) a.hdr[total] = endpos;
+        for (int k = 0; k < kOpT / kWave; ++k) agg += wsum[k];
+        uint64_t pre = 0;
+        const bool ok = op_prefix(a, g, agg, lane, &pre);
+        if (lane == 0) {
+            base = pre;
+            lb_ok = ok;
         }
     }
     __syncthreads();
-    for (int j = wv; j < EC; j += kScanT / kWave) {
-        const uint64_t c = cb + j;
-        if (c > a.nc) break;
-        if ((uint32_t)lane < cnts[j]) {
-            const uint64_t f = a.opfl[c * kOpRec + lane];
-            put_frame(a, k0s[j] + lane, c * kChunk + (f & 0xFFFFu), (uint32_t)(f >> 32), (uint8_t)(f >> 16));
-        }
+    if (!lb_ok) {   // (block-uniform) a look-back that ran out: the graph path
+        if (tid == 0) op_fail(a, c);
+        return;
+    }
+    if (!mine) return;
+    const uint64_t k0 = base + before;
+#pragma unroll
+    for (int r = 0; r < kOpReg; ++r)
+        if ((uint64_t)r < cnt) put_frame(a, k0 + r, B + (reg[r] & 0xFFFFu), (uint32_t)(reg[r] >> 32), (uint8_t)(reg[r] >> 16));
+    for (uint64_t i = kOpReg; i < cnt; ++i) {
+        const uint64_t f = a.opfl[c * kOpRec + i];
+        put_frame(a, k0 + i, B + (f & 0xFFFFu), (uint32_t)(f >> 32), (uint8_t)(f >> 16));
+    }
+    if (ended) {   // the chain ends in this chunk: the results
+        const uint64_t total = k0 + cnt;
+        a.result[0] = total;
+        a.result[1] = endpos;
+        a.result[2] = ended == 2 ? endpos : ~0ull;
+        if (total <= a.max_frames) a.hdr[total] = endpos;
     }
 }
 
-// K4, both paths: the other parity's counters zeroed for the next call (a grid-stride loop)
+// K4, both paths: the previous call's failure copies zeroed for the next call
 __device__ __forceinline__ void op_clear_prev(const ScanArgs& a) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kScanT + threadIdx.x; i < a.opc_words; i += (uint64_t)gridDim.x * kScanT)
-        a.opc_prev[i] = 0;
     if (blockIdx.x == 0 && threadIdx.x < kFailCopies) a.opfail_prev[threadIdx.x * kFailStride] = 0;
 }
 
@@ -875,8 +830,7 @@ __device__ __forceinline__ u32x4 k1_load(const uint8_t* p) {
     return *(const NETC_GLOBAL u32x4u*)p;
 }
 
-// ONE: the one-pass path after the parse -- T(c) published (op_publish_t), then the chunk's walk
-// from its speculated entry (op_chunk).
+// ONE: the one-pass path's prediction T(c) after the parse (op_publish_t).
 template <bool NT, bool ONE>
 __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     if (threadIdx.x == 0 && blockIdx.x == 0) OP_TRACE(0, 1);
@@ -884,7 +838,6 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     __shared__ uint32_t stage[4][kStageWords];   // per wave: its chunk's bytes (+ 16 after)
     __shared__ unsigned long long set[4][kSet];
     __shared__ uint16_t queue[4][kQCap];
-    __shared__ OpHand hand;   // (ONE) the waves' T and W hand-over words
 #ifdef NETC_SCAN_K1_EXP
     __shared__ uint32_t qn[4];
     if ((threadIdx.x & 63) == 0) qn[threadIdx.x / 64] = 0;
@@ -894,18 +847,11 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     // then scalar (SGPR arithmetic, scalar branches) instead of per-lane VALU
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(tid / kWave);
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
-    if constexpr (ONE) {   // each wave clears its hand-over words before any wave of the block reads them
-        if (lane == 0) hand[0][wv] = hand[1][wv] = kHPend;
-        __syncthreads();
-    }
     if (c > a.nc) return;
     const uint64_t B = c * kChunk, Bend = B + kChunk;
     if (lane == 0 && a.start / kChunk == c) append_cand(a, a.start, true);   // the root node
     if (B >= a.len) {   // the virtual chunk: no bytes
-        if constexpr (ONE) {
-            op_publish_t(a, c, kTNone, lane, wv, hand);
-            op_chunk(a, c, kTNone, stage[wv], lane, wv, hand);
-        }
+        if constexpr (ONE) op_publish_t(a, c, kTNone, lane);
         return;
     }
     uint32_t d[4][4], nx[4];
@@ -1083,10 +1029,7 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
     }
     if (total > (uint32_t)kQCap) {   // wave-uniform (adversarial payloads, non-strict mode)
         if (lane == 0) atomicOr(a.ovf, kOvfQueue);
-        if constexpr (ONE) {
-            op_publish_t(a, c, kTFail, lane, wv, hand);
-            if (lane == 0) op_fail(a, c);
-        }
+        if constexpr (ONE) op_publish_t(a, c, kTFail, lane);
         return;
     }
     uint32_t at = incl - mine;
@@ -1131,10 +1074,11 @@ __global__ __launch_bounds__(256) void scan_exits(ScanArgs a) {
         const uint64_t bn = __ballot(nodes != 0);
         const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(nodes), kWave - 1);
         const uint64_t t = __ballot(ovf) ? kTFail : (n == 0 ? kTNone : (n > 1 ? kTMulti : readlane64(ex, __builtin_ctzll(bn))));
-        op_publish_t(a, c, t, lane, wv, hand);
-        if (lane == 0) OP_STAMP_ADD(t == kTNone ? 5 : t == kTMulti ? 7 : t == kTFail ? 8 : 6, 1);
-        op_chunk(a, c, t, stage[wv], lane, wv, hand);
-        if (lane == 0) OP_STAMP_MAX(1, __builtin_amdgcn_s_memrealtime());
+        op_publish_t(a, c, t, lane);
+        if (lane == 0) {
+            OP_STAMP_ADD(t == kTNone ? 5 : t == kTMulti ? 7 : t == kTFail ? 8 : 6, 1);
+            OP_STAMP_MAX(1, __builtin_amdgcn_s_memrealtime());
+        }
     }
 }
 
@@ -2332,8 +2276,7 @@ __global__ __launch_bounds__(kScanT) void scan_emit(ScanArgs a, uint64_t tiles) 
     const uint64_t tile = (uint64_t)blockIdx.x * EC / kTileChunks;   // EC divides kTileChunks
     if (tid == 0 && blockIdx.x == 0) OP_TRACE(8, 1);
     op_clear_prev(a);
-    if (onepass_done(a)) {   // K1 walked every chunk: the descriptors, the results, the clearing
-        op_emit<EC>(a);
+    if (onepass_done(a)) {   // the one-pass launch wrote the frames and results: only the clearing
         if (tid < EC) {
             const uint64_t c = (uint64_t)blockIdx.x * EC + tid;
             if (c <= a.nc) {
@@ -2569,7 +2512,7 @@ std::mutex& stream_scratch_mu() {
 // regions; flags, ccount and ext first -- the region every call leaves zeroed.
 struct Layout {
     uint64_t flags, ccount, ext, tarr, cleared, cand, link, nterm, ncnt, wsum, pbits, anq, anc, anc_n, flist, text,
-        tcount, tinfo, st_t, st_x, opfl, opin, opc, opf, total;
+        tcount, tinfo, st_t, st_g, opfl, opf, total;
 };
 Layout layout_for(uint64_t cap) {
     auto align = [](uint64_t x) { return (x + 63) & ~63ull; };
@@ -2580,7 +2523,6 @@ Layout layout_for(uint64_t cap) {
     l.ccount = o;  o = align(o + cap * 4);
     l.ext = o;     o = align(o + slots);
     l.tarr = o;    o = align(o + tiles * 4);
-    l.opc = o;     o = align(o + 2 * op_counter_words(cap) * 4);   // one-pass counters, two parities
     l.opf = o;     o = align(o + 2 * kFailCopies * kFailStride * 4);  // one-pass failure words, two sets
     l.cleared = o;
     l.cand = o;    o = align(o + slots * 8);
@@ -2597,9 +2539,8 @@ Layout layout_for(uint64_t cap) {
     l.tcount = o;  o = align(o + tiles * 4);
     l.tinfo = o;   o = align(o + tiles * sizeof(TileInfo));
     l.st_t = o;    o = align(o + cap * 8);   // one-pass status words (epochs: never cleared per call)
-    l.st_x = o;    o = align(o + cap * 8);
+    l.st_g = o;    o = align(o + (cap / kOpT + 1) * 8);
     l.opfl = o;    o = align(o + cap * kOpRec * 8);
-    l.opin = o;    o = align(o + cap * 16);
     l.total = o;
     return l;
 }
@@ -2722,26 +2663,26 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     a.opfail = (uint32_t*)(m + l.opf) + ((s.calls & 1) ? kFailCopies * kFailStride : 0);
     a.opfail_prev = (uint32_t*)(m + l.opf) + ((s.calls & 1) ? 0 : kFailCopies * kFailStride);
     ++s.calls;
-    // the one-pass path: knob SCAN_ONEPASS (1: up to kOnePassCap, 2: up to kOnePassMax; off by
-    // default -- it measured 126 us against the graph path's 41 at config 2).  Each
-    // call has its own epoch; when the 24-bit epoch wraps, the status words are cleared once, so a
-    // word left from 2^24 calls ago cannot match.
+    // the one-pass path: knob SCAN_ONEPASS (0 never, 1 up to kOnePassCap, 2 up to kOnePassMax),
+    // by default up to kOnePassMax of stream (config 2: 34.6-35.1 us against the graph path's
+    // 41.5-41.8; a stream it cannot resolve pays its launch before the graph path).
+    // Each call has its own epoch; when the 24-bit epoch wraps, the status words are cleared once,
+    // so a word left from 2^24 calls ago cannot match.
     const int64_t op = knob(NETC_GPU_KNOB_SCAN_ONEPASS);
     const int64_t fuse = knob(NETC_GPU_KNOB_SCAN_FUSE);
-    a.onepass = op > 0 && len <= (op == 1 ? kOnePassCap : kOnePassMax) ? 1 : 0;
+    // A dense stream has a frame start in every chunk from the start on, so a caller whose frame
+    // capacity is below that count (it expects larger frames) would only pay the launch (a 64 MiB
+    // sample of config 4's mix: 46.0 against 35.9 us, r06t): no one-pass launch then.
+    const bool may_be_dense = max_frames >= (len - (start < len ? start : len)) / kChunk;
+    a.onepass = op != 0 && len <= (op == 1 ? kOnePassCap : kOnePassMax) && (may_be_dense || op > 0) ? 1 : 0;
     if (++s.epoch >= (1ull << 24) - 1) {   // (all-ones never: an exit-set entry's ~0 must not match)
         if ((e = hipMemsetAsync(m + l.st_t, 0, l.opfl - l.st_t, stream)) != hipSuccess) return e;
         s.epoch = 1;
     }
     a.epoch = s.epoch;
     a.st_t = (uint64_t*)(m + l.st_t);
-    a.st_x = (uint64_t*)(m + l.st_x);
     a.opfl = (uint64_t*)(m + l.opfl);
-    a.opin = (uint64_t*)(m + l.opin);
-    a.opc_words = op_counter_words(s.cap);
-    a.opc_tiles = s.cap / kOpGroup;
-    a.opc = (uint32_t*)(m + l.opc) + ((s.calls & 1) ? a.opc_words : 0);      // (s.calls: already counted)
-    a.opc_prev = (uint32_t*)(m + l.opc) + ((s.calls & 1) ? 0 : a.opc_words);
+    a.st_g = (uint64_t*)(m + l.st_g);
     a.ccount = (uint32_t*)(m + l.ccount);
     a.ext = m + l.ext;
     a.tarr = (uint32_t*)(m + l.tarr);
@@ -2778,6 +2719,7 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
 #if defined(NETC_SCAN_K1_ONLY) || defined(NETC_SCAN_K1_EXP)
     return hipGetLastError();   // diagnostic builds only (tools/): K1 timed alone
 #endif
+    if (a.onepass) hipLaunchKernelGGL(scan_op_walk, dim3((unsigned)((chunks + kOpT - 1) / kOpT)), dim3(kOpT), 0, stream, a);
     // K2, K3a, K3b: by default K2 and then K3a + K3b as one launch up to kMergeTiles (256) tiles
     // (scan_tiles_resolve), three launches above.  NETC_GPU_KNOB_SCAN_FUSE (tests and A/B):
     // 0 three launches at every size; 1 K2 + K3a + K3b as one launch up to kFuseTiles tiles
@@ -2799,7 +2741,8 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
         else
             hipLaunchKernelGGL(scan_links<kBlkChunks>, dim3(blk), dim3(kScanT), 0, stream, a);
     };
-    // the one-pass path: K2 + K3 fused by default (one gated launch; SCAN_FUSE 2: the split launches)
+    // the one-pass path: K2 + K3 fused by default (one gated launch; SCAN_FUSE 2: the split launches,
+    // which measured 3.8 us slower at config 2 when the one-pass launch resolves the call, r06r)
     const bool fused = tiles <= (uint64_t)kFuseTiles && (fuse == 1 || (a.onepass && fuse < 0 && !big));
     if (fused) {   // (32 chunks per K2 block: the tiles' arrival counts)
         hipLaunchKernelGGL(scan_links_fused, dim3(blk), dim3(kScanT), 0, stream, a, tiles, blk);

@@ -389,12 +389,13 @@ def test_emit_block_sizes(torch_cuda, gpu_knob, emit):
 
 @pytest.mark.parametrize("onepass,fuse", [("1", "-1"), ("1", "2"), ("0", "-1")])
 def test_onepass_and_graph_paths(torch_cuda, gpu_knob, onepass, fuse):
-    """the one-pass path (dense streams: K1's chunks speculate their entries from their
-    predecessors, walk and check them; K2 + K3 only read a flag; K4 sums the counts and writes the
-    frames) and the graph path (knob SCAN_ONEPASS = 0) on the same streams: identical results;
-    dense strict streams finish on the one-pass path (netc_gpu_scan_diag bit 32), streams with
-    chunk-covering frames or chunks of more than 64 frames on the graph kernels.  K2 + K3 are one
-    gated launch by default, separate ones with SCAN_FUSE = 2."""
+    """the one-pass path (dense streams: K1 publishes each chunk's exit prediction; the next launch
+    speculates every chunk's entry from its predecessors, walks and checks it, scans the counts and
+    writes the frames; K2 + K3 and K4 only read a flag) and the graph path (knob SCAN_ONEPASS = 0)
+    on the same streams: identical results; dense strict streams finish on the one-pass path
+    (netc_gpu_scan_diag bit 32), streams with chunk-covering frames or chunks of more than 64
+    frames on the graph kernels.  K2 + K3 are one gated launch by default, separate ones with
+    SCAN_FUSE = 2."""
     gpu_knob("SCAN_ONEPASS", onepass)
     gpu_knob("SCAN_FUSE", fuse)
     rng = np.random.default_rng(97)

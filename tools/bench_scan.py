@@ -22,7 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workloads", default="c2,c4")
+    ap.add_argument("--workloads", default="c2,c4", help="c2, c4 (256 MiB of the config-4 mix), c4s (64 MiB of it)")
     ap.add_argument("--non-strict", action="store_true", help="flags 0: the reference's semantics (speculative pass)")
     ap.add_argument("--unmasked", action="store_true", help="unmasked frames (server-to-client direction)")
     ap.add_argument("--rsv1", action="store_true",
@@ -44,9 +44,9 @@ def main():
     s = torch.cuda.Stream(dev)
     sh = s.cuda_stream
     for wl in args.workloads.split(","):
-        off, keys, total = synth.config(wl)
-        if wl == "c4":   # 256 MiB of the config-4 size mix keeps the host-side encode short
-            cut = int(np.searchsorted(off, 256 << 20))
+        off, keys, total = synth.config("c4" if wl == "c4s" else wl)
+        if wl in ("c4", "c4s"):   # 256 MiB of the config-4 size mix keeps the host-side encode short
+            cut = int(np.searchsorted(off, (256 if wl == "c4" else 64) << 20))   # c4s: 64 MiB of it
             off, keys = off[: cut + 1], keys[:cut]
         rng = np.random.default_rng(5)
         payload = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)

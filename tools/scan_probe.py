@@ -84,8 +84,7 @@ def stamps(torch, lib, run_scan, wire, name):
     t0 = int(v[0])
     us = lambda t: (int(t) - t0) / 100.0 if t else None
     out = {"case": name, "k1_start": 0.0, "k1_last_wave_end": us(v[1]), "t_none": int(v[5]), "t_single": int(v[6]),
-           "t_multi": int(v[7]), "t_fail": int(v[8]), "wait_sum_us": int(v[9]) / 100.0, "wait_max_us": int(v[10]) / 100.0,
-           "waits_over_2us": int(v[11])}
+           "t_multi": int(v[7]), "t_fail": int(v[8])}
     import json
     print(json.dumps(out), flush=True)
 
