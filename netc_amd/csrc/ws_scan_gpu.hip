@@ -714,7 +714,10 @@ __global__ __launch_bounds__(kOpT) void scan_op_walk(ScanArgs a) {
                 endpos = term_pos(v);
                 break;
             }
-            if (cnt == (uint64_t)kOpRec) {   // a chunk of more frames: the graph path
+            // a chunk of more than kOpRec frames -- or one projected to hold more, from the mean
+            // length of its first ones (16-B frames: ~190 a chunk, walked a hop at a time) -- takes
+            // the graph path
+            if (cnt == (uint64_t)kOpRec || (cnt >= 4 && (p - e) * ((uint64_t)kOpRec - cnt) < (Bend - p) * cnt)) {
                 bad = true;
                 break;
             }
