@@ -664,8 +664,8 @@ __global__ __launch_bounds__(kOpT) void scan_op_walk(ScanArgs a) {
             } else {
                 // p: where the chain enters chunk c - k + 1 (c - k == c0 with a Multi T: the start)
                 uint64_t p = tp == kTMulti ? a.start : (tp == kTNone ? kXEnd : tp);
-                for (uint32_t hops = 0; p < B && !bad; ++hops) {   // through the Multi chunks to B
-                    if (hops == (uint32_t)(kOpRec * kOpBack)) {
+                for (uint64_t hops = 0; p < B && !bad; ++hops) {   // through the Multi chunks to B
+                    if (hops == (uint64_t)kOpRec * k) {   // (each of them may hold kOpRec frames)
                         bad = true;
                         break;
                     }
