@@ -290,6 +290,7 @@ struct ScanArgs {
                            // loop always; NETC_SCAN_FAST_RANK=0, tests)
     // the one-pass path (scan_exits<_, true>; see "One pass" below)
     int onepass;           // this call runs it (the host's choice: knob SCAN_ONEPASS, stream size)
+    uint64_t op_walk;      // frames a chunk's walk may be projected to (kOpWalk; kOpRec when forced by the knob)
     uint32_t* opfail;      // this call's one-pass failure words: kFailCopies, kFailStride apart (two sets,
     uint32_t* opfail_prev; // ... alternate calls; K4 zeroes the previous call's, as for ovf)
     uint64_t* st_t;        // per chunk: its exit prediction T (epoch-tagged; K1)
@@ -562,6 +563,8 @@ static constexpr uint64_t kOnePassCap = 256ull << 20;                   // knob 
 static constexpr int kOpRec = 64;                                       // frames one chunk may hold
 static constexpr int kOpT = 256;                                        // chunks per scan_op_walk block
 static constexpr int kOpReg = 6;                                        // ... frames of a chunk held in registers
+static constexpr uint64_t kOpWalk = 16;                                 // frames a chunk's walk is projected to at most
+static constexpr uint64_t kOpDensest = 12;                              // frames per chunk a caller may expect (max_frames)
 static constexpr int kFailCopies = kWave, kFailStride = 16;             // the failure word's copies, 64 B apart
 
 __device__ __forceinline__ void op_put(uint64_t* p, uint64_t v) {
@@ -714,10 +717,10 @@ __global__ __launch_bounds__(kOpT) void scan_op_walk(ScanArgs a) {
                 endpos = term_pos(v);
                 break;
             }
-            // a chunk of more than kOpRec frames -- or one projected to hold more, from the mean
-            // length of its first ones (16-B frames: ~190 a chunk, walked a hop at a time) -- takes
-            // the graph path
-            if (cnt == (uint64_t)kOpRec || (cnt >= 4 && (p - e) * ((uint64_t)kOpRec - cnt) < (Bend - p) * cnt)) {
+            // a chunk of more than kOpRec frames -- or one projected to hold more than kOpWalk, from
+            // the mean length of its first ones (walked a hop at a time, such a chunk costs more
+            // than the graph path) -- takes the graph path
+            if (cnt == (uint64_t)kOpRec || (cnt >= 4 && (p - e) * (a.op_walk - cnt) < (Bend - p) * cnt)) {
                 bad = true;
                 break;
             }
@@ -2676,8 +2679,13 @@ hipError_t launch_scan_frames(const uint8_t* wire, uint64_t len, uint64_t start,
     // A dense stream has a frame start in every chunk from the start on, so a caller whose frame
     // capacity is below that count (it expects larger frames) would only pay the launch (a 64 MiB
     // sample of config 4's mix: 46.0 against 35.9 us, r06t): no one-pass launch then.
-    const bool may_be_dense = max_frames >= (len - (start < len ? start : len)) / kChunk;
+    // ... and one expecting more than kOpDensest frames a chunk gets nothing from it either: each
+    // chunk's thread walks its frames a hop at a time (uniform 128-B frames, ~30 a chunk: 111-118
+    // against 86 us on the graph path; 16-B frames 390 against 270, r06x).
+    const uint64_t span = (len - (start < len ? start : len)) / kChunk;
+    const bool may_be_dense = max_frames >= span && max_frames <= kOpDensest * (span + 1);
     a.onepass = op != 0 && len <= (op == 1 ? kOnePassCap : kOnePassMax) && (may_be_dense || op > 0) ? 1 : 0;
+    a.op_walk = op > 0 ? (uint64_t)kOpRec : kOpWalk;
     if (++s.epoch >= (1ull << 24) - 1) {   // (all-ones never: an exit-set entry's ~0 must not match)
         if ((e = hipMemsetAsync(m + l.st_t, 0, l.opfl - l.st_t, stream)) != hipSuccess) return e;
         s.epoch = 1;
