@@ -157,11 +157,12 @@ int netc_gpu_tune(int unroll, int max_blocks, int flags);
  *                      else 0]                                      (NETC_ENC_PF)
  *   SCAN_BLOCK_CHUNKS  chunks per block of the frame scan's link and emit phases: 32 or 64
  *                      [32 up to 128 MiB of stream, 64 above]       (NETC_SCAN_BLOCK_CHUNKS)
- *   SCAN_ONEPASS       the frame scan's one-pass path (K1's chunks speculate their entries
- *                      from their predecessors' exit predictions and walk their frames; the
- *                      graph kernels then only check a flag): 0 never, 1 up to 256 MiB of
- *                      stream, 2 up to 128 MiB [off: slower than the graph path at config 2,
- *                      DESIGN.md §16.4]                             (NETC_SCAN_ONEPASS)
+ *   SCAN_ONEPASS       the frame scan's one-pass path (K1 publishes each chunk's exit
+ *                      prediction; one launch speculates every chunk's entry from them, walks
+ *                      and checks it and writes the frames; the graph kernels then only check
+ *                      a flag): 0 never, 1 forced up to 256 MiB of stream, 2 forced up to
+ *                      128 MiB [up to 128 MiB when max_frames allows 1-12 frames per 4 KiB
+ *                      chunk; DESIGN.md §16.4]                      (NETC_SCAN_ONEPASS)
  *   INJECT_FAULT       fault injection for tests: the ingest / egress ring submission this
  *                      countdown reaches (0 = the next one) fails as NETC_GPU_ELAUNCH
  *                      without launching, then the knob disarms itself [off]
