@@ -126,7 +126,10 @@ int netc_gpu_encode_frames_class(int device, void *d_wire, size_t wire_capacity,
  * scan stops at the first frame that does not (its offset is CONSUMED — keep the
  * bytes from there for the next call) or, in strict mode, at a rejected header
  * (ERROR = CONSUMED = its offset).  Frames past max_frames are counted but not
- * recorded.  Asynchronous on `stream`; read d_result after synchronising.
+ * recorded.  max_frames is also a density hint: when it allows 1 to 12 frames per 4 KiB of
+ * stream (up to 128 MiB), the scan first tries its one-pass path for dense streams, with the
+ * same results either way (NETC_GPU_KNOB_SCAN_ONEPASS, include/ws/mask.h).
+ * Asynchronous on `stream`; read d_result after synchronising.
  * Scratch memory is allocated on first use per (device, stream) and reused until
  * netc_gpu_stream_release(device, stream) (include/ws/mask.h) frees it: call that
  * before destroying a stream the scan ran on.
